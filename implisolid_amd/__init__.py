@@ -1,0 +1,289 @@
+"""implisolid_amd -- MI355X-native implicit-surface polygoniser (Python host side).
+
+The product is the shared library ``implisolid_amd/lib/libimplisolid_mi355x.so`` (HIP, gfx950),
+whose C ABI (``include/implisolid.h``) is a drop-in for ImpliSolid's ``mcc2.cpp`` interface.  This
+module binds it with ctypes and mirrors the reference's JavaScript front-end calls for the same
+path (``implisolid_main.js``: ``make_geometry`` :201-249, ``query_implicit_values`` :291-333,
+``query_a_normal`` :335-368), so Python callers get the reference's behaviour.
+
+There is no CPU fallback: if the library is missing or no GPU is present the calls raise.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libimplisolid_mi355x.so")
+
+# every symbol declared in include/implisolid.h
+ABI_SYMBOLS = [
+    "build_geometry", "build_geometry_u", "get_v_size", "get_f_size", "get_f", "get_v", "finish_geometry",
+    "get_f_ptr", "get_v_ptr", "set_object", "unset_object", "set_x", "unset_x", "calculate_implicit_values",
+    "get_values_ptr", "get_values_size", "calculate_implicit_gradients", "get_gradients_ptr",
+    "get_gradients_size", "get_pointset_ptr", "get_pointset_size", "about", "implisolid_last_error",
+    "implisolid_set_error_mode", "implisolid_eval_points", "implisolid_program_info",
+    "implisolid_slab_create", "implisolid_slab_destroy", "implisolid_slab_eval", "implisolid_slab_count",
+    "implisolid_slab_emit", "implisolid_slab_counters", "implisolid_slab_counts", "implisolid_slab_grid",
+    "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
+    "implisolid_slab_download",
+]
+
+_lib = None
+
+
+class ImplisolidError(RuntimeError):
+    pass
+
+
+def build(jobs=8):
+    """Compile the HIP library in-tree (make -C implisolid_amd)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-j%d" % jobs, "-C", _HERE], check=True)
+
+
+def lib():
+    """The loaded C ABI.  Raises if the HIP library has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("implisolid_amd: %s is missing -- run implisolid_amd.build() (make -C implisolid_amd)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    c_char_p, c_int, c_bool, c_void_p = ctypes.c_char_p, ctypes.c_int, ctypes.c_bool, ctypes.c_void_p
+    fp = ctypes.POINTER(ctypes.c_float)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    up = ctypes.POINTER(ctypes.c_uint32)
+    sig = {
+        "build_geometry": ([c_char_p, c_char_p], None),
+        "build_geometry_u": ([c_char_p, c_char_p, c_char_p], None),
+        "get_v_size": ([], c_int), "get_f_size": ([], c_int),
+        "get_f": ([ip, c_int], None), "get_v": ([fp, c_int], None),
+        "finish_geometry": ([], None), "get_f_ptr": ([], c_void_p), "get_v_ptr": ([], c_void_p),
+        "set_object": ([c_char_p, c_bool], c_int), "unset_object": ([c_int], c_bool),
+        "set_x": ([c_void_p, c_int], c_bool), "unset_x": ([], None),
+        "calculate_implicit_values": ([], None), "get_values_ptr": ([], c_void_p), "get_values_size": ([], c_int),
+        "calculate_implicit_gradients": ([c_bool], None), "get_gradients_ptr": ([], c_void_p),
+        "get_gradients_size": ([], c_int), "get_pointset_ptr": ([c_char_p], c_void_p),
+        "get_pointset_size": ([c_char_p], c_int), "about": ([], None),
+        "implisolid_last_error": ([], c_char_p), "implisolid_set_error_mode": ([c_int], None),
+        "implisolid_eval_points": ([fp, ctypes.c_int64, fp, fp], c_int),
+        "implisolid_program_info": ([c_char_p, c_int, ip, fp], c_int),
+        "implisolid_slab_create": ([c_char_p, c_char_p, c_int, c_int], c_void_p),
+        "implisolid_slab_destroy": ([c_void_p], None),
+        "implisolid_slab_eval": ([c_void_p, c_void_p], c_int),
+        "implisolid_slab_count": ([c_void_p, c_void_p], c_int),
+        "implisolid_slab_emit": ([c_void_p, c_void_p, c_void_p], c_int),
+        "implisolid_slab_counters": ([c_void_p], c_void_p),
+        "implisolid_slab_counts": ([c_void_p, c_void_p, up], c_int),
+        "implisolid_slab_grid": ([c_void_p, ip], c_int),
+        "implisolid_slab_verts": ([c_void_p], c_void_p),
+        "implisolid_slab_faces": ([c_void_p], c_void_p),
+        "implisolid_slab_field": ([c_void_p], c_void_p),
+        "implisolid_slab_set_offsets": ([c_void_p, ctypes.c_uint32, ctypes.c_uint32], c_int),
+        "implisolid_slab_download": ([c_void_p, fp, ip, c_void_p], c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    L.implisolid_set_error_mode(1)   # Python callers get exceptions instead of abort()
+    _lib = L
+    return L
+
+
+def _s(x):
+    if isinstance(x, (dict, list)):
+        x = json.dumps(x)
+    return x.encode() if isinstance(x, str) else x
+
+
+def _check():
+    err = lib().implisolid_last_error()
+    if err:
+        raise ImplisolidError(err.decode(errors="replace"))
+
+
+def last_error():
+    return lib().implisolid_last_error().decode(errors="replace")
+
+
+# ---- mesh API (implisolid_main.js make_geometry :201-249) -----------------------------------------
+def make_geometry(shape, mc_settings):
+    """Polygonise an MP5 shape; returns (verts float32 [V,3], faces int32 [F,3]) host copies."""
+    L = lib()
+    L.finish_geometry()             # implisolid_main.js:214-217
+    L.build_geometry(_s(shape), _s(mc_settings))
+    _check()
+    nv, nf = L.get_v_size(), L.get_f_size()
+    v = np.empty((nv, 3), np.float32)
+    f = np.empty((nf, 3), np.int32)
+    if nv:
+        L.get_v(v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), nv)
+    if nf:
+        L.get_f(f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nf)
+    L.finish_geometry()
+    return v, f
+
+
+def get_pointset(name):
+    L = lib()
+    n = L.get_pointset_size(_s(name))
+    p = L.get_pointset_ptr(_s(name))
+    if not p or n <= 0:
+        return None
+    return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_float)), shape=(n * 3,)).copy().reshape(n, 3)
+
+
+# ---- direct evaluation (implisolid_main.js:291-368) ---------------------------------------------------
+class ImplicitService:
+    """set_object / set_x / calculate_implicit_values / calculate_implicit_gradients."""
+
+    def __init__(self, shape, ignore_root_matrix=False):
+        L = lib()
+        self.id = L.set_object(_s(shape), bool(ignore_root_matrix))
+        if self.id != 1:
+            raise ImplisolidError(last_error() or "set_object failed")
+
+    def close(self):
+        if self.id:
+            lib().unset_object(self.id)
+            self.id = 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def eval(self, pts, gradient=False):
+        """Any number of points (additive implisolid_eval_points; no 50k limit)."""
+        p = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 3)
+        f = np.empty(p.shape[0], np.float32)
+        g = np.empty((p.shape[0], 3), np.float32) if gradient else None
+        fp = ctypes.POINTER(ctypes.c_float)
+        rc = lib().implisolid_eval_points(p.ctypes.data_as(fp), p.shape[0], f.ctypes.data_as(fp),
+                                          g.ctypes.data_as(fp) if gradient else None)
+        if rc != 0:
+            raise ImplisolidError(last_error())
+        return (f, g) if gradient else f
+
+    def query_implicit_values(self, pts):
+        """The reference call sequence set_x / calculate_implicit_values / get_values / unset_x."""
+        L = lib()
+        p = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 3)
+        if not L.set_x(p.ctypes.data_as(ctypes.c_void_p), p.shape[0]):
+            raise ImplisolidError(last_error())
+        try:
+            L.calculate_implicit_values()
+            _check()
+            n = L.get_values_size()
+            ptr = L.get_values_ptr()
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy() if n else np.zeros(0, np.float32)
+        finally:
+            L.unset_x()
+
+    def query_normals(self, pts, normalize_and_invert=True):
+        L = lib()
+        p = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 3)
+        if not L.set_x(p.ctypes.data_as(ctypes.c_void_p), p.shape[0]):
+            raise ImplisolidError(last_error())
+        try:
+            L.calculate_implicit_gradients(bool(normalize_and_invert))
+            _check()
+            n = L.get_gradients_size()
+            ptr = L.get_gradients_ptr()
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy().reshape(-1, 3)
+        finally:
+            L.unset_x()
+
+
+def program_info(shape, ignore_root_matrix=False):
+    """Host-only: compile an MP5 tree; returns (n_instr, depth, n_mats, inverse matrices [n,12])."""
+    L = lib()
+    info = (ctypes.c_int32 * 4)()
+    mats = np.zeros((256, 12), np.float32)
+    rc = L.implisolid_program_info(_s(shape), int(bool(ignore_root_matrix)), info,
+                                   mats.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    if rc != 0:
+        raise ImplisolidError(last_error())
+    return info[0], info[1], info[2], mats[:info[2]].copy()
+
+
+# ---- device slab pipeline (bench / multi-GPU) -----------------------------------------------------
+class Slab:
+    """One Z-slab of one object on the current device.  Stream = a hipStream_t handle (int)."""
+
+    def __init__(self, shape, mc_settings, rank=0, nranks=1):
+        self.h = lib().implisolid_slab_create(_s(shape), _s(mc_settings), int(rank), int(nranks))
+        if not self.h:
+            raise ImplisolidError(last_error())
+        g = (ctypes.c_int32 * 8)()
+        lib().implisolid_slab_grid(self.h, g)
+        self.R, self.res, self.cz0, self.cz1, self.cz_emit, self.fz0, self.fz1, self.depth = list(g)
+
+    def _rc(self, rc):
+        if rc != 0:
+            raise ImplisolidError(last_error())
+
+    def eval(self, stream=0):
+        self._rc(lib().implisolid_slab_eval(self.h, ctypes.c_void_p(stream)))
+
+    def count(self, stream=0):
+        self._rc(lib().implisolid_slab_count(self.h, ctypes.c_void_p(stream)))
+
+    def emit(self, d_offsets=0, stream=0):
+        self._rc(lib().implisolid_slab_emit(self.h, ctypes.c_void_p(d_offsets or None), ctypes.c_void_p(stream)))
+
+    def counters_ptr(self):
+        return lib().implisolid_slab_counters(self.h)
+
+    def counts(self, stream=0):
+        out = (ctypes.c_uint32 * 3)()
+        self._rc(lib().implisolid_slab_counts(self.h, ctypes.c_void_p(stream), out))
+        return int(out[0]), int(out[1]), bool(out[2])
+
+    def set_offsets(self, voff, foff):
+        self._rc(lib().implisolid_slab_set_offsets(self.h, int(voff), int(foff)))
+
+    def download(self, nv, nf, stream=0):
+        v = np.empty((nv, 3), np.float32)
+        f = np.empty((nf, 3), np.int32)
+        self._rc(lib().implisolid_slab_download(self.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.c_void_p(stream)))
+        return v, f
+
+    def run(self, stream=0):
+        """eval + count + emit with the host-set offsets; returns (nv, nf) (blocking)."""
+        self.eval(stream)
+        self.count(stream)
+        nv, nf, grew = self.counts(stream)
+        self.emit(0, stream)
+        nv, nf, of = self.counts(stream)
+        if of:
+            self.emit(0, stream)
+            nv, nf, of = self.counts(stream)
+            if of:
+                raise ImplisolidError("slab output overflow")
+        return nv, nf
+
+    def verts_ptr(self):
+        return lib().implisolid_slab_verts(self.h)
+
+    def faces_ptr(self):
+        return lib().implisolid_slab_faces(self.h)
+
+    def field_ptr(self):
+        return lib().implisolid_slab_field(self.h)
+
+    def close(self):
+        if self.h:
+            lib().implisolid_slab_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,394 @@
+// abi.hip -- the extern "C" drop-in boundary (mcc2.cpp:88-134) over the MI355X engine.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/implisolid.h"
+#include "engine.hpp"
+#include "host.hpp"
+#include "ob02.hpp"
+
+using namespace impli;
+
+namespace {
+
+int g_error_mode = 0;           // 0: abort like the reference, 1: report and return
+thread_local std::string g_last_error;
+
+void report(const std::string& msg, bool reference_aborts) {
+    g_last_error = msg;
+    std::fprintf(stderr, "%s\n", msg.c_str());
+    if (reference_aborts && g_error_mode == 0) std::abort();
+}
+
+struct GeometryState {               // state_t, mcc2.cpp:165-193
+    bool active = false;
+    std::vector<float> verts;
+    std::vector<int32_t> faces;
+};
+GeometryState g_state;
+
+std::map<std::string, std::vector<float>> g_pointsets;   // pointset_set.hpp:8
+
+struct EvalService {                 // ifunction_service, mcc2.cpp:699-705
+    bool has_object = false;
+    bool has_x = false;
+    std::vector<float> x, f, grad;
+};
+EvalService g_eval;
+
+Engine& engine() {
+    static std::unique_ptr<Engine> e;
+    if (!e) e.reset(new Engine());
+    return *e;
+}
+
+hipStream_t abi_stream() {
+    static hipStream_t s = nullptr;
+    if (!s) IMPLI_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+}
+
+void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.cpp:309-444
+    if (g_state.active) {
+        report("build_geometry() called in a bad state.", false);
+        return;
+    }
+    Program prog = compile_mp5(shape_json, st.ignore_root_matrix);
+    Engine& E = engine();
+    hipStream_t s = abi_stream();
+    E.set_object(prog);
+    E.set_grid(st.resolution, st.box, 0, 1);
+    SlabCounts c = E.marching_cubes(s);   // polygonize_step_0
+    int64_t nv = c.n_verts(), nf = c.n_faces();
+    Ob02 ob(E, s);
+    ob.load_mesh(E.d_verts(), nv, E.d_faces(), nf);
+    for (int rep = 0; rep < st.overall_repeats; ++rep) {
+        for (int i = 0; i < st.vresampl_iters; ++i) ob.vertex_resampling(st.vresampl_c);   // step 1
+        if (st.projection) ob.centroids_projection(st.qem);                             // step 2
+        if (st.subdiv && (st.overall_repeats <= 1 || rep == st.overall_repeats - 1)) {
+            report("subdivision (polygonize_step_3) is not implemented by this build; result is unsubdivided", false);
+        }
+    }
+    g_state.verts.resize((size_t)nv * 3);
+    g_state.faces.resize((size_t)nf * 3);
+    ob.fetch(g_state.verts.data(), g_state.faces.data());
+    // STORE_POINTSET (pointset_set.hpp:11-25) replaces; vertex_resampling.hpp:176-211 uses
+    // map::emplace on a never-cleared global, so the first resampling point sets persist
+    for (auto& kv : ob.pointsets()) {
+        const bool first_wins = kv.first == "pre_resampling_vertices" || kv.first == "post_resampling_vertices";
+        if (first_wins && g_pointsets.count(kv.first)) continue;
+        g_pointsets[kv.first] = kv.second;
+    }
+    g_state.active = true;                 // polygonize_terminate, ob02:163-176
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* implisolid_last_error(void) { return g_last_error.c_str(); }
+void implisolid_set_error_mode(int mode) { g_error_mode = mode; }
+
+void build_geometry(const char* shape_json, const char* mc_json) {
+    g_last_error.clear();
+    MCSettings st;
+    try {
+        st = parse_mc_settings(mc_json);
+    } catch (const InputError& e) {
+        report(e.what(), true);
+        return;
+    }
+    try {
+        grand_algorithm(shape_json, st);
+    } catch (const InputError& e) {
+        report(e.what(), true);
+    } catch (const std::exception& e) {
+        report(std::string("build_geometry failed: ") + e.what(), false);
+    }
+}
+
+void build_geometry_u(const char* shape_json, const char* mc_json, const char* call_specs) {
+    try {
+        (void)Json::parse(call_specs ? call_specs : "{}");   // worker_call_specs.hpp:28-40
+    } catch (const JsonError& e) {
+        report(std::string("call_specs: ") + e.what(), true);
+        return;
+    }
+    build_geometry(shape_json, mc_json);
+}
+
+int get_v_size(void) { return (int)(g_state.verts.size() / 3); }
+int get_f_size(void) { return (int)(g_state.faces.size() / 3); }
+
+void get_v(float* v_out, int vcount) {
+    const size_t n = g_state.verts.size();
+    std::memcpy(v_out, g_state.verts.data(), n * sizeof(float));
+    if ((size_t)vcount * 3 != n) std::fprintf(stderr, "sizes dont match: %g %d\n", (double)n / 3., vcount);
+}
+
+void get_f(int* f_out, int fcount) {
+    const size_t n = g_state.faces.size();
+    std::memcpy(f_out, g_state.faces.data(), n * sizeof(int));
+    if ((size_t)fcount * 3 != n) std::fprintf(stderr, "sizes dont match: %g %d\n", (double)n / 3., fcount);
+}
+
+void* get_v_ptr(void) { return g_state.verts.data(); }
+void* get_f_ptr(void) { return g_state.faces.data(); }
+
+void finish_geometry(void) { g_state.active = false; }
+
+// ---- direct evaluation ------------------------------------------------------------------------
+int set_object(const char* shape_json, bool ignore_root_matrix) {
+    if (g_eval.has_object) {
+        report("Error: You cannot unset() the object before a set_object(json).", false);
+        return 0;
+    }
+    try {
+        Program p = compile_mp5(shape_json, ignore_root_matrix);
+        engine().set_object(p);
+    } catch (const InputError& e) {
+        report(e.what(), true);
+        return 0;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return 0;
+    }
+    g_eval.has_object = true;
+    return 1;
+}
+
+bool unset_object(int id) {
+    if (!g_eval.has_object) {
+        report("Error: You cannot unset() the object before a set_object(json).", false);
+        return false;
+    }
+    if (id <= 0) {
+        report("Incorrect ID: use the same id returned by set_object(json).", false);
+        return false;
+    }
+    if (id != 1) {
+        report("Incorrect ID. For now, The only id is 1", false);
+        return false;
+    }
+    g_eval.has_object = false;
+    return true;
+}
+
+bool set_x(void* verts, int n) {
+    if (g_eval.has_x) {
+        report("Error: You set() before unset()ing the previous set().", false);
+        return false;
+    }
+    if (n < 0 || n >= 10000 * 5) {
+        report("Error: n is outside [0, 50000].", false);
+        return false;
+    }
+    const float* p = static_cast<const float*>(verts);
+    g_eval.x.assign(p, p + 3 * (size_t)n);
+    g_eval.f.assign((size_t)n, 0.f);
+    g_eval.grad.assign(3 * (size_t)n, 0.f);
+    g_eval.has_x = true;
+    return true;
+}
+
+void unset_x(void) {
+    if (!g_eval.has_x) {
+        report("Error: You cannot unset() before a set().", false);
+        return;
+    }
+    g_eval.has_x = false;
+    g_eval.x.clear();
+    g_eval.f.clear();
+    g_eval.grad.clear();
+}
+
+int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* grad_out) {
+    if (!g_eval.has_object) {
+        report("Error: You need to set_x() and set_object() first.", false);
+        return -1;
+    }
+    if (n <= 0) return 0;
+    try {
+        Engine& E = engine();
+        hipStream_t s = abi_stream();
+        DevBuf& dx = E.scratch(0);
+        DevBuf& df = E.scratch(1);
+        DevBuf& dg = E.scratch(2);
+        dx.reserve((size_t)n * 12);
+        df.reserve((size_t)n * 4);
+        if (grad_out) dg.reserve((size_t)n * 12);
+        IMPLI_HIP(hipMemcpyAsync(dx.p, xyz, (size_t)n * 12, hipMemcpyHostToDevice, s));
+        E.eval_points(dx.as<float>(), n, df.as<float>(), grad_out ? dg.as<float>() : nullptr, s);
+        if (f_out) IMPLI_HIP(hipMemcpyAsync(f_out, df.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        if (grad_out) IMPLI_HIP(hipMemcpyAsync(grad_out, dg.p, (size_t)n * 12, hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
+void calculate_implicit_values(void) {
+    if (!g_eval.has_x || !g_eval.has_object) {
+        report("Error: You need to set_x() and set_object() first.", false);
+        return;
+    }
+    implisolid_eval_points(g_eval.x.data(), (int64_t)g_eval.f.size(), g_eval.f.data(), nullptr);
+}
+
+void* get_values_ptr(void) { return g_eval.has_x ? g_eval.f.data() : nullptr; }
+int get_values_size(void) { return (int)g_eval.f.size(); }
+
+void calculate_implicit_gradients(bool normalize_and_invert) {
+    if (!g_eval.has_x || !g_eval.has_object) {
+        report("Error: You need to set_x() and set_object() first.", false);
+        return;
+    }
+    const int64_t n = (int64_t)g_eval.f.size();
+    std::vector<float> fv((size_t)n);
+    implisolid_eval_points(g_eval.x.data(), n, fv.data(), g_eval.grad.data());
+    if (normalize_and_invert) {   // mcc2.cpp:852-871
+        int problems = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            float* g = &g_eval.grad[3 * i];
+            const float x = g[0], y = g[1], z = g[2];
+            const float norm = std::sqrt(x * x + y * y + z * z);
+            float factor;
+            if (norm > 0.0001) factor = (float)(-1.0 / (double)norm);
+            else { factor = -42.0f; problems++; }
+            g[0] = x * factor; g[1] = y * factor; g[2] = z * factor;
+        }
+        if (problems > 0) std::fprintf(stderr, " problems %d\n", problems);
+    }
+}
+
+void* get_gradients_ptr(void) {
+    if (!g_eval.has_x || !g_eval.has_object) {
+        report("Error: You need to set_x() and set_object() first.", false);
+        return nullptr;
+    }
+    return g_eval.grad.data();
+}
+
+int get_gradients_size(void) {
+    if (!g_eval.has_x || !g_eval.has_object) {
+        report("Error: You need to set_x() and set_object() first.", false);
+        return 0;
+    }
+    return (int)g_eval.grad.size();
+}
+
+void* get_pointset_ptr(char* id) {
+    auto it = g_pointsets.find(std::string(id));
+    return it == g_pointsets.end() ? nullptr : it->second.data();
+}
+int get_pointset_size(char* id) {
+    auto it = g_pointsets.find(std::string(id));
+    return it == g_pointsets.end() ? 0 : (int)(it->second.size() / 3);
+}
+
+void about(void) {
+    std::fprintf(stderr, "Build Info: \n%s %s\n", __DATE__, __TIME__);
+    std::fprintf(stderr, "implisolid-mi355x: HIP gfx950 polygoniser (eval + marching cubes + OB02)\n");
+    std::fprintf(stderr, "CONFIG: ROOT_TOLERANCE=%g \n", (double)(float)(0.001 / 10.0));
+}
+
+int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int32_t info[4], float* mats_out) {
+    g_last_error.clear();
+    try {
+        const Program p = compile_mp5(shape_json, ignore_root_matrix != 0);
+        info[0] = p.n_instr;
+        info[1] = p.max_depth;
+        info[2] = p.n_mats;
+        info[3] = 0;
+        if (mats_out) std::memcpy(mats_out, p.mats, sizeof(float) * 12 * (size_t)p.n_mats);
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
+// ---- device slab pipeline ----------------------------------------------------------------------
+struct implisolid_slab {
+    Engine engine;
+};
+
+implisolid_slab* implisolid_slab_create(const char* shape_json, const char* mc_json, int rank, int nranks) {
+    g_last_error.clear();
+    try {
+        MCSettings st = parse_mc_settings(mc_json);
+        Program p = compile_mp5(shape_json, st.ignore_root_matrix);
+        auto* s = new implisolid_slab();
+        s->engine.set_object(p);
+        s->engine.set_grid(st.resolution, st.box, rank, nranks);
+        return s;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return nullptr;
+    }
+}
+void implisolid_slab_destroy(implisolid_slab* s) { delete s; }
+
+#define SLAB_TRY(expr)                                 \
+    try {                                              \
+        expr;                                          \
+    } catch (const std::exception& e) {                \
+        report(e.what(), false);                       \
+        return -1;                                     \
+    }                                                  \
+    return 0;
+
+int implisolid_slab_eval(implisolid_slab* s, void* stream) { SLAB_TRY(s->engine.eval_field((hipStream_t)stream)) }
+int implisolid_slab_count(implisolid_slab* s, void* stream) { SLAB_TRY(s->engine.count((hipStream_t)stream)) }
+int implisolid_slab_emit(implisolid_slab* s, const uint32_t* d_offsets, void* stream) {
+    SLAB_TRY(s->engine.emit(d_offsets, (hipStream_t)stream))
+}
+const uint32_t* implisolid_slab_counters(implisolid_slab* s) { return s->engine.d_counters(); }
+int implisolid_slab_counts(implisolid_slab* s, void* stream, uint32_t out[3]) {
+    try {
+        bool of = false;
+        SlabCounts c = s->engine.read_counts((hipStream_t)stream, &of);
+        const bool grew = s->engine.ensure_capacity(c);
+        out[0] = c.n_verts();
+        out[1] = c.n_faces();
+        out[2] = (of || grew) ? 1u : 0u;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+int implisolid_slab_grid(implisolid_slab* s, int32_t out[8]) {
+    const GridDesc& g = s->engine.grid();
+    const int32_t v[8] = {g.R, g.res, g.cz0, g.cz1, g.cz_emit, g.fz0, g.fz1, s->engine.depth()};
+    std::memcpy(out, v, sizeof v);
+    return 0;
+}
+int implisolid_slab_set_offsets(implisolid_slab* s, uint32_t voff, uint32_t foff) {
+    SLAB_TRY(s->engine.set_offsets(voff, foff))
+}
+int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, void* stream) {
+    try {
+        bool of = false;
+        const SlabCounts c = s->engine.read_counts((hipStream_t)stream, &of);
+        if (of) throw HipError("slab output overflowed; call implisolid_slab_counts and emit again");
+        s->engine.download(verts, faces, c, (hipStream_t)stream);
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
+int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
+float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+// engine.hip -- buffer management and stage sequencing for the MI355X polygoniser.
+#include "engine.hpp"
+
+#include <cstdio>
+#include <cstring>
+
+#include "ifunc_device.hpp"
+
+namespace impli {
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void DevBuf::reserve(size_t n) {
+    if (n <= bytes && p) return;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    IMPLI_HIP(hipMalloc(&p, want));
+    bytes = want;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+Engine::Engine() {
+    // rabbit table + the object's trailing members (F8d: out-of-table reads) + zero padding
+    std::vector<float> tab(dev::kRabbitPadded, 0.f);
+    for (int i = 0; i < dev::kRabbitN; ++i) std::memcpy(&tab[i], &IMPLI_RABBIT_BITS[i], 4);
+    const uint32_t tail[4] = {IMPLI_RABBIT_GRID_SIZE_BITS, IMPLI_RABBIT_ORIGIN_X_BITS, IMPLI_RABBIT_ORIGIN_Y_BITS,
+                              IMPLI_RABBIT_ORIGIN_Z_BITS};
+    std::memcpy(&tab[dev::kRabbitN], tail, sizeof tail);
+    rabbit_.reserve(tab.size() * sizeof(float));
+    IMPLI_HIP(hipMemcpy(rabbit_.p, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
+    CaseInfo cases[256];
+    build_case_table(cases);
+    cases_.reserve(sizeof cases);
+    IMPLI_HIP(hipMemcpy(cases_.p, cases, sizeof cases, hipMemcpyHostToDevice));
+    prog_.reserve(sizeof(Program));
+    counters_.reserve(16 * sizeof(uint32_t));
+    overflow_.reserve(16);
+    offsets_.reserve(16);
+    IMPLI_HIP(hipMemset(offsets_.p, 0, 16));
+}
+
+void Engine::set_offsets(uint32_t voff, uint32_t foff) {
+    const uint32_t h[2] = {voff, foff};
+    IMPLI_HIP(hipMemcpy(offsets_.p, h, sizeof h, hipMemcpyHostToDevice));
+}
+
+void Engine::download(float* verts, int32_t* faces, const SlabCounts& c, hipStream_t s) {
+    if (c.n_verts()) IMPLI_HIP(hipMemcpyAsync(verts, verts_.p, (size_t)c.n_verts() * 12, hipMemcpyDeviceToHost, s));
+    if (c.n_faces()) IMPLI_HIP(hipMemcpyAsync(faces, faces_.p, (size_t)c.n_faces() * 12, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+}
+
+Engine::~Engine() {
+    DevBuf* all[] = {&offsets_, &prog_, &rabbit_, &cases_, &field_, &unit_cnt_, &active_units_, &counters_, &vid3_,
+                     &records_, &verts_, &faces_, &overflow_};
+    for (auto* b : all) b->release();
+    for (auto& b : scratch_) b.release();
+}
+
+void Engine::set_object(const Program& prog) {
+    IMPLI_HIP(hipMemcpy(prog_.p, &prog, sizeof(Program), hipMemcpyHostToDevice));
+    depth_ = prog.max_depth;
+    have_object_ = true;
+}
+
+void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
+    const int res = R + 5;
+    const int layers = res - 3;            // cell layers 1 .. res-3
+    const int base = layers / nranks, extra = layers % nranks;
+    const int z0 = 1 + rank * base + (rank < extra ? rank : extra);
+    const int z1 = z0 + base + (rank < extra ? 1 : 0);
+    const int halo = (rank > 0) ? 1 : 0;   // one cell layer recomputed below the slab (owner rule)
+    grid_ = make_grid(R, box, z0 - halo, z1, z0);
+    const int64_t nu = n_units(grid_);
+    field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0 + 1) * sizeof(float));
+    unit_cnt_.reserve((size_t)(nu + 1) * 3 * sizeof(uint32_t));
+    active_units_.reserve((size_t)(nu + 1) * sizeof(uint32_t));
+    vid3_.reserve((size_t)grid_.n_cells * 3 * sizeof(uint32_t));
+    const int64_t m2 = (int64_t)grid_.m * grid_.m;
+    ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
+                               (uint32_t)std::min<int64_t>(6 * m2, 1u << 31), 0});
+    have_grid_ = true;
+}
+
+bool Engine::ensure_capacity(const SlabCounts& c) {
+    bool grew = false;
+    auto grow = [&](DevBuf& b, int64_t& cap, int64_t need, size_t elem) {
+        if (need <= cap) return;
+        int64_t nc = cap ? cap : 1024;
+        while (nc < need) nc *= 2;
+        b.reserve((size_t)nc * elem);
+        cap = nc;
+        grew = true;
+    };
+    grow(verts_, cap_v_, (int64_t)c.n_verts() + 1, 3 * sizeof(float));
+    grow(faces_, cap_f_, (int64_t)c.n_faces() + 1, 3 * sizeof(int32_t));
+    grow(records_, cap_rec_, (int64_t)c.act_total + 1, sizeof(uint4));
+    return grew;
+}
+
+MCBuffers Engine::buffers() const {
+    MCBuffers b{};
+    b.field = field_.as<float>();
+    b.unit_cnt = unit_cnt_.as<uint32_t>();
+    b.active_units = active_units_.as<uint32_t>();
+    b.counters = counters_.as<uint32_t>();
+    b.vid3 = vid3_.as<uint32_t>();
+    b.records = records_.as<uint4>();
+    b.verts = verts_.as<float>();
+    b.faces = faces_.as<int32_t>();
+    b.cap_v = cap_v_;
+    b.cap_f = cap_f_;
+    b.cap_rec = cap_rec_;
+    b.offsets = nullptr;
+    b.overflow = overflow_.as<uint32_t>();
+    return b;
+}
+
+void Engine::eval_field(hipStream_t s) {
+    if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
+    launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
+    IMPLI_HIP(hipGetLastError());
+}
+
+void Engine::count(hipStream_t s) {
+    IMPLI_HIP(hipMemsetAsync(counters_.p, 0, 16 * sizeof(uint32_t), s));
+    IMPLI_HIP(hipMemsetAsync(overflow_.p, 0, 16, s));
+    MCBuffers b = buffers();
+    launch_mc_count(cases_.as<CaseInfo>(), grid_, b, s);
+    launch_mc_scan(grid_, b, s);
+    IMPLI_HIP(hipGetLastError());
+}
+
+void Engine::emit(const uint32_t* d_offsets, hipStream_t s) {
+    MCBuffers b = buffers();
+    b.offsets = d_offsets ? d_offsets : offsets_.as<uint32_t>();
+    launch_mc_emit(cases_.as<CaseInfo>(), grid_, b, s);
+    IMPLI_HIP(hipGetLastError());
+}
+
+SlabCounts Engine::read_counts(hipStream_t s, bool* overflow) {
+    uint32_t h[16], of = 0;
+    IMPLI_HIP(hipMemcpyAsync(h, counters_.p, sizeof h, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipMemcpyAsync(&of, overflow_.p, sizeof of, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    if (overflow) *overflow = of != 0;
+    return SlabCounts{h[2], h[3], h[4], h[5]};
+}
+
+SlabCounts Engine::marching_cubes(hipStream_t s) {
+    eval_field(s);
+    count(s);
+    emit(nullptr, s);
+    bool of = false;
+    SlabCounts c = read_counts(s, &of);
+    if (of || ensure_capacity(c)) {
+        ensure_capacity(c);
+        IMPLI_HIP(hipMemsetAsync(overflow_.p, 0, 16, s));
+        emit(nullptr, s);
+        c = read_counts(s, &of);
+        if (of) throw HipError("marching cubes: output capacity overflow after resize");
+    }
+    return c;
+}
+
+void Engine::eval_points(const float* d_xyz, int64_t n, float* d_f, float* d_grad, hipStream_t s) {
+    if (!have_object_) throw InputError("engine: no object set");
+    launch_eval_points(prog_.as<Program>(), depth_, rabbit_.as<float>(), d_xyz, n, d_f, d_grad, s);
+    IMPLI_HIP(hipGetLastError());
+}
+
+}  // namespace impli

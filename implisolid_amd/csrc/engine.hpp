@@ -1,0 +1,85 @@
+// engine.hpp -- device-resident polygoniser state for one GPU (one Z-slab of one object).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "host.hpp"
+#include "kernels.hpp"
+
+namespace impli {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+void hip_check(hipError_t e, const char* what);
+#define IMPLI_HIP(x) ::impli::hip_check((x), #x)
+
+// grow-only device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void reserve(size_t n);
+    void release();
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct SlabCounts {
+    uint32_t own_total, tri_total, act_total, halo_own;
+    uint32_t n_verts() const { return own_total - halo_own; }
+    uint32_t n_faces() const { return tri_total; }
+};
+
+class Engine {
+public:
+    Engine();
+    ~Engine();
+
+    // object + grid.  rank/nranks select a Z-slab of cell layers (rank 0 of 1 = whole grid).
+    void set_object(const Program& prog);
+    void set_grid(int R, const float box[6], int rank, int nranks);
+
+    // the MC pipeline, all asynchronous on `stream`
+    void eval_field(hipStream_t stream);
+    void count(hipStream_t stream);                           // K2 + scan
+    void emit(const uint32_t* d_offsets, hipStream_t stream); // K3 + K4 (offsets: [Voff, Foff] or null)
+    // host-side offsets used when emit() gets no device offsets
+    void set_offsets(uint32_t voff, uint32_t foff);
+    // blocking copy of this slab's emitted mesh
+    void download(float* verts, int32_t* faces, const SlabCounts& c, hipStream_t stream);
+    // blocking: totals of this slab and the overflow flag
+    SlabCounts read_counts(hipStream_t stream, bool* overflow);
+    // make sure the output buffers can hold the counted mesh (re-run emit() after growing)
+    bool ensure_capacity(const SlabCounts& c);
+
+    // whole single-GPU marching cubes: eval + count + emit (+ retry on overflow); returns counts
+    SlabCounts marching_cubes(hipStream_t stream);
+
+    // direct evaluation at device points
+    void eval_points(const float* d_xyz, int64_t n, float* d_f, float* d_grad, hipStream_t stream);
+
+    const GridDesc& grid() const { return grid_; }
+    float* d_verts() const { return verts_.as<float>(); }
+    int32_t* d_faces() const { return faces_.as<int32_t>(); }
+    float* d_field() const { return field_.as<float>(); }
+    const uint32_t* d_counters() const { return counters_.as<uint32_t>(); }
+    int depth() const { return depth_; }
+    const Program* d_program() const { return prog_.as<Program>(); }
+    const float* d_rabbit() const { return rabbit_.as<float>(); }
+
+    DevBuf& scratch(int k) { return scratch_[k]; }
+
+private:
+    MCBuffers buffers() const;
+
+    GridDesc grid_{};
+    int depth_ = 1;
+    bool have_grid_ = false, have_object_ = false;
+    DevBuf prog_, rabbit_, cases_;
+    DevBuf offsets_, field_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
+    DevBuf scratch_[16];
+};
+
+}  // namespace impli

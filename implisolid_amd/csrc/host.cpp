@@ -1,0 +1,252 @@
+// host.cpp -- mc-settings parser, MP5-JSON -> node-program compiler, float LU inverse.
+#include "host.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+namespace impli {
+
+// ---------------------------------------------------------------------------------------------
+// basic_functions.hpp:77-128.  ublas lu_factorize: per column the first row with the largest |a|
+// is the pivot (index_norm_inf), the sub-column is scaled by value_type(1)/pivot, the trailing
+// block gets m(r,c) -= l(r)*u(c); lu_substitute: row swaps, unit-lower forward solve, upper back
+// solve with "t = e(n,l) /= u(n,n); if (t != 0) e(m,l) -= u(m,n)*t" (triangular.hpp).
+bool invert_matrix12(const float in[12], float out[12]) {
+    float a[4][4];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c) a[r][c] = in[r * 4 + c];
+    a[3][0] = a[3][1] = a[3][2] = 0.f;
+    a[3][3] = 1.f;
+    int perm[4] = {0, 1, 2, 3};
+    for (int i = 0; i < 4; ++i) {
+        int piv = i;
+        float best = 0.f;
+        for (int r = i; r < 4; ++r) {
+            float u = std::fabs(a[r][i]);
+            if (u > best) { best = u; piv = r; }
+        }
+        if (a[piv][i] == 0.f) return false;   // singular: the reference returns false, matrix untouched
+        if (piv != i) {
+            perm[i] = piv;
+            for (int c = 0; c < 4; ++c) std::swap(a[piv][c], a[i][c]);
+        }
+        const float inv = 1.f / a[i][i];
+        for (int r = i + 1; r < 4; ++r) a[r][i] *= inv;
+        for (int r = i + 1; r < 4; ++r)
+            for (int c = i + 1; c < 4; ++c) {
+                const float p = a[r][i] * a[i][c];
+                a[r][c] -= p;
+            }
+    }
+    float e[4][4];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) e[r][c] = (r == c) ? 1.f : 0.f;
+    for (int i = 0; i < 4; ++i)
+        if (perm[i] != i)
+            for (int c = 0; c < 4; ++c) std::swap(e[i][c], e[perm[i]][c]);
+    for (int n = 0; n < 4; ++n)
+        for (int l = 0; l < 4; ++l) {
+            const float t = e[n][l];
+            if (t != 0.f)
+                for (int m = n + 1; m < 4; ++m) {
+                    const float p = a[m][n] * t;
+                    e[m][l] -= p;
+                }
+        }
+    for (int n = 3; n >= 0; --n)
+        for (int l = 3; l >= 0; --l) {
+            const float t = (e[n][l] /= a[n][n]);
+            if (t != 0.f)
+                for (int m = n - 1; m >= 0; --m) {
+                    const float p = a[m][n] * t;
+                    e[m][l] -= p;
+                }
+        }
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c) out[r * 4 + c] = e[r][c];
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+MCSettings parse_mc_settings(const char* text) {
+    Json d;
+    try {
+        d = Json::parse(text);
+    } catch (const JsonError& e) {
+        throw InputError(e.what());
+    }
+    MCSettings s;
+    std::string why;
+    float box[6];
+    const char* keys[6] = {"box.xmin", "box.xmax", "box.ymin", "box.ymax", "box.zmin", "box.zmax"};
+    bool ok = true;
+    for (int i = 0; i < 6; ++i) {
+        float v;
+        if (!d.get_float(keys[i], &v) || std::isnan(v)) ok = false;
+        box[i] = v;
+    }
+    if (!ok) {   // :176-191
+        for (int i = 0; i < 6; ++i) box[i] = (i % 2) ? 1.f : -1.f;
+        why += "  err2 (missing or incorrect box)";
+    }
+    std::memcpy(s.box, box, sizeof box);
+    {   // :193-206 resolution must be an integer-valued number
+        const float r = d.get_float("resolution", -1.f);
+        int ri = (int)r;
+        if (ri == -1) ri = 28;
+        if ((float)ri != r) why += "  err3 (resolution must be integer)";
+        s.resolution = ri;
+        if (s.resolution <= 2) why += "  err4 (resolution must be > 2)";
+    }
+    s.vresampl_c = d.get_float("vresampl.c", 1.0f);
+    s.vresampl_iters = d.get_int("vresampl.iters", 0);
+    auto read_bool = [&](const char* name, bool dflt, const char* forbidden) {   // :107-141
+        int v = d.get_int(name, -1);
+        bool r = (v == -1) ? dflt : (v != 0);
+        if (d.get_int(forbidden, 9123456) != 9123456) why += std::string("  use ") + name;
+        return r;
+    };
+    s.projection = read_bool("projection.enabled", false, "projection.enable");
+    s.qem = read_bool("qem.enabled", false, "qem.enable");
+    s.subdiv = read_bool("subdiv.enabled", true, "subdiv.enable");
+    s.post_subdiv_noise = d.get_float("debug.post_subdiv_noise", 0.01f);
+    s.overall_repeats = d.get_int("overall_repeats", 1);
+    s.ignore_root_matrix = d.get_bool("ignore_root_matrix", false);
+    if (s.qem && !s.projection) why += "  err7 (qem needs projection)";
+    if (s.resolution > 65535) why += "  resolution exceeds the reference's dim_t";
+    if (!why.empty()) throw InputError("Aborting because of a problem in mc_settings_from_json. Abort reasons: " + why);
+    return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct Builder {
+    Program p{};
+    int depth = 0, max_depth = 0;
+
+    int add_matrix(const float m[12]) {
+        if (p.n_mats >= kMaxProgram) throw InputError("MP5 tree too large");
+        float inv[12];
+        if (!invert_matrix12(m, inv)) throw InputError("singular MP5 matrix");
+        std::memcpy(p.mats[p.n_mats], inv, sizeof inv);
+        return p.n_mats++;
+    }
+    void emit(OpCode op, int32_t type, int32_t mat) {
+        if (p.n_instr >= kMaxProgram) throw InputError("MP5 tree too large");
+        p.instr[p.n_instr++] = Instr{op, type, mat, 0};
+    }
+
+    static void matrix12(const Json& d, float m[12]) {   // getMatrix12 object_factory.hpp:21-30
+        const Json* mj = d.find("matrix");
+        if (!mj || mj->kind != Json::Array || mj->items.size() < 12)
+            throw InputError("MP5 node needs a 12- or 16-entry \"matrix\"");
+        for (int i = 0; i < 12; ++i) {
+            float v;
+            if (!mj->items[i].second.as_float(&v)) throw InputError("bad matrix entry");
+            m[i] = v;
+        }
+    }
+
+    // A "subtree" pushes exactly one value; it sees the parent's local point on top of the stack.
+    void leaf(NodeType t, const float m[12]) {
+        const int k = add_matrix(m);
+        emit(OP_XFORM, t, k);
+        push_point();
+        emit(OP_PRIM, t, k);
+        pop_point();
+    }
+    void push_point() { if (++depth > max_depth) max_depth = depth; if (depth >= kMaxDepth) throw InputError("MP5 tree too deep"); }
+    void pop_point() { --depth; }
+
+    // node = XFORM(m); child a; child b; CSG(t)
+    template <class A, class B>
+    void csg(NodeType t, const float m[12], A&& a, B&& b) {
+        const int k = add_matrix(m);
+        emit(OP_XFORM, t, k);
+        push_point();
+        a();
+        b();
+        emit(OP_CSG, t, k);
+        pop_point();
+    }
+
+    void node(const Json& d, bool ignore) {
+        static const float eye[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        std::string t = d.get_string("type", "");
+        float m[12];
+        struct { const char* name; NodeType t; } prims[] = {
+            {"implicit_double_mushroom", NT_DMUSHROOM},        // object_factory.hpp:86-100
+            {"icube", NT_CUBE}, {"cube", NT_CUBE},             // :110-119 (rabbit SDF, F3)
+            {"icylinder", NT_CYLINDER}, {"cylinder", NT_CYLINDER},  // :121-132
+            {"iellipsoid", NT_ELLIPSOID}, {"ellipsoid", NT_ELLIPSOID},  // :134-143
+            {"icone", NT_CONE}, {"cone", NT_CONE},             // :144-152
+            {"iheart", NT_HEART},                              // :153-162
+            {"itorus", NT_TORUS},                              // :163-173
+        };
+        for (auto& pr : prims)
+            if (t == pr.name) {
+                matrix12(d, m);
+                if (ignore) std::memcpy(m, eye, sizeof m);
+                leaf(pr.t, m);
+                return;
+            }
+        if (t == "Union") {   // :537-580: left-deep chain, identity on the intermediate unions
+            matrix12(d, m);
+            if (ignore) std::memcpy(m, eye, sizeof m);
+            const Json* ch = d.find("children");
+            if (!ch || ch->kind != Json::Array || ch->items.size() < 2)
+                throw InputError("Union needs at least two children");
+            union_chain(*ch, (int)ch->items.size() - 1, m);
+            return;
+        }
+        if (t == "Intersection" || t == "Difference") {   // :581-653, binary
+            matrix12(d, m);
+            if (ignore) std::memcpy(m, eye, sizeof m);
+            const Json* ch = d.find("children");
+            if (!ch || ch->kind != Json::Array || ch->items.size() < 2)
+                throw InputError(t + " needs two children");
+            csg(t == "Intersection" ? NT_INTERSECTION : NT_DIFFERENCE, m,
+                [&] { node(ch->items[0].second, false); }, [&] { node(ch->items[1].second, false); });
+            return;
+        }
+        static const char* unsupported[] = {"tetrahedron", "inf_screw", "screw_diff_two_plane", "screw", "sdf_3d",
+                                            "half_plane", "screw_gradient_wrong", "top_bottom_lid", "rawjscode",
+                                            "meta_balls", "extrusion"};
+        for (auto* u : unsupported)
+            if (t == u) throw InputError("MP5 type \"" + t + "\" is outside the implemented node families");
+        throw InputError("Invalid object you asked for: \"" + t + "\"");
+    }
+
+    // union of children[0..k] = U(union of children[0..k-1], children[k]) with matrix m at the top
+    void union_chain(const Json& ch, int k, const float m[12]) {
+        static const float eye[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        if (k == 0) {
+            node(ch.items[0].second, false);
+            return;
+        }
+        csg(NT_UNION, m, [&] { union_chain(ch, k - 1, eye); }, [&] { node(ch.items[k].second, false); });
+    }
+};
+
+}  // namespace
+
+Program compile_mp5(const Json& shape, bool ignore_root_matrix) {
+    Builder b;
+    b.node(shape, ignore_root_matrix);
+    b.p.max_depth = b.max_depth + 1;
+    return b.p;
+}
+
+Program compile_mp5(const char* shape_json, bool ignore_root_matrix) {
+    Json d;
+    try {
+        d = Json::parse(shape_json);
+    } catch (const JsonError& e) {
+        throw InputError(e.what());
+    }
+    return compile_mp5(d, ignore_root_matrix);
+}
+
+}  // namespace impli

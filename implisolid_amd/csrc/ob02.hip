@@ -1,0 +1,759 @@
+// ob02.hip -- Ohtake-Belyaev mesh refinement (vertex resampling, centroid projection, QEM) on gfx950.
+//
+// Every reference pass that is vectorised over "all faces" or "all vertices" is independent per
+// element, so each becomes one lane per element.  Order-dependent float reductions stay serial
+// inside one lane (umbrella sums in ascending face order, the 3-term kij sum); the one global
+// serial reduction (compute_average_edge_length) is done in the reference order on the host.
+//
+// Reference map:
+//   topology  make_neighbour_faces_of_vertex  mesh_algorithms.hpp:178-209  -> CSR umbrellas
+//             make_edge_lookup / build_faces_of_faces  :50-131             -> hash of (vmin,vmax)
+//   step 1    process2_vertex_resampling_relaxation_v1  vertex_resampling.hpp:152-225
+//   step 2    compute_average_edge_length cp:70-82; set_centers_on_surface cp:421-1214;
+//             bisection bisection.hpp:117-459; vertex_apply_qem qem.hpp:321-599
+// (cp = centroids_projection.cpp)
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "ifunc_device.hpp"
+#include "ob02.hpp"
+
+namespace impli {
+
+using namespace dev;
+
+namespace {
+
+constexpr float kRootTol = (float)(0.001 / 10.0);   // configs.hpp:33
+constexpr int kBisectCap = 200;                      // the reference has no cap (bisection.hpp:360-372)
+constexpr uint64_t kEmpty = ~0ull;
+
+#define DEPTH_LAUNCH(depth, KERNEL, GRID, BLOCK, STREAM, ...)                              \
+    do {                                                                                   \
+        if ((depth) <= 4) KERNEL<4><<<(GRID), (BLOCK), 0, (STREAM)>>>(__VA_ARGS__);        \
+        else if ((depth) <= 8) KERNEL<8><<<(GRID), (BLOCK), 0, (STREAM)>>>(__VA_ARGS__);   \
+        else if ((depth) <= 12) KERNEL<12><<<(GRID), (BLOCK), 0, (STREAM)>>>(__VA_ARGS__); \
+        else KERNEL<16><<<(GRID), (BLOCK), 0, (STREAM)>>>(__VA_ARGS__);                    \
+    } while (0)
+
+inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+__device__ __forceinline__ float norm2f(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
+
+// ---- topology --------------------------------------------------------------------------------
+__global__ void k_degree(const int32_t* __restrict__ f, int64_t n3, uint32_t* __restrict__ deg) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n3) atomicAdd(&deg[f[i]], 1u);
+}
+
+// exclusive scan of n uint32 into out[0..n] (one workgroup of 1024 lanes)
+__global__ __launch_bounds__(1024) void k_scan_u32(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, int64_t n) {
+    __shared__ uint32_t s_w[16];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int64_t chunk = (n + 1023) / 1024;
+    const int64_t a = t * chunk, e = (a + chunk < n) ? a + chunk : n;
+    uint32_t sum = 0;
+    for (int64_t i = a; i < e; ++i) sum += in[i];
+    uint32_t x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+        if (w < wid) pre += s_w[w];
+        tot += s_w[w];
+    }
+    uint32_t run = pre + x - sum;
+    for (int64_t i = a; i < e; ++i) {
+        const uint32_t v = in[i];
+        out[i] = run;
+        run += v;
+    }
+    if (t == 0) out[n] = tot;
+}
+
+__global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const uint32_t* __restrict__ off,
+                                uint32_t* __restrict__ fill, int32_t* __restrict__ lst) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * nf) return;
+    const int32_t v = f[i];
+    const uint32_t p = atomicAdd(&fill[v], 1u);
+    lst[off[v] + p] = (int32_t)(i / 3);
+}
+
+// make_neighbour_faces_of_vertex lists faces in ascending order: sort each small umbrella
+__global__ void k_sort_umbrella(const uint32_t* __restrict__ off, int32_t* __restrict__ lst, int64_t nv) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= nv) return;
+    const uint32_t a = off[v], e = off[v + 1];
+    for (uint32_t i = a + 1; i < e; ++i) {
+        const int32_t x = lst[i];
+        uint32_t j = i;
+        while (j > a && lst[j - 1] > x) { lst[j] = lst[j - 1]; --j; }
+        lst[j] = x;
+    }
+}
+
+struct EdgeTab {
+    unsigned long long* key;
+    uint32_t* first;
+    uint32_t* last;
+    uint32_t* cnt;
+    uint32_t* slot_of;   // 3 * nf
+    uint64_t mask;
+};
+
+__global__ void k_edge_insert(const int32_t* __restrict__ f, int64_t nf, int64_t nv, EdgeTab t) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * nf) return;
+    const int64_t fi = i / 3;
+    const int vj = (int)(i - fi * 3);
+    const uint64_t e1 = (uint32_t)f[i], e2 = (uint32_t)f[fi * 3 + (vj + 1) % 3];
+    const unsigned long long key = (e2 > e1) ? e1 + e2 * (uint64_t)nv : e2 + e1 * (uint64_t)nv;
+    uint64_t s = (key * 0x9E3779B97F4A7C15ull >> 17) & t.mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&t.key[s], kEmpty, key);
+        if (prev == kEmpty || prev == key) break;
+        s = (s + 1) & t.mask;
+    }
+    atomicMin(&t.first[s], (uint32_t)fi);
+    atomicMax(&t.last[s], (uint32_t)fi);
+    atomicAdd(&t.cnt[s], 1u);
+    t.slot_of[i] = (uint32_t)s;
+}
+
+// build_faces_of_faces: fof = first != face ? first : last; "last" of an edge seen once is the
+// value-initialised 0 of faces_of_edges (mesh_algorithms.hpp:111-121)
+__global__ void k_fof(int64_t nf, EdgeTab t, int32_t* __restrict__ fof) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * nf) return;
+    const uint32_t s = t.slot_of[i];
+    const uint32_t fi = (uint32_t)(i / 3);
+    const uint32_t first = t.first[s];
+    fof[i] = (int32_t)((first != fi) ? first : (t.cnt[s] >= 2 ? t.last[s] : 0u));
+}
+
+// ---- step 1 ----------------------------------------------------------------------------------
+__device__ __forceinline__ V3 centroid(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t j) {
+    const int32_t a = f[3 * j], b = f[3 * j + 1], c = f[3 * j + 2];
+    // compute_centroids implicit_vectorised_algorithms.hpp:161-171
+    return V3{(v[3 * a] + v[3 * b] + v[3 * c]) / (float)(3.0), (v[3 * a + 1] + v[3 * b + 1] + v[3 * c + 1]) / (float)(3.0),
+              (v[3 * a + 2] + v[3 * b + 2] + v[3 * c + 2]) / (float)(3.0)};
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_centroid_normals(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                          const float* __restrict__ v, const int32_t* __restrict__ f,
+                                                          int64_t nf, float* __restrict__ C, float* __restrict__ N) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nf) return;
+    const V3 c = centroid(v, f, j);
+    V3 g;
+    (void)eval_fg<D>(prog, tab, c.x, c.y, c.z, g);
+    const float nm = norm2f(g.x, g.y, g.z);   // normalize_1111 normalise_inplace.hpp:60-70
+    C[3 * j] = c.x; C[3 * j + 1] = c.y; C[3 * j + 2] = c.z;
+    N[3 * j] = g.x / nm; N[3 * j + 1] = g.y / nm; N[3 * j + 2] = g.z / nm;
+}
+
+__device__ __forceinline__ float kij(int64_t i, int64_t j, const float* __restrict__ C, const float* __restrict__ N);
+
+// glibc 2.35 e_acosf.c (fdlibm), the libm std::acos(float) of vertex_resampling.hpp:75 resolves to
+__device__ __forceinline__ float glibc_acosf(float x) {
+    const float one = 1.0f, pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f,
+                pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f, pS3 = -4.0055535734e-02f,
+                pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f, qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f,
+                qS3 = -6.8828397989e-01f, qS4 = 7.7038154006e-02f;
+    const int32_t hx = __float_as_int(x), ix = hx & 0x7fffffff;
+    if (ix == 0x3f800000) return (hx > 0) ? 0.0f : pi + 2.0f * pio2_lo;
+    if (ix > 0x3f800000) return (x - x) / (x - x);
+    if (ix < 0x3f000000) {
+        if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+        const float z = x * x;
+        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const float r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    } else if (hx < 0) {
+        const float z = (one + x) * 0.5f;
+        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const float s = sqrtf(z);
+        const float r = p / q;
+        const float w = r * s - pio2_lo;
+        return pi - 2.0f * (s + w);
+    } else {
+        const float z = (one - x) * 0.5f;
+        const float s = sqrtf(z);
+        const float df = __int_as_float(__float_as_int(s) & (int32_t)0xfffff000);
+        const float c = (z - df * df) / (s + df);
+        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const float r = p / q;
+        const float w = r * s + c;
+        return 2.0f * (df + w);
+    }
+}
+
+// vertex_resampling.hpp:47-77
+__device__ __forceinline__ float kij(int64_t i, int64_t j, const float* __restrict__ C, const float* __restrict__ N) {
+    float mimj = N[3 * i] * N[3 * j] + N[3 * i + 1] * N[3 * j + 1] + N[3 * i + 2] * N[3 * j + 2];
+    if (mimj > 1.0f) mimj = 1.0f;
+    if (mimj < -1.0f) mimj = -1.0f;
+    const float pipj = norm2f(C[3 * i] - C[3 * j], C[3 * i + 1] - C[3 * j + 1], C[3 * i + 2] - C[3 * j + 2]);
+    if (pipj == 0) return 0;
+    return glibc_acosf(mimj) / pipj;
+}
+
+__global__ void k_face_weights(const float* __restrict__ C, const float* __restrict__ N, const int32_t* __restrict__ fof,
+                               int64_t nf, float c, float* __restrict__ W) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nf) return;
+    float ki = 0;   // wi, vertex_resampling.hpp:79-91
+    for (int j = 0; j < 3; ++j) ki += kij(i, fof[3 * i + j], C, N);
+    W[i] = (float)(1.0 + (double)(c * ki));
+}
+
+__global__ void k_resample(const uint32_t* __restrict__ off, const int32_t* __restrict__ lst, const float* __restrict__ W,
+                           const float* __restrict__ C, int64_t nv, float* __restrict__ out) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= nv) return;
+    const uint32_t a = off[v], e = off[v + 1];
+    float sw = 0;   // vertex_resampling_VV1 :108-140
+    for (uint32_t k = a; k < e; ++k) sw += W[lst[k]];
+    float x = 0, y = 0, z = 0;
+    for (uint32_t k = a; k < e; ++k) {
+        const int32_t fj = lst[k];
+        const float w = W[fj] / sw;
+        x += w * C[3 * fj];
+        y += w * C[3 * fj + 1];
+        z += w * C[3 * fj + 2];
+    }
+    out[3 * v] = x; out[3 * v + 1] = y; out[3 * v + 2] = z;
+}
+
+// ---- step 2 ----------------------------------------------------------------------------------
+// compute_average_edge_length cp:70-82 terms, in the reference's order (summed serially on host)
+__global__ void k_edge_norms(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t nf, float* __restrict__ o) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nf) return;
+    const float* a = v + 3 * f[3 * j];
+    const float* b = v + 3 * f[3 * j + 1];
+    const float* c = v + 3 * f[3 * j + 2];
+    o[3 * j] = norm2f(a[0] - b[0], a[1] - b[1], a[2] - b[2]);
+    o[3 * j + 1] = norm2f(a[0] - c[0], a[1] - c[1], a[2] - c[2]);
+    o[3 * j + 2] = norm2f(c[0] - b[0], c[1] - b[1], c[2] - b[2]);
+}
+
+__device__ __forceinline__ float get_sign(float v) { return (v > kRootTol) ? 1.f : (v < -kRootTol) ? -1.f : 0.f; }
+
+// normalise_inplace (normalise_inplace.hpp:26-54)
+__device__ __forceinline__ V3 normalise_min(V3 a, float min_norm) {
+    float nm = norm2f(a.x, a.y, a.z);
+    nm = (nm < min_norm) ? 1.0f : nm;
+    const float factor = (float)(1.0 / (double)nm);
+    return V3{a.x * factor, a.y * factor, a.z * factor};
+}
+
+__device__ __forceinline__ V3 cross3(V3 a, V3 b) {
+    return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+// produce_facet_normals (implicit_vectorised_algorithms.hpp:52-133)
+__device__ __forceinline__ V3 facet_normal(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t j) {
+    const float* p0 = v + 3 * f[3 * j];
+    const float* p1 = v + 3 * f[3 * j + 1];
+    const float* p2 = v + 3 * f[3 * j + 2];
+    const float x1 = p1[0] - p0[0], y1 = p1[1] - p0[1], z1 = p1[2] - p0[2];
+    const float x2 = p2[0] - p0[0], y2 = p2[1] - p0[1], z2 = p2[2] - p0[2];
+    float x = y1 * z2 - z1 * y2, y = z1 * x2 - x1 * z2, z = x1 * y2 - y1 * x2;
+    const float micro = (float)(1.0 / 1000.0), nano = (float)((double)micro / 1000.0);
+    const float min_area = (30 * nano) * (30 * nano);
+    const float n2 = x * x + y * y + z * z;
+    if (n2 < min_area * min_area) {
+        const float o = (float)(1.0 / (double)sqrtf(3.0f));
+        return V3{o, o, o};
+    }
+    const float n = sqrtf(n2);
+    return V3{x / n, y / n, z / n};
+}
+
+struct ProjArgs {
+    const float* v;
+    const int32_t* f;
+    int64_t nf;
+    const float* alphas;
+    int nal;
+    float max_dist;
+    const float* pert;      // type-2 perturbations (3 per centroid), only for the late pass
+    float* out;             // projected centroids
+    float* fn;              // facet normals (written by the early pass)
+    float* fc;              // f(centroid) (written by the early pass)
+    uint32_t* pend;         // early pass: unresolved centroid list; [0] is the count at pend_count
+    uint32_t* pend_count;
+    uint32_t* cap_hits;
+};
+
+// cp:904-1191 for one centroid: zero tests, swap (x1 outside), vectorised bisection restated per point
+template <int D>
+__device__ void finalize(const Program* prog, const float* tab, V3 x, float fcv, bool found, V3 best, float* out,
+                         uint32_t* cap_hits) {
+    const float f2 = eval_f<D>(prog, tab, best.x, best.y, best.z);
+    const bool z2 = fabsf(f2) <= kRootTol, z1 = fabsf(fcv) <= kRootTol;
+    if (z1) best = x;
+    V3 r;
+    if (found && !(z1 || z2)) {
+        V3 x1 = x, x2 = best;
+        if (f2 < -kRootTol) { const V3 t = x1; x1 = x2; x2 = t; }
+        V3 mid = x1;
+        int it = 0;
+        for (; it < kBisectCap; ++it) {
+            mid.x = (float)((double)(x1.x + x2.x) / 2.);
+            mid.y = (float)((double)(x1.y + x2.y) / 2.);
+            mid.z = (float)((double)(x1.z + x2.z) / 2.);
+            const float vm = eval_f<D>(prog, tab, mid.x, mid.y, mid.z);
+            if (fabsf(vm) <= kRootTol) break;
+            if (vm < -kRootTol) x1 = mid;
+            if (vm > +kRootTol) x2 = mid;
+        }
+        if (it == kBisectCap) atomicAdd(cap_hits, 1u);
+        r = mid;
+    } else if (z1 || z2) {
+        r = best;
+    } else {
+        r = x;
+    }
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+
+template <int D>
+__device__ __forceinline__ bool try_direction(const Program* prog, const float* tab, V3 x, V3 d, float sc,
+                                              const float* alphas, int na, float max_dist, V3& best) {
+    for (int ai = 0; ai < na; ++ai) {
+        const float cc = max_dist * alphas[ai];   // (length_factor * alpha) * 4.0 / 4.0 is exact
+        const V3 p{x.x + cc * d.x, x.y + cc * d.y, x.z + cc * d.z};
+        const float fa = eval_f<D>(prog, tab, p.x, p.y, p.z);
+        if (get_sign(fa) * sc <= 0) { best = p; return true; }
+    }
+    return false;
+}
+
+// set_centers_on_surface, direction types 0 (gradient) and 1 (mesh normal)
+template <int D>
+__global__ __launch_bounds__(256) void k_project_early(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                       ProjArgs a) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= a.nf) return;
+    const V3 x = centroid(a.v, a.f, j);
+    const V3 fnv = facet_normal(a.v, a.f, j);
+    a.fn[3 * j] = fnv.x; a.fn[3 * j + 1] = fnv.y; a.fn[3 * j + 2] = fnv.z;
+    V3 g;
+    const float fcv = eval_fg<D>(prog, tab, x.x, x.y, x.z, g);
+    a.fc[j] = fcv;
+    V3 gd = normalise_min(g, 0.000001f);
+    const float sc = get_sign(fcv);
+    if (sc < 0.0f) { gd.x = -gd.x; gd.y = -gd.y; gd.z = -gd.z; }
+    const V3 d0{-gd.x * sc, -gd.y * sc, -gd.z * sc};
+    V3 best = x;
+    bool found = try_direction<D>(prog, tab, x, d0, sc, a.alphas, a.nal, a.max_dist, best);
+    if (!found) found = try_direction<D>(prog, tab, x, fnv, sc, a.alphas, a.nal < 10 ? a.nal : 10, a.max_dist, best);
+    if (!found) {
+        a.pend[atomicAdd(a.pend_count, 1u)] = (uint32_t)j;
+        return;
+    }
+    finalize<D>(prog, tab, x, fcv, true, best, a.out + 3 * j, a.cap_hits);
+}
+
+// types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes)
+template <int D>
+__global__ __launch_bounds__(256) void k_project_late(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                      ProjArgs a) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= *a.pend_count) return;
+    const int64_t j = a.pend[k];
+    const V3 x = centroid(a.v, a.f, j);
+    const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
+    const float fcv = a.fc[j];
+    const float sc = get_sign(fcv);
+    const int n10 = a.nal < 10 ? a.nal : 10;
+    const V3 pv{a.pert[3 * j], a.pert[3 * j + 1], a.pert[3 * j + 2]};
+    V3 z = cross3(fnv, pv);               // cp:250-259, add_inplace is a no-op (F9)
+    const float nz = norm2f(z.x, z.y, z.z);
+    z = V3{z.x / nz, z.y / nz, z.z / nz};  // normalize_1111
+    V3 z2 = normalise_min(cross3(fnv, z), 0.000001f);   // cp:297-312
+    V3 best = x;
+    bool found = try_direction<D>(prog, tab, x, z, sc, a.alphas, n10, a.max_dist, best);
+    if (!found) found = try_direction<D>(prog, tab, x, z2, sc, a.alphas, n10, a.max_dist, best);
+    for (int ax = 0; ax < 3 && !found; ++ax) {
+        const V3 d{ax == 0 ? 1.f : 0.f, ax == 1 ? 1.f : 0.f, ax == 2 ? 1.f : 0.f};
+        found = try_direction<D>(prog, tab, x, d, sc, a.alphas, n10, a.max_dist, best);
+    }
+    finalize<D>(prog, tab, x, fcv, found, found ? best : x, a.out + 3 * j, a.cap_hits);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_normals_at(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                    const float* __restrict__ P, int64_t n, float* __restrict__ G) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    V3 g;
+    (void)eval_fg<D>(prog, tab, P[3 * j], P[3 * j + 1], P[3 * j + 2], g);
+    const float nm = norm2f(g.x, g.y, g.z);
+    G[3 * j] = g.x / nm; G[3 * j + 1] = g.y / nm; G[3 * j + 2] = g.z / nm;
+}
+
+// ---- QEM: Eigen 3.3 JacobiSVD<Matrix3f> restated (Eigen/src/SVD/JacobiSVD.h, Jacobi/Jacobi.h) ----
+struct JRot { float c, s; };
+__device__ __forceinline__ void rot_rows(float W[3][3], int p, int q, JRot j) {
+    if (j.c == 1.f && j.s == 0.f) return;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float xi = W[p][k], yi = W[q][k];
+        W[p][k] = j.c * xi + j.s * yi;
+        W[q][k] = -j.s * xi + j.c * yi;
+    }
+}
+__device__ __forceinline__ void rot_cols(float W[3][3], int p, int q, JRot j) {
+    if (j.c == 1.f && j.s == 0.f) return;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float xi = W[k][p], yi = W[k][q];
+        W[k][p] = j.c * xi + j.s * yi;
+        W[k][q] = -j.s * xi + j.c * yi;
+    }
+}
+__device__ __forceinline__ JRot make_jacobi(float x, float y, float z) {
+    const float deno = 2.f * fabsf(y);
+    if (deno < 1.17549435e-38f) return JRot{1.f, 0.f};
+    const float tau = (x - z) / deno;
+    const float w = sqrtf(tau * tau + 1.f);
+    const float t = (tau > 0.f) ? 1.f / (tau + w) : 1.f / (tau - w);
+    const float sign_t = t > 0.f ? 1.f : -1.f;
+    const float n = 1.f / sqrtf(t * t + 1.f);
+    return JRot{n, -sign_t * (y / fabsf(y)) * fabsf(t) * n};
+}
+__device__ __forceinline__ void jacobi_2x2(float W[3][3], int p, int q, JRot& jl, JRot& jr) {
+    float m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+    JRot r1;
+    const float t = m00 + m11, d = m10 - m01;
+    if (fabsf(d) < 1.17549435e-38f) r1 = JRot{1.f, 0.f};
+    else {
+        const float u = t / d;
+        const float tmp = sqrtf(1.f + u * u);
+        r1 = JRot{u / tmp, 1.f / tmp};
+    }
+    if (!(r1.c == 1.f && r1.s == 0.f)) {
+        const float a0 = m00, b0 = m10, a1 = m01, b1 = m11;
+        m00 = r1.c * a0 + r1.s * b0; m10 = -r1.s * a0 + r1.c * b0;
+        m01 = r1.c * a1 + r1.s * b1; m11 = -r1.s * a1 + r1.c * b1;
+    }
+    jr = make_jacobi(m00, m01, m11);
+    const JRot rt{jr.c, -jr.s};
+    jl = JRot{r1.c * rt.c - r1.s * rt.s, r1.c * rt.s + r1.s * rt.c};
+}
+__device__ int jacobi_svd3(const float A[3][3], float thr, float S[3], float U[3][3], float V[3][3]) {
+    const float precision = 2.f * 1.1920929e-07f, consider_zero = 1.17549435e-38f;
+    float scale = 0.f;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) { const float a = fabsf(A[r][c]); if (a > scale) scale = a; }
+    if (scale == 0.f) scale = 1.f;
+    float W[3][3];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) { W[r][c] = A[r][c] / scale; U[r][c] = (r == c) ? 1.f : 0.f; V[r][c] = (r == c) ? 1.f : 0.f; }
+    float maxd = 0.f;
+    for (int i = 0; i < 3; ++i) { const float a = fabsf(W[i][i]); if (a > maxd) maxd = a; }
+    bool finished = false;
+    for (int sweep = 0; !finished && sweep < 100; ++sweep) {
+        finished = true;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                const float threshold = consider_zero > precision * maxd ? consider_zero : precision * maxd;
+                if (fabsf(W[p][q]) > threshold || fabsf(W[q][p]) > threshold) {
+                    finished = false;
+                    JRot jl, jr;
+                    jacobi_2x2(W, p, q, jl, jr);
+                    rot_rows(W, p, q, jl);
+                    rot_cols(U, p, q, jl);
+                    const JRot jrt{jr.c, -jr.s};
+                    rot_cols(W, p, q, jrt);
+                    rot_cols(V, p, q, jrt);
+                    const float a = fabsf(W[p][p]), b = fabsf(W[q][q]);
+                    const float mx = a > b ? a : b;
+                    if (mx > maxd) maxd = mx;
+                }
+            }
+    }
+    for (int i = 0; i < 3; ++i) {
+        const float a = W[i][i];
+        S[i] = fabsf(a);
+        if (a < 0.f) for (int r = 0; r < 3; ++r) U[r][i] = -U[r][i];
+    }
+    for (int i = 0; i < 3; ++i) S[i] *= scale;
+    int nonzero = 3;
+    for (int i = 0; i < 3; ++i) {
+        int pos = i;
+        float mx = S[i];
+        for (int k = i + 1; k < 3; ++k) if (S[k] > mx) { mx = S[k]; pos = k; }
+        if (mx == 0.f) { nonzero = i; break; }
+        if (pos != i) {
+            float t = S[i]; S[i] = S[pos]; S[pos] = t;
+            for (int r = 0; r < 3; ++r) {
+                t = U[r][i]; U[r][i] = U[r][pos]; U[r][pos] = t;
+                t = V[r][i]; V[r][i] = V[r][pos]; V[r][pos] = t;
+            }
+        }
+    }
+    float pt = S[0] * thr;
+    if (pt < consider_zero) pt = consider_zero;
+    int i = nonzero - 1;
+    while (i >= 0 && S[i] < pt) --i;
+    return i + 1;
+}
+
+// vertex_apply_qem (qem.hpp:321-599) with get_A_b (:256-316), one lane per vertex
+__global__ __launch_bounds__(256) void k_qem(float* __restrict__ verts, int64_t nv, const uint32_t* __restrict__ off,
+                                             const int32_t* __restrict__ lst, const float* __restrict__ C,
+                                             const float* __restrict__ N, float maxd) {
+    const int64_t vi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (vi >= nv) return;
+    float* v = verts + 3 * vi;
+    const float ox = v[0], oy = v[1], oz = v[2];
+    float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, b[3] = {0.f, 0.f, 0.f};
+    for (uint32_t k = off[vi]; k < off[vi + 1]; ++k) {
+        const int32_t ni = lst[k];
+        const float nx = N[3 * ni], ny = N[3 * ni + 1], nz = N[3 * ni + 2];
+        const float Px = C[3 * ni] - ox, Py = C[3 * ni + 1] - oy, Pz = C[3 * ni + 2] - oz;
+        const float nn00 = nx * nx, nn01 = nx * ny, nn02 = nx * nz, nn11 = ny * ny, nn12 = ny * nz, nn22 = nz * nz;
+        A[0][0] += nn00; A[0][1] += nn01; A[0][2] += nn02;
+        A[1][0] += nn01; A[1][1] += nn11; A[1][2] += nn12;
+        A[2][2] += nn22; A[2][0] += nn02; A[2][1] += nn12;
+        b[0] -= nn00 * Px + nn01 * Py + nn02 * Pz;
+        b[1] -= nn01 * Px + nn11 * Py + nn12 * Pz;
+        b[2] -= nn02 * Px + nn12 * Py + nn22 * Pz;
+    }
+    float S[3], U[3][3], V[3][3];
+    const int rank = jacobi_svd3(A, (float)(1.0 / 680.0), S, U, V);
+    float y[3] = {0.f, 0.f, 0.f}, utb[3];
+    for (int i = 0; i < 3; ++i) utb[i] = (-U[0][i]) * b[0] + ((-U[1][i]) * b[1] + (-U[2][i]) * b[2]);
+    for (int i = 0; i < rank; ++i) y[i] = utb[i] / S[i];
+    float nx[3];
+    for (int r = 0; r < 3; ++r) nx[r] = (V[r][0] * y[0] + (V[r][1] * y[1] + V[r][2] * y[2])) + v[r];
+    if (maxd > 0) {
+        const float dx = nx[0] - v[0], dy = nx[1] - v[1], dz = nx[2] - v[2];
+        const float dist2 = dx * dx + dy * dy + dz * dz;
+        if (dist2 <= maxd * maxd) { v[0] = nx[0]; v[1] = nx[1]; v[2] = nx[2]; }
+        else {
+            const float dist = sqrtf(dist2);
+            float len = (float)(maxd * 1.5);
+            if (len > dist) len = dist;
+            v[0] += dx / dist * len; v[1] += dy / dist * len; v[2] += dz / dist * len;
+        }
+    } else {
+        v[0] = nx[0]; v[1] = nx[1]; v[2] = nx[2];
+    }
+}
+
+// ---- host helpers ------------------------------------------------------------------------------
+// make_alpha_list cp:144-194
+std::vector<float> make_alpha_list(float initial_step, float min_step, float max_dist, int max_iter) {
+    std::vector<float> a;
+    const float unit = max_dist;
+    float step = initial_step;
+    while (step > min_step) {
+        step = (float)(step * 0.5);
+        const int total = (int)std::floor((double)(max_dist / std::fabs(step)) + 0.001);
+        const int ms = max_iter < total ? max_iter : total;
+        for (int i = 1; i < ms + 1; i += 2) {
+            const float alpha = (float)i * step;
+            a.push_back(alpha / unit);
+            a.push_back(-alpha / unit);
+        }
+        if (a.size() > 100000) break;   // guards a pathological max_dist
+    }
+    return a;
+}
+
+// boost::random::mt11213b (seed 12) + uniform_01<float>: make_random_pm1(n, 3, 1e-6)
+std::vector<float> make_random_pm1(int64_t n, float amplitude) {
+    std::vector<uint32_t> x(351);
+    x[0] = 12u;
+    for (int i = 1; i < 351; ++i) x[i] = 1812433253u * (x[i - 1] ^ (x[i - 1] >> 30)) + (uint32_t)i;
+    int idx = 351;
+    auto next = [&]() -> uint32_t {
+        if (idx >= 351) {
+            for (int k = 0; k < 351; ++k) {
+                const uint32_t y = (x[k] & (0xffffffffu << 19)) | (x[(k + 1) % 351] & ~(0xffffffffu << 19));
+                x[k] = x[(k + 175) % 351] ^ (y >> 1) ^ ((y & 1u) ? 0xccab8ee7u : 0u);
+            }
+            idx = 0;
+        }
+        uint32_t z = x[idx++];
+        z ^= (z >> 11);
+        z ^= (z << 7) & 0x31b6ab00u;
+        z ^= (z << 15) & 0xffe50000u;
+        z ^= (z >> 17);
+        return z;
+    };
+    const float factor = 1.0f / ((float)4294967295u + 1.0f);
+    std::vector<float> out((size_t)(3 * n));
+    for (auto& o : out) {
+        float r;
+        do { r = (float)next() * factor; } while (!(r < 1.0f));
+        o = (float)(((double)r * 2.0 - 1.0) * (double)amplitude);
+    }
+    return out;
+}
+
+}  // namespace
+
+Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
+    misc_.reserve(64);
+}
+
+void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_) {
+    nv = nv_;
+    nf = nf_;
+    verts_.reserve((size_t)(nv + 1) * 12);
+    vnew_.reserve((size_t)(nv + 1) * 12);
+    faces_.reserve((size_t)(nf + 1) * 12);
+    if (nv) IMPLI_HIP(hipMemcpyAsync(verts_.p, d_verts, (size_t)nv * 12, hipMemcpyDeviceToDevice, s));
+    if (nf) IMPLI_HIP(hipMemcpyAsync(faces_.p, d_faces, (size_t)nf * 12, hipMemcpyDeviceToDevice, s));
+    // umbrellas
+    deg_.reserve((size_t)(nv + 1) * 4);
+    uoff_.reserve((size_t)(nv + 2) * 4);
+    ulst_.reserve((size_t)(3 * nf + 1) * 4);
+    IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
+    if (nf) k_degree<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
+    k_scan_u32<<<1, 1024, 0, s>>>(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv);
+    IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
+    if (nf) k_fill_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(),
+                                                             deg_.as<uint32_t>(), ulst_.as<int32_t>());
+    if (nv) k_sort_umbrella<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), nv);
+    // faces of faces
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)(4 * nf + 16)) cap <<= 1;
+    etab_.reserve((size_t)cap * (8 + 12) + (size_t)(3 * nf + 1) * 4);
+    EdgeTab t;
+    t.key = etab_.as<unsigned long long>();
+    t.first = reinterpret_cast<uint32_t*>(t.key + cap);
+    t.last = t.first + cap;
+    t.cnt = t.last + cap;
+    t.slot_of = t.cnt + cap;
+    t.mask = cap - 1;
+    IMPLI_HIP(hipMemsetAsync(t.key, 0xff, (size_t)cap * 8, s));
+    IMPLI_HIP(hipMemsetAsync(t.first, 0xff, (size_t)cap * 4, s));
+    IMPLI_HIP(hipMemsetAsync(t.last, 0, (size_t)cap * 8, s));   // last + cnt
+    fof_.reserve((size_t)(3 * nf + 1) * 4);
+    if (nf) {
+        k_edge_insert<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, nv, t);
+        k_fof<<<blocks_for(3 * nf), 256, 0, s>>>(nf, t, fof_.as<int32_t>());
+    }
+    cen_.reserve((size_t)(nf + 1) * 12);
+    nrm_.reserve((size_t)(nf + 1) * 12);
+    w_.reserve((size_t)(nf + 1) * 4);
+    IMPLI_HIP(hipGetLastError());
+}
+
+void Ob02::store_pointset(const char* key, const float* d, int64_t n, bool keep_first) {
+    if (!capture_pointsets) return;
+    if (keep_first && pointsets_.count(key)) return;
+    std::vector<float> h((size_t)n * 3);
+    if (n) IMPLI_HIP(hipMemcpyAsync(h.data(), d, (size_t)n * 12, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    pointsets_[key] = std::move(h);
+}
+
+void Ob02::vertex_resampling(float c) {
+    if (!nf) return;
+    store_pointset("pre_resampling_vertices", verts_.as<float>(), nv, true);   // vertex_resampling.hpp:176-180
+    DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), verts_.as<float>(),
+                 faces_.as<int32_t>(), nf, cen_.as<float>(), nrm_.as<float>());
+    k_face_weights<<<blocks_for(nf), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(), nf, c, w_.as<float>());
+    k_resample<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), w_.as<float>(), cen_.as<float>(),
+                                              nv, vnew_.as<float>());
+    std::swap(verts_, vnew_);
+    IMPLI_HIP(hipGetLastError());
+    store_pointset("post_resampling_vertices", verts_.as<float>(), nv, true);   // :207-211
+}
+
+float Ob02::average_edge_length() {
+    norms_.reserve((size_t)(nf + 1) * 12);
+    k_edge_norms<<<blocks_for(nf), 256, 0, s>>>(verts_.as<float>(), faces_.as<int32_t>(), nf, norms_.as<float>());
+    std::vector<float> h((size_t)nf * 3);
+    IMPLI_HIP(hipMemcpyAsync(h.data(), norms_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    float el = 0.f;   // the reference starts from an uninitialised float (F8a); defined as 0
+    for (float x : h) el += x;
+    return (float)((double)el / (3. * (double)nf));
+}
+
+void Ob02::centroids_projection(bool enable_qem) {
+    if (!nf) return;
+    const float avg = average_edge_length();
+    avg_edge_ = avg;
+    const std::vector<float> alphas = make_alpha_list((float)(avg * 1.0), (float)(0.001 * 1.0), avg, 20);
+    alphas_.reserve((alphas.size() + 1) * 4);
+    if (!alphas.empty())
+        IMPLI_HIP(hipMemcpyAsync(alphas_.p, alphas.data(), alphas.size() * 4, hipMemcpyHostToDevice, s));
+    proj_.reserve((size_t)(nf + 1) * 12);
+    fn_.reserve((size_t)(nf + 1) * 12);
+    pend_.reserve((size_t)(nf + 2) * 4);
+    DevBuf& fcbuf = w_;   // f(centroid) per face; the resampling weights are dead here
+    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 64, s));
+    ProjArgs a{};
+    a.v = verts_.as<float>();
+    a.f = faces_.as<int32_t>();
+    a.nf = nf;
+    a.alphas = alphas_.as<float>();
+    a.nal = (int)alphas.size();
+    a.max_dist = avg;
+    a.out = proj_.as<float>();
+    a.fn = fn_.as<float>();
+    a.fc = fcbuf.as<float>();
+    a.pend = pend_.as<uint32_t>();
+    a.pend_count = misc_.as<uint32_t>();
+    a.cap_hits = misc_.as<uint32_t>() + 1;
+    // pre_p_centroids (cp:1236-1238): the centroids themselves
+    if (capture_pointsets) {
+        DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), a.v, a.f, nf,
+                     cen_.as<float>(), nrm_.as<float>());
+        store_pointset("pre_p_centroids", cen_.as<float>(), nf, false);
+    }
+    DEPTH_LAUNCH(E.depth(), k_project_early, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), a);
+    uint32_t hm[2];
+    IMPLI_HIP(hipMemcpyAsync(hm, misc_.p, 8, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    if (hm[0] > 0) {   // some centroids need the randomised directions (types 2-6)
+        const std::vector<float> pert = make_random_pm1(nf, 0.000001f);
+        pert_.reserve(pert.size() * 4);
+        IMPLI_HIP(hipMemcpyAsync(pert_.p, pert.data(), pert.size() * 4, hipMemcpyHostToDevice, s));
+        a.pert = pert_.as<float>();
+        DEPTH_LAUNCH(E.depth(), k_project_late, blocks_for(hm[0]), 256, s, E.d_program(), E.d_rabbit(), a);
+        IMPLI_HIP(hipMemcpyAsync(hm, misc_.p, 8, hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+    }
+    cap_hits_ += hm[1];
+    IMPLI_HIP(hipGetLastError());
+    store_pointset("post_p_centroids", proj_.as<float>(), nf, false);
+    store_pointset("pre_qem_verts", verts_.as<float>(), nv, false);
+    if (enable_qem) {
+        grad_.reserve((size_t)(nf + 1) * 12);
+        DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>(), nf,
+                     grad_.as<float>());
+        if (nv) k_qem<<<blocks_for(nv), 256, 0, s>>>(verts_.as<float>(), nv, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
+                                                     proj_.as<float>(), grad_.as<float>(), avg);
+        IMPLI_HIP(hipGetLastError());
+        store_pointset("post_qem_verts", verts_.as<float>(), nv, false);
+    }
+}
+
+void Ob02::fetch(float* verts, int32_t* faces) {
+    if (nv) IMPLI_HIP(hipMemcpyAsync(verts, verts_.p, (size_t)nv * 12, hipMemcpyDeviceToHost, s));
+    if (nf) IMPLI_HIP(hipMemcpyAsync(faces, faces_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace impli

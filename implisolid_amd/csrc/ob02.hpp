@@ -1,0 +1,41 @@
+// ob02.hpp -- the Ohtake-Belyaev refinement loop on the GPU (polygonizer steps 1 and 2).
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace impli {
+
+class Ob02 {
+public:
+    Ob02(Engine& e, hipStream_t s);
+    // takes a copy of the MC mesh (device pointers) and builds the face/vertex topology
+    void load_mesh(const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf);
+    // step 1: apply_vertex_resampling_to_MC_buffers__VMS (apply_v_s_to_mc_buffers.hpp:280-326)
+    void vertex_resampling(float c);
+    // step 2: centroids_projection (centroids_projection.cpp:1219-1311)
+    void centroids_projection(bool enable_qem);
+    // blocking copy of the current mesh to host
+    void fetch(float* verts, int32_t* faces);
+    const std::map<std::string, std::vector<float>>& pointsets() const { return pointsets_; }
+    float last_average_edge() const { return avg_edge_; }
+    uint32_t bisection_cap_hits() const { return cap_hits_; }
+    bool capture_pointsets = true;
+
+private:
+    void store_pointset(const char* key, const float* d, int64_t n, bool keep_first);
+    float average_edge_length();
+
+    Engine& E;
+    hipStream_t s;
+    int64_t nv = 0, nf = 0;
+    DevBuf verts_, faces_, vnew_, cen_, nrm_, w_, fof_, uoff_, ulst_, etab_, deg_, proj_, grad_, fn_, norms_,
+        alphas_, pert_, pend_, misc_;
+    float avg_edge_ = 0.f;
+    uint32_t cap_hits_ = 0;
+    std::map<std::string, std::vector<float>> pointsets_;
+};
+
+}  // namespace impli

@@ -1,0 +1,63 @@
+// program.hpp -- the implicit-function tree compiled to a flat, wave-uniform node program.
+//
+// The reference evaluates its tree of virtual implicit_function objects node by node over whole
+// batches, copying the batch at every transformed node (prepare_inner_vectors,
+// basic_functions.hpp:361-379).  Here the tree (object_factory.hpp:56-758) is compiled once on the
+// host into a post-order program that every lane of a wave interprets in lock step: the program
+// counter, the stack depths and the matrices are uniform, so they live in SGPRs and the
+// per-sample state (point stack, value stack) lives in VGPRs.
+//
+//   XFORM k   push M_k^-1 * top-point            (the node's own inverse matrix)
+//   PRIM t    pop point, push f_t(point)         (egg, rabbit cube, cylinder, cone, heart, torus,
+//                                                 double mushroom)
+//   CSG t     pop point, pop f2, f1, push f1 (op) f2   (Union / Intersection / Difference)
+//
+// With gradients enabled every value slot carries (f, gx, gy, gz) and every XFORM'd node applies
+// M^-T to the selected gradient on the way up, exactly like eval_gradient in
+// transformed_union.hpp:54-84 (children's f and grad are computed once and reused).
+#pragma once
+#include <stdint.h>
+
+namespace impli {
+
+enum NodeType : int32_t {
+    NT_UNION = 0,
+    NT_INTERSECTION = 1,
+    NT_DIFFERENCE = 2,
+    NT_ELLIPSOID = 3,
+    NT_CUBE = 4,
+    NT_CYLINDER = 5,
+    NT_CONE = 6,
+    NT_HEART = 7,
+    NT_TORUS = 8,
+    NT_DMUSHROOM = 9,
+};
+
+enum OpCode : int32_t {
+    OP_XFORM = 0,
+    OP_PRIM = 1,
+    OP_CSG = 2,
+};
+
+struct Instr {
+    int32_t op;    // OpCode
+    int32_t type;  // PRIM/CSG: NodeType
+    int32_t mat;   // index of the node's inverse matrix (XFORM: the one to apply)
+    int32_t pad;
+};
+
+constexpr int kMaxProgram = 256;   // instructions
+constexpr int kMaxDepth = 16;      // point/value stack depth (tree depth + 1)
+
+// Device-resident program (one per object).  Matrices are the inverse transforms
+// (inv_transf_matrix), row-major 3x4.
+struct Program {
+    int32_t n_instr;
+    int32_t max_depth;
+    int32_t n_mats;
+    int32_t pad;
+    Instr instr[kMaxProgram];
+    float mats[kMaxProgram][12];
+};
+
+}  // namespace impli

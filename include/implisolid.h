@@ -1,0 +1,115 @@
+/*
+ * implisolid.h -- C ABI of the MI355X-native implicit-surface polygoniser.
+ *
+ * Drop-in replacement for the extern "C" interface of ImpliSolid's mcc2.cpp.  Every declaration
+ * below names the reference declaration it replaces (/root/reference/js_iteration_2/mcc2.cpp,
+ * declarations :88-134, definitions as cited).  Signatures, argument meaning, ownership and error
+ * behaviour are the reference's; the work runs on the GPU (HIP, gfx950).
+ *
+ * Thread-safety: like the reference, one global geometry slot and one direct-eval slot; not
+ * reentrant.  build_geometry returns after the result is host resident.
+ */
+#ifndef IMPLISOLID_H
+#define IMPLISOLID_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- mesh API ------------------------------------------------------------------------------ */
+/* mcc2.cpp:89 / :446-464  polygonise the MP5 shape with the given mc_settings JSON.  Refuses (with
+   a message) while a previous result is active: call finish_geometry() first (:316-319). */
+void build_geometry(const char* shape_parameters_json, const char* mc_parameters_json);
+/* mcc2.cpp:90 (declared, body commented out at :296-302): build_geometry + worker call specs
+   ({"progressCallback_id", "call_id", "shape_id"}); progress callbacks are not emitted. */
+void build_geometry_u(const char* shape_parameters_json, const char* mc_parameters_json, const char* call_specs);
+/* mcc2.cpp:91 / :470-473  vertex count */
+int get_v_size(void);
+/* mcc2.cpp:92 / :466-469  face count */
+int get_f_size(void);
+/* mcc2.cpp:93 / :496-511  copy 3*fcount int32 vertex indices */
+void get_f(int* f_out, int fcount);
+/* mcc2.cpp:94 / :474-492  copy 3*vcount float32 coordinates */
+void get_v(float* v_out, int vcount);
+/* mcc2.cpp:95 / :540-552  release the slot (buffers stay valid until the next build) */
+void finish_geometry(void);
+/* mcc2.cpp:96 / :521-525  library-owned int32 triplets */
+void* get_f_ptr(void);
+/* mcc2.cpp:97 / :515-519  library-owned float32 xyz */
+void* get_v_ptr(void);
+
+/* ---- direct evaluation API ------------------------------------------------------------------ */
+/* mcc2.cpp:106 / :726-741  returns 1, or 0 if an object is already set */
+int set_object(const char* shape_parameters_json, bool ignore_root_matrix);
+/* mcc2.cpp:107 / :743-763 */
+bool unset_object(int id);
+/* mcc2.cpp:109 / :765-799  0 <= n < 50000 points, float32 xyz */
+bool set_x(void* verts, int n);
+/* mcc2.cpp:110 / :800-812 */
+void unset_x(void);
+/* mcc2.cpp:112 / :815-822 */
+void calculate_implicit_values(void);
+/* mcc2.cpp:113 / :827-829 */
+void* get_values_ptr(void);
+/* mcc2.cpp:114 / :830-832 */
+int get_values_size(void);
+/* mcc2.cpp:116 / :834-889  with normalize_and_invert: g <- -g/|g| (factor -42 if |g| <= 1e-4) */
+void calculate_implicit_gradients(bool normalize_and_invert);
+/* mcc2.cpp:117 / :890-903 */
+void* get_gradients_ptr(void);
+/* mcc2.cpp:118 / :904-911  = 3n */
+int get_gradients_size(void);
+
+/* ---- misc ------------------------------------------------------------------------------------ */
+/* mcc2.cpp:122 / :203-209  debug point sets (pre/post_resampling_vertices, pre/post_p_centroids,
+   pre/post_qem_verts); NULL if absent */
+void* get_pointset_ptr(char* id);
+/* mcc2.cpp:123 / :210-215 */
+int get_pointset_size(char* id);
+/* mcc2.cpp:126 / :574-617  build information */
+void about(void);
+
+/* ---- additive API (not in the reference) ---------------------------------------------------- */
+/* last error message of this thread's calls ("" if none) */
+const char* implisolid_last_error(void);
+/* 0 (default): abort() where the reference aborts (bad settings, unknown MP5 type);
+   1: print the same message, record it in implisolid_last_error() and return */
+void implisolid_set_error_mode(int mode);
+/* evaluate n >= 0 points (no 50k limit) of the current set_object(); grad may be NULL */
+int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* grad_out);
+
+/* host-only: compile an MP5 tree to the node program; info = {n_instr, depth, n_mats, 0};
+   mats_out receives n_mats inverse matrices (12 floats each, up to 256) */
+int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int32_t info[4], float* mats_out);
+
+/* Device-resident slab pipeline (benchmarks / multi-GPU Z-slab runs).  A slab engine owns the
+   device buffers of one Z-slab of one object on the current HIP device.  `stream` is a
+   hipStream_t (may be NULL); nothing blocks except implisolid_slab_counts. */
+typedef struct implisolid_slab implisolid_slab;
+implisolid_slab* implisolid_slab_create(const char* shape_json, const char* mc_json, int rank, int nranks);
+void implisolid_slab_destroy(implisolid_slab* s);
+int implisolid_slab_eval(implisolid_slab* s, void* stream);            /* field (K1) */
+int implisolid_slab_count(implisolid_slab* s, void* stream);           /* counts + scan (K2) */
+/* d_offsets: device uint32[2] = this slab's {vertex, face} offset in the global numbering, or NULL
+   for the host-set offsets (implisolid_slab_set_offsets, default 0) */
+int implisolid_slab_emit(implisolid_slab* s, const uint32_t* d_offsets, void* stream);
+/* device uint32[16]: [2] owned verts incl. halo, [3] faces, [4] active cells, [5] halo verts */
+const uint32_t* implisolid_slab_counters(implisolid_slab* s);
+/* blocking: out[0] = vertices, out[1] = faces of this slab, out[2] = overflow flag; grows the
+   output buffers when needed (then emit again) */
+int implisolid_slab_counts(implisolid_slab* s, void* stream, uint32_t out[3]);
+int implisolid_slab_grid(implisolid_slab* s, int32_t out[8]);
+int implisolid_slab_set_offsets(implisolid_slab* s, uint32_t voff, uint32_t foff);
+/* blocking copy of the slab's emitted vertices (3*V floats) and faces (3*F ints, global ids) */
+int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, void* stream);   /* R, res, cz0, cz1, cz_emit, fz0, fz1, depth */
+float* implisolid_slab_verts(implisolid_slab* s);     /* device pointers */
+int32_t* implisolid_slab_faces(implisolid_slab* s);
+float* implisolid_slab_field(implisolid_slab* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

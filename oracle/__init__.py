@@ -1,0 +1,360 @@
+"""CPU oracle for the implicit-surface polygoniser hot path -- TEST INFRASTRUCTURE ONLY.
+
+This package restates the reference (ynotstartups/implisolid, ``js_iteration_2/``) on the CPU so the
+MI355X path can be checked against it.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import it; the product (``implisolid_amd``) never does.
+
+* ``oracle/*.c`` (built to ``oracle/build/liboracle.so`` by ``oracle/Makefile``): implicit-function
+  evaluation, marching cubes with first-appearance numbering, vertex resampling, centroid
+  projection + bisection, QEM.  Each C function cites the reference file:line it restates.
+* this module: the MP5-JSON factory (``object_factory.hpp:56-758``) and the mc-settings parser
+  (``polygoniser_settings.hpp:147-305``) restated in Python, the ``grand_algorithm`` driver
+  (``mcc2.cpp:309-444``) and ctypes bindings.
+
+Parity status: **parity unpinned** -- the reference ships no tests, fixtures or golden vectors and
+cannot be compiled here (Boost/Eigen/emscripten.h are absent; header stand-ins are not allowed), so
+the oracle is a restatement checked by construction, by property tests and by the exhaustive
+glibc-acosf check (see DESIGN.md "Oracle").
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+
+UNION, INTERSECTION, DIFFERENCE, ELLIPSOID, CUBE, CYLINDER, CONE, HEART, TORUS, DMUSHROOM = range(10)
+
+# MP5 "type" strings accepted by object_factory.hpp:86-653 for the plain-arithmetic node families.
+PRIMITIVE_TYPES = {
+    "implicit_double_mushroom": DMUSHROOM,   # object_factory.hpp:86-100
+    "icube": CUBE, "cube": CUBE,             # :110-119
+    "icylinder": CYLINDER, "cylinder": CYLINDER,  # :121-132
+    "iellipsoid": ELLIPSOID, "ellipsoid": ELLIPSOID,  # :134-143
+    "icone": CONE, "cone": CONE,             # :144-152
+    "iheart": HEART,                         # :153-162
+    "itorus": TORUS,                         # :163-173
+}
+# types the reference knows but this build does not evaluate (Eigen-based or JS callbacks)
+KNOWN_UNSUPPORTED = {"tetrahedron", "inf_screw", "screw_diff_two_plane", "screw", "sdf_3d",
+                     "half_plane", "screw_gradient_wrong", "top_bottom_lid", "rawjscode",
+                     "meta_balls", "extrusion"}
+
+
+class OrNode(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("child", ctypes.c_int32 * 2),
+                ("m", ctypes.c_float * 12), ("minv", ctypes.c_float * 12)]
+
+
+class OrMesh(ctypes.Structure):
+    _fields_ = [("verts", ctypes.POINTER(ctypes.c_float)), ("faces", ctypes.POINTER(ctypes.c_int32)),
+                ("nv", ctypes.c_int64), ("nf", ctypes.c_int64)]
+
+
+_lib = None
+
+
+def build():
+    """Compile oracle/*.c (make -C oracle)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        fp = ctypes.POINTER(ctypes.c_float)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        npp = ctypes.POINTER(OrNode)
+        L.or_invert_matrix.argtypes = [fp, fp]
+        L.or_tree_prepare.argtypes = [npp, ctypes.c_int]
+        L.or_eval.argtypes = [npp, ctypes.c_int, fp, ctypes.c_int64, fp]
+        L.or_grad.argtypes = [npp, ctypes.c_int, fp, ctypes.c_int64, fp]
+        L.or_acosf.argtypes = [ctypes.c_float]
+        L.or_acosf.restype = ctypes.c_float
+        L.or_marching_cubes.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, ctypes.POINTER(OrMesh)]
+        L.or_mesh_free.argtypes = [ctypes.POINTER(OrMesh)]
+        L.or_mc_field.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, fp]
+        L.or_vertex_resampling.argtypes = [npp, ctypes.c_int, ctypes.c_float, fp, ctypes.c_int64, ip,
+                                           ctypes.c_int64, fp]
+        L.or_centroids_projection.argtypes = [npp, ctypes.c_int, fp, ctypes.c_int64, ip, ctypes.c_int64,
+                                              ctypes.c_int, fp, fp]
+        _lib = L
+    return _lib
+
+
+# ---------------------------------------------------------------------------------------------
+# number parsing: boost::property_tree get_value<float> reads with a C++ stream (strtof semantics)
+_libc = ctypes.CDLL(None)
+_libc.strtof.restype = ctypes.c_float
+_libc.strtof.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p)]
+
+
+def strtof(s):
+    s = str(s).strip()
+    b = s.encode()
+    end = ctypes.c_char_p()
+    v = _libc.strtof(b, ctypes.byref(end))
+    return np.float32(v)
+
+
+def _loads(text):
+    """JSON with numbers kept as their source text (ptree stores strings)."""
+    if isinstance(text, (dict, list)):
+        return text
+    return json.loads(text, parse_float=str, parse_int=str)
+
+
+def _matrix12(d):
+    """getMatrix12 object_factory.hpp:21-30: the first 12 entries (16-entry matrices overflow the
+    reference's REAL[12], F8b -- we accept 12 or 16 and use the first 12)."""
+    vals = d.get("matrix")
+    if vals is None or len(vals) < 12:
+        raise ValueError("MP5 node needs a 12- or 16-entry 'matrix'")
+    return [strtof(v) for v in vals[:12]]
+
+
+EYE12 = [np.float32(v) for v in (1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0)]
+
+
+def mp5_to_nodes(shape, ignore_root_matrix=False):
+    """object_factory (object_factory.hpp:56-758) -> flat node list + root index."""
+    nodes = []
+
+    def add(t, m, c0=-1, c1=-1):
+        nodes.append((t, (c0, c1), m))
+        return len(nodes) - 1
+
+    def build_node(d, ignore):
+        t = d.get("type")
+        if t in PRIMITIVE_TYPES:
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            return add(PRIMITIVE_TYPES[t], m)
+        if t == "Union":                          # object_factory.hpp:537-580, left-deep chain
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            ch = d.get("children") or []
+            if len(ch) < 2:
+                raise ValueError("Union needs at least two children (one child is UB in the reference)")
+            a = build_node(ch[0], False)
+            for k in range(1, len(ch)):
+                b = build_node(ch[k], False)
+                if k == len(ch) - 1:
+                    a = add(UNION, m, a, b)       # o_matrix of the last step is the object
+                else:
+                    a = add(UNION, list(EYE12), a, b)  # o_plain
+            return a
+        if t in ("Intersection", "Difference"):   # :581-653, binary (extra children ignored)
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            ch = d.get("children") or []
+            if len(ch) < 2:
+                raise ValueError("%s needs two children" % t)
+            a = build_node(ch[0], False)
+            b = build_node(ch[1], False)
+            return add(INTERSECTION if t == "Intersection" else DIFFERENCE, m, a, b)
+        if t in KNOWN_UNSUPPORTED:
+            raise NotImplementedError("MP5 type %r is outside the implemented node families" % t)
+        raise ValueError("Invalid object you asked for: %r" % t)   # the reference abort()s
+
+    root = build_node(_loads(shape), ignore_root_matrix)
+    arr = (OrNode * len(nodes))()
+    for i, (t, (c0, c1), m) in enumerate(nodes):
+        arr[i].type = t
+        arr[i].child[0] = c0
+        arr[i].child[1] = c1
+        for k in range(12):
+            arr[i].m[k] = float(m[k])
+    lib().or_tree_prepare(arr, len(nodes))
+    return arr, root
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _ip(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def invert_matrix(m12):
+    a = np.ascontiguousarray(m12, dtype=np.float32)
+    o = np.zeros(12, np.float32)
+    lib().or_invert_matrix(_fp(a), _fp(o))
+    return o
+
+
+def eval_implicit(tree, pts):
+    nodes, root = tree
+    p = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 3)
+    f = np.empty(p.shape[0], np.float32)
+    lib().or_eval(nodes, root, _fp(p), p.shape[0], _fp(f))
+    return f
+
+
+def eval_gradient(tree, pts):
+    nodes, root = tree
+    p = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 3)
+    g = np.empty((p.shape[0], 3), np.float32)
+    lib().or_grad(nodes, root, _fp(p), p.shape[0], _fp(g))
+    return g
+
+
+def acosf(x):
+    return np.float32(lib().or_acosf(float(x)))
+
+
+def mc_field(tree, resolution, box):
+    nodes, root = tree
+    res = resolution + 5
+    out = np.empty(res ** 3, np.float32)
+    b = np.asarray(box, np.float32)
+    if lib().or_mc_field(nodes, root, resolution, _fp(b), _fp(out)) != 0:
+        raise MemoryError
+    return out.reshape(res, res, res)
+
+
+def marching_cubes(tree, resolution, box):
+    nodes, root = tree
+    b = np.asarray(box, np.float32)
+    m = OrMesh()
+    if lib().or_marching_cubes(nodes, root, resolution, _fp(b), ctypes.byref(m)) != 0:
+        raise MemoryError
+    v = np.ctypeslib.as_array(m.verts, shape=(m.nv * 3,)).copy().reshape(-1, 3) if m.nv else np.zeros((0, 3), np.float32)
+    f = np.ctypeslib.as_array(m.faces, shape=(m.nf * 3,)).copy().reshape(-1, 3) if m.nf else np.zeros((0, 3), np.int32)
+    lib().or_mesh_free(ctypes.byref(m))
+    return v.astype(np.float32), f.astype(np.int32)
+
+
+def vertex_resampling(tree, verts, faces, c):
+    nodes, root = tree
+    v = np.ascontiguousarray(verts, dtype=np.float32).copy()
+    f = np.ascontiguousarray(faces, dtype=np.int32)
+    cen = np.empty((f.shape[0], 3), np.float32)
+    if lib().or_vertex_resampling(nodes, root, float(np.float32(c)), _fp(v), v.shape[0], _ip(f), f.shape[0], _fp(cen)):
+        raise MemoryError
+    return v, cen
+
+
+def centroids_projection(tree, verts, faces, enable_qem):
+    nodes, root = tree
+    v = np.ascontiguousarray(verts, dtype=np.float32).copy()
+    f = np.ascontiguousarray(faces, dtype=np.int32)
+    cen = np.empty((f.shape[0], 3), np.float32)
+    avg = np.zeros(1, np.float32)
+    if lib().or_centroids_projection(nodes, root, _fp(v), v.shape[0], _ip(f), f.shape[0], int(bool(enable_qem)),
+                                     _fp(cen), _fp(avg)):
+        raise MemoryError
+    return v, cen, float(avg[0])
+
+
+# ---------------------------------------------------------------------------------------------
+# polygoniser_settings.hpp:147-305 parse_mc_properties_json
+class MCSettings:
+    def __init__(self):
+        self.box = [np.float32(-1), np.float32(1)] * 3
+        self.resolution = 28
+        self.ignore_root_matrix = False
+        self.overall_repeats = 1
+        self.vresampl_iters = 0
+        self.vresampl_c = np.float32(1.0)
+        self.projection = False
+        self.qem = False
+        self.subdiv = True
+        self.post_subdiv_noise = np.float32(0.01)
+
+
+def _get(d, path):
+    cur = d
+    for k in path.split("."):
+        if not isinstance(cur, dict) or k not in cur:
+            return None
+        cur = cur[k]
+    return cur
+
+
+def _get_int(d, path, default):
+    v = _get(d, path)
+    if v is None or isinstance(v, (dict, list)):
+        return default
+    try:
+        s = str(v).strip()
+        if not s.lstrip("-").isdigit():
+            return default
+        return int(s)
+    except ValueError:
+        return default
+
+
+def _get_float(d, path, default):
+    v = _get(d, path)
+    if v is None or isinstance(v, (dict, list)):
+        return default
+    try:
+        float(str(v))
+    except ValueError:
+        return default
+    return strtof(v)
+
+
+def parse_mc_settings(text):
+    d = _loads(text)
+    s = MCSettings()
+    box = [_get_float(d, "box." + k, None) for k in ("xmin", "xmax", "ymin", "ymax", "zmin", "zmax")]
+    if any(v is None for v in box):
+        raise ValueError("Error: missing or incorrect values in mc_parameters_json (box)")
+    s.box = [np.float32(v) for v in box]
+    r = _get_float(d, "resolution", np.float32(-1))
+    ri = int(r)
+    if ri == -1:
+        ri = 28
+    if np.float32(ri) != r:
+        raise ValueError("Error: resolution must be integer")
+    if ri <= 2:
+        raise ValueError("Error: resolution must be > 2")
+    s.resolution = ri
+    s.vresampl_c = _get_float(d, "vresampl.c", np.float32(1.0))
+    s.vresampl_iters = _get_int(d, "vresampl.iters", 0)
+
+    def rb(name, default):
+        v = _get_int(d, name, -1)
+        return default if v == -1 else bool(v)
+    s.projection = rb("projection.enabled", False)
+    s.qem = rb("qem.enabled", False)
+    s.subdiv = rb("subdiv.enabled", True)
+    s.post_subdiv_noise = _get_float(d, "debug.post_subdiv_noise", np.float32(0.01))
+    s.overall_repeats = _get_int(d, "overall_repeats", 1)
+    irm = _get(d, "ignore_root_matrix")
+    s.ignore_root_matrix = str(irm).strip() in ("true", "1") if irm is not None else False
+    if s.qem and not s.projection:
+        raise ValueError("Invalid settings: QEM will not be applied if centroid projection is disabled")
+    return s
+
+
+def polygonize(shape_json, mc_json, taps=None):
+    """grand_algorithm (mcc2.cpp:309-444): MC, then overall_repeats x [resampling x iters;
+    projection (+QEM)].  Subdivision (step 3) is outside the implemented scope."""
+    s = parse_mc_settings(mc_json)
+    tree = mp5_to_nodes(shape_json, s.ignore_root_matrix)
+    v, f = marching_cubes(tree, s.resolution, s.box)
+    if taps is not None:
+        taps["mc_verts"] = v.copy()
+    for rep in range(s.overall_repeats):
+        for _ in range(s.vresampl_iters):
+            v, _c = vertex_resampling(tree, v, f, s.vresampl_c)
+        if s.projection:
+            v, cen, _avg = centroids_projection(tree, v, f, s.qem)
+            if taps is not None:
+                taps.setdefault("post_p_centroids", []).append(cen)
+        if s.subdiv and (s.overall_repeats <= 1 or rep == s.overall_repeats - 1):
+            raise NotImplementedError("subdivision (polygonize_step_3) is outside the implemented scope")
+    return v, f

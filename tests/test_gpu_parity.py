@@ -1,0 +1,190 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit-exact.
+
+Integer/index outputs (faces) must be identical; float outputs (field values, gradients,
+vertices) must be bit-identical too, because both sides execute the same IEEE operations in the
+reference's order (no FMA contraction, correctly rounded division/sqrt).
+"""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import mesh_edges
+
+pytestmark = pytest.mark.gpu
+
+
+def _trees():
+    from implisolid_amd import scenes
+    out = {
+        "sphere": {"type": "iellipsoid", "matrix": scenes.EYE},
+        "union_sphere_cube": scenes.union_sphere_cube(),
+        "config3_tree": scenes.config3()[0],
+    }
+    for t in ["iellipsoid", "icylinder", "icone", "itorus", "implicit_double_mushroom", "iheart", "cube"]:
+        out["leaf_" + t] = {"type": t, "matrix": scenes.st(0.5, 0.125, -0.0625, 0.03125)}
+    out["difference"] = {"type": "Difference", "matrix": scenes.st(1, 0.015625, 0, 0), "children": [
+        {"type": "icylinder", "matrix": scenes.st(0.5, 0, 0, 0)}, {"type": "iellipsoid", "matrix": scenes.st(0.5, 0.25, 0, 0)}]}
+    out["intersection"] = {"type": "Intersection", "matrix": scenes.EYE, "children": [
+        {"type": "itorus", "matrix": scenes.st(0.25, 0, 0, 0)}, {"type": "icone", "matrix": scenes.st(1, 0, 0, -0.25)}]}
+    return out
+
+
+TREES = _trees()
+
+
+@pytest.mark.parametrize("name", sorted(TREES))
+def test_eval_points_bit_exact(impli, oracle, name):
+    shape = TREES[name]
+    rng = np.random.default_rng(1234)
+    pts = rng.uniform(-1.1, 1.1, size=(60000, 3)).astype(np.float32)
+    tree = oracle.mp5_to_nodes(json.dumps(shape))
+    f_ref = oracle.eval_implicit(tree, pts)
+    g_ref = oracle.eval_gradient(tree, pts)
+    with impli.ImplicitService(shape) as svc:
+        f, g = svc.eval(pts, gradient=True)
+        f2 = svc.eval(pts)
+    assert np.array_equal(f.view(np.uint32), f_ref.view(np.uint32)), np.flatnonzero(f != f_ref)[:10]
+    assert np.array_equal(f2.view(np.uint32), f_ref.view(np.uint32))
+    assert np.array_equal(g.view(np.uint32), g_ref.view(np.uint32)), np.flatnonzero((g != g_ref).any(1))[:10]
+
+
+def test_direct_eval_abi_matches_reference_semantics(impli, oracle):
+    shape = TREES["union_sphere_cube"]
+    pts = np.random.default_rng(5).uniform(-1, 1, size=(1000, 3)).astype(np.float32)
+    tree = oracle.mp5_to_nodes(json.dumps(shape))
+    with impli.ImplicitService(shape) as svc:
+        f = svc.query_implicit_values(pts)
+        n = svc.query_normals(pts, normalize_and_invert=True)
+    assert np.array_equal(f, oracle.eval_implicit(tree, pts))
+    g = oracle.eval_gradient(tree, pts)
+    nrm = np.sqrt(g[:, 0] * g[:, 0] + g[:, 1] * g[:, 1] + g[:, 2] * g[:, 2]).astype(np.float32)
+    fac = np.where(nrm > 0.0001, (-1.0 / nrm.astype(np.float64)).astype(np.float32), np.float32(-42.0))
+    assert np.array_equal(n, (g * fac[:, None]).astype(np.float32))
+
+
+def test_set_x_limit_and_errors(impli):
+    L = impli.lib()
+    assert L.set_object(b'{"type":"iellipsoid","matrix":[1,0,0,0,0,1,0,0,0,0,1,0]}', False) == 1
+    assert L.set_object(b'{"type":"iellipsoid","matrix":[1,0,0,0,0,1,0,0,0,0,1,0]}', False) == 0
+    big = np.zeros((50000, 3), np.float32)
+    assert not L.set_x(big.ctypes.data, 50000)          # mcc2.cpp:770 limit kept
+    assert L.set_x(big.ctypes.data, 49999)
+    L.unset_x()
+    assert not L.unset_object(2)
+    assert L.unset_object(1)
+
+
+def _mc_compare(impli, oracle, shape, mc):
+    v, f = impli.make_geometry(shape, mc)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    assert f.shape == fr.shape and v.shape == vr.shape, (f.shape, fr.shape, v.shape, vr.shape)
+    assert np.array_equal(f, fr)
+    assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), np.abs(v - vr).max()
+    return v, f
+
+
+def test_config1_sphere_mc(impli, oracle):
+    from implisolid_amd import scenes
+    shape, mc = scenes.config1()
+    v, f = _mc_compare(impli, oracle, shape, mc)
+    assert v.shape == (3318, 3) and f.shape == (6632, 3)
+    _, cnt = mesh_edges(f)
+    assert (cnt == 2).all()
+
+
+@pytest.mark.parametrize("R", [32, 64, 128])
+def test_union_sphere_cube_mc(impli, oracle, R):
+    from implisolid_amd import scenes
+    _mc_compare(impli, oracle, scenes.union_sphere_cube(), scenes.mc_settings(R, 1.0))
+
+
+@pytest.mark.parametrize("seed", [20251015, 7, 11, 13])
+def test_random_tree_mc(impli, oracle, seed):
+    from implisolid_amd import scenes
+    _mc_compare(impli, oracle, scenes.random_tree(seed, 10), scenes.mc_settings(48, 1.0))
+
+
+def test_anisotropic_box_mc(impli, oracle):
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(40, 1.0)
+    mc["box"] = {"xmin": -0.7, "xmax": 0.9, "ymin": -1.1, "ymax": 0.6, "zmin": -0.55, "zmax": 0.8}
+    _mc_compare(impli, oracle, scenes.union_sphere_cube(), mc)
+
+
+def test_empty_and_full(impli, oracle):
+    from implisolid_amd import scenes
+    # surface entirely outside the box -> empty mesh; box inside the solid -> sealed shell only
+    far = {"type": "iellipsoid", "matrix": scenes.st(0.25, 3.0, 0, 0)}
+    v, f = _mc_compare(impli, oracle, far, scenes.mc_settings(16, 1.0))
+    assert len(f) == 0 and len(v) == 0
+    big = {"type": "iellipsoid", "matrix": scenes.st(8, 0, 0, 0)}
+    _mc_compare(impli, oracle, big, scenes.mc_settings(16, 1.0))
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 5])
+def test_zslab_split_identical(impli, oracle, nranks):
+    """Z-slab decomposition (one-layer recomputed halo, global offsets) == single GPU."""
+    from implisolid_amd import scenes
+    shape, mc = scenes.union_sphere_cube(), scenes.mc_settings(64, 1.0)
+    ref_v, ref_f = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    slabs = [impli.Slab(shape, mc, r, nranks) for r in range(nranks)]
+    counts = []
+    for s in slabs:
+        s.eval()
+        s.count()
+        counts.append(s.counts()[:2])
+    voff = np.concatenate([[0], np.cumsum([c[0] for c in counts])])
+    foff = np.concatenate([[0], np.cumsum([c[1] for c in counts])])
+    vs, fs = [], []
+    for r, s in enumerate(slabs):
+        s.set_offsets(int(voff[r]), int(foff[r]))
+        s.emit()
+        nv, nf, of = s.counts()
+        assert not of
+        v, f = s.download(nv, nf)
+        vs.append(v)
+        fs.append(f)
+        s.close()
+    v = np.concatenate(vs)
+    f = np.concatenate(fs)
+    assert np.array_equal(f, ref_f)
+    assert np.array_equal(v.view(np.uint32), ref_v.view(np.uint32))
+
+
+def _ob02_compare(impli, oracle, shape, mc, exact=True):
+    v, f = impli.make_geometry(shape, mc)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    assert np.array_equal(f, fr)
+    if exact:
+        bad = np.flatnonzero((v != vr).any(1))
+        assert bad.size == 0, (bad.size, bad[:10], np.abs(v - vr).max())
+    return v, vr
+
+
+def test_ob02_resampling_only(impli, oracle):
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(40, 1.0, vresampl_iters=2, vresampl_c=0.4)
+    _ob02_compare(impli, oracle, scenes.union_sphere_cube(), mc)
+
+
+def test_ob02_projection_no_qem(impli, oracle):
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(40, 1.0, vresampl_iters=1, vresampl_c=0.4, projection=1, qem=0)
+    _ob02_compare(impli, oracle, scenes.union_sphere_cube(), mc)
+    ref_tree = oracle.mp5_to_nodes(json.dumps(scenes.union_sphere_cube()))
+    p = impli.get_pointset("post_p_centroids")
+    assert p is not None and p.shape[1] == 3
+
+
+@pytest.mark.parametrize("R", [32, 48])
+def test_ob02_full_config2_shape(impli, oracle, R):
+    from implisolid_amd import scenes
+    shape, mc = scenes.config2(R)
+    _ob02_compare(impli, oracle, shape, mc)
+
+
+def test_ob02_config3_tree_small(impli, oracle):
+    from implisolid_amd import scenes
+    shape, mc = scenes.config3(40)
+    _ob02_compare(impli, oracle, shape, mc)
