@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: eval + marching cubes (Mvoxels/s) of the config-4 scene on 1..N MI355X.
+
+Workload (BASELINE.json configs[3], the largest single-GPU configuration the metric is quoted on):
+config 3's seeded 21-node MP5 CSG tree at R = 512 over the box [-1, 1]^3.  One step = field
+evaluation of the (R+1)^3 stored samples + marching-cubes count / scan / vertex + face emission,
+with the mesh left resident in HBM (no host copy in the timed region).
+
+N > 1 (torchrun, one process per GPU, RCCL): the cell layers are split into Z-slabs (strong
+scaling, total work fixed).  Each rank recomputes one halo cell layer below its slab; the only
+exchange is an all-gather of the per-slab (vertex, face) counts, which gives every rank its global
+numbering offsets on the device.  The result is byte-identical to one GPU (tests/).
+
+Prints ONE JSON line (rank 0).  Extra fields: per-kernel times from HIP events on the launch
+stream, the HBM roofline of the dominant kernel, a VALU side metric, and the CPU baseline (the
+oracle restatement, single thread, on a bounded sample of the same workload).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3     # vector FP32 peak (same doc)
+
+# algorithmic FP ops per sample for one instruction of the node program
+OP_FLOPS = {"xform": 18, "csg": 2, 3: 9, 4: 45, 5: 24, 6: 20, 7: 24, 8: 14, 9: 12}
+
+
+def program_flops(shape):
+    import implisolid_amd as I
+    n_instr, depth, n_mats, _ = I.program_info(shape)
+    # count leaves / CSG nodes from the JSON (the program has one XFORM per node)
+    def walk(d):
+        t = d["type"]
+        if "children" in d:
+            kids = d["children"]
+            n = len(kids) - 1 if t == "Union" else 1
+            return OP_FLOPS["csg"] * n + OP_FLOPS["xform"] * n + sum(walk(c) for c in (kids if t == "Union" else kids[:2]))
+        code = {"iellipsoid": 3, "ellipsoid": 3, "cube": 4, "icube": 4, "icylinder": 5, "cylinder": 5, "icone": 6,
+                "cone": 6, "iheart": 7, "itorus": 8, "implicit_double_mushroom": 9}[t]
+        return OP_FLOPS["xform"] + OP_FLOPS[code]
+    return walk(shape), n_instr, depth
+
+
+def cpu_baseline(shape, target_s=15.0):
+    """Oracle (CPU restatement, 1 thread) eval + MC of the same tree on a bounded sample."""
+    import oracle
+    oracle.build()
+    tree = oracle.mp5_to_nodes(json.dumps(shape))
+    box = [-1.0, 1.0] * 3
+    R = 48
+    t0 = time.perf_counter()
+    oracle.marching_cubes(tree, R, box)
+    dt = time.perf_counter() - t0
+    # scale the sample so it runs about target_s seconds
+    R = int(max(48, min(384, R * (target_s / max(dt, 1e-3)) ** (1 / 3))))
+    t0 = time.perf_counter()
+    v, f = oracle.marching_cubes(tree, R, box)
+    dt = time.perf_counter() - t0
+    return {"value": R ** 3 / dt / 1e6, "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+            "sample": "oracle restatement (C, 1 thread) eval+MC of the same tree at %d^3 on this host (%.1f s, %d faces)"
+                      % (R, dt, f.shape[0])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--resolution", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--also-256", action="store_true", default=True)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import implisolid_amd as I
+    from implisolid_amd import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def run(R, steps, warmup):
+        shape, mc = scenes.config4(R)
+        slab = I.Slab(shape, mc, rank, world)
+        cnt = torch.zeros(4, dtype=torch.int32, device=dev)
+        gathered = torch.zeros(world, 4, dtype=torch.int32, device=dev)
+        offs = torch.zeros(2, dtype=torch.int32, device=dev)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+
+        def step(e=None):
+            if e: e[0].record(stream)
+            slab.eval(sp)
+            if e: e[1].record(stream)
+            slab.count(sp)
+            if e: e[2].record(stream)
+            if world > 1:
+                slab.copy_counts(cnt.data_ptr(), sp)
+                dist.all_gather_into_tensor(gathered, cnt)
+                v = gathered[:, 0] - gathered[:, 3]
+                f = gathered[:, 1]
+                offs[0] = v[:rank].sum()
+                offs[1] = f[:rank].sum()
+                slab.emit(offs.data_ptr(), sp)
+            else:
+                slab.emit(0, sp)
+            if e: e[3].record(stream)
+
+        # warmup (first call sizes the output buffers)
+        for _ in range(max(1, warmup)):
+            step()
+        nv, nf, grew = slab.counts(sp)
+        if grew:
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(ev[k])
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        nv, nf, of = slab.counts(sp)
+        if of:
+            raise RuntimeError("output overflow in the timed region")
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        tot = torch.tensor([nv, nf], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tot)
+        el = float(t.item())
+        kms = {"eval": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
+               "mc_count_scan": float(np.mean([e[1].elapsed_time(e[2]) for e in ev])),
+               "mc_emit": float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))}
+        info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, shape=shape,
+                    slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth)
+        slab.close()
+        return info
+
+    main_run = run(args.resolution, args.steps, args.warmup)
+    r256 = run(256, args.steps, args.warmup) if (args.also_256 and args.resolution != 256) else None
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    R = main_run["R"]
+    ms = main_run["elapsed"] / args.steps * 1e3
+    value = R ** 3 / (ms * 1e-3) / 1e6
+    flops_per_sample, n_instr, depth = program_flops(main_run["shape"])
+    kms = main_run["kernels_ms"]
+    # rank-0 slab sizes for the per-kernel roofline
+    layers = main_run["slab_layers"]
+    samples = (R + 1) ** 2 * min(R + 1, layers + 1)
+    cells = (R + 2) ** 2 * layers
+    dom = max(kms, key=kms.get)
+    alg_bytes = {"eval": 4.0 * samples,
+                 "mc_count_scan": 4.0 * samples,
+                 "mc_emit": 12.0 * (main_run["nv"] + main_run["nf"]) / max(1, args.gpus)}
+    achieved = alg_bytes[dom] / (kms[dom] * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic_r01.json")
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get(dom)
+        except Exception:
+            traffic = None
+    valu_tflops = flops_per_sample * samples / (kms["eval"] * 1e-3) / 1e12
+    out = {
+        "metric": "Mvoxels/s (eval+MC) at 256^3 & 512^3",
+        "value": round(value, 2),
+        "unit": "Mvoxels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "config4: seeded 21-node MP5 CSG tree (scenes.config4, seed 20251015), box [-1,1]^3, "
+                        "R=%d, eval+MC, mesh resident in HBM" % R,
+            "resolution": R, "voxels": R ** 3, "samples": (R + 1) ** 3, "cells": (R + 2) ** 3,
+            "verts": main_run["nv"], "faces": main_run["nf"], "program_instr": n_instr, "tree_depth": depth,
+            "parallelism": "zslab%d" % world,
+        },
+        "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes[dom]},
+        "valu": {"kernel": "eval", "flops_per_sample": flops_per_sample, "achieved": round(valu_tflops, 2),
+                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(valu_tflops / FP32_PEAK_TFLOPS, 4)},
+    }
+    if r256:
+        ms256 = r256["elapsed"] / args.steps * 1e3
+        out["value_256"] = round(256 ** 3 / (ms256 * 1e-3) / 1e6, 2)
+        out["ms_per_step_256"] = round(ms256, 4)
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(main_run["shape"])
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

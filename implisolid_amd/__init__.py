@@ -27,7 +27,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_create", "implisolid_slab_destroy", "implisolid_slab_eval", "implisolid_slab_count",
     "implisolid_slab_emit", "implisolid_slab_counters", "implisolid_slab_counts", "implisolid_slab_grid",
     "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
-    "implisolid_slab_download",
+    "implisolid_slab_download", "implisolid_slab_copy_counts",
 ]
 
 _lib = None
@@ -83,6 +83,7 @@ def lib():
         "implisolid_slab_field": ([c_void_p], c_void_p),
         "implisolid_slab_set_offsets": ([c_void_p, ctypes.c_uint32, ctypes.c_uint32], c_int),
         "implisolid_slab_download": ([c_void_p, fp, ip, c_void_p], c_int),
+        "implisolid_slab_copy_counts": ([c_void_p, c_void_p, c_void_p], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -243,6 +244,10 @@ class Slab:
         out = (ctypes.c_uint32 * 3)()
         self._rc(lib().implisolid_slab_counts(self.h, ctypes.c_void_p(stream), out))
         return int(out[0]), int(out[1]), bool(out[2])
+
+    def copy_counts(self, d_dst, stream=0):
+        """async: counters [own incl. halo, faces, active, halo] -> device uint32[4] at d_dst"""
+        self._rc(lib().implisolid_slab_copy_counts(self.h, ctypes.c_void_p(d_dst), ctypes.c_void_p(stream)))
 
     def set_offsets(self, voff, foff):
         self._rc(lib().implisolid_slab_set_offsets(self.h, int(voff), int(foff)))

@@ -372,6 +372,10 @@ int implisolid_slab_grid(implisolid_slab* s, int32_t out[8]) {
     std::memcpy(out, v, sizeof v);
     return 0;
 }
+int implisolid_slab_copy_counts(implisolid_slab* s, uint32_t* d_dst, void* stream) {
+    SLAB_TRY(IMPLI_HIP(hipMemcpyAsync(d_dst, s->engine.d_counters() + 2, 4 * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                      (hipStream_t)stream)))
+}
 int implisolid_slab_set_offsets(implisolid_slab* s, uint32_t voff, uint32_t foff) {
     SLAB_TRY(s->engine.set_offsets(voff, foff))
 }

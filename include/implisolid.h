@@ -102,6 +102,9 @@ const uint32_t* implisolid_slab_counters(implisolid_slab* s);
    output buffers when needed (then emit again) */
 int implisolid_slab_counts(implisolid_slab* s, void* stream, uint32_t out[3]);
 int implisolid_slab_grid(implisolid_slab* s, int32_t out[8]);
+/* async device copy of counters[2..5] (owned verts incl. halo, faces, active cells, halo verts)
+   into d_dst (uint32[4]) on `stream` -- for device-side all-gathers */
+int implisolid_slab_copy_counts(implisolid_slab* s, uint32_t* d_dst, void* stream);
 int implisolid_slab_set_offsets(implisolid_slab* s, uint32_t voff, uint32_t foff);
 /* blocking copy of the slab's emitted vertices (3*V floats) and faces (3*F ints, global ids) */
 int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, void* stream);   /* R, res, cz0, cz1, cz_emit, fz0, fz1, depth */
