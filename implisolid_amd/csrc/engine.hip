@@ -57,7 +57,7 @@ void Engine::download(float* verts, int32_t* faces, const SlabCounts& c, hipStre
 }
 
 Engine::~Engine() {
-    DevBuf* all[] = {&offsets_, &prog_, &rabbit_, &cases_, &field_, &unit_cnt_, &active_units_, &counters_, &vid3_,
+    DevBuf* all[] = {&offsets_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
                      &records_, &verts_, &faces_, &overflow_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -79,8 +79,10 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     grid_ = make_grid(R, box, z0 - halo, z1, z0);
     const int64_t nu = n_units(grid_);
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0 + 1) * sizeof(float));
-    unit_cnt_.reserve((size_t)(nu + 1) * 3 * sizeof(uint32_t));
+    unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
     active_units_.reserve((size_t)(nu + 1) * sizeof(uint32_t));
+    scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
+    ci_.reserve((size_t)grid_.n_cells + 64);
     vid3_.reserve((size_t)grid_.n_cells * 3 * sizeof(uint32_t));
     const int64_t m2 = (int64_t)grid_.m * grid_.m;
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
@@ -107,7 +109,9 @@ bool Engine::ensure_capacity(const SlabCounts& c) {
 MCBuffers Engine::buffers() const {
     MCBuffers b{};
     b.field = field_.as<float>();
-    b.unit_cnt = unit_cnt_.as<uint32_t>();
+    b.unit_cnt = unit_cnt_.as<uint4>();
+    b.ci = ci_.as<uint8_t>();
+    b.scan_blk = scan_blk_.as<uint32_t>();
     b.active_units = active_units_.as<uint32_t>();
     b.counters = counters_.as<uint32_t>();
     b.vid3 = vid3_.as<uint32_t>();

@@ -77,7 +77,7 @@ private:
     int depth_ = 1;
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, field_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    DevBuf offsets_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     DevBuf scratch_[16];
 };

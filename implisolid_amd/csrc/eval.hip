@@ -6,6 +6,8 @@
 //                Replaces prepare_grid + eval_shape (marching_cubes.hpp:1662-1725) -- the
 //                reference's res^3 x 12 B point grid and its per-node batch copies never exist.
 // k_eval_points: arbitrary points (direct-eval ABI, mcc2.cpp:815-911) with optional gradient.
+#include <cstdlib>
+
 #include "ifunc_device.hpp"
 #include "kernels.hpp"
 
@@ -47,13 +49,17 @@ __global__ __launch_bounds__(256) void k_eval_points(const Program* __restrict__
     }
 }
 
-#define IMPLI_DEPTH_DISPATCH(depth, KERNEL, ...)                     \
-    do {                                                             \
-        if ((depth) <= 4) KERNEL<4><<<__VA_ARGS__>>>;                \
-        else if ((depth) <= 8) KERNEL<8><<<__VA_ARGS__>>>;           \
-        else if ((depth) <= 12) KERNEL<12><<<__VA_ARGS__>>>;         \
-        else KERNEL<16><<<__VA_ARGS__>>>;                            \
-    } while (0)
+// Stack capacity actually instantiated.  Below 12 slots LLVM lowers the uniform-index stack
+// accesses to v_cndmask select chains (8 compares + 8 selects per access); from 12 slots on it
+// uses VGPR index mode (s_set_gpr_idx_on + one v_mov), measured 1.7x faster on the config-4 tree.
+// IMPLISOLID_EVAL_DEPTH overrides the floor (experiments).
+static int eval_depth(int depth) {
+    static int floor_d = [] {
+        const char* s = std::getenv("IMPLISOLID_EVAL_DEPTH");
+        return s ? std::atoi(s) : 12;
+    }();
+    return depth > floor_d ? depth : floor_d;
+}
 
 void launch_eval_field(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g, float* d_field,
                        hipStream_t s) {
@@ -61,6 +67,7 @@ void launch_eval_field(const Program* d_prog, int depth, const float* d_rabbit, 
     const int layers = g.fz1 - g.fz0;
     if (layers <= 0) return;
     dim3 grid((plane + 255) / 256, layers);
+    depth = eval_depth(depth);
     if (depth <= 4) k_eval_field<4><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
     else if (depth <= 8) k_eval_field<8><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
     else if (depth <= 12) k_eval_field<12><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
@@ -71,6 +78,7 @@ void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit,
                         float* d_f, float* d_grad, hipStream_t s) {
     if (n <= 0) return;
     const unsigned blocks = (unsigned)((n + 255) / 256);
+    depth = eval_depth(depth);
     if (depth <= 4) k_eval_points<4><<<blocks, 256, 0, s>>>(d_prog, d_rabbit, d_xyz, n, d_f, d_grad);
     else if (depth <= 8) k_eval_points<8><<<blocks, 256, 0, s>>>(d_prog, d_rabbit, d_xyz, n, d_f, d_grad);
     else if (depth <= 12) k_eval_points<12><<<blocks, 256, 0, s>>>(d_prog, d_rabbit, d_xyz, n, d_f, d_grad);

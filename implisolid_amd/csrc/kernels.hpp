@@ -45,11 +45,15 @@ void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit,
 
 // MC pipeline
 constexpr int kUnitCells = 1024;       // cells per counting unit (contiguous in linear cell order)
+constexpr int kScanUPT = 8;            // units per lane in the unit scan
+constexpr int kScanBlock = 1024 * kScanUPT;
 struct MCBuffers {
     const float* field;
-    uint32_t* unit_cnt;      // 3 * n_units: own, tri, act (then scanned in place to exclusive bases)
-    uint32_t* active_units;  // n_units
-    uint32_t* counters;      // [0] n_active_units, [1] halo_own, [2..5] totals own/tri/act/halo
+    uint8_t* ci;             // cube index per cell (n_cells)
+    uint4* unit_cnt;         // per unit {own, tri, act, halo own}; scanned in place to exclusive bases
+    uint32_t* scan_blk;      // 8 per scan block: partial sums (5 components), then exclusive bases
+    uint32_t* active_units;  // compacted list of units with work
+    uint32_t* counters;      // [0] n_active_units, [1] halo own, [2..5] totals own/tri/act/halo
     uint32_t* vid3;          // 3 * n_cells
     uint4* records;          // active cells: {L, ci, fbase, 0}
     float* verts;            // 3 * cap_v
@@ -63,5 +67,6 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 
 inline int64_t n_units(const GridDesc& g) { return (g.n_cells + kUnitCells - 1) / kUnitCells; }
+inline int64_t n_scan_blocks(const GridDesc& g) { return (n_units(g) + kScanBlock - 1) / kScanBlock; }
 
 }  // namespace impli

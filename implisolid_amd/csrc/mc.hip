@@ -79,14 +79,20 @@ struct CellVals {
 
 __device__ __forceinline__ unsigned load_cell(const float* __restrict__ field, const GridDesc& g, int cx, int cy, int cz,
                                               CellVals& v) {
-    v.f[0] = corner(field, g, cx, cy, cz);
-    v.f[1] = corner(field, g, cx + 1, cy, cz);
-    v.f[2] = corner(field, g, cx, cy + 1, cz);
-    v.f[3] = corner(field, g, cx + 1, cy + 1, cz);
-    v.f[4] = corner(field, g, cx, cy, cz + 1);
-    v.f[5] = corner(field, g, cx + 1, cy, cz + 1);
-    v.f[6] = corner(field, g, cx, cy + 1, cz + 1);
-    v.f[7] = corner(field, g, cx + 1, cy + 1, cz + 1);
+    // corners with a coordinate in {1, res-2} are sealed (-1e7): cells 1 and res-3 of each axis
+    const bool lo_x = cx >= 2, hi_x = cx + 1 <= g.R + 2, lo_y = cy >= 2, hi_y = cy + 1 <= g.R + 2, lo_z = cz >= 2,
+               hi_z = cz + 1 <= g.R + 2;
+    const int n = g.n, nn = g.n * g.n;
+    const int base = (cx - 2) + (cy - 2) * n + (cz - g.fz0) * nn;   // field is < 2^31 elements
+    const float S = -10000000.0f;
+    v.f[0] = (lo_x && lo_y && lo_z) ? field[base] : S;
+    v.f[1] = (hi_x && lo_y && lo_z) ? field[base + 1] : S;
+    v.f[2] = (lo_x && hi_y && lo_z) ? field[base + n] : S;
+    v.f[3] = (hi_x && hi_y && lo_z) ? field[base + n + 1] : S;
+    v.f[4] = (lo_x && lo_y && hi_z) ? field[base + nn] : S;
+    v.f[5] = (hi_x && lo_y && hi_z) ? field[base + nn + 1] : S;
+    v.f[6] = (lo_x && hi_y && hi_z) ? field[base + nn + n] : S;
+    v.f[7] = (hi_x && hi_y && hi_z) ? field[base + nn + n + 1] : S;
     unsigned ci = 0;   // polygonize_single_cube :553-560
     if (v.f[0] < 0.f) ci |= 1;
     if (v.f[1] < 0.f) ci |= 2;
@@ -147,8 +153,7 @@ __device__ __forceinline__ unsigned f_act(unsigned long long p) { return (unsign
 
 __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ uint8_t s_ntri[256], s_nown[256];
-    __shared__ unsigned long long s_red[4];
-    __shared__ unsigned s_halo[4];
+    __shared__ uint4 s_red[4];
     const int t = threadIdx.x;
     s_ntri[t] = cases[t].ntri;
     s_nown[t] = cases[t].nown;
@@ -163,141 +168,211 @@ __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ c
             cell_coords(g, L, cx, cy, cz);
             CellVals v;
             const unsigned ci = load_cell(b.field, g, cx, cy, cz, v);
+            b.ci[L] = (uint8_t)ci;
             const unsigned no = s_nown[ci], nt = s_ntri[ci];
             own += no;
             if (cz >= g.cz_emit) { tri += nt; act += nt ? 1u : 0u; }
             else halo_own += no;
         }
     }
-    // block reduce
-    unsigned long long p = pack3(own, tri, act);
     const int lane = t & 63, wid = t >> 6;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) p += __shfl_down(p, o, 64);
-    unsigned h = halo_own;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) h += __shfl_down(h, o, 64);
-    if (lane == 0) { s_red[wid] = p; s_halo[wid] = h; }
+    for (int o = 32; o > 0; o >>= 1) {
+        own += __shfl_down(own, o, 64);
+        tri += __shfl_down(tri, o, 64);
+        act += __shfl_down(act, o, 64);
+        halo_own += __shfl_down(halo_own, o, 64);
+    }
+    if (lane == 0) s_red[wid] = make_uint4(own, tri, act, halo_own);
     __syncthreads();
     if (t == 0) {
-        const unsigned long long s = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-        const unsigned hs = s_halo[0] + s_halo[1] + s_halo[2] + s_halo[3];
-        b.unit_cnt[3 * u + 0] = f_own(s);
-        b.unit_cnt[3 * u + 1] = f_tri(s);
-        b.unit_cnt[3 * u + 2] = f_act(s);
-        if (s) b.active_units[atomicAdd(&b.counters[0], 1u)] = u;
-        if (hs) atomicAdd(&b.counters[1], hs);
+        uint4 s = s_red[0];
+        for (int w = 1; w < 4; ++w) { s.x += s_red[w].x; s.y += s_red[w].y; s.z += s_red[w].z; s.w += s_red[w].w; }
+        b.unit_cnt[u] = s;
     }
 }
 
-// exclusive scan of unit_cnt (3 components) in place, one workgroup of 1024 lanes
-// (unit sums fit 20-bit packed fields, slab totals do not: three separate 32-bit scans here)
-__global__ __launch_bounds__(1024) void k_mc_scan(uint32_t* __restrict__ cnt, int64_t nu, uint32_t* __restrict__ counters) {
-    __shared__ uint32_t s_w[3][16];
+// ---- unit scan: partial sums per scan block, top-level scan, apply + compaction of active units ----
+struct Cnt5 { uint32_t c[5]; };
+__device__ __forceinline__ Cnt5 unit_c5(uint4 v) {
+    Cnt5 r;
+    r.c[0] = v.x; r.c[1] = v.y; r.c[2] = v.z; r.c[3] = v.w; r.c[4] = (v.x | v.y) ? 1u : 0u;
+    return r;
+}
+
+// inclusive block scan (1024 lanes) of 5 components; returns exclusive, fills total
+__device__ __forceinline__ Cnt5 block_scan5(Cnt5 v, Cnt5& total, uint32_t (*s_w)[16]) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int64_t chunk = (nu + 1023) / 1024;
-    const int64_t a = t * chunk, e = (a + chunk < nu) ? a + chunk : nu;
-    uint32_t sum[3] = {0, 0, 0};
-    for (int64_t i = a; i < e; ++i)
-        for (int c = 0; c < 3; ++c) sum[c] += cnt[3 * i + c];
-    uint32_t run[3], tot[3];
-    for (int c = 0; c < 3; ++c) {
-        const uint32_t incl = wave_incl_scan<uint32_t>(sum[c], lane);
-        if (lane == 63) s_w[c][wid] = incl;
-        run[c] = incl - sum[c];
+    Cnt5 incl;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        incl.c[c] = wave_incl_scan<uint32_t>(v.c[c], lane);
+        if (lane == 63) s_w[c][wid] = incl.c[c];
     }
     __syncthreads();
-    for (int c = 0; c < 3; ++c) {
+    Cnt5 ex;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
         uint32_t pre = 0, tt = 0;
         for (int w = 0; w < 16; ++w) {
-            if (w < wid) pre += s_w[c][w];
-            tt += s_w[c][w];
+            const uint32_t x = s_w[c][w];
+            if (w < wid) pre += x;
+            tt += x;
         }
-        run[c] += pre;
-        tot[c] = tt;
+        ex.c[c] = pre + incl.c[c] - v.c[c];
+        total.c[c] = tt;
     }
-    for (int64_t i = a; i < e; ++i)
-        for (int c = 0; c < 3; ++c) {
-            const uint32_t v = cnt[3 * i + c];
-            cnt[3 * i + c] = run[c];
-            run[c] += v;
+    __syncthreads();
+    return ex;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_partial(const uint4* __restrict__ cnt, int64_t nu, uint32_t* __restrict__ blk) {
+    __shared__ uint32_t s_w[5][16];
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanUPT;
+    Cnt5 sum = {{0, 0, 0, 0, 0}};
+    for (int i = 0; i < kScanUPT; ++i)
+        if (base + i < nu) {
+            const Cnt5 c = unit_c5(cnt[base + i]);
+            for (int k = 0; k < 5; ++k) sum.c[k] += c.c[k];
         }
-    if (t == 0) {
-        counters[2] = tot[0];
-        counters[3] = tot[1];
-        counters[4] = tot[2];
-        counters[5] = counters[1];
+    Cnt5 tot;
+    (void)block_scan5(sum, tot, s_w);
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 5; ++k) blk[8 * blockIdx.x + k] = tot.c[k];
+}
+
+__global__ __launch_bounds__(64) void k_scan_top(uint32_t* __restrict__ blk, int nb, uint32_t* __restrict__ counters) {
+    if (threadIdx.x != 0) return;
+    uint32_t run[5] = {0, 0, 0, 0, 0};
+    for (int b = 0; b < nb; ++b)
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t v = blk[8 * b + k];
+            blk[8 * b + k] = run[k];
+            run[k] += v;
+        }
+    counters[0] = run[4];
+    counters[1] = run[3];
+    counters[2] = run[0];
+    counters[3] = run[1];
+    counters[4] = run[2];
+    counters[5] = run[3];
+}
+
+__global__ __launch_bounds__(1024) void k_scan_apply(uint4* __restrict__ cnt, int64_t nu, const uint32_t* __restrict__ blk,
+                                                     uint32_t* __restrict__ active) {
+    __shared__ uint32_t s_w[5][16];
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanUPT;
+    uint4 v[kScanUPT];
+    Cnt5 sum = {{0, 0, 0, 0, 0}};
+    for (int i = 0; i < kScanUPT; ++i) {
+        v[i] = (base + i < nu) ? cnt[base + i] : make_uint4(0, 0, 0, 0);
+        const Cnt5 c = unit_c5(v[i]);
+        for (int k = 0; k < 5; ++k) sum.c[k] += c.c[k];
+    }
+    Cnt5 tot;
+    Cnt5 run = block_scan5(sum, tot, s_w);
+    for (int k = 0; k < 5; ++k) run.c[k] += blk[8 * blockIdx.x + k];
+    for (int i = 0; i < kScanUPT; ++i) {
+        if (base + i >= nu) break;
+        const Cnt5 c = unit_c5(v[i]);
+        cnt[base + i] = make_uint4(run.c[0], run.c[1], run.c[2], run.c[3]);
+        if (c.c[4]) active[run.c[4]] = (uint32_t)(base + i);
+        for (int k = 0; k < 5; ++k) run.c[k] += c.c[k];
     }
 }
 
+// K3: one wave per active unit; lane l owns 16 consecutive cells (one 16-byte load of cube indices)
 __global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ CaseInfo s_case[256];
-    __shared__ unsigned long long s_scan[4];
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     s_case[t] = cases[t];
     __syncthreads();
     const uint32_t n_active = b.counters[0];
     const uint32_t H = b.counters[1];
     const uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
-    for (uint32_t a = blockIdx.x; a < n_active; a += gridDim.x) {
+    constexpr int CPL = kUnitCells / 64;   // 16 cells per lane
+    for (uint32_t a = blockIdx.x * 4 + wid; a < n_active; a += gridDim.x * 4) {
         const uint32_t u = b.active_units[a];
-        const uint32_t vb = b.unit_cnt[3 * u], fb = b.unit_cnt[3 * u + 1], ab = b.unit_cnt[3 * u + 2];
-        unsigned long long run = 0;
-        for (int k = 0; k < kUnitCells / 256; ++k) {
-            const uint32_t L = u * kUnitCells + k * 256 + t;
-            const bool valid = L < (uint64_t)g.n_cells;
-            int cx = 0, cy = 0, cz = 0;
-            unsigned ci = 0;
-            CellVals v;
-            if (valid) {
-                cell_coords(g, L, cx, cy, cz);
-                ci = load_cell(b.field, g, cx, cy, cz, v);
+        const uint4 base = b.unit_cnt[u];   // exclusive {vbase, fbase, abase, hbase}
+        const uint32_t L0 = u * kUnitCells + lane * CPL;
+        uint8_t cis[CPL];
+        if (L0 + CPL <= (uint64_t)g.n_cells) {
+            const uint4 q = *reinterpret_cast<const uint4*>(b.ci + L0);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) cis[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        } else {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) cis[k] = (L0 + k < (uint64_t)g.n_cells) ? b.ci[L0 + k] : 0;
+        }
+        // lane-local sums (halo cells own vertices but emit nothing)
+        int cx, cy, cz;
+        cell_coords(g, L0 < (uint64_t)g.n_cells ? L0 : 0u, cx, cy, cz);
+        const int czs = cz, cys = cy, cxs = cx;
+        unsigned own = 0, tri = 0, act = 0;
+        {
+            int x = cxs, y = cys, z = czs;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const CaseInfo& C = s_case[cis[k]];
+                own += C.nown;
+                if (z >= g.cz_emit) { tri += C.ntri; act += C.ntri ? 1u : 0u; }
+                if (++x > g.m) { x = 1; if (++y > g.m) { y = 1; ++z; } }
             }
+        }
+        const unsigned long long p = pack3(own, tri, act);
+        const unsigned long long incl = wave_incl_scan<unsigned long long>(p, lane);
+        unsigned long long pre = incl - p;
+        uint32_t vrun = base.x + f_own(pre), frun = base.y + f_tri(pre), arun = base.z + f_act(pre);
+        int x = cxs, y = cys, z = czs;
+        for (int k = 0; k < CPL; ++k) {
+            const uint32_t L = L0 + k;
+            const unsigned ci = cis[k];
             const CaseInfo& C = s_case[ci];
-            const bool emit = valid && cz >= g.cz_emit;
-            const unsigned own = valid ? C.nown : 0u;
-            const unsigned tri = emit ? C.ntri : 0u;
-            const unsigned act = (emit && C.ntri) ? 1u : 0u;
-            unsigned long long tot;
-            const unsigned long long pre = run + block_excl_scan(pack3(own, tri, act), tot, s_scan);
-            run += tot;
-            if (own) {
-                const uint32_t vloc = vb + f_own(pre);   // slab-local id, halo vertices first
-                // render_geometry :1044-1053 and the owner's VIntX/Y/Z (:400-495)
-                const float fx = ((float)cx + g.i0[0]) * g.w[0];
-                const float fy = ((float)cy + g.i0[1]) * g.w[1];
-                const float fz = ((float)cz + g.i0[2]) * g.w[2];
+            const bool valid = L < (uint64_t)g.n_cells;
+            const bool emit = valid && z >= g.cz_emit;
+            if (valid && C.nown) {
+                const float fx = ((float)x + g.i0[0]) * g.w[0];
+                const float fy = ((float)y + g.i0[1]) * g.w[1];
+                const float fz = ((float)z + g.i0[2]) * g.w[2];
                 const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
+                const float f7 = corner(b.field, g, x + 1, y + 1, z + 1);
 #pragma unroll
                 for (int slot = 0; slot < 3; ++slot) {
                     const int r = C.rank[slot];
                     if (r < 0) continue;
-                    const uint32_t vid = vloc + (uint32_t)r;
+                    const uint32_t vid = vrun + (uint32_t)r;
                     b.vid3[(size_t)L * 3 + slot] = Voff + vid - H;
                     if (!emit) continue;
                     const uint32_t out = vid - H;
                     if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
                     float px, py, pz;
                     if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
-                        const float mu = (0.f - v.f[5]) / (v.f[7] - v.f[5]);
+                        const float f5 = corner(b.field, g, x + 1, y, z + 1);
+                        const float mu = (0.f - f5) / (f7 - f5);
                         px = fx2; py = fy + mu * g.w[1]; pz = fz2;
                     } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
-                        const float mu = (0.f - v.f[6]) / (v.f[7] - v.f[6]);
+                        const float f6 = corner(b.field, g, x, y + 1, z + 1);
+                        const float mu = (0.f - f6) / (f7 - f6);
                         px = fx + mu * g.w[0]; py = fy2; pz = fz2;
                     } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
-                        const float mu = (0.f - v.f[3]) / (v.f[7] - v.f[3]);
+                        const float f3 = corner(b.field, g, x + 1, y + 1, z);
+                        const float mu = (0.f - f3) / (f7 - f3);
                         px = fx2; py = fy2; pz = fz + mu * g.w[2];
                     }
                     b.verts[3 * (size_t)out] = px;
                     b.verts[3 * (size_t)out + 1] = py;
                     b.verts[3 * (size_t)out + 2] = pz;
                 }
+                vrun += C.nown;
             }
-            if (act) {
-                const uint32_t ri = ab + f_act(pre);
-                if (ri < (uint64_t)b.cap_rec) b.records[ri] = make_uint4(L, ci, fb + f_tri(pre), 0u);
+            if (emit && C.ntri) {
+                if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun, 0u);
                 else *b.overflow = 1u;
+                ++arun;
+                frun += C.ntri;
             }
+            if (++x > g.m) { x = 1; if (++y > g.m) { y = 1; ++z; } }
         }
     }
 }
@@ -345,11 +420,14 @@ void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
 }
 
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
-    k_mc_scan<<<1, 1024, 0, s>>>(b.unit_cnt, n_units(g), b.counters);
+    const int64_t nu = n_units(g), nb = n_scan_blocks(g);
+    if (nb > 0) k_scan_partial<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk);
+    k_scan_top<<<1, 64, 0, s>>>(b.scan_blk, (int)nb, b.counters);
+    if (nb > 0) k_scan_apply<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk, b.active_units);
 }
 
 void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
-    k_mc_verts<<<2048, 256, 0, s>>>(d_cases, g, b);
+    k_mc_verts<<<1024, 256, 0, s>>>(d_cases, g, b);
     k_mc_faces<<<2048, 256, 0, s>>>(d_cases, g, b);
 }
 
