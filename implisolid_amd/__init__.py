@@ -27,7 +27,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_create", "implisolid_slab_destroy", "implisolid_slab_eval", "implisolid_slab_count",
     "implisolid_slab_emit", "implisolid_slab_counters", "implisolid_slab_counts", "implisolid_slab_grid",
     "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
-    "implisolid_slab_download", "implisolid_slab_copy_counts",
+    "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
 ]
 
 _lib = None
@@ -84,6 +84,8 @@ def lib():
         "implisolid_slab_set_offsets": ([c_void_p, ctypes.c_uint32, ctypes.c_uint32], c_int),
         "implisolid_slab_download": ([c_void_p, fp, ip, c_void_p], c_int),
         "implisolid_slab_copy_counts": ([c_void_p, c_void_p, c_void_p], c_int),
+        "implisolid_slab_read_field": ([c_void_p, fp, ctypes.c_int64], ctypes.c_int64),
+        "implisolid_set_pruning": ([c_int], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -104,6 +106,11 @@ def _check():
     err = lib().implisolid_last_error()
     if err:
         raise ImplisolidError(err.decode(errors="replace"))
+
+
+def set_pruning(on):
+    """Per-brick interval pruning of the field evaluation (default on; bit-identical results)."""
+    lib().implisolid_set_pruning(1 if on else 0)
 
 
 def last_error():
@@ -281,6 +288,17 @@ class Slab:
 
     def field_ptr(self):
         return lib().implisolid_slab_field(self.h)
+
+    def read_field(self):
+        """Blocking host copy of the stored field samples, shape (layers, n, n)."""
+        L = lib()
+        n = L.implisolid_slab_read_field(self.h, None, 0)
+        _check()
+        out = np.empty(n, np.float32)
+        L.implisolid_slab_read_field(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n)
+        _check()
+        n_side = self.R + 1
+        return out.reshape(-1, n_side, n_side)
 
     def close(self):
         if self.h:

@@ -95,6 +95,8 @@ extern "C" {
 const char* implisolid_last_error(void) { return g_last_error.c_str(); }
 void implisolid_set_error_mode(int mode) { g_error_mode = mode; }
 
+void implisolid_set_pruning(int on) { impli::Engine::set_pruning(on); }
+
 void build_geometry(const char* shape_json, const char* mc_json) {
     g_last_error.clear();
     MCSettings st;
@@ -394,5 +396,21 @@ int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, v
 float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
 int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
 float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
+
+int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capacity) {
+    try {
+        const GridDesc& g = s->engine.grid();
+        const int64_t n = (int64_t)g.n * g.n * (int64_t)(g.fz1 - g.fz0);
+        if (out) {
+            if (capacity < n) throw InputError("implisolid_slab_read_field: buffer too small");
+            IMPLI_HIP(hipDeviceSynchronize());
+            IMPLI_HIP(hipMemcpy(out, s->engine.d_field(), (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+        }
+        return n;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+}
 
 }  // extern "C"

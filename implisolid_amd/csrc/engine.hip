@@ -1,7 +1,9 @@
 // engine.hip -- buffer management and stage sequencing for the MI355X polygoniser.
 #include "engine.hpp"
 
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "ifunc_device.hpp"
@@ -25,6 +27,19 @@ void DevBuf::release() {
     bytes = 0;
 }
 
+static std::atomic<int> g_pruning{-1};
+
+void Engine::set_pruning(int on) { g_pruning.store(on ? 1 : 0); }
+bool Engine::pruning() {
+    int v = g_pruning.load();
+    if (v < 0) {
+        const char* e = std::getenv("IMPLISOLID_PRUNE");
+        v = (e && e[0] == '0') ? 0 : 1;
+        g_pruning.store(v);
+    }
+    return v != 0;
+}
+
 Engine::Engine() {
     // rabbit table + the object's trailing members (F8d: out-of-table reads) + zero padding
     std::vector<float> tab(dev::kRabbitPadded, 0.f);
@@ -32,6 +47,11 @@ Engine::Engine() {
     const uint32_t tail[4] = {IMPLI_RABBIT_GRID_SIZE_BITS, IMPLI_RABBIT_ORIGIN_X_BITS, IMPLI_RABBIT_ORIGIN_Y_BITS,
                               IMPLI_RABBIT_ORIGIN_Z_BITS};
     std::memcpy(&tab[dev::kRabbitN], tail, sizeof tail);
+    tab_range_ = float2{tab[0], tab[0]};
+    for (float v : tab) {
+        tab_range_.x = v < tab_range_.x ? v : tab_range_.x;
+        tab_range_.y = v > tab_range_.y ? v : tab_range_.y;
+    }
     rabbit_.reserve(tab.size() * sizeof(float));
     IMPLI_HIP(hipMemcpy(rabbit_.p, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
     CaseInfo cases[256];
@@ -57,7 +77,7 @@ void Engine::download(float* verts, int32_t* faces, const SlabCounts& c, hipStre
 }
 
 Engine::~Engine() {
-    DevBuf* all[] = {&offsets_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
+    DevBuf* all[] = {&offsets_, &modes_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
                      &records_, &verts_, &faces_, &overflow_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -66,6 +86,7 @@ Engine::~Engine() {
 void Engine::set_object(const Program& prog) {
     IMPLI_HIP(hipMemcpy(prog_.p, &prog, sizeof(Program), hipMemcpyHostToDevice));
     depth_ = prog.max_depth;
+    n_csg_ = prog.n_csg;
     have_object_ = true;
 }
 
@@ -78,6 +99,7 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     const int halo = (rank > 0) ? 1 : 0;   // one cell layer recomputed below the slab (owner rule)
     grid_ = make_grid(R, box, z0 - halo, z1, z0);
     const int64_t nu = n_units(grid_);
+    modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0 + 1) * sizeof(float));
     unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
     active_units_.reserve((size_t)(nu + 1) * sizeof(uint32_t));
@@ -128,7 +150,11 @@ MCBuffers Engine::buffers() const {
 
 void Engine::eval_field(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
-    launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
+    if (n_csg_ > 0 && pruning())
+        launch_eval_field_pruned(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_,
+                                 modes_.as<uint64_t>(), field_.as<float>(), s);
+    else
+        launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
     IMPLI_HIP(hipGetLastError());
 }
 

@@ -70,14 +70,21 @@ public:
 
     DevBuf& scratch(int k) { return scratch_[k]; }
 
+    // per-brick interval pruning of the field evaluation (process-wide switch, default on;
+    // IMPLISOLID_PRUNE=0 or implisolid_set_pruning(0) turns it off)
+    static void set_pruning(int on);
+    static bool pruning();
+
 private:
     MCBuffers buffers() const;
 
     GridDesc grid_{};
     int depth_ = 1;
+    int n_csg_ = 0;
+    float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    DevBuf offsets_, modes_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     DevBuf scratch_[16];
 };

@@ -5,10 +5,16 @@
 //                program and matrices), the result is written once, coalesced, x fastest.
 //                Replaces prepare_grid + eval_shape (marching_cubes.hpp:1662-1725) -- the
 //                reference's res^3 x 12 B point grid and its per-node batch copies never exist.
+// k_brick_modes / k_eval_field_pruned: the same field, computed per brick of kBX x kBY x kBZ
+//                samples.  A first pass bounds every node of the program over each brick
+//                (ifunc_interval.hpp) and records which CSG operands provably win; the second
+//                pass (one wave per brick) skips the losing subtrees.  Bit-identical to
+//                k_eval_field (tests/test_gpu_parity.py::test_pruned_field_identical).
 // k_eval_points: arbitrary points (direct-eval ABI, mcc2.cpp:815-911) with optional gradient.
 #include <cstdlib>
 
 #include "ifunc_device.hpp"
+#include "ifunc_interval.hpp"
 #include "kernels.hpp"
 
 namespace impli {
@@ -30,6 +36,70 @@ __global__ __launch_bounds__(256) void k_eval_field(const Program* __restrict__ 
     const float z = ((float)sz * g.w[2] + g.lo[2]) - 2.f * g.w[2];
     const float f = eval_f<D>(prog, tab, x, y, z);
     field[(size_t)blockIdx.y * plane + i] = 0.f + f;   // eval_shape: field (zero) += value
+}
+
+__device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, int& by, int& bz) {
+    bx = b % bg.nbx;
+    const int t = b / bg.nbx;
+    by = t % bg.nby;
+    bz = t / bg.nby;
+}
+
+// sample coordinate of stored index s along an axis (prepare_grid, marching_cubes.hpp:1691-1693)
+__device__ __forceinline__ float sample_xy(const GridDesc& g, int axis, int s) {
+    return ((float)(s + 2) * g.w[axis] + g.lo[axis]) - 2.f * g.w[axis];
+}
+__device__ __forceinline__ float sample_z(const GridDesc& g, int layer) {
+    return ((float)(g.fz0 + layer) * g.w[2] + g.lo[2]) - 2.f * g.w[2];
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_brick_modes(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                     float2 tab_range, GridDesc g, BrickGrid bg,
+                                                     uint64_t* __restrict__ modes) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= bg.n_bricks) return;
+    int bx, by, bz;
+    brick_of(b, bg, bx, by, bz);
+    const int layers = g.fz1 - g.fz0;
+    const int x0 = bx * kBX, x1 = min(x0 + kBX - 1, g.n - 1);
+    const int y0 = by * kBY, y1 = min(y0 + kBY - 1, g.n - 1);
+    const int z0 = bz * kBZ, z1 = min(z0 + kBZ - 1, layers - 1);
+    // the sample coordinate is monotone in the index, so the end samples bound the brick
+    Box p{Iv{sample_xy(g, 0, x0), sample_xy(g, 0, x1)}, Iv{sample_xy(g, 1, y0), sample_xy(g, 1, y1)},
+          Iv{sample_z(g, z0), sample_z(g, z1)}};
+    uint64_t m;
+    (void)eval_iv<D>(prog, tab, tab_range, p, m);
+    modes[b] = m;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __restrict__ prog,
+                                                           const float* __restrict__ tab, GridDesc g, BrickGrid bg,
+                                                           const uint64_t* __restrict__ modes,
+                                                           float* __restrict__ field) {
+    const int b = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (b >= bg.n_bricks) return;
+    const int lane = threadIdx.x & 63;
+    int bx, by, bz;
+    brick_of(b, bg, bx, by, bz);
+    const uint64_t m64 = modes[b];
+    const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
+                       (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
+    const int n = g.n;
+    const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
+    const bool ok = sx < n && sy < n;
+    const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
+    const int layers = g.fz1 - g.fz0;
+    const size_t plane = (size_t)n * n;
+    float* out = field + (size_t)sy * n + sx;
+#pragma unroll 1
+    for (int k = 0; k < kBZ; ++k) {
+        const int layer = bz * kBZ + k;
+        if (layer >= layers) break;
+        const float f = eval_f_pruned<D>(prog, tab, m, x, y, sample_z(g, layer));
+        if (ok) out[(size_t)layer * plane] = 0.f + f;
+    }
 }
 
 template <int D>
@@ -72,6 +142,34 @@ void launch_eval_field(const Program* d_prog, int depth, const float* d_rabbit, 
     else if (depth <= 8) k_eval_field<8><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
     else if (depth <= 12) k_eval_field<12><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
     else k_eval_field<16><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
+}
+
+BrickGrid brick_grid(const GridDesc& g) {
+    BrickGrid bg;
+    bg.nbx = (g.n + kBX - 1) / kBX;
+    bg.nby = (g.n + kBY - 1) / kBY;
+    bg.nbz = (g.fz1 - g.fz0 + kBZ - 1) / kBZ;
+    if (bg.nbz < 0) bg.nbz = 0;
+    bg.n_bricks = bg.nbx * bg.nby * bg.nbz;
+    return bg;
+}
+
+void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range,
+                              const GridDesc& g, uint64_t* d_modes, float* d_field, hipStream_t s) {
+    const BrickGrid bg = brick_grid(g);
+    if (bg.n_bricks <= 0) return;
+    depth = eval_depth(depth);
+    const unsigned tb = (unsigned)((bg.n_bricks + 255) / 256), eb = (unsigned)((bg.n_bricks + 3) / 4);
+#define IMPLI_PRUNED(DD)                                                                             \
+    do {                                                                                             \
+        k_brick_modes<DD><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes);           \
+        k_eval_field_pruned<DD><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_field);      \
+    } while (0)
+    if (depth <= 4) IMPLI_PRUNED(4);
+    else if (depth <= 8) IMPLI_PRUNED(8);
+    else if (depth <= 12) IMPLI_PRUNED(12);
+    else IMPLI_PRUNED(16);
+#undef IMPLI_PRUNED
 }
 
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,

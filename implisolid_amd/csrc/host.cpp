@@ -133,9 +133,10 @@ struct Builder {
         std::memcpy(p.mats[p.n_mats], inv, sizeof inv);
         return p.n_mats++;
     }
-    void emit(OpCode op, int32_t type, int32_t mat) {
+    int emit(OpCode op, int32_t type, int32_t mat, int32_t csg = -1) {
         if (p.n_instr >= kMaxProgram) throw InputError("MP5 tree too large");
-        p.instr[p.n_instr++] = Instr{op, type, mat, 0};
+        p.instr[p.n_instr] = Instr{(int16_t)op, (int16_t)type, (int16_t)mat, (int16_t)csg, -1, -1, -1, 0};
+        return p.n_instr++;
     }
 
     static void matrix12(const Json& d, float m[12]) {   // getMatrix12 object_factory.hpp:21-30
@@ -160,16 +161,27 @@ struct Builder {
     void push_point() { if (++depth > max_depth) max_depth = depth; if (depth >= kMaxDepth) throw InputError("MP5 tree too deep"); }
     void pop_point() { --depth; }
 
-    // node = XFORM(m); child a; child b; CSG(t)
+    // node = XFORM(m); child a; child b; CSG(t).  Each operand subtree starts with its own XFORM,
+    // which records where the subtree ends so a pruned operand can be skipped in one jump.
     template <class A, class B>
     void csg(NodeType t, const float m[12], A&& a, B&& b) {
         const int k = add_matrix(m);
+        const int id = p.n_csg++;
         emit(OP_XFORM, t, k);
         push_point();
+        const int a0 = p.n_instr;
         a();
+        mark_operand(a0, id, 0);
+        const int b0 = p.n_instr;
         b();
-        emit(OP_CSG, t, k);
+        mark_operand(b0, id, 1);
+        emit(OP_CSG, t, k, id);
         pop_point();
+    }
+    void mark_operand(int start, int csg_id, int child) {
+        p.instr[start].skip_csg = (int16_t)csg_id;
+        p.instr[start].skip_child = (int16_t)child;
+        p.instr[start].skip_to = (int16_t)p.n_instr;
     }
 
     void node(const Json& d, bool ignore) {

@@ -40,11 +40,20 @@ enum OpCode : int32_t {
 };
 
 struct Instr {
-    int32_t op;    // OpCode
-    int32_t type;  // PRIM/CSG: NodeType
-    int32_t mat;   // index of the node's inverse matrix (XFORM: the one to apply)
-    int32_t pad;
+    int16_t op;          // OpCode
+    int16_t type;        // PRIM/CSG: NodeType
+    int16_t mat;         // index of the node's inverse matrix (XFORM: the one to apply)
+    int16_t csg;         // OP_CSG: index of this CSG node (pruning modes), else -1
+    int16_t skip_csg;    // XFORM that starts a CSG operand: that CSG node's index, else -1
+    int16_t skip_child;  // ... operand 0 or 1
+    int16_t skip_to;     // ... first instruction after the operand's subtree
+    int16_t pad;
 };
+static_assert(sizeof(Instr) == 16, "Instr layout");
+
+// Per-brick pruning: 2 bits per CSG node (index < kMaxPruned): both operands, left only, right only.
+enum PruneMode : uint32_t { PM_BOTH = 0, PM_LEFT = 1, PM_RIGHT = 2 };
+constexpr int kMaxPruned = 32;
 
 constexpr int kMaxProgram = 256;   // instructions
 constexpr int kMaxDepth = 16;      // point/value stack depth (tree depth + 1)
@@ -55,7 +64,7 @@ struct Program {
     int32_t n_instr;
     int32_t max_depth;
     int32_t n_mats;
-    int32_t pad;
+    int32_t n_csg;
     Instr instr[kMaxProgram];
     float mats[kMaxProgram][12];
 };

@@ -78,6 +78,10 @@ const char* implisolid_last_error(void);
 /* 0 (default): abort() where the reference aborts (bad settings, unknown MP5 type);
    1: print the same message, record it in implisolid_last_error() and return */
 void implisolid_set_error_mode(int mode);
+
+/* Additive: per-brick interval pruning of CSG operands during field evaluation (default on;
+ * environment IMPLISOLID_PRUNE=0 also disables).  Results are bit-identical either way. */
+void implisolid_set_pruning(int on);
 /* evaluate n >= 0 points (no 50k limit) of the current set_object(); grad may be NULL */
 int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* grad_out);
 
@@ -111,6 +115,9 @@ int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, v
 float* implisolid_slab_verts(implisolid_slab* s);     /* device pointers */
 int32_t* implisolid_slab_faces(implisolid_slab* s);
 float* implisolid_slab_field(implisolid_slab* s);
+/* blocking copy of the slab's stored field samples (n*n*layers floats, x fastest); with out ==
+ * NULL returns the sample count only */
+int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capacity);
 
 #ifdef __cplusplus
 }

@@ -188,3 +188,38 @@ def test_ob02_config3_tree_small(impli, oracle):
     from implisolid_amd import scenes
     shape, mc = scenes.config3(40)
     _ob02_compare(impli, oracle, shape, mc)
+
+
+def _field(impli, shape, mc, prune):
+    impli.set_pruning(prune)
+    try:
+        s = impli.Slab(shape, mc)
+        s.eval()
+        f = s.read_field()
+        s.close()
+    finally:
+        impli.set_pruning(True)
+    return f
+
+
+@pytest.mark.parametrize("name", sorted(TREES))
+def test_pruned_field_identical(impli, name):
+    """Per-brick interval pruning must not change a single bit of the field."""
+    from implisolid_amd import scenes
+    for R, box in [(64, None), (37, {"xmin": -0.7, "xmax": 0.9, "ymin": -1.1, "ymax": 0.6, "zmin": -0.55, "zmax": 0.8})]:
+        mc = scenes.mc_settings(R, 1.0)
+        if box:
+            mc["box"] = box
+        a = _field(impli, TREES[name], mc, True)
+        b = _field(impli, TREES[name], mc, False)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
+
+
+@pytest.mark.parametrize("seed", list(range(100, 124)))
+def test_pruned_field_random_trees(impli, seed):
+    from implisolid_amd import scenes
+    shape = scenes.random_tree(seed, 3 + seed % 10)
+    mc = scenes.mc_settings(48, 1.0)
+    a = _field(impli, shape, mc, True)
+    b = _field(impli, shape, mc, False)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
