@@ -82,6 +82,7 @@ def main():
     import torch
     import torch.distributed as dist
     import implisolid_amd as I
+    from implisolid_amd import distributed as D
     from implisolid_amd import scenes
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,7 +101,6 @@ def main():
         shape, mc = scenes.config4(R)
         slab = I.Slab(shape, mc, rank, world)
         cnt = torch.zeros(4, dtype=torch.int32, device=dev)
-        gathered = torch.zeros(world, 4, dtype=torch.int32, device=dev)
         offs = torch.zeros(2, dtype=torch.int32, device=dev)
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
 
@@ -112,11 +112,7 @@ def main():
             if e: e[2].record(stream)
             if world > 1:
                 slab.copy_counts(cnt.data_ptr(), sp)
-                dist.all_gather_into_tensor(gathered, cnt)
-                v = gathered[:, 0] - gathered[:, 3]
-                f = gathered[:, 1]
-                offs[0] = v[:rank].sum()
-                offs[1] = f[:rank].sum()
+                D.global_offsets(cnt, rank, world, out=offs)
                 slab.emit(offs.data_ptr(), sp)
             else:
                 slab.emit(0, sp)

@@ -28,6 +28,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_emit", "implisolid_slab_counters", "implisolid_slab_counts", "implisolid_slab_grid",
     "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
     "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
+    "implisolid_parse_settings", "implisolid_slab_partition",
 ]
 
 _lib = None
@@ -86,6 +87,8 @@ def lib():
         "implisolid_slab_copy_counts": ([c_void_p, c_void_p, c_void_p], c_int),
         "implisolid_slab_read_field": ([c_void_p, fp, ctypes.c_int64], ctypes.c_int64),
         "implisolid_set_pruning": ([c_int], None),
+        "implisolid_parse_settings": ([c_char_p, fp, ip, fp], c_int),
+        "implisolid_slab_partition": ([c_int, c_int, c_int, ip], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -106,6 +109,30 @@ def _check():
     err = lib().implisolid_last_error()
     if err:
         raise ImplisolidError(err.decode(errors="replace"))
+
+
+def parse_settings(mc_settings):
+    """Host-side mc-settings parse (no GPU): dict of the parsed values; raises on invalid input."""
+    L = lib()
+    box = (ctypes.c_float * 6)()
+    ints = (ctypes.c_int32 * 7)()
+    fl = (ctypes.c_float * 2)()
+    if L.implisolid_parse_settings(_s(mc_settings), box, ints, fl) != 0:
+        raise ImplisolidError(last_error())
+    keys = ["resolution", "ignore_root_matrix", "overall_repeats", "vresampl_iters", "projection", "qem", "subdiv"]
+    out = {k: int(v) for k, v in zip(keys, ints)}
+    out["box"] = [np.float32(b) for b in box]
+    out["vresampl_c"] = np.float32(fl[0])
+    out["post_subdiv_noise"] = np.float32(fl[1])
+    return out
+
+
+def slab_partition(R, rank, nranks):
+    """(z0, z1, halo): the cell layers a rank owns in the Z-slab decomposition."""
+    out = (ctypes.c_int32 * 3)()
+    if lib().implisolid_slab_partition(int(R), int(rank), int(nranks), out) != 0:
+        raise ImplisolidError(last_error())
+    return int(out[0]), int(out[1]), int(out[2])
 
 
 def set_pruning(on):

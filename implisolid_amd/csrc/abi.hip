@@ -97,6 +97,41 @@ void implisolid_set_error_mode(int mode) { g_error_mode = mode; }
 
 void implisolid_set_pruning(int on) { impli::Engine::set_pruning(on); }
 
+int implisolid_parse_settings(const char* mc_json, float box[6], int32_t ints[7], float floats[2]) {
+    g_last_error.clear();
+    try {
+        const MCSettings s = parse_mc_settings(mc_json);
+        for (int k = 0; k < 6; ++k) box[k] = s.box[k];
+        ints[0] = s.resolution;
+        ints[1] = s.ignore_root_matrix;
+        ints[2] = s.overall_repeats;
+        ints[3] = s.vresampl_iters;
+        ints[4] = s.projection;
+        ints[5] = s.qem;
+        ints[6] = s.subdiv;
+        floats[0] = s.vresampl_c;
+        floats[1] = s.post_subdiv_noise;
+    } catch (const std::exception& e) {
+        report(e.what(), true);   // polygoniser_settings.hpp:297-301 aborts
+        return -1;
+    }
+    return 0;
+}
+
+int implisolid_slab_partition(int R, int rank, int nranks, int32_t out[3]) {
+    g_last_error.clear();
+    try {
+        const SlabRange r = slab_partition(R, rank, nranks);
+        out[0] = r.z0;
+        out[1] = r.z1;
+        out[2] = r.halo;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
 void build_geometry(const char* shape_json, const char* mc_json) {
     g_last_error.clear();
     MCSettings st;

@@ -91,13 +91,8 @@ void Engine::set_object(const Program& prog) {
 }
 
 void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
-    const int res = R + 5;
-    const int layers = res - 3;            // cell layers 1 .. res-3
-    const int base = layers / nranks, extra = layers % nranks;
-    const int z0 = 1 + rank * base + (rank < extra ? rank : extra);
-    const int z1 = z0 + base + (rank < extra ? 1 : 0);
-    const int halo = (rank > 0) ? 1 : 0;   // one cell layer recomputed below the slab (owner rule)
-    grid_ = make_grid(R, box, z0 - halo, z1, z0);
+    const SlabRange sr = slab_partition(R, rank, nranks);   // one halo layer below (owner rule)
+    grid_ = make_grid(R, box, sr.z0 - sr.halo, sr.z1, sr.z0);
     const int64_t nu = n_units(grid_);
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0 + 1) * sizeof(float));

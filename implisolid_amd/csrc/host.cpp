@@ -261,4 +261,15 @@ Program compile_mp5(const char* shape_json, bool ignore_root_matrix) {
     return compile_mp5(d, ignore_root_matrix);
 }
 
+SlabRange slab_partition(int R, int rank, int nranks) {
+    if (R < 1 || nranks < 1 || rank < 0 || rank >= nranks) throw InputError("slab_partition: bad arguments");
+    const int layers = (R + 5) - 3;   // cell layers 1 .. res-3
+    const int base = layers / nranks, extra = layers % nranks;
+    SlabRange r;
+    r.z0 = 1 + rank * base + (rank < extra ? rank : extra);
+    r.z1 = r.z0 + base + (rank < extra ? 1 : 0);
+    r.halo = (rank > 0) ? 1 : 0;
+    return r;
+}
+
 }  // namespace impli

@@ -37,6 +37,11 @@ MCSettings parse_mc_settings(const char* json_text);
 Program compile_mp5(const char* shape_json, bool ignore_root_matrix);
 Program compile_mp5(const Json& shape, bool ignore_root_matrix);
 
+// Z-slab decomposition of the cell layers 1 .. res-3 (res = R + 5) over nranks: rank r owns
+// layers [z0, z1) and recomputes `halo` (0 or 1) layer below z0 (owner rule).
+struct SlabRange { int z0, z1, halo; };
+SlabRange slab_partition(int R, int rank, int nranks);
+
 // basic_functions.hpp:77-128 invert_matrix (ublas LU on a float 4x4 with last row 0,0,0,1)
 bool invert_matrix12(const float in[12], float out[12]);
 

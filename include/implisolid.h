@@ -82,6 +82,16 @@ void implisolid_set_error_mode(int mode);
 /* Additive: per-brick interval pruning of CSG operands during field evaluation (default on;
  * environment IMPLISOLID_PRUNE=0 also disables).  Results are bit-identical either way. */
 void implisolid_set_pruning(int on);
+
+/* Additive, host only: the parsed mc-settings (polygoniser_settings.hpp:147-305 semantics).
+ * ints = resolution, ignore_root_matrix, overall_repeats, vresampl.iters, projection, qem, subdiv;
+ * floats = vresampl.c, debug.post_subdiv_noise.  0, or -1 with implisolid_last_error() set where
+ * the reference would abort() (error mode 0 aborts, as the reference). */
+int implisolid_parse_settings(const char* mc_json, float box[6], int32_t ints[7], float floats[2]);
+
+/* Additive, host only: Z-slab decomposition used by the slab API -- rank owns cell layers
+ * [out[0], out[1]) and recomputes out[2] (0/1) halo layers below. */
+int implisolid_slab_partition(int R, int rank, int nranks, int32_t out[3]);
 /* evaluate n >= 0 points (no 50k limit) of the current set_object(); grad may be NULL */
 int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* grad_out);
 

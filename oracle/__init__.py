@@ -77,6 +77,8 @@ def lib():
         L.or_grad.argtypes = [npp, ctypes.c_int, fp, ctypes.c_int64, fp]
         L.or_acosf.argtypes = [ctypes.c_float]
         L.or_acosf.restype = ctypes.c_float
+        L.or_acosf_check.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        L.or_acosf_check.restype = ctypes.c_int64
         L.or_marching_cubes.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, ctypes.POINTER(OrMesh)]
         L.or_mesh_free.argtypes = [ctypes.POINTER(OrMesh)]
         L.or_mc_field.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, fp]
@@ -211,6 +213,11 @@ def eval_gradient(tree, pts):
 
 def acosf(x):
     return np.float32(lib().or_acosf(float(x)))
+
+
+def acosf_check(start, stride, count):
+    """Mismatches of the acosf restatement against the host libm over a strided bit-pattern range."""
+    return int(lib().or_acosf_check(start, stride, count))
 
 
 def mc_field(tree, resolution, box):

@@ -403,3 +403,16 @@ float or_acosf(float x) {
         return 2.0f * (df + w);
     }
 }
+
+/* self-check of the restatement against the host libm's acosf (glibc 2.35 in this image):
+ * number of mismatching bit patterns among start, start+stride, ... (count values) */
+int64_t or_acosf_check(uint32_t start, uint32_t stride, uint64_t count) {
+    int64_t bad = 0;
+    uint32_t u = start;
+    for (uint64_t k = 0; k < count; k++, u += stride) {
+        const float x = bitsf(u);
+        const float a = or_acosf(x), b = acosf(x);
+        if (!(fbits(a) == fbits(b) || (a != a && b != b))) bad++;
+    }
+    return bad;
+}

@@ -57,6 +57,7 @@ void or_grad(const or_node* nodes, int root, const float* xyz, int64_t n, float*
 
 /* glibc-2.35 acosf restatement (vertex_resampling.hpp:75 calls std::acos(float)) */
 float or_acosf(float x);
+int64_t or_acosf_check(uint32_t start, uint32_t stride, uint64_t count);
 
 /* ---- marching cubes: MarchingCubes::produce_mesh (marching_cubes.hpp:1728-1738) ---- */
 typedef struct {

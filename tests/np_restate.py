@@ -1,0 +1,295 @@
+"""Second, independent restatement of the hot path in vectorised numpy -- TEST INFRASTRUCTURE ONLY.
+
+Written directly from the reference sources (cited per function), not from oracle/*.c, so that the
+C oracle is cross-checked by a different implementation (different language, vectorised order of
+evaluation, numpy's ``np.unique`` instead of a hash map for first-appearance numbering).  numpy
+float32/float64 arithmetic is one IEEE operation per ufunc call, with no FMA contraction, so
+results are comparable bit for bit.
+
+Covered: the MP5 factory for scale+translate trees, node evaluation (egg, rabbit cube, cylinder,
+cone, heart, torus, double mushroom, union/intersection/difference), prepare_grid + sealing and
+marching cubes with the std::map first-appearance vertex numbering.
+"""
+import json
+
+import numpy as np
+
+f32 = np.float32
+
+
+def _tables():
+    import os
+    import re
+    here = os.path.dirname(os.path.abspath(__file__))
+    txt = open(os.path.join(here, "..", "implisolid_amd", "csrc", "generated", "tables.h")).read()
+    cases = re.search(r"IMPLI_MC_TRI_CASES\[256\] = \{(.*?)\};", txt, re.S).group(1)
+    tri = re.findall(r'"([0-9a-f]*)"', cases)
+    assert len(tri) == 256
+    bits = re.search(r"IMPLI_RABBIT_BITS\[\d+\] = \{(.*?)\};", txt, re.S).group(1)
+    rabbit = np.array([int(t, 16) for t in re.findall(r"0x[0-9a-fA-F]+", bits)], np.uint32).view(np.float32)
+    consts = {k: np.array([int(v, 16)], np.uint32).view(np.float32)[0]
+              for k, v in re.findall(r"#define IMPLI_RABBIT_(GRID_SIZE|ORIGIN_X|ORIGIN_Y|ORIGIN_Z)_BITS (0x[0-9a-fA-F]+)", txt)}
+    return tri, rabbit, consts
+
+
+TRI, RABBIT, RCONST = _tables()
+# cube.hpp:68-72: the object's members that follow the table in memory (read by out-of-table
+# indices at the upper faces, F8d), then zero padding
+RABBIT_PADDED = np.concatenate([RABBIT, np.array([RCONST["GRID_SIZE"], RCONST["ORIGIN_X"], RCONST["ORIGIN_Y"],
+                                                  RCONST["ORIGIN_Z"]], np.float32), np.zeros(1000, np.float32)])
+
+
+# ---- primitives ---------------------------------------------------------------------------------
+def egg(x, y, z):                      # egg.hpp:93-128 (a = b = c = 0.5)
+    u = (x - f32(0)) / f32(0.5)
+    v = (y - f32(0)) / f32(0.5)
+    w = (z - f32(0)) / f32(0.5)
+    return f32(1) - (u * u + v * v + w * w)
+
+
+def cube(x, y, z):                     # cube.hpp:176-272 (rabbit SDF, trilinear)
+    sx, sy, sz = 22, 18, 22
+    gs, ox, oy, oz = RCONST["GRID_SIZE"], RCONST["ORIGIN_X"], RCONST["ORIGIN_Y"], RCONST["ORIGIN_Z"]
+    out = ((ox + gs * f32(sx) < x) | (x < ox) | (oy + gs * f32(sy) < y) | (y < oy) |
+           (oz + gs * f32(sz) < z) | (z < oz))
+    res = np.full(x.shape, f32(10000), np.float32)
+    i = ~out
+    X, Y, Z = x[i], y[i], z[i]
+    xg = ((X - ox) / gs).astype(np.int64)
+    yg = ((Y - oy) / gs).astype(np.int64)
+    zg = ((Z - oz) / gs).astype(np.int64)
+    xl = ox + xg.astype(np.float32) * gs
+    yl = oy + yg.astype(np.float32) * gs
+    zl = oz + zg.astype(np.float32) * gs
+    xd, yd, zd = (X - xl) / gs, (Y - yl) / gs, (Z - zl) / gs
+    b = xg + yg * sx + zg * sx * sy
+    T = RABBIT_PADDED
+    r000, r100, r010, r110 = T[b], T[b + 1], T[b + sx], T[b + 1 + sx]
+    r001, r101, r011, r111 = T[b + sx * sy], T[b + 1 + sx * sy], T[b + sx + sx * sy], T[b + 1 + sx + sx * sy]
+    one = f32(1)
+    c00 = r000 * (one - xd) + r100 * xd
+    c01 = r001 * (one - xd) + r101 * xd
+    c10 = r010 * (one - xd) + r110 * xd
+    c11 = r011 * (one - xd) + r111 * xd
+    c0 = c00 * (one - yd) + c10 * yd
+    c1 = c01 * (one - yd) + c11 * yd
+    res[i] = c0 * (one - zd) + c1 * zd
+    return -res
+
+
+def _stdmin(a, b):                     # std::min(a, b) == (b < a) ? b : a
+    return np.where(b < a, b, a)
+
+
+def cylinder(x, y, z):                 # scylinder.hpp:97-166 (r .5, length 1, centre (0,0,-.5), axis z)
+    w0, w1, w2, X, Y, Zc = f32(0), f32(0), f32(1), f32(0), f32(0), f32(-0.5)
+    t0 = (x - X) * w0 + (y - Y) * w1 + (z - Zc) * w2
+    t1 = f32(1) - t0
+    a, b, c = x - w0 * t0 - X, y - w1 * t0 - Y, z - w2 * t0 - Zc
+    r_ = f32(0.5) - np.sqrt(a * a + b * b + c * c)
+    return _stdmin(t0, _stdmin(t1, r_))
+
+
+def cone(x, y, z):                     # scone.hpp:81-151 (h 1, r1 0, r2 .5, centre (0,0,.5))
+    q = f32(0.5) / f32(1)
+    a2, z0 = q * q, f32(0.5)
+    f = -np.sqrt((x - f32(0)) * (x - f32(0)) + (y - f32(0)) * (y - f32(0))) + np.sqrt((z - z0) * (z - z0) * a2)
+    up, lo = -(z - z0) - f32(0), (z - z0) + f32(1)
+    return _stdmin(f, _stdmin(up, lo))
+
+
+def heart(x, y, z):                    # heart.hpp:82-132 (std::pow(T, 3) in double)
+    d2, d3 = y.astype(np.float64), z.astype(np.float64)
+    T = (x * x).astype(np.float64) + (9. / 4.) * d2 * d2 + (z * z).astype(np.float64) - 1.
+    t3 = np.power(T, 3.0)
+    a = x * x * z * z * z
+    b = (9. / 200.) * d2 * d2 * d3 * d3 * d3
+    return (-(t3 - a.astype(np.float64) - b)).astype(np.float32)
+
+
+def torus(x, y, z):                    # torus.hpp:68-124 (r 4, rx = ry = rz = .2; std::pow -> double)
+    r, rx, ry, rz = f32(4), f32(0.2), f32(0.2), f32(0.2)
+    sq = lambda v: v.astype(np.float64) * v.astype(np.float64)
+    s = sq(x / rx) + sq(y / ry)
+    q = np.float64(r) - np.sqrt(s)
+    return (1. - q * q - sq(z / rz)).astype(np.float32)
+
+
+def dmushroom(x, y, z):                # object_factory.hpp:86-100 + double_mushroom.hpp:90-160
+    r = f32(0.9) / f32(2)
+    a = f32(0.4 / 2)
+    c = f32(1) / f32(1 / 0.2)
+    a2, b2, c2 = a * a, a * a, c * c
+    sq = lambda v: v.astype(np.float64) * v.astype(np.float64)
+    v = sq(x - f32(0)) / np.float64(a2) + sq(y - f32(0)) / np.float64(b2) - sq(z - f32(0)) / np.float64(c2) - 1
+    out = (-v).astype(np.float32)
+    out = np.where(z < -r, r + z, out)
+    out = np.where(z > r, r - z, out)
+    return out.astype(np.float32)
+
+
+PRIMS = {"iellipsoid": egg, "ellipsoid": egg, "cube": cube, "icube": cube, "icylinder": cylinder,
+         "cylinder": cylinder, "icone": cone, "cone": cone, "iheart": heart, "itorus": torus,
+         "implicit_double_mushroom": dmushroom}
+
+
+# ---- factory + evaluation (object_factory.hpp:56-758; transformed_*.hpp) -------------------------
+def _inverse_scale_translate(m):
+    """Inverse of a scale+translate matrix.  For such a matrix ublas' LU (basic_functions.hpp:77-128)
+    needs no pivoting, L = I and back substitution gives exactly 1/s and (0 - t*1)/s = -t/s."""
+    m = np.asarray([np.float32(float(v)) for v in m[:12]], np.float32)
+    for k in (1, 2, 4, 6, 8, 9):
+        if m[k] != 0:
+            raise ValueError("only scale+translate matrices")
+    inv = np.zeros(12, np.float32)
+    for r, (d, t) in enumerate(((0, 3), (5, 7), (10, 11))):
+        s = m[d]
+        inv[d] = f32(1) / s
+        inv[t] = -m[t] / s
+    return inv
+
+
+def _xform(mi, x, y, z):               # matrix_vector_product basic_functions.hpp:140-177
+    return (mi[0] * x + mi[1] * y + mi[2] * z + mi[3],
+            mi[4] * x + mi[5] * y + mi[6] * z + mi[7],
+            mi[8] * x + mi[9] * y + mi[10] * z + mi[11])
+
+
+EYE = [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0]
+
+
+def evaluate(shape, x, y, z, _root=True):
+    """f at float32 points for an MP5 tree of scale+translate nodes."""
+    d = json.loads(shape) if isinstance(shape, str) else shape
+    t = d["type"]
+    mi = _inverse_scale_translate(d["matrix"])
+    X, Y, Z = _xform(mi, x, y, z)
+    if t in PRIMS:
+        return PRIMS[t](X, Y, Z)
+    ch = d["children"]
+    if t == "Union":     # left-deep chain, identity intermediates (object_factory.hpp:545-580)
+        acc = evaluate(ch[0], X, Y, Z, False)
+        for k in range(1, len(ch)):
+            f2 = evaluate(ch[k], X, Y, Z, False)
+            acc = np.where(acc > f2, acc, f2)                    # transformed_union.hpp:48
+        # intermediates carry identity matrices: x' = 1*x + 0*y + 0*z + 0 == x for finite x
+        return acc
+    f1 = evaluate(ch[0], X, Y, Z, False)
+    f2 = evaluate(ch[1], X, Y, Z, False)
+    if t == "Intersection":
+        return np.where(f1 > f2, f2, f1)                         # transformed_intersection.hpp:50
+    if t == "Difference":
+        return np.where(f1 < -f2, f1, -f2)                       # transformed_subtract.hpp:52
+    raise ValueError(t)
+
+
+# ---- marching cubes (marching_cubes.hpp) -----------------------------------------------------------
+def field(shape, R, box):
+    """prepare_grid (:1662-1698) + eval_shape (:1702-1725) + seal_exterior (:895-963); [z, y, x]."""
+    res = R + 5
+    box = [f32(b) for b in box]
+    w = [(box[1] - box[0]) / f32(R), (box[3] - box[2]) / f32(R), (box[5] - box[4]) / f32(R)]
+    s = np.arange(res).astype(np.float32)
+    cx = s * w[0] + box[0] - f32(2) * w[0]
+    cy = s * w[1] + box[2] - f32(2) * w[1]
+    cz = s * w[2] + box[4] - f32(2) * w[2]
+    Z, Y, X = np.meshgrid(cz, cy, cx, indexing="ij")
+    F = f32(0) + evaluate(shape, X.ravel(), Y.ravel(), Z.ravel()).reshape(res, res, res)
+    for sl in (0, 1, res - 2, res - 1):
+        F[sl, :, :] = F[:, sl, :] = F[:, :, sl] = f32(-1e7)
+    return F, w
+
+
+# edge -> (corner a, corner b, axis, base-offset (dx, dy, dz)) for polygonize_single_cube (:518-718);
+# corners: 0 q, 1 qx, 2 qy, 3 qxy, 4 qz, 5 qxz, 6 qyz, 7 qxyz
+EDGES = [(0, 1, 0, (0, 0, 0)), (1, 3, 1, (1, 0, 0)), (2, 3, 0, (0, 1, 0)), (0, 2, 1, (0, 0, 0)),
+         (4, 5, 0, (0, 0, 1)), (5, 7, 1, (1, 0, 1)), (6, 7, 0, (0, 1, 1)), (4, 6, 1, (0, 0, 1)),
+         (0, 4, 2, (0, 0, 0)), (1, 5, 2, (1, 0, 0)), (3, 7, 2, (1, 1, 0)), (2, 6, 2, (0, 1, 0))]
+CORNER_OFF = [(0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (0, 0, 1), (1, 0, 1), (0, 1, 1), (1, 1, 1)]
+CORNER_BIT = [1, 2, 8, 4, 16, 32, 128, 64]
+
+
+def marching_cubes(F, w, box, R):
+    """render_geometry (:1019-1072) + posnormtriv/flush_geometry_queue's first-appearance map."""
+    res = R + 5
+    n = res - 3                        # cells 1 .. res-3 per axis
+    box = [f32(b) for b in box]
+    corner = [F[1 + dz:1 + dz + n, 1 + dy:1 + dy + n, 1 + dx:1 + dx + n] for dx, dy, dz in CORNER_OFF]
+    ci = np.zeros((n, n, n), np.int64)
+    for k in range(8):
+        ci |= np.where(corner[k] < f32(0), CORNER_BIT[k], 0)
+    ntri = np.array([len(t) for t in TRI])
+    act = np.flatnonzero(ntri[ci.ravel()] > 0)           # z-major cell order
+    if act.size == 0:
+        return np.zeros((0, 3), np.float32), np.zeros((0, 3), np.int32)
+    cases = ci.ravel()[act]
+    tri_pad = np.full((256, 15), -1, np.int64)
+    for c, t in enumerate(TRI):
+        tri_pad[c, :len(t)] = [int(ch, 16) for ch in t]
+    E = tri_pad[cases]                                    # (nA, 15) in table order
+    cell_rep = np.repeat(act, 15).reshape(-1, 15)
+    valid = E >= 0
+    e = E[valid]
+    cell = cell_rep[valid]
+    zi = cell // (n * n) + 1
+    yi = (cell // n) % n + 1
+    xi = cell % n + 1
+    ea = np.array([x[0] for x in EDGES])[e]
+    eb = np.array([x[1] for x in EDGES])[e]
+    axis = np.array([x[2] for x in EDGES])[e]
+    off = np.array([x[3] for x in EDGES])[e]
+    cof = np.array(CORNER_OFF)
+    fa = F[zi + cof[ea, 2], yi + cof[ea, 1], xi + cof[ea, 0]]
+    fb = F[zi + cof[eb, 2], yi + cof[eb, 1], xi + cof[eb, 0]]
+    xi0, yi0, zi0 = box[0] / w[0] - f32(2), box[2] / w[1] - f32(2), box[4] / w[2] - f32(2)
+    fx = (xi.astype(np.float32) + xi0) * w[0]
+    fy = (yi.astype(np.float32) + yi0) * w[1]
+    fz = (zi.astype(np.float32) + zi0) * w[2]
+    fx = np.where(off[:, 0] == 1, fx + w[0], fx)
+    fy = np.where(off[:, 1] == 1, fy + w[1], fy)
+    fz = np.where(off[:, 2] == 1, fz + w[2], fz)
+    mu = (f32(0) - fa) / (fb - fa)                        # VIntX/Y/Z (:400-495)
+    px = np.where(axis == 0, fx + mu * w[0], fx)
+    py = np.where(axis == 1, fy + mu * w[1], fy)
+    pz = np.where(axis == 2, fz + mu * w[2], fz)
+    # edge code = 3 * linear index of the low endpoint + axis
+    lin = (zi + off[:, 2]).astype(np.int64) * res * res + (yi + off[:, 1]) * res + (xi + off[:, 0])
+    code = lin * 3 + axis
+    uniq, first, inv = np.unique(code, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")             # first appearance
+    rank = np.empty_like(order)
+    rank[order] = np.arange(order.size)
+    faces = rank[inv].reshape(-1, 3).astype(np.int32)
+    src = first[order]
+    global _LAST_CODES
+    _LAST_CODES = code[src]
+    verts = np.stack([px[src], py[src], pz[src]], axis=1).astype(np.float32)
+    return verts, faces
+
+
+_LAST_CODES = None
+
+
+def polygonize_mc(shape, R, box):
+    F, w = field(shape, R, box)
+    return marching_cubes(F, w, box, R)
+
+
+def owner_cell_z(verts_codes, R):
+    """Owner cell layer (zi) of each vertex's edge under the owner rule: the cell that
+    holds the edge as its local edge 5 (Y, low end at cell+(1,0,1)), 6 (X, +(0,1,1)) or 10
+    (Z, +(1,1,0))."""
+    res = R + 5
+    code = np.asarray(verts_codes, np.int64)
+    axis = code % 3
+    lin = code // 3
+    z = lin // (res * res)
+    # X edge: owner z = z - 1; Y edge: z - 1; Z edge: z
+    return np.where(axis == 2, z, z - 1)
+
+
+def mc_with_codes(F, w, box, R):
+    """marching_cubes() plus the edge code of every vertex (first-appearance order)."""
+    global _LAST_CODES
+    v, f = marching_cubes(F, w, box, R)
+    return v, f, _LAST_CODES

@@ -1,0 +1,327 @@
+"""CPU suite (no GPU): the oracle against the golden vectors and the independent numpy
+restatement, the host logic of the C ABI, the library's exported symbols, and the multi-rank
+numbering exchange over gloo (world size 2 and 3)."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, mesh_edges
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import np_restate  # noqa: E402
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+REFERENCE = "/root/reference"
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+# ---- tables and libm-level pins -------------------------------------------------------------------
+@pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference tree not mounted")
+def test_tables_extracted_from_reference():
+    """generated/tables.h == the reference's MC tables (marching_cubes.hpp:1207-1502) and rabbit
+    table (cube.hpp:68-72)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "extract_tables.py"), "--check"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_mc_tables_self_consistent():
+    # every case's triangle list uses exactly the edges whose endpoints differ in sign
+    for c, t in enumerate(np_restate.TRI):
+        assert len(t) % 3 == 0
+        used = {int(ch, 16) for ch in t}
+        crossing = {e for e, (a, b, _, _) in enumerate(np_restate.EDGES)
+                    if bool(c & np_restate.CORNER_BIT[a]) != bool(c & np_restate.CORNER_BIT[b])}
+        assert used == crossing, c
+
+
+def test_acosf_restatement_matches_glibc_strided(oracle):
+    # vertex_resampling.hpp:75 std::acos(float): the restated glibc-2.35 acosf, every 61st pattern
+    assert oracle.acosf_check(0, 61, (1 << 32) // 61) == 0
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not os.environ.get("IMPLISOLID_SLOW"), reason="exhaustive (~50 s): set IMPLISOLID_SLOW=1")
+def test_acosf_restatement_matches_glibc_exhaustive(oracle):
+    assert oracle.acosf_check(0, 1, 1 << 32) == 0
+
+
+# ---- oracle vs the independent numpy restatement ------------------------------------------------
+def _trees():
+    from implisolid_amd import scenes
+    t = {"sphere": ({"type": "iellipsoid", "matrix": scenes.EYE}, [-0.6, 0.6] * 3, 32),
+         "union_sphere_cube": (scenes.union_sphere_cube(), [-1, 1] * 3, 40),
+         "config3_tree": (scenes.config3()[0], [-1, 1] * 3, 40),
+         "anisotropic": (scenes.union_sphere_cube(), [-0.7, 0.9, -1.1, 0.6, -0.55, 0.8], 36)}
+    for seed in (7, 11, 13, 101, 102):
+        t["random_%d" % seed] = (scenes.random_tree(seed, 3 + seed % 10), [-1, 1] * 3, 40)
+    return t
+
+
+TREES = _trees()
+
+
+@pytest.mark.parametrize("name", sorted(TREES))
+def test_oracle_field_and_mc_match_numpy_restatement(oracle, name):
+    shape, box, R = TREES[name]
+    tree = oracle.mp5_to_nodes(json.dumps(shape))
+    F, w = np_restate.field(shape, R, box)
+    Fo = oracle.mc_field(tree, R, box)
+    assert np.array_equal(_u32(F), _u32(Fo))
+    v, f = np_restate.marching_cubes(F, w, box, R)
+    vo, fo = oracle.marching_cubes(tree, R, box)
+    assert np.array_equal(f, fo)
+    assert np.array_equal(_u32(v), _u32(vo))
+
+
+def test_point_eval_matches_numpy_restatement(oracle):
+    rng = np.random.default_rng(3)
+    pts = rng.uniform(-1.3, 1.3, size=(20000, 3)).astype(np.float32)
+    for name, (shape, _, _) in TREES.items():
+        fo = oracle.eval_implicit(oracle.mp5_to_nodes(json.dumps(shape)), pts)
+        fn = np_restate.evaluate(shape, pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy())
+        assert np.array_equal(_u32(fo), _u32(fn)), name
+
+
+# ---- golden fixtures ------------------------------------------------------------------------------
+def test_golden_config1(oracle):
+    g = np.load(os.path.join(GOLDEN, "config1_mc.npz"))
+    v, f = oracle.polygonize(str(g["shape"]), str(g["mc"]))
+    assert v.shape == (3318, 3) and f.shape == (6632, 3)
+    assert np.array_equal(f, g["faces"]) and np.array_equal(_u32(v), _u32(g["verts"]))
+
+
+def test_golden_point_values(oracle):
+    g = np.load(os.path.join(GOLDEN, "points_eval.npz"))
+    trees = json.loads(str(g["trees"]))
+    pts = g["points"]
+    for name, sh in trees.items():
+        tree = oracle.mp5_to_nodes(json.dumps(sh))
+        assert np.array_equal(_u32(oracle.eval_implicit(tree, pts)), _u32(g["f_" + name])), name
+        assert np.array_equal(_u32(oracle.eval_gradient(tree, pts)), _u32(g["g_" + name])), name
+
+
+def test_golden_config2_ob02(oracle):
+    g = np.load(os.path.join(GOLDEN, "config2_r32_ob02.npz"))
+    taps = {}
+    v, f = oracle.polygonize(str(g["shape"]), str(g["mc"]), taps=taps)
+    assert np.array_equal(f, g["faces"]) and np.array_equal(_u32(v), _u32(g["verts"]))
+    assert np.array_equal(_u32(np.asarray(taps["post_p_centroids"])), _u32(g["tap_post_p_centroids"]))
+
+
+def test_golden_mc_summaries(oracle):
+    import hashlib
+    d = json.load(open(os.path.join(GOLDEN, "mc_summaries.json")))
+    for name, s in d.items():
+        v, f = oracle.marching_cubes(oracle.mp5_to_nodes(json.dumps(s["shape"])), s["R"], s["box"])
+        assert (v.shape[0], f.shape[0]) == (s["n_verts"], s["n_faces"]), name
+        assert hashlib.sha256(np.ascontiguousarray(f).tobytes()).hexdigest() == s["sha256_faces"], name
+        assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"], name
+    # SURVEY.md §8a (independent numpy estimate): config 2 scene at R=128 -> V 56 684, F 113 360
+    assert (d["config2_mc_r128"]["n_verts"], d["config2_mc_r128"]["n_faces"]) == (56684, 113360)
+    assert 56684 - 113360 // 2 == 4          # Euler characteristic: two sphere-like components
+
+
+# ---- mesh properties ------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["sphere", "union_sphere_cube", "config3_tree"])
+def test_mc_output_is_closed_edge_manifold(oracle, name):
+    shape, box, R = TREES[name]
+    v, f = oracle.marching_cubes(oracle.mp5_to_nodes(json.dumps(shape)), R, box)
+    _, cnt = mesh_edges(f)
+    assert (cnt == 2).all()
+    assert (np.bincount(f.ravel(), minlength=len(v)) > 0).all()      # every vertex referenced
+    if name == "sphere":
+        assert len(v) - len(f) // 2 == 2                              # Euler characteristic
+
+
+def test_owner_rule_matches_first_appearance_order():
+    """The GPU numbering rule: a vertex is created by the cell owning its edge (local edge 5, 6 or
+    10), ordered by owner cell z-major.  First-appearance ids must be non-decreasing in owner layer,
+    which is what lets Z-slabs number independently and concatenate."""
+    for name in ["union_sphere_cube", "config3_tree", "random_7"]:
+        shape, box, R = TREES[name]
+        F, w = np_restate.field(shape, R, box)
+        v, f, codes = np_restate.mc_with_codes(F, w, box, R)
+        z = np_restate.owner_cell_z(codes, R)
+        assert (np.diff(z) >= 0).all(), name
+
+
+def test_ob02_properties(oracle):
+    """Projected centroids lie on the surface to the bisection tolerance (configs.hpp:33)."""
+    from implisolid_amd import scenes
+    shape, mc = scenes.config2(32)
+    taps = {}
+    oracle.polygonize(json.dumps(shape), json.dumps(mc), taps=taps)
+    tree = oracle.mp5_to_nodes(json.dumps(shape))
+    cen = np.asarray(taps["post_p_centroids"][-1])
+    fv = np.abs(oracle.eval_implicit(tree, cen))
+    assert np.median(fv) <= 1e-4 and (fv <= 1e-4).mean() > 0.95
+
+
+# ---- host logic of the C ABI (no GPU calls) -------------------------------------------------------
+def _header_functions():
+    txt = open(os.path.join(ROOT, "include", "implisolid.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\([^;{]*\)\s*;", txt, flags=re.M)
+    return sorted(set(names))
+
+
+def test_abi_exports_every_declared_symbol(impli):
+    names = _header_functions()
+    assert len(names) >= 40, names
+    L = impli.lib()
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(names) <= set(impli.ABI_SYMBOLS) | {"main"}, set(names) - set(impli.ABI_SYMBOLS)
+
+
+def test_host_matrix_inverse_matches_oracle(impli, oracle):
+    """compile_mp5's inverse (host C++) == the oracle's LU restatement, bit for bit, including
+    general (rotation + shear) matrices where the LU operation order matters."""
+    rng = np.random.default_rng(11)
+    for trial in range(40):
+        m = rng.uniform(-1, 1, 12).astype(np.float32)
+        m[[0, 5, 10]] += np.float32(2.0)
+        shape = {"type": "iellipsoid", "matrix": [float(x) for x in m]}
+        n_instr, depth, n_mats, mats = impli.program_info(shape)
+        tree = oracle.mp5_to_nodes(json.dumps(shape))
+        ref = np.array(tree[0][tree[1]].minv[:], np.float32)
+        assert np.array_equal(_u32(mats[0]), _u32(ref)), trial
+
+
+def test_program_compiles_reference_factory_semantics(impli):
+    from implisolid_amd import scenes
+    # n-ary union -> left-deep chain: 3 children = 2 union nodes
+    u3 = {"type": "Union", "matrix": scenes.EYE, "children": [
+        {"type": "iellipsoid", "matrix": scenes.EYE}, {"type": "icone", "matrix": scenes.EYE},
+        {"type": "itorus", "matrix": scenes.EYE}]}
+    n_instr, depth, n_mats, _ = impli.program_info(u3)
+    assert n_instr == 3 * 2 + 2 * 2     # 3 leaves (XFORM + PRIM) + 2 unions (XFORM + CSG)
+    for bad, msg in [({"type": "bogus", "matrix": scenes.EYE}, "Invalid"),
+                     ({"type": "screw", "matrix": scenes.EYE}, "outside the implemented"),
+                     ({"type": "iellipsoid"}, "matrix")]:
+        with pytest.raises(Exception) as e:
+            impli.program_info(bad)
+        assert msg.lower() in str(e.value).lower(), str(e.value)
+
+
+def test_settings_parser_matches_oracle(impli, oracle):
+    from implisolid_amd import scenes
+    cases = [scenes.config1()[1], scenes.config2(64)[1],
+             dict(scenes.mc_settings(40, 1.0), resolution="40", ignore_root_matrix="true"),
+             dict(scenes.mc_settings(40, 1.0), overall_repeats=0)]
+    for mc in cases:
+        a = impli.parse_settings(mc)
+        b = oracle.parse_mc_settings(json.dumps(mc))
+        assert [np.float32(x) for x in a["box"]] == [np.float32(x) for x in b.box]
+        assert (a["resolution"], a["overall_repeats"], a["vresampl_iters"]) == (b.resolution, b.overall_repeats, b.vresampl_iters)
+        assert (bool(a["projection"]), bool(a["qem"]), bool(a["subdiv"]), bool(a["ignore_root_matrix"])) == \
+               (b.projection, b.qem, b.subdiv, b.ignore_root_matrix)
+        assert a["vresampl_c"] == b.vresampl_c
+    for bad in [dict(scenes.mc_settings(40, 1.0), resolution=40.5), dict(scenes.mc_settings(40, 1.0), resolution=2),
+                {"resolution": 40}, dict(scenes.mc_settings(40, 1.0), qem={"enabled": 1})]:
+        with pytest.raises(Exception):
+            impli.parse_settings(bad)
+        with pytest.raises(ValueError):
+            oracle.parse_mc_settings(json.dumps(bad))
+
+
+def test_invalid_settings_abort_in_reference_mode(impli):
+    """Error mode 0 (the default for C callers) aborts like polygoniser_settings.hpp:297-301."""
+    code = ("import ctypes, implisolid_amd as I; L = I.lib(); L.implisolid_set_error_mode(0); "
+            "import numpy as np; b=(ctypes.c_float*6)(); i=(ctypes.c_int32*7)(); f=(ctypes.c_float*2)(); "
+            "L.implisolid_parse_settings(b'{\"resolution\": 40}', b, i, f)")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True)
+    assert r.returncode != 0 and "Abort" in r.stderr
+
+
+def test_slab_partition_covers_all_layers(impli):
+    for R in (16, 61, 512):
+        for n in (1, 2, 3, 8):
+            parts = [impli.slab_partition(R, r, n) for r in range(n)]
+            layers = [z for (z0, z1, _) in parts for z in range(z0, z1)]
+            assert layers == list(range(1, R + 3))                  # cells 1 .. res-3
+            assert [h for (_, _, h) in parts] == [0] + [1] * (n - 1)
+
+
+# ---- multi-rank numbering exchange (gloo, CPU) -----------------------------------------------------
+def _slab_counts(codes, faces_cell_z, R, z0, z1, halo):
+    """counts int32[4] a rank's Slab.count() produces: own vertices incl. halo, faces, -, halo."""
+    oz = np_restate.owner_cell_z(codes, R)
+    own = int(((oz >= z0 - halo) & (oz < z1)).sum())
+    hal = int(((oz >= z0 - halo) & (oz < z0)).sum())
+    nf = int(((faces_cell_z >= z0) & (faces_cell_z < z1)).sum())
+    return [own, nf, 0, hal]
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import implisolid_amd as I
+    from implisolid_amd import distributed as D
+    from implisolid_amd import scenes
+    import np_restate as N
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        shape, box, R = scenes.union_sphere_cube(), [-1, 1] * 3, 40
+        F, w = N.field(shape, R, box)
+        v, f, codes = N.mc_with_codes(F, w, box, R)
+        oz = N.owner_cell_z(codes, R)          # owner layer of every vertex (first-appearance order)
+        ci_layers = _face_layers(F, R)         # cell layer of every face (emission order)
+        z0, z1, halo = I.slab_partition(R, rank, world)
+        cnt = torch.tensor(_slab_counts(codes, ci_layers, R, z0, z1, halo), dtype=torch.int32)
+        offs, gathered = D.global_offsets(cnt, rank, world)
+        # expected: this rank's vertices/faces start where the global first-appearance numbering
+        # places its first owned vertex / first face
+        exp_v = int((oz < z0).sum())
+        exp_f = int((ci_layers < z0).sum())
+        ok = (int(offs[0]) == exp_v and int(offs[1]) == exp_f and int(gathered[:, 1].sum()) == len(f)
+              and int((gathered[:, 0] - gathered[:, 3]).sum()) == len(v))
+        q.put((rank, ok, [int(offs[0]), int(offs[1])], [exp_v, exp_f]))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, False, repr(e), None))
+
+
+def _face_layers(F, R):
+    """cell layer zi of every face, in emission order (z-major cells, table order)."""
+    res = R + 5
+    n = res - 3
+    corner = [F[1 + dz:1 + dz + n, 1 + dy:1 + dy + n, 1 + dx:1 + dx + n] for dx, dy, dz in np_restate.CORNER_OFF]
+    ci = np.zeros((n, n, n), np.int64)
+    for k in range(8):
+        ci |= np.where(corner[k] < np.float32(0), np_restate.CORNER_BIT[k], 0)
+    ntri = np.array([len(t) // 3 for t in np_restate.TRI])
+    per_cell = ntri[ci.ravel()]
+    zi = np.arange(per_cell.size) // (n * n) + 1
+    return np.repeat(zi, per_cell)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_zslab_offsets_gloo(world):
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, got, exp in sorted(res):
+        assert ok, (rank, got, exp)
