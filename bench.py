@@ -76,7 +76,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--resolution", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--also-256", action="store_true", default=True)
+    ap.add_argument("--skip-256", action="store_true", help="do not also time R=256")
+    ap.add_argument("--prune", type=int, default=None, help="pruning level 0/1/2 (default: library default 2)")
     args = ap.parse_args()
 
     import torch
@@ -85,6 +86,8 @@ def main():
     from implisolid_amd import distributed as D
     from implisolid_amd import scenes
 
+    if args.prune is not None:
+        I.set_pruning(args.prune)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -148,12 +151,12 @@ def main():
                "mc_count_scan": float(np.mean([e[1].elapsed_time(e[2]) for e in ev])),
                "mc_emit": float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))}
         info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, shape=shape,
-                    slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth)
+                    slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats())
         slab.close()
         return info
 
     main_run = run(args.resolution, args.steps, args.warmup)
-    r256 = run(256, args.steps, args.warmup) if (args.also_256 and args.resolution != 256) else None
+    r256 = run(256, args.steps, args.warmup) if (not args.skip_256 and args.resolution != 256) else None
 
     if rank != 0:
         if world > 1:
@@ -204,6 +207,7 @@ def main():
             "parallelism": "zslab%d" % world,
         },
         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
+        "bricks": dict(zip(["total", "mixed", "sign_filled"], main_run["bricks"])),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes[dom]},

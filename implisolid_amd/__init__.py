@@ -28,7 +28,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_emit", "implisolid_slab_counters", "implisolid_slab_counts", "implisolid_slab_grid",
     "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
     "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
-    "implisolid_parse_settings", "implisolid_slab_partition",
+    "implisolid_parse_settings", "implisolid_slab_partition", "implisolid_slab_brick_stats",
 ]
 
 _lib = None
@@ -89,6 +89,7 @@ def lib():
         "implisolid_set_pruning": ([c_int], None),
         "implisolid_parse_settings": ([c_char_p, fp, ip, fp], c_int),
         "implisolid_slab_partition": ([c_int, c_int, c_int, ip], c_int),
+        "implisolid_slab_brick_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -135,9 +136,12 @@ def slab_partition(R, rank, nranks):
     return int(out[0]), int(out[1]), int(out[2])
 
 
-def set_pruning(on):
-    """Per-brick interval pruning of the field evaluation (default on; bit-identical results)."""
-    lib().implisolid_set_pruning(1 if on else 0)
+def set_pruning(level):
+    """Per-brick pruning level of the field evaluation: 0 off, 1 CSG operand pruning (field
+    bit-identical), 2 (default) + sign-filled bricks (mesh bit-identical).  True means 2."""
+    if level is True:
+        level = 2
+    lib().implisolid_set_pruning(int(level))
 
 
 def last_error():
@@ -315,6 +319,12 @@ class Slab:
 
     def field_ptr(self):
         return lib().implisolid_slab_field(self.h)
+
+    def brick_stats(self):
+        """[bricks, mixed-sign bricks, sign-filled bricks] of the last eval."""
+        out = (ctypes.c_int64 * 3)()
+        self._rc(lib().implisolid_slab_brick_stats(self.h, out))
+        return [int(x) for x in out]
 
     def read_field(self):
         """Blocking host copy of the stored field samples, shape (layers, n, n)."""

@@ -95,7 +95,7 @@ extern "C" {
 const char* implisolid_last_error(void) { return g_last_error.c_str(); }
 void implisolid_set_error_mode(int mode) { g_error_mode = mode; }
 
-void implisolid_set_pruning(int on) { impli::Engine::set_pruning(on); }
+void implisolid_set_pruning(int level) { impli::Engine::set_pruning(level); }
 
 int implisolid_parse_settings(const char* mc_json, float box[6], int32_t ints[7], float floats[2]) {
     g_last_error.clear();
@@ -431,6 +431,16 @@ int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, v
 float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
 int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
 float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
+
+int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]) {
+    try {
+        s->engine.brick_stats(out, 0);
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
 
 int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capacity) {
     try {

@@ -29,15 +29,37 @@ void DevBuf::release() {
 
 static std::atomic<int> g_pruning{-1};
 
-void Engine::set_pruning(int on) { g_pruning.store(on ? 1 : 0); }
-bool Engine::pruning() {
+void Engine::set_pruning(int level) { g_pruning.store(level < 0 ? 0 : level > 2 ? 2 : level); }
+int Engine::pruning() {
     int v = g_pruning.load();
     if (v < 0) {
         const char* e = std::getenv("IMPLISOLID_PRUNE");
-        v = (e && e[0] == '0') ? 0 : 1;
+        v = e ? std::atoi(e) : 2;
+        v = v < 0 ? 0 : v > 2 ? 2 : v;
         g_pruning.store(v);
     }
-    return v != 0;
+    return v;
+}
+
+void Engine::brick_stats(int64_t out[3], hipStream_t s) {
+    const BrickGrid bg = brick_grid(grid_);
+    std::vector<uint8_t> c((size_t)bg.n_bricks);
+    IMPLI_HIP(hipStreamSynchronize(s));
+    if (bg.n_bricks) IMPLI_HIP(hipMemcpy(c.data(), cls_.p, c.size(), hipMemcpyDeviceToHost));
+    int64_t mixed = 0, filled = 0;
+    for (int b = 0; b < bg.n_bricks; ++b) {
+        const int bx = b % bg.nbx, by = (b / bg.nbx) % bg.nby, bz = b / (bg.nbx * bg.nby);
+        const uint8_t k = c[b];
+        if (k == kBrickMixed) { ++mixed; continue; }
+        auto nb = [&](bool in, int i) { return in ? c[i] : (uint8_t)kBrickNeg; };
+        const int sy = bg.nbx, sz = bg.nbx * bg.nby;
+        if (nb(bx > 0, b - 1) == k && nb(bx + 1 < bg.nbx, b + 1) == k && nb(by > 0, b - sy) == k &&
+            nb(by + 1 < bg.nby, b + sy) == k && nb(bz > 0, b - sz) == k && nb(bz + 1 < bg.nbz, b + sz) == k)
+            ++filled;
+    }
+    out[0] = bg.n_bricks;
+    out[1] = mixed;
+    out[2] = filled;
 }
 
 Engine::Engine() {
@@ -77,7 +99,7 @@ void Engine::download(float* verts, int32_t* faces, const SlabCounts& c, hipStre
 }
 
 Engine::~Engine() {
-    DevBuf* all[] = {&offsets_, &modes_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
+    DevBuf* all[] = {&offsets_, &modes_, &cls_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
                      &records_, &verts_, &faces_, &overflow_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -95,6 +117,7 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     grid_ = make_grid(R, box, sr.z0 - sr.halo, sr.z1, sr.z0);
     const int64_t nu = n_units(grid_);
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
+    cls_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0 + 1) * sizeof(float));
     unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
     active_units_.reserve((size_t)(nu + 1) * sizeof(uint32_t));
@@ -145,9 +168,10 @@ MCBuffers Engine::buffers() const {
 
 void Engine::eval_field(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
-    if (n_csg_ > 0 && pruning())
+    const int level = pruning();
+    if (level > 0)
         launch_eval_field_pruned(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_,
-                                 modes_.as<uint64_t>(), field_.as<float>(), s);
+                                 modes_.as<uint64_t>(), cls_.as<uint8_t>(), level >= 2, field_.as<float>(), s);
     else
         launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
     IMPLI_HIP(hipGetLastError());

@@ -70,10 +70,13 @@ public:
 
     DevBuf& scratch(int k) { return scratch_[k]; }
 
-    // per-brick interval pruning of the field evaluation (process-wide switch, default on;
-    // IMPLISOLID_PRUNE=0 or implisolid_set_pruning(0) turns it off)
-    static void set_pruning(int on);
-    static bool pruning();
+    // per-brick interval pruning of the field evaluation (process-wide level, default 2;
+    // IMPLISOLID_PRUNE=<level> or implisolid_set_pruning(level)):
+    //   0 off, 1 CSG operand pruning (field bit-identical), 2 + sign-only bricks (mesh bit-identical)
+    static void set_pruning(int level);
+    static int pruning();
+    // brick statistics of the last pruned eval: [bricks, mixed, sign-filled]; blocking
+    void brick_stats(int64_t out[3], hipStream_t stream);
 
 private:
     MCBuffers buffers() const;
@@ -84,7 +87,7 @@ private:
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, modes_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    DevBuf offsets_, modes_, cls_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     DevBuf scratch_[16];
 };

@@ -7,9 +7,13 @@
 //                reference's res^3 x 12 B point grid and its per-node batch copies never exist.
 // k_brick_modes / k_eval_field_pruned: the same field, computed per brick of kBX x kBY x kBZ
 //                samples.  A first pass bounds every node of the program over each brick
-//                (ifunc_interval.hpp) and records which CSG operands provably win; the second
-//                pass (one wave per brick) skips the losing subtrees.  Bit-identical to
-//                k_eval_field (tests/test_gpu_parity.py::test_pruned_field_identical).
+//                (ifunc_interval.hpp), records which CSG operands provably win and the brick's
+//                sign class; the second pass (one wave per brick) skips the losing subtrees.
+//                Level 1: bit-identical to k_eval_field (test_pruned_field_identical).
+//                Level 2 (sign_fill): bricks that are sign-definite together with their face
+//                neighbours get +-1 instead of exact values -- no cell edge touching them changes
+//                sign, so marching cubes reads only their sign and the mesh is bit-identical
+//                (test_sign_fill_field_equivalent + every MC parity test).
 // k_eval_points: arbitrary points (direct-eval ABI, mcc2.cpp:815-911) with optional gradient.
 #include <cstdlib>
 
@@ -56,7 +60,7 @@ __device__ __forceinline__ float sample_z(const GridDesc& g, int layer) {
 template <int D>
 __global__ __launch_bounds__(256) void k_brick_modes(const Program* __restrict__ prog, const float* __restrict__ tab,
                                                      float2 tab_range, GridDesc g, BrickGrid bg,
-                                                     uint64_t* __restrict__ modes) {
+                                                     uint64_t* __restrict__ modes, uint8_t* __restrict__ cls) {
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= bg.n_bricks) return;
     int bx, by, bz;
@@ -69,16 +73,34 @@ __global__ __launch_bounds__(256) void k_brick_modes(const Program* __restrict__
     Box p{Iv{sample_xy(g, 0, x0), sample_xy(g, 0, x1)}, Iv{sample_xy(g, 1, y0), sample_xy(g, 1, y1)},
           Iv{sample_z(g, z0), sample_z(g, z1)}};
     uint64_t m;
-    (void)eval_iv<D>(prog, tab, tab_range, p, m);
+    const Iv root = eval_iv<D>(prog, tab, tab_range, p, m);
     modes[b] = m;
+    // sign class of the whole brick: MC sets a cube-index bit iff f < 0
+    cls[b] = (root.lo >= 0.f) ? kBrickPos : (root.hi < 0.f) ? kBrickNeg : kBrickMixed;
+}
+
+// A brick needs exact values only if one of its samples can be the end of a sign-changing cell
+// edge.  Edges are axis aligned, so that requires the brick or a face neighbour to differ in
+// sign class.  Neighbours outside the stored grid count as negative: sealed samples are -1e7
+// (and a slab's unstored layers are never touched by its cells).
+__device__ __forceinline__ uint32_t brick_fill_class(const uint8_t* __restrict__ cls, const BrickGrid& bg, int b,
+                                                     int bx, int by, int bz) {
+    const uint32_t c = cls[b];
+    if (c == kBrickMixed) return kBrickMixed;
+    const int sy = bg.nbx, sz = bg.nbx * bg.nby;
+    const uint32_t xm = bx > 0 ? cls[b - 1] : kBrickNeg, xp = bx + 1 < bg.nbx ? cls[b + 1] : kBrickNeg;
+    const uint32_t ym = by > 0 ? cls[b - sy] : kBrickNeg, yp = by + 1 < bg.nby ? cls[b + sy] : kBrickNeg;
+    const uint32_t zm = bz > 0 ? cls[b - sz] : kBrickNeg, zp = bz + 1 < bg.nbz ? cls[b + sz] : kBrickNeg;
+    return (xm == c && xp == c && ym == c && yp == c && zm == c && zp == c) ? c : (uint32_t)kBrickMixed;
 }
 
 template <int D>
 __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __restrict__ prog,
                                                            const float* __restrict__ tab, GridDesc g, BrickGrid bg,
                                                            const uint64_t* __restrict__ modes,
+                                                           const uint8_t* __restrict__ cls, int sign_fill,
                                                            float* __restrict__ field) {
-    const int b = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
     if (b >= bg.n_bricks) return;
     const int lane = threadIdx.x & 63;
     int bx, by, bz;
@@ -93,6 +115,18 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __rest
     const int layers = g.fz1 - g.fz0;
     const size_t plane = (size_t)n * n;
     float* out = field + (size_t)sy * n + sx;
+    if (sign_fill) {
+        const uint32_t fc = brick_fill_class(cls, bg, b, bx, by, bz);
+        if (fc != kBrickMixed) {   // only the sign is ever read: any value of that sign will do
+            const float v = (fc == kBrickPos) ? 1.f : -1.f;
+            for (int k = 0; k < kBZ; ++k) {
+                const int layer = bz * kBZ + k;
+                if (layer >= layers) break;
+                if (ok) out[(size_t)layer * plane] = v;
+            }
+            return;
+        }
+    }
 #pragma unroll 1
     for (int k = 0; k < kBZ; ++k) {
         const int layer = bz * kBZ + k;
@@ -155,15 +189,17 @@ BrickGrid brick_grid(const GridDesc& g) {
 }
 
 void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range,
-                              const GridDesc& g, uint64_t* d_modes, float* d_field, hipStream_t s) {
+                              const GridDesc& g, uint64_t* d_modes, uint8_t* d_cls, int sign_fill, float* d_field,
+                              hipStream_t s) {
     const BrickGrid bg = brick_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
     const unsigned tb = (unsigned)((bg.n_bricks + 255) / 256), eb = (unsigned)((bg.n_bricks + 3) / 4);
 #define IMPLI_PRUNED(DD)                                                                             \
     do {                                                                                             \
-        k_brick_modes<DD><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes);           \
-        k_eval_field_pruned<DD><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_field);      \
+        k_brick_modes<DD><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);    \
+        k_eval_field_pruned<DD><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, sign_fill, \
+                                                   d_field);                                         \
     } while (0)
     if (depth <= 4) IMPLI_PRUNED(4);
     else if (depth <= 8) IMPLI_PRUNED(8);

@@ -42,10 +42,12 @@ void launch_eval_field(const Program* d_prog, int depth, const float* d_rabbit, 
 // direct evaluation at arbitrary points (implicit values / gradients)
 // pruned field evaluation: bricks of kBX x kBY x kBZ stored samples (x fastest)
 constexpr int kBX = 16, kBY = 4, kBZ = 4;
+enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2 };
 struct BrickGrid { int nbx, nby, nbz, n_bricks; };
 BrickGrid brick_grid(const GridDesc& g);
 void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range,
-                              const GridDesc& g, uint64_t* d_modes, float* d_field, hipStream_t s);
+                              const GridDesc& g, uint64_t* d_modes, uint8_t* d_cls, int sign_fill, float* d_field,
+                              hipStream_t s);
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
                         float* d_f, float* d_grad /* nullable: values only */, hipStream_t s);
 

@@ -79,9 +79,12 @@ const char* implisolid_last_error(void);
    1: print the same message, record it in implisolid_last_error() and return */
 void implisolid_set_error_mode(int mode);
 
-/* Additive: per-brick interval pruning of CSG operands during field evaluation (default on;
- * environment IMPLISOLID_PRUNE=0 also disables).  Results are bit-identical either way. */
-void implisolid_set_pruning(int on);
+/* Additive: per-brick interval pruning of the field evaluation (process-wide; environment
+ * IMPLISOLID_PRUNE=<level> sets the initial level).  0 off; 1 CSG operands proven irrelevant over a
+ * brick are skipped (field bit-identical); 2 (default) additionally fills bricks that are
+ * sign-definite together with their face neighbours with +-1 (only their sign is ever read, so
+ * the mesh is bit-identical). */
+void implisolid_set_pruning(int level);
 
 /* Additive, host only: the parsed mc-settings (polygoniser_settings.hpp:147-305 semantics).
  * ints = resolution, ignore_root_matrix, overall_repeats, vresampl.iters, projection, qem, subdiv;
@@ -128,6 +131,8 @@ float* implisolid_slab_field(implisolid_slab* s);
 /* blocking copy of the slab's stored field samples (n*n*layers floats, x fastest); with out ==
  * NULL returns the sample count only */
 int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capacity);
+/* bricks of the last slab eval: out = [bricks, mixed-sign bricks, sign-filled bricks] (blocking) */
+int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]);
 
 #ifdef __cplusplus
 }

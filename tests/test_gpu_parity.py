@@ -122,6 +122,17 @@ def test_empty_and_full(impli, oracle):
     _mc_compare(impli, oracle, big, scenes.mc_settings(16, 1.0))
 
 
+@pytest.mark.parametrize("level", [0, 1, 2])
+def test_mc_identical_at_every_pruning_level(impli, oracle, level):
+    from implisolid_amd import scenes
+    impli.set_pruning(level)
+    try:
+        _mc_compare(impli, oracle, scenes.config3()[0], scenes.mc_settings(64, 1.0))
+        _mc_compare(impli, oracle, scenes.union_sphere_cube(), scenes.mc_settings(50, 1.0))
+    finally:
+        impli.set_pruning(2)
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 5])
 def test_zslab_split_identical(impli, oracle, nranks):
     """Z-slab decomposition (one-layer recomputed halo, global offsets) == single GPU."""
@@ -190,16 +201,29 @@ def test_ob02_config3_tree_small(impli, oracle):
     _ob02_compare(impli, oracle, shape, mc)
 
 
-def _field(impli, shape, mc, prune):
-    impli.set_pruning(prune)
+def _field(impli, shape, mc, level):
+    impli.set_pruning(level)
     try:
         s = impli.Slab(shape, mc)
         s.eval()
         f = s.read_field()
         s.close()
     finally:
-        impli.set_pruning(True)
+        impli.set_pruning(2)
     return f
+
+
+def _needed_samples(f):
+    """Stored samples whose exact value marching cubes can read: ends of a sign-changing axis
+    edge, including edges to the sealed (-1e7) border."""
+    neg = f < 0
+    p = np.pad(neg, 1, constant_values=True)      # sealed neighbours are negative
+    c = p[1:-1, 1:-1, 1:-1]
+    need = np.zeros_like(c)
+    for ax in range(3):
+        for d in (-1, 1):
+            need |= c != np.roll(p, d, axis=ax)[1:-1, 1:-1, 1:-1]
+    return need
 
 
 @pytest.mark.parametrize("name", sorted(TREES))
@@ -210,9 +234,13 @@ def test_pruned_field_identical(impli, name):
         mc = scenes.mc_settings(R, 1.0)
         if box:
             mc["box"] = box
-        a = _field(impli, TREES[name], mc, True)
-        b = _field(impli, TREES[name], mc, False)
+        a = _field(impli, TREES[name], mc, 1)
+        b = _field(impli, TREES[name], mc, 0)
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
+        c = _field(impli, TREES[name], mc, 2)
+        assert np.array_equal(c < 0, b < 0)
+        need = _needed_samples(b)
+        assert np.array_equal(c[need].view(np.uint32), b[need].view(np.uint32))
 
 
 @pytest.mark.parametrize("seed", list(range(100, 124)))
@@ -220,6 +248,52 @@ def test_pruned_field_random_trees(impli, seed):
     from implisolid_amd import scenes
     shape = scenes.random_tree(seed, 3 + seed % 10)
     mc = scenes.mc_settings(48, 1.0)
-    a = _field(impli, shape, mc, True)
-    b = _field(impli, shape, mc, False)
+    a = _field(impli, shape, mc, 1)
+    b = _field(impli, shape, mc, 0)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
+    c = _field(impli, shape, mc, 2)
+    assert np.array_equal(c < 0, b < 0)
+    need = _needed_samples(b)
+    assert np.array_equal(c[need].view(np.uint32), b[need].view(np.uint32))
+
+
+# ---- against the committed golden fixtures (tests/golden/make_golden.py) ---------------------------
+def _golden(name):
+    import os
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)
+
+
+def test_golden_config1_gpu(impli):
+    g = np.load(_golden("config1_mc.npz"))
+    v, f = impli.make_geometry(str(g["shape"]), str(g["mc"]))
+    assert np.array_equal(f, g["faces"]) and np.array_equal(v.view(np.uint32), g["verts"].view(np.uint32))
+
+
+def test_golden_points_gpu(impli):
+    g = np.load(_golden("points_eval.npz"))
+    trees = json.loads(str(g["trees"]))
+    for name, sh in trees.items():
+        with impli.ImplicitService(sh) as svc:
+            f, gr = svc.eval(g["points"], gradient=True)
+        assert np.array_equal(f.view(np.uint32), g["f_" + name].view(np.uint32)), name
+        assert np.array_equal(gr.view(np.uint32), g["g_" + name].view(np.uint32)), name
+
+
+def test_golden_config2_ob02_gpu(impli):
+    g = np.load(_golden("config2_r32_ob02.npz"))
+    v, f = impli.make_geometry(str(g["shape"]), str(g["mc"]))
+    assert np.array_equal(f, g["faces"]) and np.array_equal(v.view(np.uint32), g["verts"].view(np.uint32))
+    p = impli.get_pointset("post_p_centroids")
+    assert np.array_equal(p.view(np.uint32), g["tap_post_p_centroids"][-1].view(np.uint32))
+
+
+def test_golden_mc_summaries_gpu(impli):
+    import hashlib
+    from implisolid_amd import scenes
+    d = json.load(open(_golden("mc_summaries.json")))
+    for name, s in d.items():
+        mc = scenes.mc_settings(s["R"], 1.0)
+        v, f = impli.make_geometry(s["shape"], mc)
+        assert (len(v), len(f)) == (s["n_verts"], s["n_faces"]), name
+        assert hashlib.sha256(np.ascontiguousarray(f).tobytes()).hexdigest() == s["sha256_faces"], name
+        assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"], name
