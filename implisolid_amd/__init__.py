@@ -334,7 +334,7 @@ class Slab:
         out = np.empty(n, np.float32)
         L.implisolid_slab_read_field(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n)
         _check()
-        n_side = self.R + 1
+        n_side = self.R + 3          # samples 1 .. res-2 per axis, the sealed ring included
         return out.reshape(-1, n_side, n_side)
 
     def close(self):

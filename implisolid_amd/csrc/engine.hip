@@ -43,22 +43,19 @@ int Engine::pruning() {
 
 void Engine::brick_stats(int64_t out[3], hipStream_t s) {
     const BrickGrid bg = brick_grid(grid_);
-    std::vector<uint8_t> c((size_t)bg.n_bricks);
+    std::vector<uint8_t> c((size_t)bg.n_bricks), f((size_t)bg.n_bricks);
     IMPLI_HIP(hipStreamSynchronize(s));
-    if (bg.n_bricks) IMPLI_HIP(hipMemcpy(c.data(), cls_.p, c.size(), hipMemcpyDeviceToHost));
+    if (bg.n_bricks) {
+        IMPLI_HIP(hipMemcpy(c.data(), cls_.p, c.size(), hipMemcpyDeviceToHost));
+        IMPLI_HIP(hipMemcpy(f.data(), fill_.p, f.size(), hipMemcpyDeviceToHost));
+    }
     int64_t mixed = 0, filled = 0;
     for (int b = 0; b < bg.n_bricks; ++b) {
-        const int bx = b % bg.nbx, by = (b / bg.nbx) % bg.nby, bz = b / (bg.nbx * bg.nby);
-        const uint8_t k = c[b];
-        if (k == kBrickMixed) { ++mixed; continue; }
-        auto nb = [&](bool in, int i) { return in ? c[i] : (uint8_t)kBrickNeg; };
-        const int sy = bg.nbx, sz = bg.nbx * bg.nby;
-        if (nb(bx > 0, b - 1) == k && nb(bx + 1 < bg.nbx, b + 1) == k && nb(by > 0, b - sy) == k &&
-            nb(by + 1 < bg.nby, b + sy) == k && nb(bz > 0, b - sz) == k && nb(bz + 1 < bg.nbz, b + sz) == k)
-            ++filled;
+        mixed += (c[b] & 3) == kBrickMixed;
+        filled += f[b] != 0;
     }
     out[0] = bg.n_bricks;
-    out[1] = mixed;
+    out[1] = pruning() > 0 ? mixed : bg.n_bricks;
     out[2] = filled;
 }
 
@@ -99,7 +96,7 @@ void Engine::download(float* verts, int32_t* faces, const SlabCounts& c, hipStre
 }
 
 Engine::~Engine() {
-    DevBuf* all[] = {&offsets_, &modes_, &cls_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
+    DevBuf* all[] = {&offsets_, &modes_, &cls_, &fill_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
                      &records_, &verts_, &faces_, &overflow_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -118,7 +115,8 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     const int64_t nu = n_units(grid_);
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
     cls_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
-    field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0 + 1) * sizeof(float));
+    fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
+    field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
     unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
     active_units_.reserve((size_t)(nu + 1) * sizeof(uint32_t));
     scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
@@ -149,6 +147,10 @@ bool Engine::ensure_capacity(const SlabCounts& c) {
 MCBuffers Engine::buffers() const {
     MCBuffers b{};
     b.field = field_.as<float>();
+    b.fill = fill_.as<uint8_t>();
+    const BrickGrid bg = brick_grid(grid_);
+    b.nbx = bg.nbx;
+    b.nby = bg.nby;
     b.unit_cnt = unit_cnt_.as<uint4>();
     b.ci = ci_.as<uint8_t>();
     b.scan_blk = scan_blk_.as<uint32_t>();
@@ -169,11 +171,14 @@ MCBuffers Engine::buffers() const {
 void Engine::eval_field(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
     const int level = pruning();
-    if (level > 0)
+    if (level > 0) {
         launch_eval_field_pruned(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_,
-                                 modes_.as<uint64_t>(), cls_.as<uint8_t>(), level >= 2, field_.as<float>(), s);
-    else
+                                 modes_.as<uint64_t>(), cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2,
+                                 field_.as<float>(), s);
+    } else {
+        IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled
         launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
+    }
     IMPLI_HIP(hipGetLastError());
 }
 

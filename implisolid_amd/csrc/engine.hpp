@@ -87,7 +87,7 @@ private:
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, modes_, cls_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    DevBuf offsets_, modes_, cls_, fill_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     DevBuf scratch_[16];
 };

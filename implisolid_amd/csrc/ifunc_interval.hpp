@@ -237,35 +237,41 @@ __device__ __forceinline__ uint32_t csg_decide(int t, Iv a, Iv b, Iv& out) {
     return PM_BOTH;
 }
 
-// interval interpreter over a box; returns the root interval and the per-node modes
+// interval interpreter over a box; returns the root interval and the per-node modes.  The
+// stacks are kept as separate scalar arrays (structure of arrays) so that the uniform-index
+// accesses stay in VGPRs (arrays of Iv structs were demoted to scratch).
 template <int D>
 __device__ __forceinline__ Iv eval_iv(const Program* __restrict__ prog, const float* __restrict__ tab,
                                       float2 tab_range, Box p0, uint64_t& modes) {
-    Iv px[D], py[D], pz[D], vf[D];
+    float xl[D], xh[D], yl[D], yh[D], zl[D], zh[D], vl[D], vh[D];
     int sp = 0, vp = 0;
-    px[0] = p0.x; py[0] = p0.y; pz[0] = p0.z;
+    xl[0] = p0.x.lo; xh[0] = p0.x.hi; yl[0] = p0.y.lo; yh[0] = p0.y.hi; zl[0] = p0.z.lo; zh[0] = p0.z.hi;
     modes = 0;
     const int n = prog->n_instr;
     for (int pc = 0; pc < n; ++pc) {
         const Instr I = prog->instr[pc];
+        const Box cur{Iv{xl[sp], xh[sp]}, Iv{yl[sp], yh[sp]}, Iv{zl[sp], zh[sp]}};
         if (I.op == OP_XFORM) {
-            const Box q = xform_iv(prog->mats[I.mat], Box{px[sp], py[sp], pz[sp]});
+            const Box q = xform_iv(prog->mats[I.mat], cur);
             ++sp;
-            px[sp] = q.x; py[sp] = q.y; pz[sp] = q.z;
+            xl[sp] = q.x.lo; xh[sp] = q.x.hi; yl[sp] = q.y.lo; yh[sp] = q.y.hi; zl[sp] = q.z.lo; zh[sp] = q.z.hi;
         } else if (I.op == OP_PRIM) {
-            vf[vp++] = prim_iv(I.type, tab, tab_range, Box{px[sp], py[sp], pz[sp]});
+            const Iv r = prim_iv(I.type, tab, tab_range, cur);
+            vl[vp] = r.lo; vh[vp] = r.hi;
+            ++vp;
             --sp;
         } else {
             --sp;
-            const Iv b = vf[--vp];
-            const Iv a = vf[vp - 1];
+            --vp;
+            const Iv b{vl[vp], vh[vp]};
+            const Iv a{vl[vp - 1], vh[vp - 1]};
             Iv o;
             const uint32_t m = csg_decide(I.type, a, b, o);
             if (I.csg < kMaxPruned) modes |= (uint64_t)m << (2 * I.csg);
-            vf[vp - 1] = o;
+            vl[vp - 1] = o.lo; vh[vp - 1] = o.hi;
         }
     }
-    return vf[0];
+    return Iv{vl[0], vh[0]};
 }
 
 __device__ __forceinline__ uint32_t mode_of(uint64_t modes, int csg) {

@@ -28,7 +28,7 @@ GridDesc make_grid(int R, const float box[6], int cz0, int cz1, int cz_emit) {
     GridDesc g{};
     g.R = R;
     g.res = R + 5;
-    g.n = R + 1;
+    g.n = R + 3;
     g.m = R + 2;
     for (int a = 0; a < 3; ++a) {
         const float width = box[2 * a + 1] - box[2 * a];   // init(): marching_cubes.hpp:231-243
@@ -39,9 +39,8 @@ GridDesc make_grid(int R, const float box[6], int cz0, int cz1, int cz_emit) {
     g.cz0 = cz0;
     g.cz1 = cz1;
     g.cz_emit = cz_emit;
-    const int lo = cz0 < 2 ? 2 : cz0, hi = (cz1 > g.res - 3 ? g.res - 3 : cz1) + 1;
-    g.fz0 = lo;
-    g.fz1 = hi > lo ? hi : lo;
+    g.fz0 = cz0;        // cells [cz0, cz1) touch sample layers [cz0, cz1]
+    g.fz1 = cz1 + 1;
     g.n_cells = (int64_t)g.m * g.m * (cz1 - cz0);
     return g;
 }
@@ -67,10 +66,12 @@ void build_case_table(CaseInfo out[256]) {
 
 namespace {
 
+// stored sample (sx, sy, sz) -- sample indices in [1, res-2], the sealed ring included
+__device__ __forceinline__ int sample_index(const GridDesc& g, int sx, int sy, int sz) {
+    return (sx - 1) + (sy - 1) * g.n + (sz - g.fz0) * g.n * g.n;   // the field is < 2^31 elements
+}
 __device__ __forceinline__ float corner(const float* __restrict__ field, const GridDesc& g, int sx, int sy, int sz) {
-    const bool in = (unsigned)(sx - 2) <= (unsigned)g.R && (unsigned)(sy - 2) <= (unsigned)g.R &&
-                    (unsigned)(sz - 2) <= (unsigned)g.R;
-    return in ? field[(size_t)(sx - 2) + (size_t)(sy - 2) * g.n + (size_t)(sz - g.fz0) * g.n * g.n] : -10000000.0f;
+    return field[sample_index(g, sx, sy, sz)];
 }
 
 struct CellVals {
@@ -79,20 +80,16 @@ struct CellVals {
 
 __device__ __forceinline__ unsigned load_cell(const float* __restrict__ field, const GridDesc& g, int cx, int cy, int cz,
                                               CellVals& v) {
-    // corners with a coordinate in {1, res-2} are sealed (-1e7): cells 1 and res-3 of each axis
-    const bool lo_x = cx >= 2, hi_x = cx + 1 <= g.R + 2, lo_y = cy >= 2, hi_y = cy + 1 <= g.R + 2, lo_z = cz >= 2,
-               hi_z = cz + 1 <= g.R + 2;
     const int n = g.n, nn = g.n * g.n;
-    const int base = (cx - 2) + (cy - 2) * n + (cz - g.fz0) * nn;   // field is < 2^31 elements
-    const float S = -10000000.0f;
-    v.f[0] = (lo_x && lo_y && lo_z) ? field[base] : S;
-    v.f[1] = (hi_x && lo_y && lo_z) ? field[base + 1] : S;
-    v.f[2] = (lo_x && hi_y && lo_z) ? field[base + n] : S;
-    v.f[3] = (hi_x && hi_y && lo_z) ? field[base + n + 1] : S;
-    v.f[4] = (lo_x && lo_y && hi_z) ? field[base + nn] : S;
-    v.f[5] = (hi_x && lo_y && hi_z) ? field[base + nn + 1] : S;
-    v.f[6] = (lo_x && hi_y && hi_z) ? field[base + nn + n] : S;
-    v.f[7] = (hi_x && hi_y && hi_z) ? field[base + nn + n + 1] : S;
+    const float* q = field + sample_index(g, cx, cy, cz);
+    v.f[0] = q[0];
+    v.f[1] = q[1];
+    v.f[2] = q[n];
+    v.f[3] = q[n + 1];
+    v.f[4] = q[nn];
+    v.f[5] = q[nn + 1];
+    v.f[6] = q[nn + n];
+    v.f[7] = q[nn + n + 1];
     unsigned ci = 0;   // polygonize_single_cube :553-560
     if (v.f[0] < 0.f) ci |= 1;
     if (v.f[1] < 0.f) ci |= 2;
@@ -151,6 +148,18 @@ __device__ __forceinline__ unsigned f_own(unsigned long long p) { return (unsign
 __device__ __forceinline__ unsigned f_tri(unsigned long long p) { return (unsigned)((p >> kF) & ((1ull << kF) - 1)); }
 __device__ __forceinline__ unsigned f_act(unsigned long long p) { return (unsigned)(p >> (2 * kF)); }
 
+// cube index from the negative-corner masks of the four sample rows around a run of cells:
+// bit k of r00/r10/r01/r11 = sample x0+k of rows (y,z), (y+1,z), (y,z+1), (y+1,z+1) is < 0
+__device__ __forceinline__ unsigned ci_from_rows(unsigned r00, unsigned r10, unsigned r01, unsigned r11, int k) {
+    const unsigned a = (r00 >> k) & 3u, b = (r10 >> k) & 3u, c = (r01 >> k) & 3u, d = (r11 >> k) & 3u;
+    // corners q(1) qx(2) | qy(8) qxy(4) | qz(16) qxz(32) | qyz(128) qxyz(64)
+    return (a & 1u) | ((a >> 1) << 1) | ((b & 1u) << 3) | ((b >> 1) << 2) | ((c & 1u) << 4) | ((c >> 1) << 5) |
+           ((d & 1u) << 7) | ((d >> 1) << 6);
+}
+
+// K2: one 256-thread block per 1024-cell unit, 4 consecutive cells per thread.  Runs of 4 cells
+// in one row share their corners (20 loads instead of 32); if every brick the run touches was
+// sign-filled by the eval with one sign, the cube indices are known without touching the field.
 __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ uint8_t s_ntri[256], s_nown[256];
     __shared__ uint4 s_red[4];
@@ -159,21 +168,72 @@ __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ c
     s_nown[t] = cases[t].nown;
     __syncthreads();
     const uint32_t u = blockIdx.x;
+    const uint32_t L0 = u * kUnitCells + 4u * (uint32_t)t;
     unsigned own = 0, tri = 0, act = 0, halo_own = 0;
+    if (L0 < (uint64_t)g.n_cells) {
+        int cx, cy, cz;
+        cell_coords(g, L0, cx, cy, cz);
+        uint32_t ci4 = 0;
+        if (cx + 3 <= g.m && L0 + 3 < (uint64_t)g.n_cells) {
+            // stored coordinates of the run's first corner; the run reads x0 .. x0+4
+            const int x0 = cx - 1, y0 = cy - 1, z0 = cz - g.fz0;
+            const int bx0 = x0 / kBX, bx1 = (x0 + 4) / kBX, by0 = y0 / kBY, by1 = (y0 + 1) / kBY;
+            const int bz0 = z0 / kBZ, bz1 = (z0 + 1) / kBZ;
+            const int sby = b.nbx, sbz = b.nbx * b.nby;
+            const uint8_t* fb = b.fill;
+            unsigned f_and = 3u, f_or = 0u;
 #pragma unroll
-    for (int k = 0; k < kUnitCells / 256; ++k) {
-        const uint32_t L = u * kUnitCells + k * 256 + t;
-        if (L < (uint64_t)g.n_cells) {
-            int cx, cy, cz;
-            cell_coords(g, L, cx, cy, cz);
-            CellVals v;
-            const unsigned ci = load_cell(b.field, g, cx, cy, cz, v);
-            b.ci[L] = (uint8_t)ci;
-            const unsigned no = s_nown[ci], nt = s_ntri[ci];
-            own += no;
-            if (cz >= g.cz_emit) { tri += nt; act += nt ? 1u : 0u; }
-            else halo_own += no;
+            for (int k = 0; k < 8; ++k) {
+                const unsigned v = fb[((k & 1) ? bx1 : bx0) + ((k & 2) ? by1 : by0) * sby + ((k & 4) ? bz1 : bz0) * sbz];
+                f_and &= v;
+                f_or |= v;
+            }
+            const unsigned f0 = f_or;
+            if (f0 != 0u && f_and == f_or) {   // all eight equal and non-zero
+                // all touched bricks filled with one sign: every corner has that sign
+                ci4 = (f0 == kBrickNeg) ? 0xffffffffu : 0u;
+            } else {
+                const int n = g.n, nn = n * n;
+                const float* q = b.field + (x0 + y0 * n + z0 * nn);
+                unsigned r00 = 0, r10 = 0, r01 = 0, r11 = 0;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    r00 |= (q[k] < 0.f ? 1u : 0u) << k;
+                    r10 |= (q[n + k] < 0.f ? 1u : 0u) << k;
+                    r01 |= (q[nn + k] < 0.f ? 1u : 0u) << k;
+                    r11 |= (q[nn + n + k] < 0.f ? 1u : 0u) << k;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ci4 |= ci_from_rows(r00, r10, r01, r11, k) << (8 * k);
+            }
+            unsigned o = 0, tr = 0, ac = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const unsigned ci = (ci4 >> (8 * k)) & 255u;
+                o += s_nown[ci];
+                const unsigned nt = s_ntri[ci];
+                tr += nt;
+                ac += nt ? 1u : 0u;
+            }
+            own = o;
+            if (cz >= g.cz_emit) { tri = tr; act = ac; }
+            else halo_own = o;
+        } else {
+            // the run crosses a row end (or the slab end): cell by cell
+            int x = cx, y = cy, z = cz;
+            for (int k = 0; k < 4; ++k) {
+                if (L0 + k >= (uint64_t)g.n_cells) break;
+                CellVals v;
+                const unsigned ci = load_cell(b.field, g, x, y, z, v);
+                ci4 |= ci << (8 * k);
+                const unsigned no = s_nown[ci], nt = s_ntri[ci];
+                own += no;
+                if (z >= g.cz_emit) { tri += nt; act += nt ? 1u : 0u; }
+                else halo_own += no;
+                if (++x > g.m) { x = 1; if (++y > g.m) { y = 1; ++z; } }
+            }
         }
+        *reinterpret_cast<uint32_t*>(b.ci + L0) = ci4;   // ci has >= 64 bytes of padding
     }
     const int lane = t & 63, wid = t >> 6;
 #pragma unroll
@@ -186,9 +246,9 @@ __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ c
     if (lane == 0) s_red[wid] = make_uint4(own, tri, act, halo_own);
     __syncthreads();
     if (t == 0) {
-        uint4 s = s_red[0];
-        for (int w = 1; w < 4; ++w) { s.x += s_red[w].x; s.y += s_red[w].y; s.z += s_red[w].z; s.w += s_red[w].w; }
-        b.unit_cnt[u] = s;
+        uint4 sm = s_red[0];
+        for (int w = 1; w < 4; ++w) { sm.x += s_red[w].x; sm.y += s_red[w].y; sm.z += s_red[w].z; sm.w += s_red[w].w; }
+        b.unit_cnt[u] = sm;
     }
 }
 

@@ -214,15 +214,16 @@ def _field(impli, shape, mc, level):
 
 
 def _needed_samples(f):
-    """Stored samples whose exact value marching cubes can read: ends of a sign-changing axis
-    edge, including edges to the sealed (-1e7) border."""
+    """Stored samples whose exact value marching cubes can read: the ends of a sign-changing
+    axis edge (the sealed ring is stored, so every edge a cell has lies inside the array)."""
     neg = f < 0
-    p = np.pad(neg, 1, constant_values=True)      # sealed neighbours are negative
-    c = p[1:-1, 1:-1, 1:-1]
-    need = np.zeros_like(c)
+    need = np.zeros_like(neg)
     for ax in range(3):
-        for d in (-1, 1):
-            need |= c != np.roll(p, d, axis=ax)[1:-1, 1:-1, 1:-1]
+        a = np.moveaxis(neg, ax, 0)
+        nv = np.moveaxis(need, ax, 0)
+        d = a[1:] != a[:-1]
+        nv[1:] |= d
+        nv[:-1] |= d
     return need
 
 
