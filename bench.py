@@ -27,7 +27,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
-FP32_PEAK_TFLOPS = 157.3     # vector FP32 peak (same doc)
 
 # algorithmic FP ops per sample for one instruction of the node program
 OP_FLOPS = {"xform": 18, "csg": 2, 3: 9, 4: 45, 5: 24, 6: 20, 7: 24, 8: 14, 9: 12}
@@ -49,7 +48,7 @@ def program_flops(shape):
     return walk(shape), n_instr, depth
 
 
-def cpu_baseline(shape, target_s=15.0):
+def cpu_baseline(shape, target_s=20.0):
     """Oracle (CPU restatement, 1 thread) eval + MC of the same tree on a bounded sample."""
     import oracle
     oracle.build()
@@ -60,7 +59,7 @@ def cpu_baseline(shape, target_s=15.0):
     oracle.marching_cubes(tree, R, box)
     dt = time.perf_counter() - t0
     # scale the sample so it runs about target_s seconds
-    R = int(max(48, min(384, R * (target_s / max(dt, 1e-3)) ** (1 / 3))))
+    R = int(max(48, min(512, R * (target_s / max(dt, 1e-3)) ** (1 / 3))))
     t0 = time.perf_counter()
     v, f = oracle.marching_cubes(tree, R, box)
     dt = time.perf_counter() - t0
@@ -150,8 +149,18 @@ def main():
         kms = {"eval": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
                "mc_count_scan": float(np.mean([e[1].elapsed_time(e[2]) for e in ev])),
                "mc_emit": float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))}
-        info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, shape=shape,
-                    slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats())
+        # per-kernel durations: HIP events recorded by the engine between its launches on this
+        # stream, over a few extra steps after the timed region (so it is not perturbed)
+        slab.set_timing(True)
+        per = []
+        for _ in range(5):
+            step()
+            per.append(slab.kernel_times())
+        slab.set_timing(False)
+        kernel_ms = {k: float(np.mean([p[k] for p in per])) for k in per[0]}
+        info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, kernel_ms=kernel_ms,
+                    shape=shape, slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats(),
+                    fz=(slab.fz0, slab.fz1))
         slab.close()
         return info
 
@@ -167,25 +176,34 @@ def main():
     R = main_run["R"]
     ms = main_run["elapsed"] / args.steps * 1e3
     value = R ** 3 / (ms * 1e-3) / 1e6
-    flops_per_sample, n_instr, depth = program_flops(main_run["shape"])
     kms = main_run["kernels_ms"]
-    # rank-0 slab sizes for the per-kernel roofline
-    layers = main_run["slab_layers"]
-    samples = (R + 1) ** 2 * min(R + 1, layers + 1)
-    cells = (R + 2) ** 2 * layers
-    dom = max(kms, key=kms.get)
-    alg_bytes = {"eval": 4.0 * samples,
-                 "mc_count_scan": 4.0 * samples,
-                 "mc_emit": 12.0 * (main_run["nv"] + main_run["nf"]) / max(1, args.gpus)}
-    achieved = alg_bytes[dom] / (kms[dom] * 1e-3) / 1e9
+    kern = main_run["kernel_ms"]
+    _, n_instr, depth = program_flops(main_run["shape"])
+    # rank-0 slab: stored samples (n = R+3 per axis incl. the sealed ring), cells, bricks
+    n_side = R + 3
+    samples = n_side * n_side * (main_run["fz"][1] - main_run["fz"][0])
+    cells = (R + 2) ** 2 * main_run["slab_layers"]
+    bricks_total, bricks_mixed, bricks_filled = main_run["bricks"]
+    nv, nf = main_run["nv"], main_run["nf"]
+    # algorithmic bytes per launch (DESIGN.md "Roofline"): what each kernel must move
+    alg = {"brick_modes": 9.0 * bricks_total,                        # modes u64 + class u8 per brick
+           "eval_field": 4.0 * samples + bricks_total,               # one f32 store per sample + fill byte
+           "mc_count": 4.0 * samples + 1.0 * cells,                  # field read + cube-index byte
+           "mc_scan": 16.0 * 2 * (cells / 1024.0),                   # unit counts read + written
+           "mc_verts": 12.0 * nv / max(1, world) + 12.0 * nv / max(1, world),   # vertices + vid3 slots
+           "mc_faces": 12.0 * nf / max(1, world) + 16.0 * nf / 2 / max(1, world)}  # faces + records
+    dom = max(kern, key=kern.get)
+    achieved = alg[dom] / (kern[dom] * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic_r01.json")
     if os.path.exists(tfile):
         try:
-            traffic = json.load(open(tfile)).get(dom)
+            traffic = json.load(open(tfile)).get("bytes_per_launch", {}).get(dom)
         except Exception:
             traffic = None
-    valu_tflops = flops_per_sample * samples / (kms["eval"] * 1e-3) / 1e12
+    # whole eval+MC pipeline, B = 8 (R+1)^3 + 12 V + 12 F over the kernel time
+    b_pipe = 8.0 * (R + 1) ** 3 + 12.0 * nv + 12.0 * nf
+    t_kern = sum(kern.values()) * 1e-3
     out = {
         "metric": "Mvoxels/s (eval+MC) at 256^3 & 512^3",
         "value": round(value, 2),
@@ -203,16 +221,19 @@ def main():
             "workload": "config4: seeded 21-node MP5 CSG tree (scenes.config4, seed 20251015), box [-1,1]^3, "
                         "R=%d, eval+MC, mesh resident in HBM" % R,
             "resolution": R, "voxels": R ** 3, "samples": (R + 1) ** 3, "cells": (R + 2) ** 3,
-            "verts": main_run["nv"], "faces": main_run["nf"], "program_instr": n_instr, "tree_depth": depth,
+            "verts": nv, "faces": nf, "program_instr": n_instr, "tree_depth": depth,
             "parallelism": "zslab%d" % world,
         },
         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
-        "bricks": dict(zip(["total", "mixed", "sign_filled"], main_run["bricks"])),
+        "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
+        "bricks": {"total": bricks_total, "mixed": bricks_mixed, "sign_filled": bricks_filled,
+                   "evaluated_sample_frac": round(1.0 - bricks_filled / max(1, bricks_total), 4)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes[dom]},
-        "valu": {"kernel": "eval", "flops_per_sample": flops_per_sample, "achieved": round(valu_tflops, 2),
-                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(valu_tflops / FP32_PEAK_TFLOPS, 4)},
+                     "alg_bytes_per_launch": alg[dom],
+                     "pipeline": {"bytes": b_pipe, "kernel_ms": round(t_kern * 1e3, 4),
+                                  "achieved": round(b_pipe / t_kern / 1e9, 1),
+                                  "frac": round(b_pipe / t_kern / 1e9 / HBM_PEAK_GBS, 4)}},
     }
     if r256:
         ms256 = r256["elapsed"] / args.steps * 1e3

@@ -29,6 +29,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
     "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
     "implisolid_parse_settings", "implisolid_slab_partition", "implisolid_slab_brick_stats",
+    "implisolid_slab_set_timing", "implisolid_slab_kernel_times",
 ]
 
 _lib = None
@@ -90,6 +91,8 @@ def lib():
         "implisolid_parse_settings": ([c_char_p, fp, ip, fp], c_int),
         "implisolid_slab_partition": ([c_int, c_int, c_int, ip], c_int),
         "implisolid_slab_brick_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
+        "implisolid_slab_set_timing": ([c_void_p, c_int], c_int),
+        "implisolid_slab_kernel_times": ([c_void_p, fp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -319,6 +322,17 @@ class Slab:
 
     def field_ptr(self):
         return lib().implisolid_slab_field(self.h)
+
+    KERNELS = ("brick_modes", "eval_field", "mc_count", "mc_scan", "mc_verts", "mc_faces")
+
+    def set_timing(self, on=True):
+        self._rc(lib().implisolid_slab_set_timing(self.h, 1 if on else 0))
+
+    def kernel_times(self):
+        """ms per kernel of the last timed eval/count/emit (HIP events on the launch stream)."""
+        out = (ctypes.c_float * 6)()
+        self._rc(lib().implisolid_slab_kernel_times(self.h, out))
+        return dict(zip(self.KERNELS, [float(x) for x in out]))
 
     def brick_stats(self):
         """[bricks, mixed-sign bricks, sign-filled bricks] of the last eval."""

@@ -432,6 +432,9 @@ float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
 int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
 float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
 
+int implisolid_slab_set_timing(implisolid_slab* s, int on) { SLAB_TRY(s->engine.set_timing(on != 0)) }
+int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]) { SLAB_TRY(s->engine.kernel_times(ms)) }
+
 int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]) {
     try {
         s->engine.brick_stats(out, 0);

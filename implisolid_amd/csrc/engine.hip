@@ -95,7 +95,26 @@ void Engine::download(float* verts, int32_t* faces, const SlabCounts& c, hipStre
     IMPLI_HIP(hipStreamSynchronize(s));
 }
 
+void Engine::set_timing(bool on) {
+    if (on && !ev_[0])
+        for (auto& e : ev_) IMPLI_HIP(hipEventCreate(&e));
+    timing_ = on;
+}
+
+void Engine::kernel_times(float out[kTimedKernels]) {
+    if (!ev_[0]) throw InputError("kernel timing was never enabled");
+    IMPLI_HIP(hipEventSynchronize(ev_[8]));
+    const int pairs[kTimedKernels][2] = {{0, 1}, {1, 2}, {3, 4}, {4, 5}, {6, 7}, {7, 8}};
+    for (int k = 0; k < kTimedKernels; ++k) {
+        float ms = 0.f;
+        IMPLI_HIP(hipEventElapsedTime(&ms, ev_[pairs[k][0]], ev_[pairs[k][1]]));
+        out[k] = ms;
+    }
+}
+
 Engine::~Engine() {
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
     DevBuf* all[] = {&offsets_, &modes_, &cls_, &fill_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
                      &records_, &verts_, &faces_, &overflow_};
     for (auto* b : all) b->release();
@@ -171,14 +190,17 @@ MCBuffers Engine::buffers() const {
 void Engine::eval_field(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
     const int level = pruning();
+    mark(0, s);
     if (level > 0) {
         launch_eval_field_pruned(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_,
                                  modes_.as<uint64_t>(), cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2,
-                                 field_.as<float>(), s);
+                                 field_.as<float>(), s, timing_ ? ev_[1] : nullptr);
     } else {
         IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled
+        mark(1, s);
         launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
     }
+    mark(2, s);
     IMPLI_HIP(hipGetLastError());
 }
 
@@ -186,15 +208,20 @@ void Engine::count(hipStream_t s) {
     IMPLI_HIP(hipMemsetAsync(counters_.p, 0, 16 * sizeof(uint32_t), s));
     IMPLI_HIP(hipMemsetAsync(overflow_.p, 0, 16, s));
     MCBuffers b = buffers();
+    mark(3, s);
     launch_mc_count(cases_.as<CaseInfo>(), grid_, b, s);
+    mark(4, s);
     launch_mc_scan(grid_, b, s);
+    mark(5, s);
     IMPLI_HIP(hipGetLastError());
 }
 
 void Engine::emit(const uint32_t* d_offsets, hipStream_t s) {
     MCBuffers b = buffers();
     b.offsets = d_offsets ? d_offsets : offsets_.as<uint32_t>();
-    launch_mc_emit(cases_.as<CaseInfo>(), grid_, b, s);
+    mark(6, s);
+    launch_mc_emit(cases_.as<CaseInfo>(), grid_, b, s, timing_ ? ev_[7] : nullptr);
+    mark(8, s);
     IMPLI_HIP(hipGetLastError());
 }
 

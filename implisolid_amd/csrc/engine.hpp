@@ -75,6 +75,12 @@ public:
     //   0 off, 1 CSG operand pruning (field bit-identical), 2 + sign-only bricks (mesh bit-identical)
     static void set_pruning(int level);
     static int pruning();
+    // per-kernel HIP-event timing of the next eval/count/emit calls (stream-ordered, no sync);
+    // kernel_times() blocks and returns ms for: brick pass, field eval, MC count, unit scan,
+    // vertex emission, face emission
+    static constexpr int kTimedKernels = 6;
+    void set_timing(bool on);
+    void kernel_times(float out[kTimedKernels]);
     // brick statistics of the last pruned eval: [bricks, mixed, sign-filled]; blocking
     void brick_stats(int64_t out[3], hipStream_t stream);
 
@@ -89,6 +95,11 @@ private:
     DevBuf prog_, rabbit_, cases_;
     DevBuf offsets_, modes_, cls_, fill_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
+    bool timing_ = false;
+    hipEvent_t ev_[9] = {};
+    void mark(int i, hipStream_t s) {
+        if (timing_) IMPLI_HIP(hipEventRecord(ev_[i], s));
+    }
     DevBuf scratch_[16];
 };
 

@@ -205,7 +205,7 @@ BrickGrid brick_grid(const GridDesc& g) {
 
 void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range,
                               const GridDesc& g, uint64_t* d_modes, uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                              float* d_field, hipStream_t s) {
+                              float* d_field, hipStream_t s, hipEvent_t mid) {
     const BrickGrid bg = brick_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
@@ -213,6 +213,7 @@ void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_r
 #define IMPLI_PRUNED(DD)                                                                             \
     do {                                                                                             \
         k_brick_modes<DD><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);    \
+        if (mid) (void)hipEventRecord(mid, s);                                                       \
         k_eval_field_pruned<DD><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill,    \
                                                    sign_fill, d_field);                              \
     } while (0)

@@ -50,7 +50,7 @@ struct BrickGrid { int nbx, nby, nbz, n_bricks; };
 BrickGrid brick_grid(const GridDesc& g);
 void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range,
                               const GridDesc& g, uint64_t* d_modes, uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                              float* d_field, hipStream_t s);
+                              float* d_field, hipStream_t s, hipEvent_t mid = nullptr);
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
                         float* d_f, float* d_grad /* nullable: values only */, hipStream_t s);
 
@@ -77,7 +77,8 @@ struct MCBuffers {
 };
 void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s);
-void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
+void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s,
+                    hipEvent_t mid = nullptr /* recorded between the vertex and face kernels */);
 
 inline int64_t n_units(const GridDesc& g) { return (g.n_cells + kUnitCells - 1) / kUnitCells; }
 inline int64_t n_scan_blocks(const GridDesc& g) { return (n_units(g) + kScanBlock - 1) / kScanBlock; }

@@ -486,8 +486,9 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     if (nb > 0) k_scan_apply<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk, b.active_units);
 }
 
-void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
+void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s, hipEvent_t mid) {
     k_mc_verts<<<1024, 256, 0, s>>>(d_cases, g, b);
+    if (mid) (void)hipEventRecord(mid, s);
     k_mc_faces<<<2048, 256, 0, s>>>(d_cases, g, b);
 }
 

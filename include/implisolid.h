@@ -131,6 +131,11 @@ float* implisolid_slab_field(implisolid_slab* s);
 /* blocking copy of the slab's stored field samples (n*n*layers floats, x fastest); with out ==
  * NULL returns the sample count only */
 int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capacity);
+/* per-kernel HIP-event timing (stream-ordered, no synchronisation) of the following eval /
+ * count / emit calls; kernel_times blocks and returns milliseconds of the last timed calls for
+ * [brick pass, field eval, MC count, unit scan, vertex emission, face emission] */
+int implisolid_slab_set_timing(implisolid_slab* s, int on);
+int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]);
 /* bricks of the last slab eval: out = [bricks, mixed-sign bricks, sign-filled bricks] (blocking) */
 int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]);
 
