@@ -325,3 +325,27 @@ def test_zslab_offsets_gloo(world):
         p.join(timeout=60)
     for rank, ok, got, exp in sorted(res):
         assert ok, (rank, got, exp)
+
+
+# ---- JavaScript binding (N-API addon over the C ABI) -----------------------------------------------
+def _node_ok():
+    import shutil
+    return shutil.which("node") and os.path.exists("/usr/include/node/node_api.h")
+
+
+@pytest.mark.skipif(not _node_ok(), reason="node or node headers absent")
+def test_node_addon_exports(impli):
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "bindings", "node")], check=True)
+    js = ("const {impli1, native} = require('./bindings/node/impli1.js');"
+          "impli1.set_error_mode(1);"
+          "const ok = native.program_info(JSON.stringify({type:'iellipsoid', matrix:[1,0,0,0,0,1,0,0,0,0,1,0]}));"
+          "const bad = native.program_info('{\"type\":\"bogus\",\"matrix\":[1,0,0,0,0,1,0,0,0,0,1,0]}');"
+          "console.log(JSON.stringify({keys: Object.keys(native), ok, bad, err: impli1.last_error()}));")
+    r = subprocess.run(["node", "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    need = {"build_geometry", "get_v_size", "get_f_size", "get_v", "get_f", "finish_geometry", "set_object",
+            "unset_object", "set_x", "unset_x", "calculate_implicit_values", "get_values",
+            "calculate_implicit_gradients", "get_gradients", "get_pointset", "about"}
+    assert need <= set(out["keys"])
+    assert out["ok"] == 2 and out["bad"] == -1 and "Invalid object" in out["err"]

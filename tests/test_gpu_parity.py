@@ -298,3 +298,28 @@ def test_golden_mc_summaries_gpu(impli):
         assert (len(v), len(f)) == (s["n_verts"], s["n_faces"]), name
         assert hashlib.sha256(np.ascontiguousarray(f).tobytes()).hexdigest() == s["sha256_faces"], name
         assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"], name
+
+
+def test_node_addon_config1_gpu(impli):
+    import os
+    import shutil
+    import subprocess
+    if not (shutil.which("node") and os.path.exists("/usr/include/node/node_api.h")):
+        pytest.skip("node or node headers absent")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "bindings", "node")], check=True)
+    g = np.load(_golden("config1_mc.npz"))
+    js = ("const {make_geometry} = require('./bindings/node/impli1.js');"
+          "const fs = require('fs');"
+          "make_geometry(process.argv[1], process.argv[2], (v, f) => {"
+          "  fs.writeFileSync(process.argv[3], Buffer.from(v.buffer));"
+          "  fs.writeFileSync(process.argv[4], Buffer.from(f.buffer)); });")
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        vp, fp = os.path.join(d, "v.bin"), os.path.join(d, "f.bin")
+        r = subprocess.run(["node", "-e", js, str(g["shape"]), str(g["mc"]), vp, fp], cwd=root,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        v = np.fromfile(vp, np.float32).reshape(-1, 3)
+        f = np.fromfile(fp, np.uint32).reshape(-1, 3).astype(np.int32)
+    assert np.array_equal(f, g["faces"]) and np.array_equal(v.view(np.uint32), g["verts"].view(np.uint32))
