@@ -160,7 +160,7 @@ def main():
         kernel_ms = {k: float(np.mean([p[k] for p in per])) for k in per[0]}
         info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, kernel_ms=kernel_ms,
                     shape=shape, slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats(),
-                    fz=(slab.fz0, slab.fz1))
+                    fz=(slab.fz0, slab.fz1), jit=slab.used_jit())
         slab.close()
         return info
 
@@ -226,6 +226,7 @@ def main():
         },
         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
         "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
+        "eval_kernel": "jit" if main_run["jit"] else "interpreter",
         "bricks": {"total": bricks_total, "mixed": bricks_mixed, "sign_filled": bricks_filled,
                    "evaluated_sample_frac": round(1.0 - bricks_filled / max(1, bricks_total), 4)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

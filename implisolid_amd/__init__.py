@@ -29,7 +29,8 @@ ABI_SYMBOLS = [
     "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
     "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
     "implisolid_parse_settings", "implisolid_slab_partition", "implisolid_slab_brick_stats",
-    "implisolid_slab_set_timing", "implisolid_slab_kernel_times",
+    "implisolid_slab_set_timing", "implisolid_slab_kernel_times", "implisolid_jit_compile",
+    "implisolid_slab_used_jit", "implisolid_set_jit",
 ]
 
 _lib = None
@@ -92,6 +93,10 @@ def lib():
         "implisolid_slab_partition": ([c_int, c_int, c_int, ip], c_int),
         "implisolid_slab_brick_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
         "implisolid_slab_set_timing": ([c_void_p, c_int], c_int),
+        "implisolid_slab_used_jit": ([c_void_p], c_int),
+        "implisolid_set_jit": ([c_int], None),
+        "implisolid_jit_compile": ([c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)],
+                                   ctypes.c_int64),
         "implisolid_slab_kernel_times": ([c_void_p, fp], c_int),
     }
     for name, (args, res) in sig.items():
@@ -137,6 +142,22 @@ def slab_partition(R, rank, nranks):
     if lib().implisolid_slab_partition(int(R), int(rank), int(nranks), out) != 0:
         raise ImplisolidError(last_error())
     return int(out[0]), int(out[1]), int(out[2])
+
+
+def set_jit(on):
+    """Compile tree kernels with hipRTC for objects set from now on (default on)."""
+    lib().implisolid_set_jit(1 if on else 0)
+
+
+def jit_compile(shape):
+    """Host-only: (code-object bytes, compile seconds, generated source) of the shape's tree kernel."""
+    L = lib()
+    buf = ctypes.create_string_buffer(1 << 20)
+    secs = ctypes.c_double(0)
+    n = L.implisolid_jit_compile(_s(shape), buf, len(buf), ctypes.byref(secs))
+    if n < 0:
+        raise ImplisolidError(last_error())
+    return int(n), float(secs.value), buf.value.decode()
 
 
 def set_pruning(level):
@@ -333,6 +354,9 @@ class Slab:
         out = (ctypes.c_float * 6)()
         self._rc(lib().implisolid_slab_kernel_times(self.h, out))
         return dict(zip(self.KERNELS, [float(x) for x in out]))
+
+    def used_jit(self):
+        return bool(lib().implisolid_slab_used_jit(self.h))
 
     def brick_stats(self):
         """[bricks, mixed-sign bricks, sign-filled bricks] of the last eval."""

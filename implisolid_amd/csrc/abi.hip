@@ -10,6 +10,9 @@
 
 #include "../../include/implisolid.h"
 #include "engine.hpp"
+#include "jit.hpp"
+
+#include <chrono>
 #include "host.hpp"
 #include "ob02.hpp"
 
@@ -337,6 +340,26 @@ void about(void) {
     std::fprintf(stderr, "CONFIG: ROOT_TOLERANCE=%g \n", (double)(float)(0.001 / 10.0));
 }
 
+int64_t implisolid_jit_compile(const char* shape_json, char* source_out, int64_t capacity, double* seconds) {
+    g_last_error.clear();
+    try {
+        const Program p = compile_mp5(shape_json, false);
+        const std::string src = TreeJit::kernel_source(p);
+        if (source_out && capacity > 0) {
+            const size_t n = std::min<size_t>(src.size(), (size_t)capacity - 1);
+            std::memcpy(source_out, src.data(), n);
+            source_out[n] = 0;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        const std::vector<char> code = TreeJit::compile(src);
+        if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return (int64_t)code.size();
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+}
+
 int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int32_t info[4], float* mats_out) {
     g_last_error.clear();
     try {
@@ -431,6 +454,9 @@ int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, v
 float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
 int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
 float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
+
+int implisolid_slab_used_jit(implisolid_slab* s) { return s->engine.used_jit() ? 1 : 0; }
+void implisolid_set_jit(int on) { TreeJit::instance().set_enabled(on != 0); }
 
 int implisolid_slab_set_timing(implisolid_slab* s, int on) { SLAB_TRY(s->engine.set_timing(on != 0)) }
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]) { SLAB_TRY(s->engine.kernel_times(ms)) }

@@ -6,7 +6,10 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <cstddef>
+
 #include "ifunc_device.hpp"
+#include "jit.hpp"
 
 namespace impli {
 
@@ -125,6 +128,9 @@ void Engine::set_object(const Program& prog) {
     IMPLI_HIP(hipMemcpy(prog_.p, &prog, sizeof(Program), hipMemcpyHostToDevice));
     depth_ = prog.max_depth;
     n_csg_ = prog.n_csg;
+    prog_host_ = prog;
+    jit_tried_ = false;
+    jit_fn_ = nullptr;
     have_object_ = true;
 }
 
@@ -192,9 +198,22 @@ void Engine::eval_field(hipStream_t s) {
     const int level = pruning();
     mark(0, s);
     if (level > 0) {
-        launch_eval_field_pruned(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_,
-                                 modes_.as<uint64_t>(), cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2,
-                                 field_.as<float>(), s, timing_ ? ev_[1] : nullptr);
+        if (!jit_tried_) {   // compile the tree kernel for this shape once (cached by shape)
+            jit_fn_ = TreeJit::instance().brick_kernel(prog_host_);
+            jit_tried_ = true;
+        }
+        launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, modes_.as<uint64_t>(),
+                           cls_.as<uint8_t>(), s);
+        mark(1, s);
+        if (jit_fn_) {
+            const float* d_mats = reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
+            TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_),
+                                   modes_.as<uint64_t>(), cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2,
+                                   field_.as<float>(), s);
+        } else {
+            launch_eval_bricks_interp(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, modes_.as<uint64_t>(),
+                                      cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2, field_.as<float>(), s);
+        }
     } else {
         IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled
         mark(1, s);

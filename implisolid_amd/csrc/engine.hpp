@@ -66,6 +66,8 @@ public:
     const uint32_t* d_counters() const { return counters_.as<uint32_t>(); }
     int depth() const { return depth_; }
     const Program* d_program() const { return prog_.as<Program>(); }
+    // true if the last eval_field ran the JIT-compiled tree kernel
+    bool used_jit() const { return jit_fn_ != nullptr; }
     const float* d_rabbit() const { return rabbit_.as<float>(); }
 
     DevBuf& scratch(int k) { return scratch_[k]; }
@@ -90,6 +92,9 @@ private:
     GridDesc grid_{};
     int depth_ = 1;
     int n_csg_ = 0;
+    Program prog_host_{};
+    bool jit_tried_ = false;
+    hipFunction_t jit_fn_ = nullptr;
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;

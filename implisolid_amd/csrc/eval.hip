@@ -19,27 +19,12 @@
 
 #include "ifunc_device.hpp"
 #include "ifunc_interval.hpp"
+#include "eval_bricks.hpp"
 #include "kernels.hpp"
 
 namespace impli {
 
 using namespace dev;
-
-// sample coordinate of stored index i (sample i + 1) along an axis (prepare_grid,
-// marching_cubes.hpp:1691-1693: x * factor + min - 2 * width)
-__device__ __forceinline__ float sample_xy(const GridDesc& g, int axis, int i) {
-    return ((float)(i + 1) * g.w[axis] + g.lo[axis]) - 2.f * g.w[axis];
-}
-__device__ __forceinline__ float sample_z(const GridDesc& g, int layer) {
-    return ((float)(g.fz0 + layer) * g.w[2] + g.lo[2]) - 2.f * g.w[2];
-}
-// seal_exterior (:895-963): samples 1 and res-2 of any axis hold -1e7
-__device__ __forceinline__ bool sealed_xy(const GridDesc& g, int i) { return i == 0 || i == g.n - 1; }
-__device__ __forceinline__ bool sealed_z(const GridDesc& g, int layer) {
-    const int sz = g.fz0 + layer;
-    return sz == 1 || sz == g.res - 2;
-}
-constexpr float kSealed = -10000000.0f;
 
 template <int D>
 __global__ __launch_bounds__(256) void k_eval_field(const Program* __restrict__ prog, const float* __restrict__ tab,
@@ -54,13 +39,6 @@ __global__ __launch_bounds__(256) void k_eval_field(const Program* __restrict__ 
     if (!(sealed_xy(g, (int)sx) || sealed_xy(g, (int)sy) || sealed_z(g, layer)))
         f = 0.f + eval_f<D>(prog, tab, sample_xy(g, 0, (int)sx), sample_xy(g, 1, (int)sy), sample_z(g, layer));
     field[(size_t)layer * plane + i] = f;   // eval_shape: field (zero) += value
-}
-
-__device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, int& by, int& bz) {
-    bx = b % bg.nbx;
-    const int t = b / bg.nbx;
-    by = t % bg.nby;
-    bz = t / bg.nby;
 }
 
 template <int D>
@@ -94,19 +72,14 @@ __global__ __launch_bounds__(256) void k_brick_modes(const Program* __restrict__
     cls[b] = c;
 }
 
-// A brick needs exact values only if one of its samples can be the end of a sign-changing cell
-// edge.  Edges are axis aligned, so that requires the brick or a face neighbour to differ in
-// sign class.  Neighbours outside the stored grid hold no sample any cell of this slab reads.
-__device__ __forceinline__ uint32_t brick_fill_class(const uint8_t* __restrict__ cls, const BrickGrid& bg, int b,
-                                                     int bx, int by, int bz) {
-    const uint32_t cb = cls[b], c = cb & 3u;
-    if (c == kBrickMixed || (cb & kBrickNoFill)) return kBrickMixed;
-    const int sy = bg.nbx, sz = bg.nbx * bg.nby;
-    const uint32_t xm = bx > 0 ? cls[b - 1] & 3u : c, xp = bx + 1 < bg.nbx ? cls[b + 1] & 3u : c;
-    const uint32_t ym = by > 0 ? cls[b - sy] & 3u : c, yp = by + 1 < bg.nby ? cls[b + sy] & 3u : c;
-    const uint32_t zm = bz > 0 ? cls[b - sz] & 3u : c, zp = bz + 1 < bg.nbz ? cls[b + sz] & 3u : c;
-    return (xm == c && xp == c && ym == c && yp == c && zm == c && zp == c) ? c : (uint32_t)kBrickMixed;
-}
+template <int D>
+struct InterpEval {   // the node-program interpreter with per-brick operand skipping
+    const Program* prog;
+    const float* tab;
+    __device__ __forceinline__ float operator()(uint64_t m, float x, float y, float z) const {
+        return eval_f_pruned<D>(prog, tab, m, x, y, z);
+    }
+};
 
 template <int D>
 __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __restrict__ prog,
@@ -115,40 +88,7 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __rest
                                                            const uint8_t* __restrict__ cls,
                                                            uint8_t* __restrict__ fill, int sign_fill,
                                                            float* __restrict__ field) {
-    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-    if (b >= bg.n_bricks) return;
-    const int lane = threadIdx.x & 63;
-    int bx, by, bz;
-    brick_of(b, bg, bx, by, bz);
-    const int n = g.n;
-    const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
-    const bool ok = sx < n && sy < n;
-    const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
-    const int layers = g.fz1 - g.fz0;
-    const size_t plane = (size_t)n * n;
-    float* out = field + (size_t)sy * n + sx;
-    const uint32_t fc = sign_fill ? brick_fill_class(cls, bg, b, bx, by, bz) : (uint32_t)kBrickMixed;
-    if (lane == 0) fill[b] = (uint8_t)fc;
-    if (fc != kBrickMixed) {   // only the sign is ever read: any value of that sign will do
-        const float v = (fc == kBrickPos) ? 1.f : -1.f;
-        for (int k = 0; k < kBZ; ++k) {
-            const int layer = bz * kBZ + k;
-            if (layer >= layers) break;
-            if (ok) out[(size_t)layer * plane] = (sealed_col || sealed_z(g, layer)) ? kSealed : v;
-        }
-        return;
-    }
-    const uint64_t m64 = modes[b];
-    const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
-                       (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
-    const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
-#pragma unroll 1
-    for (int k = 0; k < kBZ; ++k) {
-        const int layer = bz * kBZ + k;
-        if (layer >= layers) break;
-        const float f = eval_f_pruned<D>(prog, tab, m, x, y, sample_z(g, layer));
-        if (ok) out[(size_t)layer * plane] = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
-    }
+    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, cls, fill, sign_fill, field);
 }
 
 template <int D>
@@ -203,25 +143,29 @@ BrickGrid brick_grid(const GridDesc& g) {
     return bg;
 }
 
-void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range,
-                              const GridDesc& g, uint64_t* d_modes, uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                              float* d_field, hipStream_t s, hipEvent_t mid) {
+void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
+                        uint64_t* d_modes, uint8_t* d_cls, hipStream_t s) {
     const BrickGrid bg = brick_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
-    const unsigned tb = (unsigned)((bg.n_bricks + 255) / 256), eb = (unsigned)((bg.n_bricks + 3) / 4);
-#define IMPLI_PRUNED(DD)                                                                             \
-    do {                                                                                             \
-        k_brick_modes<DD><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);    \
-        if (mid) (void)hipEventRecord(mid, s);                                                       \
-        k_eval_field_pruned<DD><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill,    \
-                                                   sign_fill, d_field);                              \
-    } while (0)
-    if (depth <= 4) IMPLI_PRUNED(4);
-    else if (depth <= 8) IMPLI_PRUNED(8);
-    else if (depth <= 12) IMPLI_PRUNED(12);
-    else IMPLI_PRUNED(16);
-#undef IMPLI_PRUNED
+    const unsigned tb = (unsigned)((bg.n_bricks + 255) / 256);
+    if (depth <= 4) k_brick_modes<4><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
+    else if (depth <= 8) k_brick_modes<8><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
+    else if (depth <= 12) k_brick_modes<12><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
+    else k_brick_modes<16><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
+}
+
+void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
+                               const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
+                               float* d_field, hipStream_t s) {
+    const BrickGrid bg = brick_grid(g);
+    if (bg.n_bricks <= 0) return;
+    depth = eval_depth(depth);
+    const unsigned eb = (unsigned)((bg.n_bricks + 3) / 4);
+    if (depth <= 4) k_eval_field_pruned<4><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
+    else if (depth <= 8) k_eval_field_pruned<8><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
+    else if (depth <= 12) k_eval_field_pruned<12><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
+    else k_eval_field_pruned<16><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
 }
 
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,

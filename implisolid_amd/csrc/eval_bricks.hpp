@@ -1,0 +1,89 @@
+// eval_bricks.hpp -- device side of the brick-pruned field evaluation, shared by the static
+// interpreter kernels (eval.hip) and the JIT-compiled tree kernels (jit.cpp).
+#pragma once
+#include "grid.hpp"
+
+namespace impli {
+
+// sample coordinate of stored index i (sample i + 1) along an axis (prepare_grid,
+// marching_cubes.hpp:1691-1693: x * factor + min - 2 * width)
+__device__ __forceinline__ float sample_xy(const GridDesc& g, int axis, int i) {
+    return ((float)(i + 1) * g.w[axis] + g.lo[axis]) - 2.f * g.w[axis];
+}
+__device__ __forceinline__ float sample_z(const GridDesc& g, int layer) {
+    return ((float)(g.fz0 + layer) * g.w[2] + g.lo[2]) - 2.f * g.w[2];
+}
+// seal_exterior (:895-963): samples 1 and res-2 of any axis hold -1e7
+__device__ __forceinline__ bool sealed_xy(const GridDesc& g, int i) { return i == 0 || i == g.n - 1; }
+__device__ __forceinline__ bool sealed_z(const GridDesc& g, int layer) {
+    const int sz = g.fz0 + layer;
+    return sz == 1 || sz == g.res - 2;
+}
+constexpr float kSealed = -10000000.0f;
+
+__device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, int& by, int& bz) {
+    bx = b % bg.nbx;
+    const int t = b / bg.nbx;
+    by = t % bg.nby;
+    bz = t / bg.nby;
+}
+
+// A brick needs exact values only if one of its samples can be the end of a sign-changing cell
+// edge.  Edges are axis aligned, so that requires the brick or a face neighbour to differ in
+// sign class.  Neighbours outside the stored grid hold no sample any cell of this slab reads.
+__device__ __forceinline__ uint32_t brick_fill_class(const uint8_t* __restrict__ cls, const BrickGrid& bg, int b,
+                                                     int bx, int by, int bz) {
+    const uint32_t cb = cls[b], c = cb & 3u;
+    if (c == kBrickMixed || (cb & kBrickNoFill)) return kBrickMixed;
+    const int sy = bg.nbx, sz = bg.nbx * bg.nby;
+    const uint32_t xm = bx > 0 ? cls[b - 1] & 3u : c, xp = bx + 1 < bg.nbx ? cls[b + 1] & 3u : c;
+    const uint32_t ym = by > 0 ? cls[b - sy] & 3u : c, yp = by + 1 < bg.nby ? cls[b + sy] & 3u : c;
+    const uint32_t zm = bz > 0 ? cls[b - sz] & 3u : c, zp = bz + 1 < bg.nbz ? cls[b + sz] & 3u : c;
+    return (xm == c && xp == c && ym == c && yp == c && zm == c && zp == c) ? c : (uint32_t)kBrickMixed;
+}
+
+// One wave per brick (16 x 4 lanes, 4 z layers each).  Sign-filled bricks store +-1 (the
+// sealed ring keeps -1e7); others evaluate every sample with `ev(modes, x, y, z)`.
+template <class Eval>
+__device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
+                                                 const uint64_t* __restrict__ modes,
+                                                 const uint8_t* __restrict__ cls, uint8_t* __restrict__ fill,
+                                                 int sign_fill, float* __restrict__ field) {
+    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+    if (b >= bg.n_bricks) return;
+    const int lane = threadIdx.x & 63;
+    int bx, by, bz;
+    brick_of(b, bg, bx, by, bz);
+    const int n = g.n;
+    const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
+    const bool ok = sx < n && sy < n;
+    const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
+    const int layers = g.fz1 - g.fz0;
+    const size_t plane = (size_t)n * n;
+    float* out = field + (size_t)sy * n + sx;
+    const uint32_t fc = sign_fill ? brick_fill_class(cls, bg, b, bx, by, bz) : (uint32_t)kBrickMixed;
+    if (lane == 0) fill[b] = (uint8_t)fc;
+    if (fc != kBrickMixed) {   // only the sign is ever read: any value of that sign will do
+        const float v = (fc == kBrickPos) ? 1.f : -1.f;
+        for (int k = 0; k < kBZ; ++k) {
+            const int layer = bz * kBZ + k;
+            if (layer >= layers) break;
+            if (ok) out[(size_t)layer * plane] = (sealed_col || sealed_z(g, layer)) ? kSealed : v;
+        }
+        return;
+    }
+    const uint64_t m64 = modes[b];
+    const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
+                       (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
+    const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
+#pragma unroll 1
+    for (int k = 0; k < kBZ; ++k) {
+        const int layer = bz * kBZ + k;
+        if (layer >= layers) break;
+        const float f = ev(m, x, y, sample_z(g, layer));
+        if (ok) out[(size_t)layer * plane] = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
+    }
+}
+
+
+}  // namespace impli

@@ -1,0 +1,34 @@
+// grid.hpp -- sampling grid and brick decomposition shared by the static kernels and the
+// JIT-compiled ones (device-safe: no host declarations).
+#pragma once
+#ifndef __HIPCC_RTC__   // hipRTC (jit.cpp) provides these through its prelude
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#endif
+
+namespace impli {
+
+// Sampling grid of MarchingCubes (marching_cubes.hpp:175-243, 1662-1698) for one Z-slab.
+//   res = R + 5 samples per axis; cells c in [1, res-3] per axis (render_geometry :1033-1039),
+//   m = R + 2 cells per axis.  Cells touch samples [1, res-2]; those are stored (n = R + 3 per
+//   axis, x fastest), the ring s in {1, res-2} holding seal_exterior's -1e7 (:895-963), so every
+//   corner load is unconditional.  Samples 0 and res-1 are never read by any cell.
+struct GridDesc {
+    int R, res, n, m;            // n = R + 3 stored samples per axis, m = R + 2 cells per axis
+    float w[3];                  // widthx/y/z = (max - min) / R
+    float lo[3];                 // box min
+    float i0[3];                 // render offsets xi0 = min / w - 2   (:1026-1028)
+    int cz0, cz1;                // cell layers handled by this slab [cz0, cz1) (incl. halo layer)
+    int cz_emit;                 // first layer whose faces / vertices this slab emits
+    int fz0, fz1;                // stored sample layers [fz0, fz1) = [cz0, cz1 + 1)
+    int64_t n_cells;             // m * m * (cz1 - cz0)
+};
+
+// pruned field evaluation: bricks of kBX x kBY x kBZ stored samples (x fastest)
+constexpr int kBX = 16, kBY = 4, kBZ = 4;
+enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBrickNoFill = 4 };
+// fill[b] (written by the pruned eval): kBrickPos / kBrickNeg if the brick was sign-filled --
+// then no cell corner in it needs its exact value and MC may take the sign from fill -- else 0.
+struct BrickGrid { int nbx, nby, nbz, n_bricks; };
+
+}  // namespace impli

@@ -10,8 +10,10 @@
 // glibc's pow is correctly rounded outside hard cases, so these agree with the reference
 // except on inputs whose result lies within ~2^-60 ulp of a rounding boundary.
 #pragma once
+#ifndef __HIPCC_RTC__   // hipRTC (jit.cpp) provides these through its prelude
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "generated/tables.h"
 #include "program.hpp"

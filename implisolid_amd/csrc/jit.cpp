@@ -1,0 +1,228 @@
+// jit.cpp -- code generation and hipRTC compilation of tree kernels (see jit.hpp).
+#include "jit.hpp"
+
+#include <hip/hiprtc.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <sstream>
+#include <stdexcept>
+#include <vector>
+
+#include "generated/jit_headers.inc"
+
+namespace impli {
+
+namespace {
+
+// types and macros hipRTC does not provide (the headers skip their system includes under it)
+const char* kPrelude = R"(
+typedef signed char int8_t;
+typedef unsigned char uint8_t;
+typedef short int16_t;
+typedef unsigned short uint16_t;
+typedef int int32_t;
+typedef unsigned int uint32_t;
+typedef long int64_t;
+typedef unsigned long uint64_t;
+#ifndef INFINITY
+#define INFINITY __builtin_huge_valf()
+#endif
+)";
+
+struct Node {
+    bool leaf = false;
+    int type = 0, mat = 0, csg = -1;
+    int child[2] = {-1, -1};
+};
+
+// post-order program -> tree: XFORM(m) PRIM(t) is a leaf; XFORM(m) <a> <b> CSG(t) an inner node
+int parse(const Program& p, int pc, std::vector<Node>& nodes, int& next) {
+    if (pc >= p.n_instr || p.instr[pc].op != OP_XFORM) throw std::runtime_error("jit: malformed program");
+    Node n;
+    n.mat = p.instr[pc].mat;
+    if (pc + 1 < p.n_instr && p.instr[pc + 1].op == OP_PRIM) {
+        n.leaf = true;
+        n.type = p.instr[pc + 1].type;
+        next = pc + 2;
+    } else {
+        int p1 = 0, p2 = 0;
+        n.child[0] = parse(p, pc + 1, nodes, p1);
+        n.child[1] = parse(p, p1, nodes, p2);
+        if (p2 >= p.n_instr || p.instr[p2].op != OP_CSG) throw std::runtime_error("jit: malformed program");
+        n.type = p.instr[p2].type;
+        n.csg = p.instr[p2].csg;
+        next = p2 + 1;
+    }
+    nodes.push_back(n);
+    return (int)nodes.size() - 1;
+}
+
+const char* prim_call(int t) {
+    switch (t) {
+        case NT_ELLIPSOID: return "egg_f(";
+        case NT_CUBE: return "cube_f(tab, ";
+        case NT_CYLINDER: return "cyl_f(";
+        case NT_CONE: return "cone_f(";
+        case NT_HEART: return "heart_f(";
+        case NT_TORUS: return "torus_f(";
+        case NT_DMUSHROOM: return "dm_f(";
+        default: throw std::runtime_error("jit: unknown primitive");
+    }
+}
+
+struct Emitter {
+    const std::vector<Node>& nodes;
+    std::ostringstream out;
+    int counter = 0;
+
+    // emits the code of node `i` evaluated at point (x, y, z); returns the variable holding f
+    std::string emit(int i, const std::string& x, const std::string& y, const std::string& z, int ind) {
+        const Node& n = nodes[i];
+        const int id = counter++;
+        const std::string pad(ind, ' ');
+        const std::string q = "q" + std::to_string(id), f = "f" + std::to_string(id);
+        // matrix_vector_product (basic_functions.hpp:140-177), same expression order as xform()
+        out << pad << "const V3 " << q << " = xform(M + " << 12 * n.mat << ", " << x << ", " << y << ", " << z << ");\n";
+        if (n.leaf) {
+            out << pad << "const float " << f << " = " << prim_call(n.type) << q << ".x, " << q << ".y, " << q << ".z);\n";
+            return f;
+        }
+        const std::string m = "m" + std::to_string(id), a = "a" + std::to_string(id), b = "b" + std::to_string(id);
+        out << pad << "float " << f << ";\n" << pad << "{\n";
+        out << pad << "  const uint32_t " << m << " = mode_of(modes, " << n.csg << ");\n";
+        out << pad << "  float " << a << " = 0.f, " << b << " = 0.f;\n";
+        out << pad << "  if (" << m << " != PM_RIGHT) {\n";
+        const std::string fa = emit(n.child[0], q + ".x", q + ".y", q + ".z", ind + 4);
+        out << pad << "    " << a << " = " << fa << ";\n" << pad << "  }\n";
+        out << pad << "  if (" << m << " != PM_LEFT) {\n";
+        const std::string fb = emit(n.child[1], q + ".x", q + ".y", q + ".z", ind + 4);
+        out << pad << "    " << b << " = " << fb << ";\n" << pad << "  }\n";
+        // transformed_union.hpp:48 / transformed_intersection.hpp:50 / transformed_subtract.hpp:52
+        std::string sel, right = b;
+        if (n.type == NT_UNION) sel = "(" + a + " > " + b + ") ? " + a + " : " + b;
+        else if (n.type == NT_INTERSECTION) sel = "(" + a + " > " + b + ") ? " + b + " : " + a;
+        else {
+            sel = "(" + a + " < -" + b + ") ? " + a + " : -" + b;
+            right = "-" + b;
+        }
+        out << pad << "  " << f << " = (" << m << " == PM_BOTH) ? (" << sel << ") : (" << m << " == PM_LEFT) ? " << a
+            << " : " << right << ";\n";
+        out << pad << "}\n";
+        return f;
+    }
+};
+
+void rtc_check(hiprtcResult r, const char* what) {
+    if (r != HIPRTC_SUCCESS) throw std::runtime_error(std::string(what) + ": " + hiprtcGetErrorString(r));
+}
+
+}  // namespace
+
+TreeJit& TreeJit::instance() {
+    static TreeJit j;
+    return j;
+}
+
+TreeJit::TreeJit() {
+    const char* e = std::getenv("IMPLISOLID_JIT");
+    enabled_ = !(e && e[0] == '0');
+}
+
+std::string TreeJit::kernel_source(const Program& p) {
+    std::vector<Node> nodes;
+    int next = 0;
+    const int root = parse(p, 0, nodes, next);
+    if (next != p.n_instr) throw std::runtime_error("jit: trailing instructions");
+    Emitter em{nodes};
+    const std::string f = em.emit(root, "x0", "y0", "z0", 4);
+    std::ostringstream s;
+    s << kPrelude << "#include \"eval_bricks.hpp\"\n#include \"ifunc_interval.hpp\"\n"
+      << "namespace impli {\nusing namespace dev;\n"
+      << "__device__ __forceinline__ float tree_f(const float* __restrict__ M, const float* __restrict__ tab,\n"
+      << "                                        uint64_t modes, float x0, float y0, float z0) {\n"
+      << em.out.str() << "    return " << f << ";\n}\n"
+      << "struct JitEval {\n    const float* M;\n    const float* tab;\n"
+      << "    __device__ __forceinline__ float operator()(uint64_t m, float x, float y, float z) const {\n"
+      << "        return tree_f(M, tab, m, x, y, z);\n    }\n};\n}  // namespace impli\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_eval_bricks(\n"
+      << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
+      << "    const uint8_t* cls, uint8_t* fill, int sign_fill, float* field) {\n"
+      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, cls, fill, sign_fill, field);\n}\n";
+    return s.str();
+}
+
+std::vector<char> TreeJit::compile(const std::string& src) {
+    hiprtcProgram prog = nullptr;
+    rtc_check(hiprtcCreateProgram(&prog, src.c_str(), "impli_tree.hip", kJitNumHeaders, kJitHeaderSources,
+                                  kJitHeaderNames),
+              "hiprtcCreateProgram");
+    // the static library's floating-point contract: no FMA contraction, IEEE division/sqrt
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+    if (r != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n + 1, '\0');
+        hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        throw std::runtime_error("hiprtcCompileProgram: " + log.substr(0, 4000));
+    }
+    size_t code_size = 0;
+    std::vector<char> code;
+    try {
+        rtc_check(hiprtcGetCodeSize(prog, &code_size), "hiprtcGetCodeSize");
+        code.resize(code_size);
+        rtc_check(hiprtcGetCode(prog, code.data()), "hiprtcGetCode");
+    } catch (...) {
+        hiprtcDestroyProgram(&prog);
+        throw;
+    }
+    hiprtcDestroyProgram(&prog);
+    return code;
+}
+
+hipFunction_t TreeJit::brick_kernel(const Program& p) {
+    if (!enabled_) return nullptr;
+    std::string src;
+    try {
+        src = kernel_source(p);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "implisolid: tree JIT skipped (%s)\n", e.what());
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lock(mu_);
+    auto it = cache_.find(src);
+    if (it != cache_.end()) return it->second.fn;
+    Entry ent;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        const std::vector<char> code = compile(src);
+        if (hipModuleLoadData(&ent.mod, code.data()) != hipSuccess) throw std::runtime_error("hipModuleLoadData failed");
+        if (hipModuleGetFunction(&ent.fn, ent.mod, "impli_eval_bricks") != hipSuccess)
+            throw std::runtime_error("hipModuleGetFunction failed");
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n", e.what());
+        ent.fn = nullptr;
+    }
+    compile_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (ent.fn) ++n_compiled_;
+    cache_.emplace(src, ent);
+    return ent.fn;
+}
+
+void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
+                            const BrickGrid& bg, const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill,
+                            int sign_fill, float* d_field, hipStream_t s) {
+    if (bg.n_bricks <= 0) return;
+    GridDesc gg = g;
+    BrickGrid bb = bg;
+    void* args[] = {(void*)&d_mats, (void*)&d_rabbit, (void*)&gg, (void*)&bb, (void*)&d_modes,
+                    (void*)&d_cls, (void*)&d_fill, (void*)&sign_fill, (void*)&d_field};
+    const unsigned blocks = (unsigned)((bg.n_bricks + 3) / 4);
+    if (hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+        throw std::runtime_error("hipModuleLaunchKernel(impli_eval_bricks) failed");
+}
+
+}  // namespace impli

@@ -3,25 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "grid.hpp"
 #include "program.hpp"
 
 namespace impli {
-
-// Sampling grid of MarchingCubes (marching_cubes.hpp:175-243, 1662-1698) for one Z-slab.
-//   res = R + 5 samples per axis; cells c in [1, res-3] per axis (render_geometry :1033-1039),
-//   m = R + 2 cells per axis.  Cells touch samples [1, res-2]; those are stored (n = R + 3 per
-//   axis, x fastest), the ring s in {1, res-2} holding seal_exterior's -1e7 (:895-963), so every
-//   corner load is unconditional.  Samples 0 and res-1 are never read by any cell.
-struct GridDesc {
-    int R, res, n, m;            // n = R + 3 stored samples per axis, m = R + 2 cells per axis
-    float w[3];                  // widthx/y/z = (max - min) / R
-    float lo[3];                 // box min
-    float i0[3];                 // render offsets xi0 = min / w - 2   (:1026-1028)
-    int cz0, cz1;                // cell layers handled by this slab [cz0, cz1) (incl. halo layer)
-    int cz_emit;                 // first layer whose faces / vertices this slab emits
-    int fz0, fz1;                // stored sample layers [fz0, fz1) = [cz0, cz1 + 1)
-    int64_t n_cells;             // m * m * (cz1 - cz0)
-};
 
 GridDesc make_grid(int R, const float box[6], int cz0, int cz1, int cz_emit);
 
@@ -41,16 +26,14 @@ void build_case_table(CaseInfo out[256]);
 void launch_eval_field(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g, float* d_field,
                        hipStream_t s);
 // direct evaluation at arbitrary points (implicit values / gradients)
-// pruned field evaluation: bricks of kBX x kBY x kBZ stored samples (x fastest)
-constexpr int kBX = 16, kBY = 4, kBZ = 4;
-enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBrickNoFill = 4 };
-// fill[b] (written by the pruned eval): kBrickPos / kBrickNeg if the brick was sign-filled --
-// then no cell corner in it needs its exact value and MC may take the sign from fill -- else 0.
-struct BrickGrid { int nbx, nby, nbz, n_bricks; };
 BrickGrid brick_grid(const GridDesc& g);
-void launch_eval_field_pruned(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range,
-                              const GridDesc& g, uint64_t* d_modes, uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                              float* d_field, hipStream_t s, hipEvent_t mid = nullptr);
+// K1a: interval pass -- per-brick CSG pruning modes and sign class
+void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
+                        uint64_t* d_modes, uint8_t* d_cls, hipStream_t s);
+// K1b (interpreter): brick-pruned field; the JIT variant is TreeJit::launch_bricks (jit.hpp)
+void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
+                               const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
+                               float* d_field, hipStream_t s);
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
                         float* d_f, float* d_grad /* nullable: values only */, hipStream_t s);
 

@@ -341,53 +341,47 @@ __global__ __launch_bounds__(1024) void k_scan_apply(uint4* __restrict__ cnt, in
     }
 }
 
-// K3: one wave per active unit; lane l owns 16 consecutive cells (one 16-byte load of cube indices)
+// K3: one block per active unit (persistent loop over the compacted list), 4 consecutive cells
+// per thread.  A block scan gives each cell its vertex / face / record base inside the unit;
+// the cells' work is independent, so loads of many cells are in flight at once.
 __global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ CaseInfo s_case[256];
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    __shared__ unsigned long long s_scan[4];
+    const int t = threadIdx.x;
     s_case[t] = cases[t];
     __syncthreads();
     const uint32_t n_active = b.counters[0];
     const uint32_t H = b.counters[1];
     const uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
-    constexpr int CPL = kUnitCells / 64;   // 16 cells per lane
-    for (uint32_t a = blockIdx.x * 4 + wid; a < n_active; a += gridDim.x * 4) {
+    for (uint32_t a = blockIdx.x; a < n_active; a += gridDim.x) {
         const uint32_t u = b.active_units[a];
         const uint4 base = b.unit_cnt[u];   // exclusive {vbase, fbase, abase, hbase}
-        const uint32_t L0 = u * kUnitCells + lane * CPL;
-        uint8_t cis[CPL];
-        if (L0 + CPL <= (uint64_t)g.n_cells) {
-            const uint4 q = *reinterpret_cast<const uint4*>(b.ci + L0);
-            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) cis[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-        } else {
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) cis[k] = (L0 + k < (uint64_t)g.n_cells) ? b.ci[L0 + k] : 0;
-        }
-        // lane-local sums (halo cells own vertices but emit nothing)
-        int cx, cy, cz;
-        cell_coords(g, L0 < (uint64_t)g.n_cells ? L0 : 0u, cx, cy, cz);
-        const int czs = cz, cys = cy, cxs = cx;
+        const uint32_t L0 = u * kUnitCells + 4u * (uint32_t)t;
+        const bool any = L0 < (uint64_t)g.n_cells;
+        const uint32_t ci4 = any ? *reinterpret_cast<const uint32_t*>(b.ci + L0) : 0u;
+        int cx = 1, cy = 1, cz = g.cz0;
+        if (any) cell_coords(g, L0, cx, cy, cz);
         unsigned own = 0, tri = 0, act = 0;
         {
-            int x = cxs, y = cys, z = czs;
+            int x = cx, y = cy, z = cz;
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                const CaseInfo& C = s_case[cis[k]];
-                own += C.nown;
-                if (z >= g.cz_emit) { tri += C.ntri; act += C.ntri ? 1u : 0u; }
+            for (int k = 0; k < 4; ++k) {
+                if (L0 + k < (uint64_t)g.n_cells) {
+                    const CaseInfo& C = s_case[(ci4 >> (8 * k)) & 255u];
+                    own += C.nown;
+                    if (z >= g.cz_emit) { tri += C.ntri; act += C.ntri ? 1u : 0u; }
+                }
                 if (++x > g.m) { x = 1; if (++y > g.m) { y = 1; ++z; } }
             }
         }
-        const unsigned long long p = pack3(own, tri, act);
-        const unsigned long long incl = wave_incl_scan<unsigned long long>(p, lane);
-        unsigned long long pre = incl - p;
+        unsigned long long total;
+        const unsigned long long pre = block_excl_scan(pack3(own, tri, act), total, s_scan);
         uint32_t vrun = base.x + f_own(pre), frun = base.y + f_tri(pre), arun = base.z + f_act(pre);
-        int x = cxs, y = cys, z = czs;
-        for (int k = 0; k < CPL; ++k) {
+        int x = cx, y = cy, z = cz;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
             const uint32_t L = L0 + k;
-            const unsigned ci = cis[k];
+            const unsigned ci = (ci4 >> (8 * k)) & 255u;
             const CaseInfo& C = s_case[ci];
             const bool valid = L < (uint64_t)g.n_cells;
             const bool emit = valid && z >= g.cz_emit;
@@ -396,7 +390,9 @@ __global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ c
                 const float fy = ((float)y + g.i0[1]) * g.w[1];
                 const float fz = ((float)z + g.i0[2]) * g.w[2];
                 const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
-                const float f7 = corner(b.field, g, x + 1, y + 1, z + 1);
+                const float* q = b.field + sample_index(g, x, y, z);
+                const int n = g.n, nn = g.n * g.n;
+                const float f7 = q[nn + n + 1];
 #pragma unroll
                 for (int slot = 0; slot < 3; ++slot) {
                     const int r = C.rank[slot];
@@ -408,15 +404,15 @@ __global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ c
                     if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
                     float px, py, pz;
                     if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
-                        const float f5 = corner(b.field, g, x + 1, y, z + 1);
+                        const float f5 = q[nn + 1];
                         const float mu = (0.f - f5) / (f7 - f5);
                         px = fx2; py = fy + mu * g.w[1]; pz = fz2;
                     } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
-                        const float f6 = corner(b.field, g, x, y + 1, z + 1);
+                        const float f6 = q[nn + n];
                         const float mu = (0.f - f6) / (f7 - f6);
                         px = fx + mu * g.w[0]; py = fy2; pz = fz2;
                     } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
-                        const float f3 = corner(b.field, g, x + 1, y + 1, z);
+                        const float f3 = q[n + 1];
                         const float mu = (0.f - f3) / (f7 - f3);
                         px = fx2; py = fy2; pz = fz + mu * g.w[2];
                     }
@@ -487,7 +483,8 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
 }
 
 void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s, hipEvent_t mid) {
-    k_mc_verts<<<1024, 256, 0, s>>>(d_cases, g, b);
+    const int64_t nu = n_units(g);
+    k_mc_verts<<<(unsigned)(nu < 4096 ? (nu > 0 ? nu : 1) : 4096), 256, 0, s>>>(d_cases, g, b);
     if (mid) (void)hipEventRecord(mid, s);
     k_mc_faces<<<2048, 256, 0, s>>>(d_cases, g, b);
 }

@@ -16,7 +16,9 @@
 // M^-T to the selected gradient on the way up, exactly like eval_gradient in
 // transformed_union.hpp:54-84 (children's f and grad are computed once and reused).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#endif
 
 namespace impli {
 

@@ -100,6 +100,10 @@ int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* gra
 
 /* host-only: compile an MP5 tree to the node program; info = {n_instr, depth, n_mats, 0};
    mats_out receives n_mats inverse matrices (12 floats each, up to 256) */
+/* Additive, host only (no GPU): generate and hipRTC-compile the tree kernel for this shape.
+ * Returns the code-object size (> 0), or -1 with implisolid_last_error(); optionally copies the
+ * generated source (NUL-terminated, truncated to capacity) and the compile time in seconds. */
+int64_t implisolid_jit_compile(const char* shape_json, char* source_out, int64_t capacity, double* seconds);
 int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int32_t info[4], float* mats_out);
 
 /* Device-resident slab pipeline (benchmarks / multi-GPU Z-slab runs).  A slab engine owns the
@@ -135,6 +139,11 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
  * count / emit calls; kernel_times blocks and returns milliseconds of the last timed calls for
  * [brick pass, field eval, MC count, unit scan, vertex emission, face emission] */
 int implisolid_slab_set_timing(implisolid_slab* s, int on);
+/* 1 if the slab's last eval ran the JIT-compiled tree kernel, 0 if the interpreter */
+int implisolid_slab_used_jit(implisolid_slab* s);
+/* process-wide: compile tree kernels with hipRTC for objects set from now on (default on;
+ * environment IMPLISOLID_JIT=0 starts with it off).  Results are bit-identical either way. */
+void implisolid_set_jit(int on);
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]);
 /* bricks of the last slab eval: out = [bricks, mixed-sign bricks, sign-filled bricks] (blocking) */
 int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]);

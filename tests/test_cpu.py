@@ -349,3 +349,12 @@ def test_node_addon_exports(impli):
             "calculate_implicit_gradients", "get_gradients", "get_pointset", "about"}
     assert need <= set(out["keys"])
     assert out["ok"] == 2 and out["bad"] == -1 and "Invalid object" in out["err"]
+
+
+def test_jit_tree_kernels_compile_for_gfx950(impli):
+    """Host-only: the generated tree kernel compiles with hipRTC for several shapes."""
+    from implisolid_amd import scenes
+    for shape in [{"type": "iellipsoid", "matrix": scenes.EYE}, scenes.union_sphere_cube(), scenes.config3()[0],
+                  scenes.random_tree(7, 10)]:
+        n, secs, src = impli.jit_compile(shape)
+        assert n > 1000 and "impli_eval_bricks" in src, src[:500]

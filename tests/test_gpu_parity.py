@@ -122,6 +122,28 @@ def test_empty_and_full(impli, oracle):
     _mc_compare(impli, oracle, big, scenes.mc_settings(16, 1.0))
 
 
+@pytest.mark.parametrize("name", sorted(TREES))
+def test_jit_field_matches_interpreter(impli, name):
+    """The hipRTC-compiled tree kernel and the interpreter produce the same field bit for bit."""
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(48, 1.0)
+    impli.set_jit(False)
+    try:
+        a = _field(impli, TREES[name], mc, 1)
+    finally:
+        impli.set_jit(True)
+    s = impli.Slab(TREES[name], mc)
+    impli.set_pruning(1)
+    try:
+        s.eval()
+        b = s.read_field()
+        assert s.used_jit()
+    finally:
+        impli.set_pruning(2)
+        s.close()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
+
+
 @pytest.mark.parametrize("level", [0, 1, 2])
 def test_mc_identical_at_every_pruning_level(impli, oracle, level):
     from implisolid_amd import scenes
