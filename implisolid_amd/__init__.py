@@ -30,7 +30,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
     "implisolid_parse_settings", "implisolid_slab_partition", "implisolid_slab_brick_stats",
     "implisolid_slab_set_timing", "implisolid_slab_kernel_times", "implisolid_jit_compile",
-    "implisolid_slab_used_jit", "implisolid_set_jit",
+    "implisolid_slab_used_jit", "implisolid_set_jit", "implisolid_slab_stats",
 ]
 
 _lib = None
@@ -94,6 +94,7 @@ def lib():
         "implisolid_slab_brick_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
         "implisolid_slab_set_timing": ([c_void_p, c_int], c_int),
         "implisolid_slab_used_jit": ([c_void_p], c_int),
+        "implisolid_slab_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
         "implisolid_set_jit": ([c_int], None),
         "implisolid_jit_compile": ([c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)],
                                    ctypes.c_int64),
@@ -354,6 +355,13 @@ class Slab:
         out = (ctypes.c_float * 6)()
         self._rc(lib().implisolid_slab_kernel_times(self.h, out))
         return dict(zip(self.KERNELS, [float(x) for x in out]))
+
+    def stats(self):
+        """After count(): units, active units, owned vertices, triangles, active cells, halo-owned, cells."""
+        out = (ctypes.c_int64 * 8)()
+        self._rc(lib().implisolid_slab_stats(self.h, out))
+        keys = ["units", "active_units", "own", "tri", "act", "halo_own", "cells"]
+        return dict(zip(keys, [int(x) for x in out]))
 
     def used_jit(self):
         return bool(lib().implisolid_slab_used_jit(self.h))

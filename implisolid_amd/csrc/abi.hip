@@ -455,6 +455,26 @@ float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
 int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
 float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
 
+int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {
+    try {
+        uint32_t c[6];
+        s->engine.raw_counters(c, 0);
+        const GridDesc& g = s->engine.grid();
+        out[0] = n_units(g);
+        out[1] = c[0];
+        out[2] = c[2];
+        out[3] = c[3];
+        out[4] = c[4];
+        out[5] = c[5];
+        out[6] = g.n_cells;
+        out[7] = 0;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
 int implisolid_slab_used_jit(implisolid_slab* s) { return s->engine.used_jit() ? 1 : 0; }
 void implisolid_set_jit(int on) { TreeJit::instance().set_enabled(on != 0); }
 

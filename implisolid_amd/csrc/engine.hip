@@ -63,6 +63,7 @@ void Engine::brick_stats(int64_t out[3], hipStream_t s) {
 }
 
 Engine::Engine() {
+
     // rabbit table + the object's trailing members (F8d: out-of-table reads) + zero padding
     std::vector<float> tab(dev::kRabbitPadded, 0.f);
     for (int i = 0; i < dev::kRabbitN; ++i) std::memcpy(&tab[i], &IMPLI_RABBIT_BITS[i], 4);
@@ -143,6 +144,7 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
     unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
+
     active_units_.reserve((size_t)(nu + 1) * sizeof(uint32_t));
     scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
     ci_.reserve((size_t)grid_.n_cells + 64);
@@ -190,6 +192,7 @@ MCBuffers Engine::buffers() const {
     b.cap_rec = cap_rec_;
     b.offsets = nullptr;
     b.overflow = overflow_.as<uint32_t>();
+
     return b;
 }
 
@@ -242,6 +245,11 @@ void Engine::emit(const uint32_t* d_offsets, hipStream_t s) {
     launch_mc_emit(cases_.as<CaseInfo>(), grid_, b, s, timing_ ? ev_[7] : nullptr);
     mark(8, s);
     IMPLI_HIP(hipGetLastError());
+}
+
+void Engine::raw_counters(uint32_t out[6], hipStream_t s) {
+    IMPLI_HIP(hipMemcpyAsync(out, counters_.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
 }
 
 SlabCounts Engine::read_counts(hipStream_t s, bool* overflow) {

@@ -50,7 +50,7 @@ struct MCBuffers {
     uint32_t* scan_blk;      // 8 per scan block: partial sums (5 components), then exclusive bases
     uint32_t* active_units;  // compacted list of units with work
     uint32_t* counters;      // [0] n_active_units, [1] halo own, [2..5] totals own/tri/act/halo
-    uint32_t* vid3;          // 3 * n_cells
+    uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
     uint4* records;          // active cells: {L, ci, fbase, 0}
     float* verts;            // 3 * cap_v
     int32_t* faces;          // 3 * cap_f

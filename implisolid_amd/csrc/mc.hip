@@ -160,13 +160,18 @@ __device__ __forceinline__ unsigned ci_from_rows(unsigned r00, unsigned r10, uns
 // K2: one 256-thread block per 1024-cell unit, 4 consecutive cells per thread.  Runs of 4 cells
 // in one row share their corners (20 loads instead of 32); if every brick the run touches was
 // sign-filled by the eval with one sign, the cube indices are known without touching the field.
+// owned-edge and triangle counts of a cube index; trivial cells (ci 0 / 255, ~99 % of them) skip
+// the table read
+__device__ __forceinline__ unsigned case_counts(const CaseInfo* __restrict__ cases, unsigned ci, unsigned& ntri) {
+    if (ci == 0u || ci == 255u) { ntri = 0; return 0; }
+    const uint16_t v = *reinterpret_cast<const uint16_t*>(&cases[ci]);   // {ntri, nown}
+    ntri = v & 255u;
+    return v >> 8;
+}
+
 __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
-    __shared__ uint8_t s_ntri[256], s_nown[256];
     __shared__ uint4 s_red[4];
     const int t = threadIdx.x;
-    s_ntri[t] = cases[t].ntri;
-    s_nown[t] = cases[t].nown;
-    __syncthreads();
     const uint32_t u = blockIdx.x;
     const uint32_t L0 = u * kUnitCells + 4u * (uint32_t)t;
     unsigned own = 0, tri = 0, act = 0, halo_own = 0;
@@ -207,13 +212,14 @@ __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ c
                 for (int k = 0; k < 4; ++k) ci4 |= ci_from_rows(r00, r10, r01, r11, k) << (8 * k);
             }
             unsigned o = 0, tr = 0, ac = 0;
+            if (ci4 != 0u && ci4 != 0xffffffffu) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const unsigned ci = (ci4 >> (8 * k)) & 255u;
-                o += s_nown[ci];
-                const unsigned nt = s_ntri[ci];
-                tr += nt;
-                ac += nt ? 1u : 0u;
+                for (int k = 0; k < 4; ++k) {
+                    unsigned nt;
+                    o += case_counts(cases, (ci4 >> (8 * k)) & 255u, nt);
+                    tr += nt;
+                    ac += nt ? 1u : 0u;
+                }
             }
             own = o;
             if (cz >= g.cz_emit) { tri = tr; act = ac; }
@@ -226,7 +232,8 @@ __global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ c
                 CellVals v;
                 const unsigned ci = load_cell(b.field, g, x, y, z, v);
                 ci4 |= ci << (8 * k);
-                const unsigned no = s_nown[ci], nt = s_ntri[ci];
+                unsigned nt;
+                const unsigned no = case_counts(cases, ci, nt);
                 own += no;
                 if (z >= g.cz_emit) { tri += nt; act += nt ? 1u : 0u; }
                 else halo_own += no;
@@ -341,95 +348,122 @@ __global__ __launch_bounds__(1024) void k_scan_apply(uint4* __restrict__ cnt, in
     }
 }
 
-// K3: one block per active unit (persistent loop over the compacted list), 4 consecutive cells
-// per thread.  A block scan gives each cell its vertex / face / record base inside the unit;
-// the cells' work is independent, so loads of many cells are in flight at once.
+// K3: one wave per active unit (persistent loop).  Phase 1: each lane loads 16 cube indices
+// (one 16-byte load) and the wave compacts the unit's non-trivial cells (ci != 0, 255 -- about
+// 1 % of all cells) into an LDS list, in cell order.  Phase 2: lanes take list entries 64 at a
+// time; a wave scan of (owned edges, triangles, active) gives each cell its vertex / face /
+// record base, and the cells' vertices and records are written in parallel.
+__device__ __forceinline__ unsigned long long pack4(unsigned a, unsigned b, unsigned c, unsigned d) {
+    return (unsigned long long)a | ((unsigned long long)b << 16) | ((unsigned long long)c << 32) |
+           ((unsigned long long)d << 48);
+}
+__device__ __forceinline__ unsigned fld(unsigned long long p, int i) { return (unsigned)(p >> (16 * i)) & 0xffffu; }
+
 __global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ CaseInfo s_case[256];
-    __shared__ unsigned long long s_scan[4];
-    const int t = threadIdx.x;
+    __shared__ uint32_t s_list[4][kUnitCells];   // per wave: (cell offset in unit) | ci << 16
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     s_case[t] = cases[t];
     __syncthreads();
     const uint32_t n_active = b.counters[0];
     const uint32_t H = b.counters[1];
-    const uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
-    for (uint32_t a = blockIdx.x; a < n_active; a += gridDim.x) {
+    const uint64_t halo_cells = (uint64_t)g.m * g.m * (uint64_t)(g.cz_emit - g.cz0);
+    uint32_t* list = s_list[wid];
+    constexpr int CPL = kUnitCells / 64;   // 16 cells per lane
+    for (uint32_t a = blockIdx.x * 4 + wid; a < n_active; a += gridDim.x * 4) {
         const uint32_t u = b.active_units[a];
         const uint4 base = b.unit_cnt[u];   // exclusive {vbase, fbase, abase, hbase}
-        const uint32_t L0 = u * kUnitCells + 4u * (uint32_t)t;
-        const bool any = L0 < (uint64_t)g.n_cells;
-        const uint32_t ci4 = any ? *reinterpret_cast<const uint32_t*>(b.ci + L0) : 0u;
-        int cx = 1, cy = 1, cz = g.cz0;
-        if (any) cell_coords(g, L0, cx, cy, cz);
-        unsigned own = 0, tri = 0, act = 0;
-        {
-            int x = cx, y = cy, z = cz;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (L0 + k < (uint64_t)g.n_cells) {
-                    const CaseInfo& C = s_case[(ci4 >> (8 * k)) & 255u];
-                    own += C.nown;
-                    if (z >= g.cz_emit) { tri += C.ntri; act += C.ntri ? 1u : 0u; }
-                }
-                if (++x > g.m) { x = 1; if (++y > g.m) { y = 1; ++z; } }
-            }
+        const uint32_t U0 = u * kUnitCells;
+        const uint32_t L0 = U0 + lane * CPL;
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (L0 + CPL <= (uint64_t)g.n_cells) {
+            const uint4 q = *reinterpret_cast<const uint4*>(b.ci + L0);
+            w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+        } else {
+            for (int k = 0; k < CPL; ++k)
+                if (L0 + k < (uint64_t)g.n_cells) w[k >> 2] |= (uint32_t)b.ci[L0 + k] << (8 * (k & 3));
         }
-        unsigned long long total;
-        const unsigned long long pre = block_excl_scan(pack3(own, tri, act), total, s_scan);
-        uint32_t vrun = base.x + f_own(pre), frun = base.y + f_tri(pre), arun = base.z + f_act(pre);
-        int x = cx, y = cy, z = cz;
+        // non-trivial cells of this lane
+        uint32_t mask = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t L = L0 + k;
-            const unsigned ci = (ci4 >> (8 * k)) & 255u;
+        for (int k = 0; k < CPL; ++k) {
+            const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 255u;
+            mask |= (c != 0u && c != 255u) ? (1u << k) : 0u;
+        }
+        const uint32_t cnt = (uint32_t)__popc(mask);
+        const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);
+        const uint32_t n_list = __shfl(incl, 63, 64);
+        uint32_t pos = incl - cnt;
+        while (mask) {
+            const int k = __ffs(mask) - 1;
+            mask &= mask - 1;
+            list[pos++] = (uint32_t)(lane * CPL + k) | (((w[k >> 2] >> (8 * (k & 3))) & 255u) << 16);
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t vrun0 = base.x, frun0 = base.y, arun0 = base.z;
+        for (uint32_t e0 = 0; e0 < n_list; e0 += 64) {
+            const uint32_t e = e0 + (uint32_t)lane;
+            const bool has = e < n_list;
+            const uint32_t ent = has ? list[e] : 0u;
+            const uint32_t L = U0 + (ent & 0xffffu);
+            const unsigned ci = ent >> 16;
             const CaseInfo& C = s_case[ci];
-            const bool valid = L < (uint64_t)g.n_cells;
-            const bool emit = valid && z >= g.cz_emit;
-            if (valid && C.nown) {
-                const float fx = ((float)x + g.i0[0]) * g.w[0];
-                const float fy = ((float)y + g.i0[1]) * g.w[1];
-                const float fz = ((float)z + g.i0[2]) * g.w[2];
-                const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
-                const float* q = b.field + sample_index(g, x, y, z);
-                const int n = g.n, nn = g.n * g.n;
-                const float f7 = q[nn + n + 1];
+            const bool emit = has && (uint64_t)L >= halo_cells;
+            const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
+            const unsigned long long p = pack4(own, tri, act, 0u);
+            const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
+            const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
+            if (has) {
+                int x, y, z;
+                cell_coords(g, L, x, y, z);
+                uint32_t vrun = vrun0 + fld(pre, 0);
+                if (own) {
+                    const float fx = ((float)x + g.i0[0]) * g.w[0];
+                    const float fy = ((float)y + g.i0[1]) * g.w[1];
+                    const float fz = ((float)z + g.i0[2]) * g.w[2];
+                    const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
+                    const int n = g.n, nn = g.n * g.n;
+                    const float* q = b.field + sample_index(g, x, y, z);
+                    const float f7 = q[nn + n + 1];
 #pragma unroll
-                for (int slot = 0; slot < 3; ++slot) {
-                    const int r = C.rank[slot];
-                    if (r < 0) continue;
-                    const uint32_t vid = vrun + (uint32_t)r;
-                    b.vid3[(size_t)L * 3 + slot] = Voff + vid - H;
-                    if (!emit) continue;
-                    const uint32_t out = vid - H;
-                    if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
-                    float px, py, pz;
-                    if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
-                        const float f5 = q[nn + 1];
-                        const float mu = (0.f - f5) / (f7 - f5);
-                        px = fx2; py = fy + mu * g.w[1]; pz = fz2;
-                    } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
-                        const float f6 = q[nn + n];
-                        const float mu = (0.f - f6) / (f7 - f6);
-                        px = fx + mu * g.w[0]; py = fy2; pz = fz2;
-                    } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
-                        const float f3 = q[n + 1];
-                        const float mu = (0.f - f3) / (f7 - f3);
-                        px = fx2; py = fy2; pz = fz + mu * g.w[2];
+                    for (int slot = 0; slot < 3; ++slot) {
+                        const int r = C.rank[slot];
+                        if (r < 0) continue;
+                        const uint32_t vid = vrun + (uint32_t)r;
+                        b.vid3[(size_t)L * 3 + slot] = vid - H;
+                        if (!emit) continue;
+                        const uint32_t out = vid - H;
+                        if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
+                        float px, py, pz;
+                        if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
+                            const float f5 = q[nn + 1];
+                            const float mu = (0.f - f5) / (f7 - f5);
+                            px = fx2; py = fy + mu * g.w[1]; pz = fz2;
+                        } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
+                            const float f6 = q[nn + n];
+                            const float mu = (0.f - f6) / (f7 - f6);
+                            px = fx + mu * g.w[0]; py = fy2; pz = fz2;
+                        } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
+                            const float f3 = q[n + 1];
+                            const float mu = (0.f - f3) / (f7 - f3);
+                            px = fx2; py = fy2; pz = fz + mu * g.w[2];
+                        }
+                        b.verts[3 * (size_t)out] = px;
+                        b.verts[3 * (size_t)out + 1] = py;
+                        b.verts[3 * (size_t)out + 2] = pz;
                     }
-                    b.verts[3 * (size_t)out] = px;
-                    b.verts[3 * (size_t)out + 1] = py;
-                    b.verts[3 * (size_t)out + 2] = pz;
                 }
-                vrun += C.nown;
+                if (act) {
+                    const uint32_t arun = arun0 + fld(pre, 2);
+                    if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
+                    else *b.overflow = 1u;
+                }
             }
-            if (emit && C.ntri) {
-                if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun, 0u);
-                else *b.overflow = 1u;
-                ++arun;
-                frun += C.ntri;
-            }
-            if (++x > g.m) { x = 1; if (++y > g.m) { y = 1; ++z; } }
+            vrun0 += fld(tot, 0);
+            frun0 += fld(tot, 1);
+            arun0 += fld(tot, 2);
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -453,6 +487,7 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
     __syncthreads();
     const uint32_t n_rec = b.counters[4];
     const uint32_t lim = n_rec < (uint64_t)b.cap_rec ? n_rec : (uint32_t)b.cap_rec;
+    const uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
     for (uint32_t i = blockIdx.x * 256 + t; i < lim; i += gridDim.x * 256) {
         const uint4 r = b.records[i];
         const uint32_t L = r.x, ci = r.y, fbase = r.z;
@@ -462,7 +497,7 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
         for (int k = 0; k < 3 * C.ntri; ++k) {
             const int e = C.tri[k];
             const uint32_t owner = L - (uint32_t)s_off[e];
-            out[k] = (int32_t)b.vid3[(size_t)owner * 3 + s_slot[e]];
+            out[k] = (int32_t)(Voff + b.vid3[(size_t)owner * 3 + s_slot[e]]);
         }
     }
 }
@@ -480,6 +515,10 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     if (nb > 0) k_scan_partial<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk);
     k_scan_top<<<1, 64, 0, s>>>(b.scan_blk, (int)nb, b.counters);
     if (nb > 0) k_scan_apply<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk, b.active_units);
+}
+
+void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
+    k_mc_faces<<<2048, 256, 0, s>>>(d_cases, g, b);
 }
 
 void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s, hipEvent_t mid) {
