@@ -30,7 +30,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
     "implisolid_parse_settings", "implisolid_slab_partition", "implisolid_slab_brick_stats",
     "implisolid_slab_set_timing", "implisolid_slab_kernel_times", "implisolid_jit_compile",
-    "implisolid_slab_used_jit", "implisolid_set_jit", "implisolid_slab_stats",
+    "implisolid_slab_used_jit", "implisolid_set_jit", "implisolid_slab_stats", "implisolid_slab_read_signs",
 ]
 
 _lib = None
@@ -95,6 +95,7 @@ def lib():
         "implisolid_slab_set_timing": ([c_void_p, c_int], c_int),
         "implisolid_slab_used_jit": ([c_void_p], c_int),
         "implisolid_slab_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
+        "implisolid_slab_read_signs": ([c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int64], ctypes.c_int64),
         "implisolid_set_jit": ([c_int], None),
         "implisolid_jit_compile": ([c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)],
                                    ctypes.c_int64),
@@ -360,7 +361,7 @@ class Slab:
         """After count(): units, active units, owned vertices, triangles, active cells, halo-owned, cells."""
         out = (ctypes.c_int64 * 8)()
         self._rc(lib().implisolid_slab_stats(self.h, out))
-        keys = ["units", "active_units", "own", "tri", "act", "halo_own", "cells"]
+        keys = ["units", "unused", "own", "tri", "act", "halo_own", "cells"]
         return dict(zip(keys, [int(x) for x in out]))
 
     def used_jit(self):
@@ -371,6 +372,17 @@ class Slab:
         out = (ctypes.c_int64 * 3)()
         self._rc(lib().implisolid_slab_brick_stats(self.h, out))
         return [int(x) for x in out]
+
+    def read_signs(self):
+        """Blocking host copy of the sample signs (1 where value < 0), shape (layers, n, n)."""
+        L = lib()
+        n = L.implisolid_slab_read_signs(self.h, None, 0)
+        _check()
+        out = np.empty(n, np.uint8)
+        L.implisolid_slab_read_signs(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), n)
+        _check()
+        n_side = self.R + 3
+        return out.reshape(-1, n_side, n_side)
 
     def read_field(self):
         """Blocking host copy of the stored field samples, shape (layers, n, n)."""

@@ -481,6 +481,26 @@ void implisolid_set_jit(int on) { TreeJit::instance().set_enabled(on != 0); }
 int implisolid_slab_set_timing(implisolid_slab* s, int on) { SLAB_TRY(s->engine.set_timing(on != 0)) }
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]) { SLAB_TRY(s->engine.kernel_times(ms)) }
 
+int64_t implisolid_slab_read_signs(implisolid_slab* s, uint8_t* out, int64_t capacity) {
+    try {
+        const GridDesc& g = s->engine.grid();
+        const int64_t rows = (int64_t)g.n * (g.fz1 - g.fz0), rw = sign_row_words(g);
+        const int64_t n = rows * g.n;
+        if (out) {
+            if (capacity < n) throw InputError("implisolid_slab_read_signs: buffer too small");
+            std::vector<uint64_t> w((size_t)(rows * rw));
+            IMPLI_HIP(hipDeviceSynchronize());
+            IMPLI_HIP(hipMemcpy(w.data(), s->engine.d_signs(), w.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            for (int64_t r = 0; r < rows; ++r)
+                for (int x = 0; x < g.n; ++x) out[r * g.n + x] = (uint8_t)((w[(size_t)(r * rw + x / 64)] >> (x % 64)) & 1u);
+        }
+        return n;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+}
+
 int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]) {
     try {
         s->engine.brick_stats(out, 0);

@@ -119,7 +119,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &modes_, &cls_, &fill_, &prog_, &rabbit_, &cases_, &field_, &ci_, &scan_blk_, &unit_cnt_, &active_units_, &counters_, &vid3_,
+    DevBuf* all[] = {&offsets_, &modes_, &cls_, &fill_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &counters_, &vid3_,
                      &records_, &verts_, &faces_, &overflow_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -145,9 +145,8 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
     unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
 
-    active_units_.reserve((size_t)(nu + 1) * sizeof(uint32_t));
     scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
-    ci_.reserve((size_t)grid_.n_cells + 64);
+    signs_.reserve((size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t) + 64);
     vid3_.reserve((size_t)grid_.n_cells * 3 * sizeof(uint32_t));
     const int64_t m2 = (int64_t)grid_.m * grid_.m;
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
@@ -174,14 +173,9 @@ bool Engine::ensure_capacity(const SlabCounts& c) {
 MCBuffers Engine::buffers() const {
     MCBuffers b{};
     b.field = field_.as<float>();
-    b.fill = fill_.as<uint8_t>();
-    const BrickGrid bg = brick_grid(grid_);
-    b.nbx = bg.nbx;
-    b.nby = bg.nby;
+    b.signs = signs_.as<uint64_t>();
     b.unit_cnt = unit_cnt_.as<uint4>();
-    b.ci = ci_.as<uint8_t>();
     b.scan_blk = scan_blk_.as<uint32_t>();
-    b.active_units = active_units_.as<uint32_t>();
     b.counters = counters_.as<uint32_t>();
     b.vid3 = vid3_.as<uint32_t>();
     b.records = records_.as<uint4>();
@@ -212,15 +206,17 @@ void Engine::eval_field(hipStream_t s) {
             const float* d_mats = reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
             TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_),
                                    modes_.as<uint64_t>(), cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2,
-                                   field_.as<float>(), s);
+                                   field_.as<float>(), signs_.as<uint16_t>(), s);
         } else {
             launch_eval_bricks_interp(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, modes_.as<uint64_t>(),
-                                      cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2, field_.as<float>(), s);
+                                      cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2, field_.as<float>(),
+                                      signs_.as<uint16_t>(), s);
         }
     } else {
         IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled
         mark(1, s);
         launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
+        launch_signs_from_field(grid_, field_.as<float>(), signs_.as<uint64_t>(), s);
     }
     mark(2, s);
     IMPLI_HIP(hipGetLastError());

@@ -63,6 +63,7 @@ public:
     float* d_verts() const { return verts_.as<float>(); }
     int32_t* d_faces() const { return faces_.as<int32_t>(); }
     float* d_field() const { return field_.as<float>(); }
+    const uint64_t* d_signs() const { return signs_.as<uint64_t>(); }
     const uint32_t* d_counters() const { return counters_.as<uint32_t>(); }
     int depth() const { return depth_; }
     const Program* d_program() const { return prog_.as<Program>(); }
@@ -100,7 +101,7 @@ private:
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, modes_, cls_, fill_, field_, ci_, scan_blk_, unit_cnt_, active_units_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    DevBuf offsets_, modes_, cls_, fill_, field_, signs_, scan_blk_, unit_cnt_, counters_, vid3_, records_, verts_, faces_, overflow_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
     hipEvent_t ev_[9] = {};

@@ -87,8 +87,26 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __rest
                                                            const uint64_t* __restrict__ modes,
                                                            const uint8_t* __restrict__ cls,
                                                            uint8_t* __restrict__ fill, int sign_fill,
-                                                           float* __restrict__ field) {
-    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, cls, fill, sign_fill, field);
+                                                           float* __restrict__ field, uint16_t* __restrict__ signs) {
+    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);
+}
+
+// sign bitmap of a fully evaluated field (unpruned path): one thread per 64-bit word
+__global__ __launch_bounds__(256) void k_signs_from_field(GridDesc g, const float* __restrict__ field,
+                                                          uint64_t* __restrict__ signs) {
+    const int rw = sign_row_words(g);
+    const int64_t rows = (int64_t)g.n * (g.fz1 - g.fz0);
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rows * rw) return;
+    const int64_t row = i / rw;
+    const int w = (int)(i - row * rw);
+    const float* f = field + row * g.n;
+    uint64_t bits = 0;
+    for (int k = 0; k < 64; ++k) {
+        const int x = 64 * w + k;
+        if (x < g.n && f[x] < 0.f) bits |= 1ull << k;
+    }
+    signs[i] = bits;
 }
 
 template <int D>
@@ -155,17 +173,23 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
     else k_brick_modes<16><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
 }
 
+void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s) {
+    const int64_t words = (int64_t)g.n * (g.fz1 - g.fz0) * sign_row_words(g);
+    if (words <= 0) return;
+    k_signs_from_field<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(g, d_field, d_signs);
+}
+
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                               float* d_field, hipStream_t s) {
+                               float* d_field, uint16_t* d_signs, hipStream_t s) {
     const BrickGrid bg = brick_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
     const unsigned eb = (unsigned)((bg.n_bricks + 3) / 4);
-    if (depth <= 4) k_eval_field_pruned<4><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
-    else if (depth <= 8) k_eval_field_pruned<8><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
-    else if (depth <= 12) k_eval_field_pruned<12><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
-    else k_eval_field_pruned<16><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field);
+    if (depth <= 4) k_eval_field_pruned<4><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
+    else if (depth <= 8) k_eval_field_pruned<8><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
+    else if (depth <= 12) k_eval_field_pruned<12><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
+    else k_eval_field_pruned<16><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
 }
 
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,

@@ -42,13 +42,15 @@ __device__ __forceinline__ uint32_t brick_fill_class(const uint8_t* __restrict__
     return (xm == c && xp == c && ym == c && yp == c && zm == c && zp == c) ? c : (uint32_t)kBrickMixed;
 }
 
-// One wave per brick (16 x 4 lanes, 4 z layers each).  Sign-filled bricks store +-1 (the
-// sealed ring keeps -1e7); others evaluate every sample with `ev(modes, x, y, z)`.
+// One wave per brick (16 x 4 lanes, 4 z layers each).  Every brick writes its samples' sign bits
+// (wave ballot: 64 bits = 4 rows x 16 samples).  Sign-filled bricks write only those (their field
+// values are never read); the others evaluate every sample with `ev(modes, x, y, z)` and store it.
 template <class Eval>
 __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
                                                  const uint64_t* __restrict__ modes,
                                                  const uint8_t* __restrict__ cls, uint8_t* __restrict__ fill,
-                                                 int sign_fill, float* __restrict__ field) {
+                                                 int sign_fill, float* __restrict__ field,
+                                                 uint16_t* __restrict__ signs) {
     const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
     if (b >= bg.n_bricks) return;
     const int lane = threadIdx.x & 63;
@@ -60,15 +62,19 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
     const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
     const int layers = g.fz1 - g.fz0;
     const size_t plane = (size_t)n * n;
+    const int row16 = 4 * sign_row_words(g);
     float* out = field + (size_t)sy * n + sx;
     const uint32_t fc = sign_fill ? brick_fill_class(cls, bg, b, bx, by, bz) : (uint32_t)kBrickMixed;
     if (lane == 0) fill[b] = (uint8_t)fc;
-    if (fc != kBrickMixed) {   // only the sign is ever read: any value of that sign will do
-        const float v = (fc == kBrickPos) ? 1.f : -1.f;
-        for (int k = 0; k < kBZ; ++k) {
-            const int layer = bz * kBZ + k;
-            if (layer >= layers) break;
-            if (ok) out[(size_t)layer * plane] = (sealed_col || sealed_z(g, layer)) ? kSealed : v;
+    if (fc != kBrickMixed) {   // only the sign is ever read; it is the class (sealed samples are negative too)
+        if (lane < kBY) {
+            const uint16_t w = (fc == kBrickNeg) ? 0xffffu : 0u;
+            const int y = by * kBY + lane;
+            for (int k = 0; k < kBZ; ++k) {
+                const int layer = bz * kBZ + k;
+                if (layer >= layers) break;
+                if (y < n) signs[((size_t)layer * n + y) * row16 + bx] = w;
+            }
         }
         return;
     }
@@ -81,9 +87,14 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
         const int layer = bz * kBZ + k;
         if (layer >= layers) break;
         const float f = ev(m, x, y, sample_z(g, layer));
-        if (ok) out[(size_t)layer * plane] = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
+        const float v = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
+        if (ok) out[(size_t)layer * plane] = v;
+        const uint64_t neg = __ballot(v < 0.f);
+        if (lane < kBY) {
+            const int yy = by * kBY + lane;
+            if (yy < n) signs[((size_t)layer * n + yy) * row16 + bx] = (uint16_t)(neg >> (16 * lane));
+        }
     }
 }
-
 
 }  // namespace impli

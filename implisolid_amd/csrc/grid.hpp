@@ -31,4 +31,9 @@ enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBric
 // then no cell corner in it needs its exact value and MC may take the sign from fill -- else 0.
 struct BrickGrid { int nbx, nby, nbz, n_bricks; };
 
+// Sign bitmap of the stored samples (bit set <=> sample < 0, MC's cube-index test): per stored
+// sample row (layer, y) `sign_row_words(g)` 64-bit words, sample x at bit x % 64 of word x / 64.
+// The eval kernels write it as 16-bit pieces (one per brick row, bricks are 16 samples wide).
+__host__ __device__ inline int sign_row_words(const GridDesc& g) { return (g.n + 63) / 64; }
+
 }  // namespace impli

@@ -148,8 +148,8 @@ std::string TreeJit::kernel_source(const Program& p) {
       << "        return tree_f(M, tab, m, x, y, z);\n    }\n};\n}  // namespace impli\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_eval_bricks(\n"
       << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
-      << "    const uint8_t* cls, uint8_t* fill, int sign_fill, float* field) {\n"
-      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, cls, fill, sign_fill, field);\n}\n";
+      << "    const uint8_t* cls, uint8_t* fill, int sign_fill, float* field, uint16_t* signs) {\n"
+      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);\n}\n";
     return s.str();
 }
 
@@ -214,12 +214,12 @@ hipFunction_t TreeJit::brick_kernel(const Program& p) {
 
 void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
                             const BrickGrid& bg, const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill,
-                            int sign_fill, float* d_field, hipStream_t s) {
+                            int sign_fill, float* d_field, uint16_t* d_signs, hipStream_t s) {
     if (bg.n_bricks <= 0) return;
     GridDesc gg = g;
     BrickGrid bb = bg;
     void* args[] = {(void*)&d_mats, (void*)&d_rabbit, (void*)&gg, (void*)&bb, (void*)&d_modes,
-                    (void*)&d_cls, (void*)&d_fill, (void*)&sign_fill, (void*)&d_field};
+                    (void*)&d_cls, (void*)&d_fill, (void*)&sign_fill, (void*)&d_field, (void*)&d_signs};
     const unsigned blocks = (unsigned)((bg.n_bricks + 3) / 4);
     if (hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
         throw std::runtime_error("hipModuleLaunchKernel(impli_eval_bricks) failed");

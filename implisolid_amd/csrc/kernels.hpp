@@ -33,23 +33,23 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
 // K1b (interpreter): brick-pruned field; the JIT variant is TreeJit::launch_bricks (jit.hpp)
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                               float* d_field, hipStream_t s);
+                               float* d_field, uint16_t* d_signs, hipStream_t s);
+// sign bitmap of a fully written field (unpruned path)
+void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s);
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
                         float* d_f, float* d_grad /* nullable: values only */, hipStream_t s);
 
-// MC pipeline
-constexpr int kUnitCells = 1024;       // cells per counting unit (contiguous in linear cell order)
+// MC pipeline.  Cells are numbered L = row * m + (x - 1), row = (z - cz0) * m + (y - 1); a unit is
+// kUnitRows consecutive rows (contiguous in linear order), processed by one wave.
+constexpr int kUnitRows = 4;
 constexpr int kScanUPT = 8;            // units per lane in the unit scan
 constexpr int kScanBlock = 1024 * kScanUPT;
 struct MCBuffers {
     const float* field;
-    const uint8_t* fill;     // per brick of the field (BrickGrid nbx x nby x nbz), see BrickClass
-    int nbx, nby;
-    uint8_t* ci;             // cube index per cell (n_cells)
+    const uint64_t* signs;   // sign bitmap of the stored samples (grid.hpp)
     uint4* unit_cnt;         // per unit {own, tri, act, halo own}; scanned in place to exclusive bases
     uint32_t* scan_blk;      // 8 per scan block: partial sums (5 components), then exclusive bases
-    uint32_t* active_units;  // compacted list of units with work
-    uint32_t* counters;      // [0] n_active_units, [1] halo own, [2..5] totals own/tri/act/halo
+    uint32_t* counters;      // [0] unused, [1] halo own, [2..5] totals own/tri/act/halo
     uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
     uint4* records;          // active cells: {L, ci, fbase, 0}
     float* verts;            // 3 * cap_v
@@ -63,7 +63,8 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s,
                     hipEvent_t mid = nullptr /* recorded between the vertex and face kernels */);
 
-inline int64_t n_units(const GridDesc& g) { return (g.n_cells + kUnitCells - 1) / kUnitCells; }
+__host__ __device__ inline int64_t n_rows(const GridDesc& g) { return (int64_t)g.m * (g.cz1 - g.cz0); }
+__host__ __device__ inline int64_t n_units(const GridDesc& g) { return (n_rows(g) + kUnitRows - 1) / kUnitRows; }
 inline int64_t n_scan_blocks(const GridDesc& g) { return (n_units(g) + kScanBlock - 1) / kScanBlock; }
 
 }  // namespace impli

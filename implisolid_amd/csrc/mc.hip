@@ -12,13 +12,16 @@
 // exclusive scan of triangle counts.  A vertex's coordinates are computed by its owner cell with
 // the owner's fx/fy/fz, exactly as the reference's first emission did.
 //
-//   K2 k_mc_count : per 1024-cell unit (contiguous in linear order) the sums of owned edges,
-//                   triangles and active cells; units with work are appended to a list.
-//   K2b k_mc_scan : exclusive scan of the unit sums (one workgroup).
-//   K3 k_mc_verts : per active unit, in-unit block scan; writes owned vertex positions, the
-//                   dense vid3[cell][slot] table and one record per active cell.
-//   K4 k_mc_faces : per active cell, gathers the three vertex ids of every triangle corner from
-//                   vid3 of the owner cell.
+// Signs come from the eval's sign bitmap (grid.hpp), 64 cells per bit operation; only the ~1 % of
+// non-trivial cells (corner signs not all equal) do per-cell work.  A unit = kUnitRows cell rows.
+//   K2 k_mc_count : per unit the sums of owned edges, triangles, active cells, halo-owned edges.
+//   K2b k_scan_*  : exclusive scan of the unit sums (partial sums, top level, apply).
+//   K3 k_mc_verts : per unit, the non-trivial cells in cell order: owned vertex positions (field
+//                   values read only at crossing edges), the dense vid3[cell][slot] table, records.
+//   K4 k_mc_faces : per active cell, gathers the vertex ids of its triangle corners from vid3 of
+//                   the owner cells.
+#include <cstdlib>
+
 #include "ifunc_device.hpp"
 #include "kernels.hpp"
 
@@ -70,47 +73,6 @@ namespace {
 __device__ __forceinline__ int sample_index(const GridDesc& g, int sx, int sy, int sz) {
     return (sx - 1) + (sy - 1) * g.n + (sz - g.fz0) * g.n * g.n;   // the field is < 2^31 elements
 }
-__device__ __forceinline__ float corner(const float* __restrict__ field, const GridDesc& g, int sx, int sy, int sz) {
-    return field[sample_index(g, sx, sy, sz)];
-}
-
-struct CellVals {
-    float f[8];   // f0=q f1=qx f2=qy f3=qxy f4=qz f5=qxz f6=qyz f7=qxyz
-};
-
-__device__ __forceinline__ unsigned load_cell(const float* __restrict__ field, const GridDesc& g, int cx, int cy, int cz,
-                                              CellVals& v) {
-    const int n = g.n, nn = g.n * g.n;
-    const float* q = field + sample_index(g, cx, cy, cz);
-    v.f[0] = q[0];
-    v.f[1] = q[1];
-    v.f[2] = q[n];
-    v.f[3] = q[n + 1];
-    v.f[4] = q[nn];
-    v.f[5] = q[nn + 1];
-    v.f[6] = q[nn + n];
-    v.f[7] = q[nn + n + 1];
-    unsigned ci = 0;   // polygonize_single_cube :553-560
-    if (v.f[0] < 0.f) ci |= 1;
-    if (v.f[1] < 0.f) ci |= 2;
-    if (v.f[2] < 0.f) ci |= 8;
-    if (v.f[3] < 0.f) ci |= 4;
-    if (v.f[4] < 0.f) ci |= 16;
-    if (v.f[5] < 0.f) ci |= 32;
-    if (v.f[6] < 0.f) ci |= 128;
-    if (v.f[7] < 0.f) ci |= 64;
-    return ci;
-}
-
-__device__ __forceinline__ void cell_coords(const GridDesc& g, uint32_t L, int& cx, int& cy, int& cz) {
-    const uint32_t m = (uint32_t)g.m, mm = m * m;
-    const uint32_t zr = L / mm, rem = L - zr * mm;
-    const uint32_t yr = rem / m;
-    cx = 1 + (int)(rem - yr * m);
-    cy = 1 + (int)yr;
-    cz = g.cz0 + (int)zr;
-}
-
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T x, int lane) {
 #pragma unroll
@@ -121,145 +83,90 @@ __device__ __forceinline__ T wave_incl_scan(T x, int lane) {
     return x;
 }
 
-// exclusive block scan over 256 lanes (4 waves); returns prefix, sets total
-__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long& total,
-                                                              unsigned long long* lds4) {
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const unsigned long long incl = wave_incl_scan<unsigned long long>(v, lane);
-    if (lane == 63) lds4[wid] = incl;
-    __syncthreads();
-    unsigned long long pre = 0;
-    total = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const unsigned long long s = lds4[w];
-        if (w < wid) pre += s;
-        total += s;
-    }
-    __syncthreads();
-    return pre + incl - v;
-}
-
-constexpr unsigned long long kF = 20;   // packed counter field width
-__device__ __forceinline__ unsigned long long pack3(unsigned own, unsigned tri, unsigned act) {
-    return (unsigned long long)own | ((unsigned long long)tri << kF) | ((unsigned long long)act << (2 * kF));
-}
-__device__ __forceinline__ unsigned f_own(unsigned long long p) { return (unsigned)(p & ((1ull << kF) - 1)); }
-__device__ __forceinline__ unsigned f_tri(unsigned long long p) { return (unsigned)((p >> kF) & ((1ull << kF) - 1)); }
-__device__ __forceinline__ unsigned f_act(unsigned long long p) { return (unsigned)(p >> (2 * kF)); }
-
-// cube index from the negative-corner masks of the four sample rows around a run of cells:
-// bit k of r00/r10/r01/r11 = sample x0+k of rows (y,z), (y+1,z), (y,z+1), (y+1,z+1) is < 0
-__device__ __forceinline__ unsigned ci_from_rows(unsigned r00, unsigned r10, unsigned r01, unsigned r11, int k) {
-    const unsigned a = (r00 >> k) & 3u, b = (r10 >> k) & 3u, c = (r01 >> k) & 3u, d = (r11 >> k) & 3u;
-    // corners q(1) qx(2) | qy(8) qxy(4) | qz(16) qxz(32) | qyz(128) qxyz(64)
-    return (a & 1u) | ((a >> 1) << 1) | ((b & 1u) << 3) | ((b >> 1) << 2) | ((c & 1u) << 4) | ((c >> 1) << 5) |
-           ((d & 1u) << 7) | ((d >> 1) << 6);
-}
-
-// K2: one 256-thread block per 1024-cell unit, 4 consecutive cells per thread.  Runs of 4 cells
-// in one row share their corners (20 loads instead of 32); if every brick the run touches was
-// sign-filled by the eval with one sign, the cube indices are known without touching the field.
-// owned-edge and triangle counts of a cube index; trivial cells (ci 0 / 255, ~99 % of them) skip
-// the table read
+// owned-edge and triangle counts of a cube index
 __device__ __forceinline__ unsigned case_counts(const CaseInfo* __restrict__ cases, unsigned ci, unsigned& ntri) {
-    if (ci == 0u || ci == 255u) { ntri = 0; return 0; }
     const uint16_t v = *reinterpret_cast<const uint16_t*>(&cases[ci]);   // {ntri, nown}
     ntri = v & 255u;
     return v >> 8;
 }
 
-__global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
-    __shared__ uint4 s_red[4];
-    const int t = threadIdx.x;
-    const uint32_t u = blockIdx.x;
-    const uint32_t L0 = u * kUnitCells + 4u * (uint32_t)t;
-    unsigned own = 0, tri = 0, act = 0, halo_own = 0;
-    if (L0 < (uint64_t)g.n_cells) {
-        int cx, cy, cz;
-        cell_coords(g, L0, cx, cy, cz);
-        uint32_t ci4 = 0;
-        if (cx + 3 <= g.m && L0 + 3 < (uint64_t)g.n_cells) {
-            // stored coordinates of the run's first corner; the run reads x0 .. x0+4
-            const int x0 = cx - 1, y0 = cy - 1, z0 = cz - g.fz0;
-            const int bx0 = x0 / kBX, bx1 = (x0 + 4) / kBX, by0 = y0 / kBY, by1 = (y0 + 1) / kBY;
-            const int bz0 = z0 / kBZ, bz1 = (z0 + 1) / kBZ;
-            const int sby = b.nbx, sbz = b.nbx * b.nby;
-            const uint8_t* fb = b.fill;
-            unsigned f_and = 3u, f_or = 0u;
+// 64 consecutive cells of one cell row, as sign bits.  For cell j (x = 64 c + 1 + j) the corners
+// are stored samples x-1 and x of the rows (y, z), (y+1, z), (y, z+1), (y+1, z+1): bit j of s.. and
+// t.. (t = s shifted by one sample).  nt marks the non-trivial cells (corner signs not all equal).
+struct ChunkBits {
+    uint64_t s00, t00, s10, t10, s01, t01, s11, t11, nt;
+    int y, z, x0;   // cell row and first cell x of the chunk
+};
+
+__device__ __forceinline__ void load_chunk(const GridDesc& g, const uint64_t* __restrict__ signs, int64_t row, int c,
+                                           ChunkBits& k) {
+    const int rw = sign_row_words(g);
+    k.y = (int)(row % g.m) + 1;
+    k.z = (int)(row / g.m) + g.cz0;
+    k.x0 = 64 * c + 1;
+    const int64_t r00 = ((int64_t)(k.z - g.fz0) * g.n + (k.y - 1)) * rw;   // (layer, stored y) -> word index
+    const int64_t rows[4] = {r00, r00 + rw, r00 + (int64_t)g.n * rw, r00 + (int64_t)g.n * rw + rw};
+    uint64_t s[4], t[4];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const unsigned v = fb[((k & 1) ? bx1 : bx0) + ((k & 2) ? by1 : by0) * sby + ((k & 4) ? bz1 : bz0) * sbz];
-                f_and &= v;
-                f_or |= v;
-            }
-            const unsigned f0 = f_or;
-            if (f0 != 0u && f_and == f_or) {   // all eight equal and non-zero
-                // all touched bricks filled with one sign: every corner has that sign
-                ci4 = (f0 == kBrickNeg) ? 0xffffffffu : 0u;
-            } else {
-                const int n = g.n, nn = n * n;
-                const float* q = b.field + (x0 + y0 * n + z0 * nn);
-                unsigned r00 = 0, r10 = 0, r01 = 0, r11 = 0;
-#pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                    r00 |= (q[k] < 0.f ? 1u : 0u) << k;
-                    r10 |= (q[n + k] < 0.f ? 1u : 0u) << k;
-                    r01 |= (q[nn + k] < 0.f ? 1u : 0u) << k;
-                    r11 |= (q[nn + n + k] < 0.f ? 1u : 0u) << k;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) ci4 |= ci_from_rows(r00, r10, r01, r11, k) << (8 * k);
-            }
-            unsigned o = 0, tr = 0, ac = 0;
-            if (ci4 != 0u && ci4 != 0xffffffffu) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    unsigned nt;
-                    o += case_counts(cases, (ci4 >> (8 * k)) & 255u, nt);
-                    tr += nt;
-                    ac += nt ? 1u : 0u;
-                }
-            }
-            own = o;
-            if (cz >= g.cz_emit) { tri = tr; act = ac; }
-            else halo_own = o;
-        } else {
-            // the run crosses a row end (or the slab end): cell by cell
-            int x = cx, y = cy, z = cz;
-            for (int k = 0; k < 4; ++k) {
-                if (L0 + k >= (uint64_t)g.n_cells) break;
-                CellVals v;
-                const unsigned ci = load_cell(b.field, g, x, y, z, v);
-                ci4 |= ci << (8 * k);
-                unsigned nt;
-                const unsigned no = case_counts(cases, ci, nt);
-                own += no;
-                if (z >= g.cz_emit) { tri += nt; act += nt ? 1u : 0u; }
-                else halo_own += no;
-                if (++x > g.m) { x = 1; if (++y > g.m) { y = 1; ++z; } }
-            }
-        }
-        *reinterpret_cast<uint32_t*>(b.ci + L0) = ci4;   // ci has >= 64 bytes of padding
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t w = signs[rows[q] + c];
+        const uint64_t nx = (c + 1 < rw) ? signs[rows[q] + c + 1] : 0ull;
+        s[q] = w;
+        t[q] = (w >> 1) | (nx << 63);
     }
-    const int lane = t & 63, wid = t >> 6;
+    k.s00 = s[0]; k.t00 = t[0]; k.s10 = s[1]; k.t10 = t[1]; k.s01 = s[2]; k.t01 = t[2]; k.s11 = s[3]; k.t11 = t[3];
+    const uint64_t all = s[0] & t[0] & s[1] & t[1] & s[2] & t[2] & s[3] & t[3];
+    const uint64_t any = s[0] | t[0] | s[1] | t[1] | s[2] | t[2] | s[3] | t[3];
+    const int left = g.m - 64 * c;   // cells of this chunk inside the row
+    const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+    k.nt = any & ~all & valid;
+}
+
+// cube index of cell j of a chunk, corner bits as polygonize_single_cube (:553-560)
+__device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
+    return (unsigned)((k.s00 >> j) & 1u) | ((unsigned)((k.t00 >> j) & 1u) << 1) | ((unsigned)((k.s10 >> j) & 1u) << 3) |
+           ((unsigned)((k.t10 >> j) & 1u) << 2) | ((unsigned)((k.s01 >> j) & 1u) << 4) |
+           ((unsigned)((k.t01 >> j) & 1u) << 5) | ((unsigned)((k.s11 >> j) & 1u) << 7) |
+           ((unsigned)((k.t11 >> j) & 1u) << 6);
+}
+
+// K2: one wave per unit (kUnitRows rows).  Items (row, 64-cell chunk) are spread over the lanes;
+// only non-trivial cells (~1 %) look at the case table.  -> unit_cnt[u] = {own, tri, act, halo own}
+__global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+    const int lane = threadIdx.x & 63;
+    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u >= n_units(g)) return;
+    const int nch = (g.m + 63) / 64;
+    const int64_t rows = n_rows(g);
+    unsigned own = 0, tri = 0, act = 0, hal = 0;
+    for (int i = lane; i < kUnitRows * nch; i += 64) {
+        const int64_t row = u * kUnitRows + i / nch;
+        if (row >= rows) break;
+        ChunkBits k;
+        load_chunk(g, b.signs, row, i % nch, k);
+        uint64_t nt = k.nt;
+        const bool emit = k.z >= g.cz_emit;
+        while (nt) {
+            const int j = __ffsll((unsigned long long)nt) - 1;
+            nt &= nt - 1;
+            unsigned ntri;
+            const unsigned no = case_counts(cases, chunk_ci(k, j), ntri);
+            own += no;
+            if (emit) { tri += ntri; act += ntri ? 1u : 0u; }
+            else hal += no;
+        }
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         own += __shfl_down(own, o, 64);
         tri += __shfl_down(tri, o, 64);
         act += __shfl_down(act, o, 64);
-        halo_own += __shfl_down(halo_own, o, 64);
+        hal += __shfl_down(hal, o, 64);
     }
-    if (lane == 0) s_red[wid] = make_uint4(own, tri, act, halo_own);
-    __syncthreads();
-    if (t == 0) {
-        uint4 sm = s_red[0];
-        for (int w = 1; w < 4; ++w) { sm.x += s_red[w].x; sm.y += s_red[w].y; sm.z += s_red[w].z; sm.w += s_red[w].w; }
-        b.unit_cnt[u] = sm;
-    }
+    if (lane == 0) b.unit_cnt[u] = make_uint4(own, tri, act, hal);
 }
 
-// ---- unit scan: partial sums per scan block, top-level scan, apply + compaction of active units ----
+// ---- unit scan: partial sums per scan block, top-level scan, apply ----
 struct Cnt5 { uint32_t c[5]; };
 __device__ __forceinline__ Cnt5 unit_c5(uint4 v) {
     Cnt5 r;
@@ -325,8 +232,7 @@ __global__ __launch_bounds__(64) void k_scan_top(uint32_t* __restrict__ blk, int
     counters[5] = run[3];
 }
 
-__global__ __launch_bounds__(1024) void k_scan_apply(uint4* __restrict__ cnt, int64_t nu, const uint32_t* __restrict__ blk,
-                                                     uint32_t* __restrict__ active) {
+__global__ __launch_bounds__(1024) void k_scan_apply(uint4* __restrict__ cnt, int64_t nu, const uint32_t* __restrict__ blk) {
     __shared__ uint32_t s_w[5][16];
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanUPT;
     uint4 v[kScanUPT];
@@ -343,81 +249,80 @@ __global__ __launch_bounds__(1024) void k_scan_apply(uint4* __restrict__ cnt, in
         if (base + i >= nu) break;
         const Cnt5 c = unit_c5(v[i]);
         cnt[base + i] = make_uint4(run.c[0], run.c[1], run.c[2], run.c[3]);
-        if (c.c[4]) active[run.c[4]] = (uint32_t)(base + i);
         for (int k = 0; k < 5; ++k) run.c[k] += c.c[k];
     }
 }
 
-// K3: one wave per active unit (persistent loop).  Phase 1: each lane loads 16 cube indices
-// (one 16-byte load) and the wave compacts the unit's non-trivial cells (ci != 0, 255 -- about
-// 1 % of all cells) into an LDS list, in cell order.  Phase 2: lanes take list entries 64 at a
-// time; a wave scan of (owned edges, triangles, active) gives each cell its vertex / face /
-// record base, and the cells' vertices and records are written in parallel.
+// K3: one wave per unit.  Lanes find the non-trivial cells of their (row, chunk) items; a wave scan
+// orders them (cell order) into an LDS list, processed 64 at a time: a second wave scan of (owned
+// edges, triangles, active) gives every cell its vertex / face / record base, all written in
+// parallel.  Corner values are read from the field only for owned crossing edges.
 __device__ __forceinline__ unsigned long long pack4(unsigned a, unsigned b, unsigned c, unsigned d) {
     return (unsigned long long)a | ((unsigned long long)b << 16) | ((unsigned long long)c << 32) |
            ((unsigned long long)d << 48);
 }
 __device__ __forceinline__ unsigned fld(unsigned long long p, int i) { return (unsigned)(p >> (16 * i)) & 0xffffu; }
 
+constexpr int kListCap = 1024;   // LDS list entries per wave (a window; larger units loop)
+
 __global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ CaseInfo s_case[256];
-    __shared__ uint32_t s_list[4][kUnitCells];   // per wave: (cell offset in unit) | ci << 16
+    __shared__ uint32_t s_list[4][kListCap];   // per wave: ci | j << 8 | item << 14
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     s_case[t] = cases[t];
     __syncthreads();
-    const uint32_t n_active = b.counters[0];
+    const int64_t u = (int64_t)blockIdx.x * 4 + wid;
+    if (u >= n_units(g)) return;
     const uint32_t H = b.counters[1];
-    const uint64_t halo_cells = (uint64_t)g.m * g.m * (uint64_t)(g.cz_emit - g.cz0);
+    const int nch = (g.m + 63) / 64;
+    const int64_t rows = n_rows(g);
+    const uint4 base = b.unit_cnt[u];   // exclusive {vbase, fbase, abase, hbase}
+    uint32_t vrun0 = base.x, frun0 = base.y, arun0 = base.z;
     uint32_t* list = s_list[wid];
-    constexpr int CPL = kUnitCells / 64;   // 16 cells per lane
-    for (uint32_t a = blockIdx.x * 4 + wid; a < n_active; a += gridDim.x * 4) {
-        const uint32_t u = b.active_units[a];
-        const uint4 base = b.unit_cnt[u];   // exclusive {vbase, fbase, abase, hbase}
-        const uint32_t U0 = u * kUnitCells;
-        const uint32_t L0 = U0 + lane * CPL;
-        uint32_t w[4] = {0, 0, 0, 0};
-        if (L0 + CPL <= (uint64_t)g.n_cells) {
-            const uint4 q = *reinterpret_cast<const uint4*>(b.ci + L0);
-            w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
-        } else {
-            for (int k = 0; k < CPL; ++k)
-                if (L0 + k < (uint64_t)g.n_cells) w[k >> 2] |= (uint32_t)b.ci[L0 + k] << (8 * (k & 3));
+    const int items = kUnitRows * nch;
+    for (int i0 = 0; i0 < items; i0 += 64) {
+        const int i = i0 + lane;
+        ChunkBits k;
+        k.nt = 0;
+        int64_t row = -1;
+        if (i < items) {
+            row = u * kUnitRows + i / nch;
+            if (row < rows) load_chunk(g, b.signs, row, i % nch, k);
         }
-        // non-trivial cells of this lane
-        uint32_t mask = 0;
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-            const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 255u;
-            mask |= (c != 0u && c != 255u) ? (1u << k) : 0u;
-        }
-        const uint32_t cnt = (uint32_t)__popc(mask);
+        const uint32_t cnt = (uint32_t)__popcll((unsigned long long)k.nt);
         const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);
-        const uint32_t n_list = __shfl(incl, 63, 64);
-        uint32_t pos = incl - cnt;
-        while (mask) {
-            const int k = __ffs(mask) - 1;
-            mask &= mask - 1;
-            list[pos++] = (uint32_t)(lane * CPL + k) | (((w[k >> 2] >> (8 * (k & 3))) & 255u) << 16);
-        }
-        __builtin_amdgcn_wave_barrier();
-        uint32_t vrun0 = base.x, frun0 = base.y, arun0 = base.z;
-        for (uint32_t e0 = 0; e0 < n_list; e0 += 64) {
-            const uint32_t e = e0 + (uint32_t)lane;
-            const bool has = e < n_list;
-            const uint32_t ent = has ? list[e] : 0u;
-            const uint32_t L = U0 + (ent & 0xffffu);
-            const unsigned ci = ent >> 16;
-            const CaseInfo& C = s_case[ci];
-            const bool emit = has && (uint64_t)L >= halo_cells;
-            const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
-            const unsigned long long p = pack4(own, tri, act, 0u);
-            const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
-            const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
-            if (has) {
-                int x, y, z;
-                cell_coords(g, L, x, y, z);
-                uint32_t vrun = vrun0 + fld(pre, 0);
-                if (own) {
+        const uint32_t total = __shfl(incl, 63, 64);
+        for (uint32_t w0 = 0; w0 < total; w0 += kListCap) {
+            // this window's entries, in cell order
+            uint32_t pos = incl - cnt;
+            uint64_t nt = k.nt;
+            while (nt) {
+                const int j = __ffsll((unsigned long long)nt) - 1;
+                nt &= nt - 1;
+                if (pos >= w0 && pos < w0 + kListCap)
+                    list[pos - w0] = chunk_ci(k, j) | ((uint32_t)j << 8) | ((uint32_t)i << 14);
+                ++pos;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t n_list = (total - w0 < (uint32_t)kListCap) ? total - w0 : (uint32_t)kListCap;
+            for (uint32_t e0 = 0; e0 < n_list; e0 += 64) {
+                const uint32_t e = e0 + (uint32_t)lane;
+                const bool has = e < n_list;
+                const uint32_t ent = has ? list[e] : 0u;
+                const unsigned ci = ent & 255u;
+                const int j = (int)((ent >> 8) & 63u), it = (int)(ent >> 14);
+                const int64_t erow = u * kUnitRows + it / nch;
+                const int x = 64 * (it % nch) + 1 + j;
+                const int y = (int)(erow % g.m) + 1, z = (int)(erow / g.m) + g.cz0;
+                const uint32_t L = (uint32_t)(erow * g.m + (x - 1));
+                const CaseInfo& C = s_case[ci];
+                const bool emit = has && z >= g.cz_emit;
+                const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
+                const unsigned long long p = pack4(own, tri, act, 0u);
+                const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
+                const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
+                if (has && own) {
+                    const uint32_t vrun = vrun0 + fld(pre, 0);
                     const float fx = ((float)x + g.i0[0]) * g.w[0];
                     const float fy = ((float)y + g.i0[1]) * g.w[1];
                     const float fz = ((float)z + g.i0[2]) * g.w[2];
@@ -458,12 +363,12 @@ __global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ c
                     if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
                     else *b.overflow = 1u;
                 }
+                vrun0 += fld(tot, 0);
+                frun0 += fld(tot, 1);
+                arun0 += fld(tot, 2);
             }
-            vrun0 += fld(tot, 0);
-            frun0 += fld(tot, 1);
-            arun0 += fld(tot, 2);
+            __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -507,14 +412,14 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
 void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     const int64_t nu = n_units(g);
     if (nu == 0) return;
-    k_mc_count<<<(unsigned)nu, 256, 0, s>>>(d_cases, g, b);
+    k_mc_count<<<(unsigned)((nu + 3) / 4), 256, 0, s>>>(d_cases, g, b);
 }
 
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     const int64_t nu = n_units(g), nb = n_scan_blocks(g);
     if (nb > 0) k_scan_partial<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk);
     k_scan_top<<<1, 64, 0, s>>>(b.scan_blk, (int)nb, b.counters);
-    if (nb > 0) k_scan_apply<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk, b.active_units);
+    if (nb > 0) k_scan_apply<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk);
 }
 
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
@@ -523,7 +428,7 @@ void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
 
 void launch_mc_emit(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s, hipEvent_t mid) {
     const int64_t nu = n_units(g);
-    k_mc_verts<<<(unsigned)(nu < 4096 ? (nu > 0 ? nu : 1) : 4096), 256, 0, s>>>(d_cases, g, b);
+    if (nu > 0) k_mc_verts<<<(unsigned)((nu + 3) / 4), 256, 0, s>>>(d_cases, g, b);
     if (mid) (void)hipEventRecord(mid, s);
     k_mc_faces<<<2048, 256, 0, s>>>(d_cases, g, b);
 }

@@ -148,6 +148,10 @@ int implisolid_slab_used_jit(implisolid_slab* s);
  * environment IMPLISOLID_JIT=0 starts with it off).  Results are bit-identical either way. */
 void implisolid_set_jit(int on);
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]);
+/* blocking copy of the slab's sample signs (1: value < 0), n*n*layers bytes, x fastest; with
+ * out == NULL returns the count.  At pruning level 2 sign-filled bricks keep no field values, so
+ * this (not the field) is the complete sign information marching cubes uses. */
+int64_t implisolid_slab_read_signs(implisolid_slab* s, uint8_t* out, int64_t capacity);
 /* bricks of the last slab eval: out = [bricks, mixed-sign bricks, sign-filled bricks] (blocking) */
 int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]);
 

@@ -223,16 +223,19 @@ def test_ob02_config3_tree_small(impli, oracle):
     _ob02_compare(impli, oracle, shape, mc)
 
 
-def _field(impli, shape, mc, level):
+def _field(impli, shape, mc, level, signs=False):
     impli.set_pruning(level)
     try:
         s = impli.Slab(shape, mc)
         s.eval()
         f = s.read_field()
+        sg = s.read_signs()
         s.close()
     finally:
         impli.set_pruning(2)
-    return f
+    if level < 2:   # the sign bitmap always matches a fully written field
+        assert np.array_equal(sg.astype(bool), f < 0)
+    return (f, sg) if signs else f
 
 
 def _needed_samples(f):
@@ -260,8 +263,8 @@ def test_pruned_field_identical(impli, name):
         a = _field(impli, TREES[name], mc, 1)
         b = _field(impli, TREES[name], mc, 0)
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
-        c = _field(impli, TREES[name], mc, 2)
-        assert np.array_equal(c < 0, b < 0)
+        c, cs = _field(impli, TREES[name], mc, 2, signs=True)
+        assert np.array_equal(cs.astype(bool), b < 0)
         need = _needed_samples(b)
         assert np.array_equal(c[need].view(np.uint32), b[need].view(np.uint32))
 
@@ -274,8 +277,8 @@ def test_pruned_field_random_trees(impli, seed):
     a = _field(impli, shape, mc, 1)
     b = _field(impli, shape, mc, 0)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
-    c = _field(impli, shape, mc, 2)
-    assert np.array_equal(c < 0, b < 0)
+    c, cs = _field(impli, shape, mc, 2, signs=True)
+    assert np.array_equal(cs.astype(bool), b < 0)
     need = _needed_samples(b)
     assert np.array_equal(c[need].view(np.uint32), b[need].view(np.uint32))
 
