@@ -206,11 +206,11 @@ void Engine::eval_field(hipStream_t s) {
             const float* d_mats = reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
             TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_),
                                    modes_.as<uint64_t>(), cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2,
-                                   field_.as<float>(), signs_.as<uint16_t>(), s);
+                                   field_.as<float>(), signs_.p, s);
         } else {
             launch_eval_bricks_interp(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, modes_.as<uint64_t>(),
                                       cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2, field_.as<float>(),
-                                      signs_.as<uint16_t>(), s);
+                                      signs_.p, s);
         }
     } else {
         IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled

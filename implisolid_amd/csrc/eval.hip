@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __rest
                                                            const uint64_t* __restrict__ modes,
                                                            const uint8_t* __restrict__ cls,
                                                            uint8_t* __restrict__ fill, int sign_fill,
-                                                           float* __restrict__ field, uint16_t* __restrict__ signs) {
+                                                           float* __restrict__ field, void* __restrict__ signs) {
     eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);
 }
 
@@ -181,7 +181,7 @@ void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* 
 
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                               float* d_field, uint16_t* d_signs, hipStream_t s) {
+                               float* d_field, void* d_signs, hipStream_t s) {
     const BrickGrid bg = brick_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);

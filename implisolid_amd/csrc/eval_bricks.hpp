@@ -5,6 +5,13 @@
 
 namespace impli {
 
+// one brick row of sign bits
+template <int W> struct SignPiece;
+template <> struct SignPiece<8> { typedef uint8_t type; };
+template <> struct SignPiece<16> { typedef uint16_t type; };
+template <> struct SignPiece<32> { typedef uint32_t type; };
+typedef SignPiece<kBX>::type sign_piece_t;
+
 // sample coordinate of stored index i (sample i + 1) along an axis (prepare_grid,
 // marching_cubes.hpp:1691-1693: x * factor + min - 2 * width)
 __device__ __forceinline__ float sample_xy(const GridDesc& g, int axis, int i) {
@@ -50,7 +57,8 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
                                                  const uint64_t* __restrict__ modes,
                                                  const uint8_t* __restrict__ cls, uint8_t* __restrict__ fill,
                                                  int sign_fill, float* __restrict__ field,
-                                                 uint16_t* __restrict__ signs) {
+                                                 void* __restrict__ signs_raw) {
+    sign_piece_t* signs = static_cast<sign_piece_t*>(signs_raw);
     const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
     if (b >= bg.n_bricks) return;
     const int lane = threadIdx.x & 63;
@@ -62,18 +70,18 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
     const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
     const int layers = g.fz1 - g.fz0;
     const size_t plane = (size_t)n * n;
-    const int row16 = 4 * sign_row_words(g);
+    const int row_pieces = (64 / kBX) * sign_row_words(g);
     float* out = field + (size_t)sy * n + sx;
     const uint32_t fc = sign_fill ? brick_fill_class(cls, bg, b, bx, by, bz) : (uint32_t)kBrickMixed;
     if (lane == 0) fill[b] = (uint8_t)fc;
     if (fc != kBrickMixed) {   // only the sign is ever read; it is the class (sealed samples are negative too)
         if (lane < kBY) {
-            const uint16_t w = (fc == kBrickNeg) ? 0xffffu : 0u;
+            const sign_piece_t w = (fc == kBrickNeg) ? (sign_piece_t)~(sign_piece_t)0 : (sign_piece_t)0;
             const int y = by * kBY + lane;
             for (int k = 0; k < kBZ; ++k) {
                 const int layer = bz * kBZ + k;
                 if (layer >= layers) break;
-                if (y < n) signs[((size_t)layer * n + y) * row16 + bx] = w;
+                if (y < n) signs[((size_t)layer * n + y) * row_pieces + bx] = w;
             }
         }
         return;
@@ -92,7 +100,7 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
         const uint64_t neg = __ballot(v < 0.f);
         if (lane < kBY) {
             const int yy = by * kBY + lane;
-            if (yy < n) signs[((size_t)layer * n + yy) * row16 + bx] = (uint16_t)(neg >> (16 * lane));
+            if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg >> (kBX * lane));
         }
     }
 }

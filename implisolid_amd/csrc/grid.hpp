@@ -24,8 +24,15 @@ struct GridDesc {
     int64_t n_cells;             // m * m * (cz1 - cz0)
 };
 
-// pruned field evaluation: bricks of kBX x kBY x kBZ stored samples (x fastest)
-constexpr int kBX = 16, kBY = 4, kBZ = 4;
+// pruned field evaluation: bricks of kBX x kBY x kBZ stored samples (x fastest); 8 x 8 x 16 measured
+// fastest at R = 512 (near-cubic boxes give tight intervals; tall bricks amortise the interval pass)
+#ifndef IMPLI_BRICK_X
+#define IMPLI_BRICK_X 8
+#define IMPLI_BRICK_Y 8
+#define IMPLI_BRICK_Z 16
+#endif
+constexpr int kBX = IMPLI_BRICK_X, kBY = IMPLI_BRICK_Y, kBZ = IMPLI_BRICK_Z;
+static_assert(kBX * kBY == 64 && (kBX == 8 || kBX == 16 || kBX == 32), "a brick layer is one wave");
 enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBrickNoFill = 4 };
 // fill[b] (written by the pruned eval): kBrickPos / kBrickNeg if the brick was sign-filled --
 // then no cell corner in it needs its exact value and MC may take the sign from fill -- else 0.
@@ -33,7 +40,7 @@ struct BrickGrid { int nbx, nby, nbz, n_bricks; };
 
 // Sign bitmap of the stored samples (bit set <=> sample < 0, MC's cube-index test): per stored
 // sample row (layer, y) `sign_row_words(g)` 64-bit words, sample x at bit x % 64 of word x / 64.
-// The eval kernels write it as 16-bit pieces (one per brick row, bricks are 16 samples wide).
+// The eval kernels write it as kBX-bit pieces (one per brick row).
 __host__ __device__ inline int sign_row_words(const GridDesc& g) { return (g.n + 63) / 64; }
 
 }  // namespace impli

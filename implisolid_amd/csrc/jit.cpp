@@ -148,7 +148,7 @@ std::string TreeJit::kernel_source(const Program& p) {
       << "        return tree_f(M, tab, m, x, y, z);\n    }\n};\n}  // namespace impli\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_eval_bricks(\n"
       << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
-      << "    const uint8_t* cls, uint8_t* fill, int sign_fill, float* field, uint16_t* signs) {\n"
+      << "    const uint8_t* cls, uint8_t* fill, int sign_fill, float* field, void* signs) {\n"
       << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);\n}\n";
     return s.str();
 }
@@ -214,7 +214,7 @@ hipFunction_t TreeJit::brick_kernel(const Program& p) {
 
 void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
                             const BrickGrid& bg, const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill,
-                            int sign_fill, float* d_field, uint16_t* d_signs, hipStream_t s) {
+                            int sign_fill, float* d_field, void* d_signs, hipStream_t s) {
     if (bg.n_bricks <= 0) return;
     GridDesc gg = g;
     BrickGrid bb = bg;

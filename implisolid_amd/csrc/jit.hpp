@@ -37,7 +37,7 @@ public:
     // launch the compiled brick kernel (same contract as launch_eval_field_pruned's 2nd kernel)
     static void launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
                               const BrickGrid& bg, const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill,
-                              int sign_fill, float* d_field, uint16_t* d_signs, hipStream_t s);
+                              int sign_fill, float* d_field, void* d_signs, hipStream_t s);
 
     bool enabled() const { return enabled_; }
     void set_enabled(bool on) { enabled_ = on; }

@@ -33,7 +33,7 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
 // K1b (interpreter): brick-pruned field; the JIT variant is TreeJit::launch_bricks (jit.hpp)
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
-                               float* d_field, uint16_t* d_signs, hipStream_t s);
+                               float* d_field, void* d_signs, hipStream_t s);
 // sign bitmap of a fully written field (unpruned path)
 void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s);
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
