@@ -174,6 +174,7 @@ MCBuffers Engine::buffers() const {
     MCBuffers b{};
     b.field = field_.as<float>();
     b.signs = signs_.as<uint64_t>();
+
     b.unit_cnt = unit_cnt_.as<uint4>();
     b.scan_blk = scan_blk_.as<uint32_t>();
     b.counters = counters_.as<uint32_t>();
@@ -195,10 +196,7 @@ void Engine::eval_field(hipStream_t s) {
     const int level = pruning();
     mark(0, s);
     if (level > 0) {
-        if (!jit_tried_) {   // compile the tree kernel for this shape once (cached by shape)
-            jit_fn_ = TreeJit::instance().brick_kernel(prog_host_);
-            jit_tried_ = true;
-        }
+        ensure_jit();
         launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, modes_.as<uint64_t>(),
                            cls_.as<uint8_t>(), s);
         mark(1, s);
@@ -222,6 +220,13 @@ void Engine::eval_field(hipStream_t s) {
     IMPLI_HIP(hipGetLastError());
 }
 
+void Engine::ensure_jit() {   // compile the tree kernels for this shape once (cached by shape)
+    if (jit_tried_) return;
+    const TreeJit::Kernels k = TreeJit::instance().kernels(prog_host_);
+    jit_fn_ = k.bricks;
+    jit_tried_ = true;
+}
+
 void Engine::count(hipStream_t s) {
     IMPLI_HIP(hipMemsetAsync(counters_.p, 0, 16 * sizeof(uint32_t), s));
     IMPLI_HIP(hipMemsetAsync(overflow_.p, 0, 16, s));
@@ -238,7 +243,9 @@ void Engine::emit(const uint32_t* d_offsets, hipStream_t s) {
     MCBuffers b = buffers();
     b.offsets = d_offsets ? d_offsets : offsets_.as<uint32_t>();
     mark(6, s);
-    launch_mc_emit(cases_.as<CaseInfo>(), grid_, b, s, timing_ ? ev_[7] : nullptr);
+    launch_mc_verts(cases_.as<CaseInfo>(), grid_, b, s);
+    mark(7, s);
+    launch_mc_faces(cases_.as<CaseInfo>(), grid_, b, s);
     mark(8, s);
     IMPLI_HIP(hipGetLastError());
 }

@@ -98,6 +98,7 @@ private:
     Program prog_host_{};
     bool jit_tried_ = false;
     hipFunction_t jit_fn_ = nullptr;
+    void ensure_jit();
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;

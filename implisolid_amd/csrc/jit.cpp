@@ -145,11 +145,13 @@ std::string TreeJit::kernel_source(const Program& p) {
       << em.out.str() << "    return " << f << ";\n}\n"
       << "struct JitEval {\n    const float* M;\n    const float* tab;\n"
       << "    __device__ __forceinline__ float operator()(uint64_t m, float x, float y, float z) const {\n"
-      << "        return tree_f(M, tab, m, x, y, z);\n    }\n};\n}  // namespace impli\n"
+      << "        return tree_f(M, tab, m, x, y, z);\n    }\n};\n"
+      << "}  // namespace impli\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_eval_bricks(\n"
       << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
       << "    const uint8_t* cls, uint8_t* fill, int sign_fill, float* field, void* signs) {\n"
-      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);\n}\n";
+      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);\n}\n"
+;
     return s.str();
 }
 
@@ -180,36 +182,42 @@ std::vector<char> TreeJit::compile(const std::string& src) {
         throw;
     }
     hiprtcDestroyProgram(&prog);
+    if (const char* dir = std::getenv("IMPLISOLID_JIT_DUMP")) {   // diagnostics: keep source + code object
+        static int n = 0;
+        const std::string base = std::string(dir) + "/tree_" + std::to_string(n++);
+        if (FILE* f = std::fopen((base + ".hip").c_str(), "w")) { std::fwrite(src.data(), 1, src.size(), f); std::fclose(f); }
+        if (FILE* f = std::fopen((base + ".co").c_str(), "wb")) { std::fwrite(code.data(), 1, code.size(), f); std::fclose(f); }
+    }
     return code;
 }
 
-hipFunction_t TreeJit::brick_kernel(const Program& p) {
-    if (!enabled_) return nullptr;
+TreeJit::Kernels TreeJit::kernels(const Program& p) {
+    if (!enabled_) return Kernels{};
     std::string src;
     try {
         src = kernel_source(p);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "implisolid: tree JIT skipped (%s)\n", e.what());
-        return nullptr;
+        return Kernels{};
     }
     std::lock_guard<std::mutex> lock(mu_);
     auto it = cache_.find(src);
-    if (it != cache_.end()) return it->second.fn;
+    if (it != cache_.end()) return it->second.k;
     Entry ent;
     const auto t0 = std::chrono::steady_clock::now();
     try {
         const std::vector<char> code = compile(src);
         if (hipModuleLoadData(&ent.mod, code.data()) != hipSuccess) throw std::runtime_error("hipModuleLoadData failed");
-        if (hipModuleGetFunction(&ent.fn, ent.mod, "impli_eval_bricks") != hipSuccess)
+        if (hipModuleGetFunction(&ent.k.bricks, ent.mod, "impli_eval_bricks") != hipSuccess)
             throw std::runtime_error("hipModuleGetFunction failed");
     } catch (const std::exception& e) {
         std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n", e.what());
-        ent.fn = nullptr;
+        ent.k = Kernels{};
     }
     compile_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (ent.fn) ++n_compiled_;
+    if (ent.k.bricks) ++n_compiled_;
     cache_.emplace(src, ent);
-    return ent.fn;
+    return ent.k;
 }
 
 void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,

@@ -30,9 +30,12 @@ public:
     // hipRTC-compile the source to a gfx950 code object (no GPU needed); throws with the log
     static std::vector<char> compile(const std::string& src);
 
-    // compiled brick kernel for this shape, compiling on first use; nullptr if disabled or if
-    // compilation failed (the failure is logged once and the interpreter kernel is used)
-    hipFunction_t brick_kernel(const Program& p);
+    // compiled kernels for this shape, compiling on first use; nullptr if disabled or if
+    // compilation failed (the failure is logged once and the interpreter kernels are used)
+    struct Kernels {
+        hipFunction_t bricks = nullptr;   // brick-pruned field (eval_bricks_body)
+    };
+    Kernels kernels(const Program& p);
 
     // launch the compiled brick kernel (same contract as launch_eval_field_pruned's 2nd kernel)
     static void launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
@@ -48,7 +51,7 @@ private:
     TreeJit();
     struct Entry {
         hipModule_t mod = nullptr;
-        hipFunction_t fn = nullptr;
+        Kernels k;
     };
     std::mutex mu_;
     std::unordered_map<std::string, Entry> cache_;

@@ -1,0 +1,41 @@
+// mc_types.hpp -- marching-cubes data shared by the static kernels and the JIT module
+// (device-safe: no host declarations).
+#pragma once
+#include "grid.hpp"
+#include "program.hpp"
+
+namespace impli {
+
+// per-case marching-cubes data derived from the Bourke tables
+struct CaseInfo {
+    uint8_t ntri;
+    uint8_t nown;       // crossing edges among the cell's owned edges 5, 6, 10
+    int8_t rank[3];     // first-use rank of owned slot (edge 5, 6, 10) or -1
+    uint8_t pad;
+    uint8_t tri[15];    // Bourke edge ids, 3 per triangle
+    uint8_t pad2[11];
+};
+static_assert(sizeof(CaseInfo) == 32, "CaseInfo layout");
+// MC pipeline.  Cells are numbered L = row * m + (x - 1), row = (z - cz0) * m + (y - 1); a unit is
+// kUnitRows consecutive rows (contiguous in linear order), processed by one wave.
+constexpr int kUnitRows = 4;
+constexpr int kScanUPT = 8;            // units per lane in the unit scan
+constexpr int kScanBlock = 1024 * kScanUPT;
+struct MCBuffers {
+    const float* field;
+    const uint64_t* signs;   // sign bitmap of the stored samples (grid.hpp)
+    uint4* unit_cnt;         // per unit {own, tri, act, halo own}; scanned in place to exclusive bases
+    uint32_t* scan_blk;      // 8 per scan block: partial sums (5 components), then exclusive bases
+    uint32_t* counters;      // [0] unused, [1] halo own, [2..5] totals own/tri/act/halo
+    uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
+    uint4* records;          // active cells: {L, ci, fbase, 0}
+    float* verts;            // 3 * cap_v
+    int32_t* faces;          // 3 * cap_f
+    int64_t cap_v, cap_f, cap_rec;
+    const uint32_t* offsets; // device [Voff, Foff] of this slab in the global numbering
+    uint32_t* overflow;      // set to 1 if a capacity was exceeded
+};
+__host__ __device__ inline int64_t n_rows(const GridDesc& g) { return (int64_t)g.m * (g.cz1 - g.cz0); }
+__host__ __device__ inline int64_t n_units(const GridDesc& g) { return (n_rows(g) + kUnitRows - 1) / kUnitRows; }
+
+}  // namespace impli
