@@ -99,8 +99,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
-    def run(R, steps, warmup):
-        shape, mc = scenes.config4(R)
+    def run(R, steps, warmup, scene=None):
+        shape, mc = scene if scene is not None else scenes.config4(R)
         slab = I.Slab(shape, mc, rank, world)
         cnt = torch.zeros(4, dtype=torch.int32, device=dev)
         offs = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -166,6 +166,9 @@ def main():
 
     main_run = run(args.resolution, args.steps, args.warmup)
     r256 = run(256, args.steps, args.warmup) if (not args.skip_256 and args.resolution != 256) else None
+    # a dense-surface data point: config 2's scene (sphere u rabbit, ~1.5 M vertices) at the same R
+    rdense = None if args.skip_256 else run(args.resolution, args.steps, args.warmup,
+                                           scene=(scenes.union_sphere_cube(), scenes.mc_settings(args.resolution, 1.0)))
 
     if rank != 0:
         if world > 1:
@@ -236,6 +239,12 @@ def main():
                                   "achieved": round(b_pipe / t_kern / 1e9, 1),
                                   "frac": round(b_pipe / t_kern / 1e9 / HBM_PEAK_GBS, 4)}},
     }
+    if rdense:
+        msd = rdense["elapsed"] / args.steps * 1e3
+        out["value_union_scene"] = round(R ** 3 / (msd * 1e-3) / 1e6, 2)
+        out["union_scene"] = {"workload": "config 2 scene (sphere u rabbit) at R=%d, eval+MC" % R, "ms_per_step": round(msd, 4),
+                              "verts": rdense["nv"], "faces": rdense["nf"],
+                              "kernel_ms": {k: round(v, 4) for k, v in rdense["kernel_ms"].items()}}
     if r256:
         ms256 = r256["elapsed"] / args.steps * 1e3
         out["value_256"] = round(256 ** 3 / (ms256 * 1e-3) / 1e6, 2)

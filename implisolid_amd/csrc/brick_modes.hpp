@@ -1,0 +1,104 @@
+// brick_modes.hpp -- device side of the interval pass (per-brick pruning modes and sign classes),
+// shared by the static interpreter kernels (eval.hip) and the JIT-compiled tree kernels (jit.cpp).
+//
+// Two levels: a coarse box is kBX x kBY x (kCZ kBZ) samples, a brick kBX x kBY x kBZ.  Coarse
+// boxes are bounded first; bricks of sign-definite boxes inherit the box's modes and class
+// (k_brick_inherit, eval.hip); the listed mixed boxes are refined brick by brick, starting from
+// the box's modes (an operand pruned over the box stays pruned over any sub-box).
+#pragma once
+#include "grid.hpp"
+#include "eval_bricks.hpp"
+#include "ifunc_interval.hpp"
+
+namespace impli {
+
+// Interval box of the samples [x0, x1] x [y0, y1] x layers [z0, z1]: the sample coordinate is
+// monotone in the index, so the end samples bound the box.
+__device__ __forceinline__ dev::Box sample_box(const GridDesc& g, int x0, int x1, int y0, int y1, int z0, int z1) {
+    return dev::Box{dev::Iv{sample_xy(g, 0, x0), sample_xy(g, 0, x1)}, dev::Iv{sample_xy(g, 1, y0), sample_xy(g, 1, y1)},
+                    dev::Iv{sample_z(g, z0), sample_z(g, z1)}};
+}
+
+__device__ __forceinline__ uint8_t sign_class(dev::Iv root) {   // MC sets a cube-index bit iff f < 0
+    return (root.lo >= 0.f) ? kBrickPos : (root.hi < 0.f) ? kBrickNeg : kBrickMixed;
+}
+
+// wave-aggregated append of `b` to list (order irrelevant)
+__device__ __forceinline__ void list_append(bool take, uint32_t b, uint32_t* __restrict__ list,
+                                            uint32_t* __restrict__ count) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t mask = __ballot(take);
+    if (!mask) return;
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader, 64);
+    if (take) list[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = b;
+}
+
+// the brick's class, adjusted for sealed samples (the neighbours' fill test uses it): sealed
+// samples (-1e7) only neighbour unsealed samples of the same brick -- unless the brick is nothing
+// but the sealed layer, which is negative.  A positive brick holding sealed samples has crossing
+// edges inside: kBrickNoFill.
+__device__ __forceinline__ uint8_t sealed_class(const GridDesc& g, uint8_t c, int x0, int x1, int y0, int y1, int z0,
+                                                int z1) {
+    const bool has_sealed = x0 == 0 || x1 == g.n - 1 || y0 == 0 || y1 == g.n - 1 ||
+                            g.fz0 + z0 <= 1 || g.fz0 + z1 >= g.res - 2;
+    const bool only_sealed = x0 == g.n - 1 || y0 == g.n - 1 || (z0 == z1 && (g.fz0 + z0 <= 1 || g.fz0 + z0 >= g.res - 2));
+    if (only_sealed) c = kBrickNeg;
+    if (has_sealed && c == kBrickPos) c |= kBrickNoFill;
+    return c;
+}
+
+struct BrickBox { int x0, x1, y0, y1, z0, z1; };
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ BrickBox brick_box(const GridDesc& g, int bx, int by, int bz, int zlen) {
+    const int layers = g.fz1 - g.fz0;
+    const int x0 = bx * kBX, y0 = by * kBY, z0 = bz * zlen;
+    return BrickBox{x0, imin(x0 + kBX - 1, g.n - 1), y0, imin(y0 + kBY - 1, g.n - 1), z0, imin(z0 + zlen - 1, layers - 1)};
+}
+
+// Coarse pass: one thread per coarse box -> modes, sign class; mixed boxes are listed.
+// IvEval: Iv operator()(Box p, uint64_t modes_in, uint64_t& modes) const.
+template <class IvEval>
+__device__ __forceinline__ void coarse_modes_body(const IvEval& ev, const GridDesc& g, const BrickGrid& cg,
+                                                  uint64_t* __restrict__ cmodes, uint8_t* __restrict__ ccls,
+                                                  uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    uint8_t c = kBrickPos;
+    if (b < cg.n_bricks) {
+        int bx, by, bz;
+        brick_of(b, cg, bx, by, bz);
+        const BrickBox q = brick_box(g, bx, by, bz, kBZ * kCZ);
+        uint64_t m;
+        c = sign_class(ev(sample_box(g, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1), 0ull, m));
+        cmodes[b] = m;
+        ccls[b] = c;
+    }
+    list_append(b < cg.n_bricks && c == kBrickMixed, (uint32_t)b, clist, ccount);
+}
+
+// Bricks of the listed mixed coarse boxes: one thread per (listed box, brick in it).
+template <class IvEval>
+__device__ __forceinline__ void brick_refine_body(const IvEval& ev, const GridDesc& g, const BrickGrid& bg,
+                                                  const BrickGrid& cg, const uint64_t* __restrict__ cmodes,
+                                                  const uint32_t* __restrict__ clist,
+                                                  const uint32_t* __restrict__ ccount, uint64_t* __restrict__ modes,
+                                                  uint8_t* __restrict__ cls) {
+    const uint32_t total = *ccount * kCZ;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const uint32_t cb = clist[i / kCZ];
+        int cx, cy, cz;
+        brick_of((int)cb, cg, cx, cy, cz);
+        const int bz = cz * kCZ + (int)(i % kCZ);
+        if (bz >= bg.nbz) continue;
+        const int b = cx + cy * bg.nbx + bz * bg.nbx * bg.nby;
+        const BrickBox q = brick_box(g, cx, cy, bz, kBZ);
+        uint64_t m = cmodes[cb];
+        const uint8_t c = sign_class(ev(sample_box(g, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1), m, m));
+        modes[b] = m;
+        cls[b] = sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
+    }
+}
+
+}  // namespace impli

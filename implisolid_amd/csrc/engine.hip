@@ -119,7 +119,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &modes_, &cls_, &fill_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &counters_, &vid3_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &counters_, &vid3_,
                      &records_, &verts_, &faces_, &overflow_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -141,7 +141,11 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     const int64_t nu = n_units(grid_);
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
     cls_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
+    cmodes_.reserve((size_t)(coarse_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
+    ccls_.reserve((size_t)coarse_grid(grid_).n_bricks + 64);
+    clist_.reserve(((size_t)coarse_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
+    blist_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
     unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
 
@@ -197,18 +201,21 @@ void Engine::eval_field(hipStream_t s) {
     mark(0, s);
     if (level > 0) {
         ensure_jit();
-        launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, modes_.as<uint64_t>(),
-                           cls_.as<uint8_t>(), s);
+        launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, cmodes_.as<uint64_t>(),
+                           ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>() + 13,
+                           modes_.as<uint64_t>(), cls_.as<uint8_t>(), s, &jit_iv_);
+        uint32_t* d_count = counters_.as<uint32_t>() + 12;   // brick-list length (count() resets 0..11 only)
+        launch_brick_fill(cls_.as<uint8_t>(), grid_, level >= 2, fill_.as<uint8_t>(), blist_.as<uint32_t>(), d_count,
+                          signs_.as<uint64_t>(), s);
         mark(1, s);
         if (jit_fn_) {
             const float* d_mats = reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
-            TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_),
-                                   modes_.as<uint64_t>(), cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2,
-                                   field_.as<float>(), signs_.p, s);
+            TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_), modes_.as<uint64_t>(),
+                                   blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, eval_bricks_grid(grid_),
+                                   s);
         } else {
             launch_eval_bricks_interp(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, modes_.as<uint64_t>(),
-                                      cls_.as<uint8_t>(), fill_.as<uint8_t>(), level >= 2, field_.as<float>(),
-                                      signs_.p, s);
+                                      blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, s);
         }
     } else {
         IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled
@@ -224,11 +231,13 @@ void Engine::ensure_jit() {   // compile the tree kernels for this shape once (c
     if (jit_tried_) return;
     const TreeJit::Kernels k = TreeJit::instance().kernels(prog_host_);
     jit_fn_ = k.bricks;
+    jit_iv_.coarse = k.coarse;
+    jit_iv_.refine = k.refine;
     jit_tried_ = true;
 }
 
 void Engine::count(hipStream_t s) {
-    IMPLI_HIP(hipMemsetAsync(counters_.p, 0, 16 * sizeof(uint32_t), s));
+    IMPLI_HIP(hipMemsetAsync(counters_.p, 0, 12 * sizeof(uint32_t), s));   // [12] holds the eval's brick-list length
     IMPLI_HIP(hipMemsetAsync(overflow_.p, 0, 16, s));
     MCBuffers b = buffers();
     mark(3, s);

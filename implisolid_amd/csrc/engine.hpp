@@ -98,11 +98,12 @@ private:
     Program prog_host_{};
     bool jit_tried_ = false;
     hipFunction_t jit_fn_ = nullptr;
+    JitIntervalKernels jit_iv_;
     void ensure_jit();
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, modes_, cls_, fill_, field_, signs_, scan_blk_, unit_cnt_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, counters_, vid3_, records_, verts_, faces_, overflow_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
     hipEvent_t ev_[9] = {};

@@ -15,12 +15,16 @@
 //                sign, so marching cubes reads only their sign and the mesh is bit-identical
 //                (test_sign_fill_field_equivalent + every MC parity test).
 // k_eval_points: arbitrary points (direct-eval ABI, mcc2.cpp:815-911) with optional gradient.
+#include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 
 #include "ifunc_device.hpp"
 #include "ifunc_interval.hpp"
 #include "eval_bricks.hpp"
+#include "brick_modes.hpp"
 #include "kernels.hpp"
+#include "jit.hpp"
 
 namespace impli {
 
@@ -42,34 +46,48 @@ __global__ __launch_bounds__(256) void k_eval_field(const Program* __restrict__ 
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void k_brick_modes(const Program* __restrict__ prog, const float* __restrict__ tab,
-                                                     float2 tab_range, GridDesc g, BrickGrid bg,
-                                                     uint64_t* __restrict__ modes, uint8_t* __restrict__ cls) {
+struct InterpIv {   // the interval interpreter (ifunc_interval.hpp eval_iv)
+    const Program* prog;
+    const float* tab;
+    float2 tab_range;
+    __device__ __forceinline__ Iv operator()(Box p, uint64_t modes_in, uint64_t& modes) const {
+        return eval_iv<D>(prog, tab, tab_range, p, modes_in, modes);
+    }
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void k_coarse_modes(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                      float2 tab_range, GridDesc g, BrickGrid cg,
+                                                      uint64_t* __restrict__ cmodes, uint8_t* __restrict__ ccls,
+                                                      uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount) {
+    coarse_modes_body(InterpIv<D>{prog, tab, tab_range}, g, cg, cmodes, ccls, clist, ccount);
+}
+
+// Bricks of sign-definite coarse boxes inherit the box's modes and class (valid on any sub-box).
+__global__ __launch_bounds__(256) void k_brick_inherit(GridDesc g, BrickGrid bg, BrickGrid cg,
+                                                       const uint64_t* __restrict__ cmodes,
+                                                       const uint8_t* __restrict__ ccls, uint64_t* __restrict__ modes,
+                                                       uint8_t* __restrict__ cls) {
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= bg.n_bricks) return;
     int bx, by, bz;
     brick_of(b, bg, bx, by, bz);
-    const int layers = g.fz1 - g.fz0;
-    const int x0 = bx * kBX, x1 = min(x0 + kBX - 1, g.n - 1);
-    const int y0 = by * kBY, y1 = min(y0 + kBY - 1, g.n - 1);
-    const int z0 = bz * kBZ, z1 = min(z0 + kBZ - 1, layers - 1);
-    // the sample coordinate is monotone in the index, so the end samples bound the brick
-    const Box p{Iv{sample_xy(g, 0, x0), sample_xy(g, 0, x1)}, Iv{sample_xy(g, 1, y0), sample_xy(g, 1, y1)},
-                Iv{sample_z(g, z0), sample_z(g, z1)}};
-    uint64_t m;
-    const Iv root = eval_iv<D>(prog, tab, tab_range, p, m);
-    modes[b] = m;
-    // Sign class of the brick's evaluated samples (MC sets a cube-index bit iff f < 0); the
-    // neighbours' fill test uses it.  Sealed samples (-1e7) only neighbour unsealed samples of
-    // the same brick -- unless the brick is nothing but the sealed layer, which is negative.
-    // A positive brick holding sealed samples has crossing edges inside: kBrickNoFill.
-    const bool has_sealed = x0 == 0 || x1 == g.n - 1 || y0 == 0 || y1 == g.n - 1 ||
-                            g.fz0 + z0 <= 1 || g.fz0 + z1 >= g.res - 2;
-    const bool only_sealed = x0 == g.n - 1 || y0 == g.n - 1 || (z0 == z1 && (g.fz0 + z0 <= 1 || g.fz0 + z0 >= g.res - 2));
-    uint8_t c = (root.lo >= 0.f) ? kBrickPos : (root.hi < 0.f) ? kBrickNeg : kBrickMixed;
-    if (only_sealed) c = kBrickNeg;
-    if (has_sealed && c == kBrickPos) c |= kBrickNoFill;
-    cls[b] = c;
+    const int cb = bx + by * cg.nbx + (bz / kCZ) * cg.nbx * cg.nby;
+    const uint8_t c = ccls[cb];
+    if (c == kBrickMixed) return;   // refined by k_brick_refine
+    modes[b] = cmodes[cb];
+    const BrickBox q = brick_box(g, bx, by, bz, kBZ);
+    cls[b] = sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_brick_refine(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                      float2 tab_range, GridDesc g, BrickGrid bg, BrickGrid cg,
+                                                      const uint64_t* __restrict__ cmodes,
+                                                      const uint32_t* __restrict__ clist,
+                                                      const uint32_t* __restrict__ ccount, uint64_t* __restrict__ modes,
+                                                      uint8_t* __restrict__ cls) {
+    brick_refine_body(InterpIv<D>{prog, tab, tab_range}, g, bg, cg, cmodes, clist, ccount, modes, cls);
 }
 
 template <int D>
@@ -85,10 +103,54 @@ template <int D>
 __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __restrict__ prog,
                                                            const float* __restrict__ tab, GridDesc g, BrickGrid bg,
                                                            const uint64_t* __restrict__ modes,
-                                                           const uint8_t* __restrict__ cls,
-                                                           uint8_t* __restrict__ fill, int sign_fill,
+                                                           const uint32_t* __restrict__ list,
+                                                           const uint32_t* __restrict__ count,
                                                            float* __restrict__ field, void* __restrict__ signs) {
-    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);
+    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, list, count, field, signs);
+}
+
+// Neighbour rule per brick (brick_fill_class): fill[b], and the list of bricks to evaluate
+// (mixed, or next to a brick of another class).  Wave-aggregated appends, order irrelevant.
+__global__ __launch_bounds__(256) void k_brick_fill(const uint8_t* __restrict__ cls, BrickGrid bg, int sign_fill,
+                                                    uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
+                                                    uint32_t* __restrict__ count) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    uint32_t fc = kBrickMixed;
+    if (b < bg.n_bricks) {
+        int bx, by, bz;
+        brick_of(b, bg, bx, by, bz);
+        fc = sign_fill ? brick_fill_class(cls, bg, b, bx, by, bz) : (uint32_t)kBrickMixed;
+        fill[b] = (uint8_t)fc;
+    }
+    const bool eval = b < bg.n_bricks && fc == kBrickMixed;
+    const uint64_t mask = __ballot(eval);
+    uint32_t base = 0;
+    if (lane == __ffsll((unsigned long long)mask) - 1) base = atomicAdd(count, (uint32_t)__popcll(mask));
+    base = __shfl(base, __ffsll((unsigned long long)mask) - 1, 64);
+    if (eval) list[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)b;
+}
+
+// Constant sign bits of the sign-filled bricks: one thread per 64-bit word of the bitmap (pieces
+// of evaluated bricks are rewritten by the eval kernel afterwards).
+__global__ __launch_bounds__(256) void k_sign_fill(GridDesc g, BrickGrid bg, const uint8_t* __restrict__ fill,
+                                                   uint64_t* __restrict__ signs) {
+    const int rw = sign_row_words(g);
+    const int64_t rows = (int64_t)g.n * (g.fz1 - g.fz0);
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rows * rw) return;
+    const int64_t row = i / rw;
+    const int c = (int)(i - row * rw);
+    const int layer = (int)(row / g.n), y = (int)(row - (int64_t)layer * g.n);
+    constexpr int P = 64 / kBX;   // pieces per word
+    const uint8_t* f = fill + (size_t)((layer / kBZ) * bg.nby + y / kBY) * bg.nbx;
+    uint64_t w = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int bx = c * P + j;
+        if (bx < bg.nbx && f[bx] == kBrickNeg) w |= (kBX == 64 ? ~0ull : ((1ull << kBX) - 1ull)) << (kBX * j);
+    }
+    signs[i] = w;
 }
 
 // sign bitmap of a fully evaluated field (unpruned path): one thread per 64-bit word
@@ -161,16 +223,46 @@ BrickGrid brick_grid(const GridDesc& g) {
     return bg;
 }
 
+BrickGrid coarse_grid(const GridDesc& g) {
+    BrickGrid cg = brick_grid(g);
+    cg.nbz = (g.fz1 - g.fz0 + kBZ * kCZ - 1) / (kBZ * kCZ);
+    if (cg.nbz < 0) cg.nbz = 0;
+    cg.n_bricks = cg.nbx * cg.nby * cg.nbz;
+    return cg;
+}
+
 void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
-                        uint64_t* d_modes, uint8_t* d_cls, hipStream_t s) {
-    const BrickGrid bg = brick_grid(g);
+                        uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_ccount, uint64_t* d_modes,
+                        uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit) {
+    BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
-    const unsigned tb = (unsigned)((bg.n_bricks + 255) / 256);
-    if (depth <= 4) k_brick_modes<4><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
-    else if (depth <= 8) k_brick_modes<8><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
-    else if (depth <= 12) k_brick_modes<12><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
-    else k_brick_modes<16><<<tb, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, d_modes, d_cls);
+    (void)hipMemsetAsync(d_ccount, 0, sizeof(uint32_t), s);
+    const unsigned tc = (unsigned)((cg.n_bricks + 255) / 256), tb = (unsigned)((bg.n_bricks + 255) / 256);
+    const unsigned tr = (unsigned)std::min<int64_t>(((int64_t)cg.n_bricks * kCZ + 255) / 256, 2048);
+    if (jit && jit->coarse && jit->refine) {
+        GridDesc gg = g;
+        const float* d_mats = reinterpret_cast<const float*>(reinterpret_cast<const char*>(d_prog) + offsetof(Program, mats));
+        void* ca[] = {&d_mats, &d_rabbit, &tab_range, &gg, &cg, &d_cmodes, &d_ccls, &d_clist, &d_ccount};
+        TreeJit::launch(jit->coarse, tc, ca, s, "impli_coarse_modes");
+        k_brick_inherit<<<tb, 256, 0, s>>>(g, bg, cg, d_cmodes, d_ccls, d_modes, d_cls);
+        void* ra[] = {&d_mats, &d_rabbit, &tab_range, &gg, &bg, &cg, &d_cmodes, &d_clist, &d_ccount, &d_modes, &d_cls};
+        TreeJit::launch(jit->refine, tr, ra, s, "impli_brick_refine");
+        return;
+    }
+#define IMPLI_MODES(DD)                                                                                           \
+    do {                                                                                                          \
+        k_coarse_modes<DD><<<tc, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, cg, d_cmodes, d_ccls, d_clist,     \
+                                              d_ccount);                                                          \
+        k_brick_inherit<<<tb, 256, 0, s>>>(g, bg, cg, d_cmodes, d_ccls, d_modes, d_cls);                          \
+        k_brick_refine<DD><<<tr, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, cg, d_cmodes, d_clist, d_ccount, \
+                                              d_modes, d_cls);                                                    \
+    } while (0)
+    if (depth <= 4) IMPLI_MODES(4);
+    else if (depth <= 8) IMPLI_MODES(8);
+    else if (depth <= 12) IMPLI_MODES(12);
+    else IMPLI_MODES(16);
+#undef IMPLI_MODES
 }
 
 void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s) {
@@ -179,17 +271,33 @@ void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* 
     k_signs_from_field<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(g, d_field, d_signs);
 }
 
+void launch_brick_fill(const uint8_t* d_cls, const GridDesc& g, int sign_fill, uint8_t* d_fill, uint32_t* d_list,
+                       uint32_t* d_count, uint64_t* d_signs, hipStream_t s) {
+    const BrickGrid bg = brick_grid(g);
+    if (bg.n_bricks <= 0) return;
+    (void)hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
+    k_brick_fill<<<(unsigned)((bg.n_bricks + 255) / 256), 256, 0, s>>>(d_cls, bg, sign_fill, d_fill, d_list, d_count);
+    const int64_t words = (int64_t)g.n * (g.fz1 - g.fz0) * sign_row_words(g);
+    k_sign_fill<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(g, bg, d_fill, d_signs);
+}
+
+unsigned eval_bricks_grid(const GridDesc& g) {
+    const int nb = brick_grid(g).n_bricks;
+    const unsigned want = (unsigned)((nb + 3) / 4);
+    return want < 4096u ? (want ? want : 1u) : 4096u;   // grid-stride over the list
+}
+
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
-                               const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
+                               const uint64_t* d_modes, const uint32_t* d_list, const uint32_t* d_count,
                                float* d_field, void* d_signs, hipStream_t s) {
     const BrickGrid bg = brick_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
-    const unsigned eb = (unsigned)((bg.n_bricks + 3) / 4);
-    if (depth <= 4) k_eval_field_pruned<4><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
-    else if (depth <= 8) k_eval_field_pruned<8><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
-    else if (depth <= 12) k_eval_field_pruned<12><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
-    else k_eval_field_pruned<16><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_cls, d_fill, sign_fill, d_field, d_signs);
+    const unsigned eb = eval_bricks_grid(g);
+    if (depth <= 4) k_eval_field_pruned<4><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    else if (depth <= 8) k_eval_field_pruned<8><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    else if (depth <= 12) k_eval_field_pruned<12><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    else k_eval_field_pruned<16><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
 }
 
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,

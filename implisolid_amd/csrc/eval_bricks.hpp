@@ -49,58 +49,46 @@ __device__ __forceinline__ uint32_t brick_fill_class(const uint8_t* __restrict__
     return (xm == c && xp == c && ym == c && yp == c && zm == c && zp == c) ? c : (uint32_t)kBrickMixed;
 }
 
-// One wave per brick (16 x 4 lanes, 4 z layers each).  Every brick writes its samples' sign bits
-// (wave ballot: 64 bits = 4 rows x 16 samples).  Sign-filled bricks write only those (their field
-// values are never read); the others evaluate every sample with `ev(modes, x, y, z)` and store it.
+// One wave per listed brick (kBX x kBY lanes, kBZ layers each; grid-stride over the list built by
+// k_brick_fill): every sample is evaluated with `ev(modes, x, y, z)`, stored, and its sign bit set
+// (wave ballot: 64 bits = kBY rows x kBX samples).  Sign-filled bricks never reach this kernel --
+// k_sign_fill wrote their constant sign bits.
 template <class Eval>
 __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
                                                  const uint64_t* __restrict__ modes,
-                                                 const uint8_t* __restrict__ cls, uint8_t* __restrict__ fill,
-                                                 int sign_fill, float* __restrict__ field,
-                                                 void* __restrict__ signs_raw) {
+                                                 const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                 float* __restrict__ field, void* __restrict__ signs_raw) {
     sign_piece_t* signs = static_cast<sign_piece_t*>(signs_raw);
-    const int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-    if (b >= bg.n_bricks) return;
+    const uint32_t nb = *count;
     const int lane = threadIdx.x & 63;
-    int bx, by, bz;
-    brick_of(b, bg, bx, by, bz);
     const int n = g.n;
-    const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
-    const bool ok = sx < n && sy < n;
-    const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
     const int layers = g.fz1 - g.fz0;
     const size_t plane = (size_t)n * n;
     const int row_pieces = (64 / kBX) * sign_row_words(g);
-    float* out = field + (size_t)sy * n + sx;
-    const uint32_t fc = sign_fill ? brick_fill_class(cls, bg, b, bx, by, bz) : (uint32_t)kBrickMixed;
-    if (lane == 0) fill[b] = (uint8_t)fc;
-    if (fc != kBrickMixed) {   // only the sign is ever read; it is the class (sealed samples are negative too)
-        if (lane < kBY) {
-            const sign_piece_t w = (fc == kBrickNeg) ? (sign_piece_t)~(sign_piece_t)0 : (sign_piece_t)0;
-            const int y = by * kBY + lane;
-            for (int k = 0; k < kBZ; ++k) {
-                const int layer = bz * kBZ + k;
-                if (layer >= layers) break;
-                if (y < n) signs[((size_t)layer * n + y) * row_pieces + bx] = w;
-            }
-        }
-        return;
-    }
-    const uint64_t m64 = modes[b];
-    const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
-                       (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
-    const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
+    for (uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); i < nb; i += gridDim.x * 4) {
+        const int b = __builtin_amdgcn_readfirstlane((int)list[i]);
+        int bx, by, bz;
+        brick_of(b, bg, bx, by, bz);
+        const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
+        const bool ok = sx < n && sy < n;
+        const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
+        float* out = field + (size_t)(ok ? sy : 0) * n + (ok ? sx : 0);
+        const uint64_t m64 = modes[b];
+        const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
+                           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
+        const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
 #pragma unroll 1
-    for (int k = 0; k < kBZ; ++k) {
-        const int layer = bz * kBZ + k;
-        if (layer >= layers) break;
-        const float f = ev(m, x, y, sample_z(g, layer));
-        const float v = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
-        if (ok) out[(size_t)layer * plane] = v;
-        const uint64_t neg = __ballot(v < 0.f);
-        if (lane < kBY) {
-            const int yy = by * kBY + lane;
-            if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg >> (kBX * lane));
+        for (int k = 0; k < kBZ; ++k) {
+            const int layer = bz * kBZ + k;
+            if (layer >= layers) break;
+            const float f = ev(m, x, y, sample_z(g, layer));
+            const float v = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
+            if (ok) out[(size_t)layer * plane] = v;
+            const uint64_t neg = __ballot(v < 0.f);
+            if (lane < kBY) {
+                const int yy = by * kBY + lane;
+                if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg >> (kBX * lane));
+            }
         }
     }
 }

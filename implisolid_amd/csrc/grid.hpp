@@ -29,9 +29,12 @@ struct GridDesc {
 #ifndef IMPLI_BRICK_X
 #define IMPLI_BRICK_X 8
 #define IMPLI_BRICK_Y 8
-#define IMPLI_BRICK_Z 16
+#define IMPLI_BRICK_Z 4
 #endif
 constexpr int kBX = IMPLI_BRICK_X, kBY = IMPLI_BRICK_Y, kBZ = IMPLI_BRICK_Z;
+// the interval pass runs first over coarse boxes of kBX x kBY x (kCZ kBZ) samples and refines
+// only the coarse boxes of mixed sign into bricks
+constexpr int kCZ = 4;
 static_assert(kBX * kBY == 64 && (kBX == 8 || kBX == 16 || kBX == 32), "a brick layer is one wave");
 enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBrickNoFill = 4 };
 // fill[b] (written by the pruned eval): kBrickPos / kBrickNeg if the brick was sign-filled --

@@ -237,19 +237,30 @@ __device__ __forceinline__ uint32_t csg_decide(int t, Iv a, Iv b, Iv& out) {
     return PM_BOTH;
 }
 
-// interval interpreter over a box; returns the root interval and the per-node modes.  The
-// stacks are kept as separate scalar arrays (structure of arrays) so that the uniform-index
-// accesses stay in VGPRs (arrays of Iv structs were demoted to scratch).
+__device__ __forceinline__ uint32_t mode_of(uint64_t modes, int csg);
+
+// interval interpreter over a box; returns the root interval and the per-node modes.  Operands
+// already pruned by `modes_in` (the modes of an enclosing box, valid for this sub-box) are
+// skipped and their decision kept.  The stacks are kept as separate scalar arrays (structure of
+// arrays) so that the uniform-index accesses stay in VGPRs (arrays of Iv structs were demoted to
+// scratch).
 template <int D>
 __device__ __forceinline__ Iv eval_iv(const Program* __restrict__ prog, const float* __restrict__ tab,
-                                      float2 tab_range, Box p0, uint64_t& modes) {
+                                      float2 tab_range, Box p0, uint64_t modes_in, uint64_t& modes) {
     float xl[D], xh[D], yl[D], yh[D], zl[D], zh[D], vl[D], vh[D];
     int sp = 0, vp = 0;
     xl[0] = p0.x.lo; xh[0] = p0.x.hi; yl[0] = p0.y.lo; yh[0] = p0.y.hi; zl[0] = p0.z.lo; zh[0] = p0.z.hi;
-    modes = 0;
+    modes = modes_in;
     const int n = prog->n_instr;
     for (int pc = 0; pc < n; ++pc) {
         const Instr I = prog->instr[pc];
+        if (I.skip_csg >= 0) {
+            const uint32_t m = mode_of(modes_in, I.skip_csg);
+            if (m == (I.skip_child ? (uint32_t)PM_LEFT : (uint32_t)PM_RIGHT)) {
+                pc = I.skip_to - 1;
+                continue;
+            }
+        }
         const Box cur{Iv{xl[sp], xh[sp]}, Iv{yl[sp], yh[sp]}, Iv{zl[sp], zh[sp]}};
         if (I.op == OP_XFORM) {
             const Box q = xform_iv(prog->mats[I.mat], cur);
@@ -262,13 +273,20 @@ __device__ __forceinline__ Iv eval_iv(const Program* __restrict__ prog, const fl
             --sp;
         } else {
             --sp;
-            --vp;
-            const Iv b{vl[vp], vh[vp]};
-            const Iv a{vl[vp - 1], vh[vp - 1]};
-            Iv o;
-            const uint32_t m = csg_decide(I.type, a, b, o);
-            if (I.csg < kMaxPruned) modes |= (uint64_t)m << (2 * I.csg);
-            vl[vp - 1] = o.lo; vh[vp - 1] = o.hi;
+            const uint32_t pm = mode_of(modes_in, I.csg);
+            if (pm == PM_BOTH) {
+                --vp;
+                const Iv b{vl[vp], vh[vp]};
+                const Iv a{vl[vp - 1], vh[vp - 1]};
+                Iv o;
+                const uint32_t m = csg_decide(I.type, a, b, o);
+                if (I.csg < kMaxPruned) modes |= (uint64_t)m << (2 * I.csg);
+                vl[vp - 1] = o.lo; vh[vp - 1] = o.hi;
+            } else if (pm == PM_RIGHT && I.type == NT_DIFFERENCE) {   // the kept operand is -f2
+                const float lo = vl[vp - 1];
+                vl[vp - 1] = -vh[vp - 1];
+                vh[vp - 1] = -lo;
+            }
         }
     }
     return Iv{vl[0], vh[0]};

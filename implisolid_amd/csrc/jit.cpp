@@ -114,6 +114,58 @@ struct Emitter {
     }
 };
 
+const char* prim_iv_call(int t) {
+    switch (t) {
+        case NT_ELLIPSOID: return "egg_iv(";
+        case NT_CUBE: return "cube_iv(tab, tab_range, ";
+        case NT_CYLINDER: return "cyl_iv(";
+        case NT_CONE: return "cone_iv(";
+        case NT_HEART: return "heart_iv(";
+        case NT_TORUS: return "torus_iv(";
+        case NT_DMUSHROOM: return "dm_iv(";
+        default: throw std::runtime_error("jit: unknown primitive");
+    }
+}
+
+// Interval version of the tree (eval_iv, ifunc_interval.hpp): the same primitive bounds, settle()
+// and CSG decisions, so modes and classes are bit-identical to the interpreter's.
+struct IvEmitter {
+    const std::vector<Node>& nodes;
+    std::ostringstream out;
+    int counter = 0;
+
+    std::string emit(int i, const std::string& p, int ind) {
+        const Node& n = nodes[i];
+        const int id = counter++;
+        const std::string pad(ind, ' ');
+        const std::string q = "q" + std::to_string(id), r = "r" + std::to_string(id);
+        out << pad << "const Box " << q << " = xform_iv(M + " << 12 * n.mat << ", " << p << ");\n";
+        if (n.leaf) {
+            out << pad << "const Iv " << r << " = settle(" << prim_iv_call(n.type) << q << "));\n";
+            return r;
+        }
+        const std::string m = "m" + std::to_string(id), a = "a" + std::to_string(id), b = "b" + std::to_string(id);
+        out << pad << "Iv " << r << ";\n" << pad << "{\n";
+        out << pad << "  const uint32_t " << m << " = mode_of(modes_in, " << n.csg << ");\n";
+        out << pad << "  Iv " << a << " = Iv{0.f, 0.f}, " << b << " = Iv{0.f, 0.f};\n";
+        out << pad << "  if (" << m << " != PM_RIGHT) {\n";
+        const std::string ra = emit(n.child[0], q, ind + 4);
+        out << pad << "    " << a << " = " << ra << ";\n" << pad << "  }\n";
+        out << pad << "  if (" << m << " != PM_LEFT) {\n";
+        const std::string rb = emit(n.child[1], q, ind + 4);
+        out << pad << "    " << b << " = " << rb << ";\n" << pad << "  }\n";
+        out << pad << "  if (" << m << " == PM_BOTH) {\n";
+        out << pad << "    const uint32_t d = csg_decide(" << n.type << ", " << a << ", " << b << ", " << r << ");\n";
+        if (n.csg >= 0 && n.csg < kMaxPruned) out << pad << "    modes |= (uint64_t)d << " << 2 * n.csg << ";\n";
+        else out << pad << "    (void)d;\n";
+        out << pad << "  } else if (" << m << " == PM_LEFT) {\n" << pad << "    " << r << " = " << a << ";\n";
+        out << pad << "  } else {\n" << pad << "    " << r << " = " << (n.type == NT_DIFFERENCE ? "neg(" + b + ")" : b)
+            << ";\n" << pad << "  }\n";
+        out << pad << "}\n";
+        return r;
+    }
+};
+
 void rtc_check(hiprtcResult r, const char* what) {
     if (r != HIPRTC_SUCCESS) throw std::runtime_error(std::string(what) + ": " + hiprtcGetErrorString(r));
 }
@@ -137,8 +189,10 @@ std::string TreeJit::kernel_source(const Program& p) {
     if (next != p.n_instr) throw std::runtime_error("jit: trailing instructions");
     Emitter em{nodes};
     const std::string f = em.emit(root, "x0", "y0", "z0", 4);
+    IvEmitter iv{nodes};
+    const std::string r = iv.emit(root, "p0", 4);
     std::ostringstream s;
-    s << kPrelude << "#include \"eval_bricks.hpp\"\n#include \"ifunc_interval.hpp\"\n"
+    s << kPrelude << "#include \"eval_bricks.hpp\"\n#include \"ifunc_interval.hpp\"\n#include \"brick_modes.hpp\"\n"
       << "namespace impli {\nusing namespace dev;\n"
       << "__device__ __forceinline__ float tree_f(const float* __restrict__ M, const float* __restrict__ tab,\n"
       << "                                        uint64_t modes, float x0, float y0, float z0) {\n"
@@ -146,11 +200,27 @@ std::string TreeJit::kernel_source(const Program& p) {
       << "struct JitEval {\n    const float* M;\n    const float* tab;\n"
       << "    __device__ __forceinline__ float operator()(uint64_t m, float x, float y, float z) const {\n"
       << "        return tree_f(M, tab, m, x, y, z);\n    }\n};\n"
+      << "__device__ __forceinline__ Iv tree_iv(const float* __restrict__ M, const float* __restrict__ tab,\n"
+      << "                                      float2 tab_range, Box p0, uint64_t modes_in, uint64_t& modes) {\n"
+      << "    modes = modes_in;\n"
+      << iv.out.str() << "    return " << r << ";\n}\n"
+      << "struct JitIv {\n    const float* M;\n    const float* tab;\n    float2 tab_range;\n"
+      << "    __device__ __forceinline__ Iv operator()(Box p, uint64_t mi, uint64_t& m) const {\n"
+      << "        return tree_iv(M, tab, tab_range, p, mi, m);\n    }\n};\n"
       << "}  // namespace impli\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_eval_bricks(\n"
       << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
-      << "    const uint8_t* cls, uint8_t* fill, int sign_fill, float* field, void* signs) {\n"
-      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, cls, fill, sign_fill, field, signs);\n}\n"
+      << "    const uint32_t* list, const uint32_t* count, float* field, void* signs) {\n"
+      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, list, count, field, signs);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_coarse_modes(\n"
+      << "    const float* M, const float* tab, float2 tab_range, impli::GridDesc g, impli::BrickGrid cg,\n"
+      << "    uint64_t* cmodes, uint8_t* ccls, uint32_t* clist, uint32_t* ccount) {\n"
+      << "    impli::coarse_modes_body(impli::JitIv{M, tab, tab_range}, g, cg, cmodes, ccls, clist, ccount);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_brick_refine(\n"
+      << "    const float* M, const float* tab, float2 tab_range, impli::GridDesc g, impli::BrickGrid bg,\n"
+      << "    impli::BrickGrid cg, const uint64_t* cmodes, const uint32_t* clist, const uint32_t* ccount,\n"
+      << "    uint64_t* modes, uint8_t* cls) {\n"
+      << "    impli::brick_refine_body(impli::JitIv{M, tab, tab_range}, g, bg, cg, cmodes, clist, ccount, modes, cls);\n}\n"
 ;
     return s.str();
 }
@@ -208,7 +278,9 @@ TreeJit::Kernels TreeJit::kernels(const Program& p) {
     try {
         const std::vector<char> code = compile(src);
         if (hipModuleLoadData(&ent.mod, code.data()) != hipSuccess) throw std::runtime_error("hipModuleLoadData failed");
-        if (hipModuleGetFunction(&ent.k.bricks, ent.mod, "impli_eval_bricks") != hipSuccess)
+        if (hipModuleGetFunction(&ent.k.bricks, ent.mod, "impli_eval_bricks") != hipSuccess ||
+            hipModuleGetFunction(&ent.k.coarse, ent.mod, "impli_coarse_modes") != hipSuccess ||
+            hipModuleGetFunction(&ent.k.refine, ent.mod, "impli_brick_refine") != hipSuccess)
             throw std::runtime_error("hipModuleGetFunction failed");
     } catch (const std::exception& e) {
         std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n", e.what());
@@ -221,16 +293,20 @@ TreeJit::Kernels TreeJit::kernels(const Program& p) {
 }
 
 void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
-                            const BrickGrid& bg, const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill,
-                            int sign_fill, float* d_field, void* d_signs, hipStream_t s) {
+                            const BrickGrid& bg, const uint64_t* d_modes, const uint32_t* d_list,
+                            const uint32_t* d_count, float* d_field, void* d_signs, unsigned blocks, hipStream_t s) {
     if (bg.n_bricks <= 0) return;
     GridDesc gg = g;
     BrickGrid bb = bg;
     void* args[] = {(void*)&d_mats, (void*)&d_rabbit, (void*)&gg, (void*)&bb, (void*)&d_modes,
-                    (void*)&d_cls, (void*)&d_fill, (void*)&sign_fill, (void*)&d_field, (void*)&d_signs};
-    const unsigned blocks = (unsigned)((bg.n_bricks + 3) / 4);
+                    (void*)&d_list, (void*)&d_count, (void*)&d_field, (void*)&d_signs};
     if (hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
         throw std::runtime_error("hipModuleLaunchKernel(impli_eval_bricks) failed");
+}
+
+void TreeJit::launch(hipFunction_t fn, unsigned blocks, void** args, hipStream_t s, const char* what) {
+    if (hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+        throw std::runtime_error(std::string("hipModuleLaunchKernel(") + what + ") failed");
 }
 
 }  // namespace impli

@@ -34,13 +34,18 @@ public:
     // compilation failed (the failure is logged once and the interpreter kernels are used)
     struct Kernels {
         hipFunction_t bricks = nullptr;   // brick-pruned field (eval_bricks_body)
+        hipFunction_t coarse = nullptr;   // interval pass, coarse boxes (coarse_modes_body)
+        hipFunction_t refine = nullptr;   // interval pass, bricks of mixed boxes (brick_refine_body)
     };
     Kernels kernels(const Program& p);
 
     // launch the compiled brick kernel (same contract as launch_eval_field_pruned's 2nd kernel)
     static void launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
-                              const BrickGrid& bg, const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill,
-                              int sign_fill, float* d_field, void* d_signs, hipStream_t s);
+                              const BrickGrid& bg, const uint64_t* d_modes, const uint32_t* d_list,
+                              const uint32_t* d_count, float* d_field, void* d_signs, unsigned blocks, hipStream_t s);
+
+    // launch a compiled kernel with 256-thread blocks; args as for hipModuleLaunchKernel
+    static void launch(hipFunction_t fn, unsigned blocks, void** args, hipStream_t s, const char* what);
 
     bool enabled() const { return enabled_; }
     void set_enabled(bool on) { enabled_ = on; }

@@ -18,12 +18,23 @@ void launch_eval_field(const Program* d_prog, int depth, const float* d_rabbit, 
                        hipStream_t s);
 // direct evaluation at arbitrary points (implicit values / gradients)
 BrickGrid brick_grid(const GridDesc& g);
-// K1a: interval pass -- per-brick CSG pruning modes and sign class
+// K1a: interval pass -- per-brick CSG pruning modes and sign class (coarse boxes, then the bricks
+// of mixed coarse boxes)
+BrickGrid coarse_grid(const GridDesc& g);
+// JIT-compiled interval kernels for the shape (jit.hpp); null members -> interpreter
+struct JitIntervalKernels {
+    hipFunction_t coarse = nullptr, refine = nullptr;
+};
 void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
-                        uint64_t* d_modes, uint8_t* d_cls, hipStream_t s);
-// K1b (interpreter): brick-pruned field; the JIT variant is TreeJit::launch_bricks (jit.hpp)
+                        uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_ccount, uint64_t* d_modes,
+                        uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit = nullptr);
+// K1b: neighbour rule -> fill[b], the list of bricks to evaluate, constant sign bits of the rest
+void launch_brick_fill(const uint8_t* d_cls, const GridDesc& g, int sign_fill, uint8_t* d_fill, uint32_t* d_list,
+                       uint32_t* d_count, uint64_t* d_signs, hipStream_t s);
+// K1c (interpreter): the listed bricks; the JIT variant is TreeJit::launch_bricks (jit.hpp)
+unsigned eval_bricks_grid(const GridDesc& g);
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
-                               const uint64_t* d_modes, const uint8_t* d_cls, uint8_t* d_fill, int sign_fill,
+                               const uint64_t* d_modes, const uint32_t* d_list, const uint32_t* d_count,
                                float* d_field, void* d_signs, hipStream_t s);
 // sign bitmap of a fully written field (unpruned path)
 void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s);

@@ -74,6 +74,10 @@ def random_leaf(rng, box=1.0, types=LEAF_TYPES):
             s = rng.choice([0.125, 0.25])
         if t == "iheart":
             s = rng.choice([0.25, 0.5])
+        if t == "cube":
+            # the rabbit SDF table spans ~16.5 x 13.5 x 16.5 local units: at scale 1/8 it is about
+            # the box's size (config 2's rabbit); larger scales enclose the whole box in one solid
+            s = 0.125
         if t == "cube" and not _rabbit_ok(s, tr, box):
             continue
         return {"type": t, "matrix": st(s, *tr)}

@@ -358,3 +358,4 @@ def test_jit_tree_kernels_compile_for_gfx950(impli):
                   scenes.random_tree(7, 10)]:
         n, secs, src = impli.jit_compile(shape)
         assert n > 1000 and "impli_eval_bricks" in src, src[:500]
+        assert "impli_coarse_modes" in src and "impli_brick_refine" in src

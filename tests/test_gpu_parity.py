@@ -122,26 +122,32 @@ def test_empty_and_full(impli, oracle):
     _mc_compare(impli, oracle, big, scenes.mc_settings(16, 1.0))
 
 
+@pytest.mark.parametrize("level", [1, 2])
 @pytest.mark.parametrize("name", sorted(TREES))
-def test_jit_field_matches_interpreter(impli, name):
-    """The hipRTC-compiled tree kernel and the interpreter produce the same field bit for bit."""
+def test_jit_field_matches_interpreter(impli, name, level):
+    """The hipRTC-compiled tree kernels (interval pass and field) and the interpreter produce the
+    same field, sign bitmap and brick classes bit for bit."""
     from implisolid_amd import scenes
     mc = scenes.mc_settings(48, 1.0)
-    impli.set_jit(False)
+    out = []
+    impli.set_pruning(level)
     try:
-        a = _field(impli, TREES[name], mc, 1)
+        for jit in (False, True):
+            impli.set_jit(jit)
+            s = impli.Slab(TREES[name], mc)
+            try:
+                s.eval()
+                assert s.used_jit() == jit
+                out.append((s.read_field(), s.read_signs(), s.brick_stats()))
+            finally:
+                s.close()
     finally:
         impli.set_jit(True)
-    s = impli.Slab(TREES[name], mc)
-    impli.set_pruning(1)
-    try:
-        s.eval()
-        b = s.read_field()
-        assert s.used_jit()
-    finally:
         impli.set_pruning(2)
-        s.close()
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
+    (fa, sa, ba), (fb, sb, bb) = out
+    assert np.array_equal(fa.view(np.uint32), fb.view(np.uint32)), np.flatnonzero(fa != fb)[:10]
+    assert np.array_equal(sa, sb)
+    assert ba == bb
 
 
 @pytest.mark.parametrize("level", [0, 1, 2])
