@@ -58,6 +58,36 @@ __device__ __forceinline__ BrickBox brick_box(const GridDesc& g, int bx, int by,
     return BrickBox{x0, imin(x0 + kBX - 1, g.n - 1), y0, imin(y0 + kBY - 1, g.n - 1), z0, imin(z0 + zlen - 1, layers - 1)};
 }
 
+// class of brick (bx, by, bz): a sign-definite coarse box's class (sealed-adjusted for the
+// brick), or the refined class of a brick of a mixed box
+__device__ __forceinline__ uint32_t brick_class(const GridDesc& g, const BrickGrid& bg, const BrickGrid& cg,
+                                                const uint8_t* __restrict__ ccls, const uint8_t* __restrict__ cls,
+                                                int bx, int by, int bz) {
+    const uint8_t c = ccls[bx + by * cg.nbx + (bz / kCZ) * cg.nbx * cg.nby];
+    if (c == kBrickMixed) return cls[bx + by * bg.nbx + bz * bg.nbx * bg.nby];
+    const BrickBox q = brick_box(g, bx, by, bz, kBZ);
+    return sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
+}
+
+// A brick needs exact values only if one of its samples can be the end of a sign-changing cell
+// edge.  Edges are axis aligned, so that requires the brick or a face neighbour to differ in
+// sign class.  Neighbours outside the stored grid hold no sample any cell of this slab reads.
+// c = the brick's own class (brick_class).
+__device__ __forceinline__ uint32_t brick_fill_class(const GridDesc& g, const BrickGrid& bg, const BrickGrid& cg,
+                                                     const uint8_t* __restrict__ ccls, const uint8_t* __restrict__ cls,
+                                                     uint32_t c, int bx, int by, int bz) {
+    if ((c & 3u) == kBrickMixed || (c & kBrickNoFill)) return kBrickMixed;
+    c &= 3u;
+    bool same = true;
+    if (bx > 0) same &= (brick_class(g, bg, cg, ccls, cls, bx - 1, by, bz) & 3u) == c;
+    if (bx + 1 < bg.nbx) same &= (brick_class(g, bg, cg, ccls, cls, bx + 1, by, bz) & 3u) == c;
+    if (by > 0) same &= (brick_class(g, bg, cg, ccls, cls, bx, by - 1, bz) & 3u) == c;
+    if (by + 1 < bg.nby) same &= (brick_class(g, bg, cg, ccls, cls, bx, by + 1, bz) & 3u) == c;
+    if (bz > 0) same &= (brick_class(g, bg, cg, ccls, cls, bx, by, bz - 1) & 3u) == c;
+    if (bz + 1 < bg.nbz) same &= (brick_class(g, bg, cg, ccls, cls, bx, by, bz + 1) & 3u) == c;
+    return same ? c : (uint32_t)kBrickMixed;
+}
+
 // Coarse pass: one thread per coarse box -> modes, sign class; mixed boxes are listed.
 // IvEval: Iv operator()(Box p, uint64_t modes_in, uint64_t& modes) const.
 template <class IvEval>

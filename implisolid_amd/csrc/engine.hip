@@ -46,16 +46,13 @@ int Engine::pruning() {
 
 void Engine::brick_stats(int64_t out[3], hipStream_t s) {
     const BrickGrid bg = brick_grid(grid_);
-    std::vector<uint8_t> c((size_t)bg.n_bricks), f((size_t)bg.n_bricks);
+    std::vector<uint8_t> f((size_t)bg.n_bricks);   // fill[b] = class | fill class << 4 (k_brick_fill)
     IMPLI_HIP(hipStreamSynchronize(s));
-    if (bg.n_bricks) {
-        IMPLI_HIP(hipMemcpy(c.data(), cls_.p, c.size(), hipMemcpyDeviceToHost));
-        IMPLI_HIP(hipMemcpy(f.data(), fill_.p, f.size(), hipMemcpyDeviceToHost));
-    }
+    if (bg.n_bricks) IMPLI_HIP(hipMemcpy(f.data(), fill_.p, f.size(), hipMemcpyDeviceToHost));
     int64_t mixed = 0, filled = 0;
     for (int b = 0; b < bg.n_bricks; ++b) {
-        mixed += (c[b] & 3) == kBrickMixed;
-        filled += f[b] != 0;
+        mixed += (f[b] & 3) == kBrickMixed;
+        filled += (f[b] >> 4) != 0;
     }
     out[0] = bg.n_bricks;
     out[1] = pruning() > 0 ? mixed : bg.n_bricks;
@@ -82,8 +79,7 @@ Engine::Engine() {
     cases_.reserve(sizeof cases);
     IMPLI_HIP(hipMemcpy(cases_.p, cases, sizeof cases, hipMemcpyHostToDevice));
     prog_.reserve(sizeof(Program));
-    counters_.reserve(16 * sizeof(uint32_t));
-    overflow_.reserve(16);
+    counters_.reserve(kCounterWords * sizeof(uint32_t));
     offsets_.reserve(16);
     IMPLI_HIP(hipMemset(offsets_.p, 0, 16));
 }
@@ -119,8 +115,8 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &counters_, &vid3_,
-                     &records_, &verts_, &faces_, &overflow_};
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &counters_, &lmodes_, &vid3_,
+                     &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
 }
@@ -146,11 +142,15 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     clist_.reserve(((size_t)coarse_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     blist_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
+    lmodes_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint64_t));
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
     unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
 
     scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
-    signs_.reserve((size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t) + 64);
+    const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
+    signs_.reserve(sign_bytes + 64);
+    // the pieces past the last brick of a row are never written by the pruned path: keep them 0
+    IMPLI_HIP(hipMemset(signs_.p, 0, sign_bytes + 64));
     vid3_.reserve((size_t)grid_.n_cells * 3 * sizeof(uint32_t));
     const int64_t m2 = (int64_t)grid_.m * grid_.m;
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
@@ -190,7 +190,7 @@ MCBuffers Engine::buffers() const {
     b.cap_f = cap_f_;
     b.cap_rec = cap_rec_;
     b.offsets = nullptr;
-    b.overflow = overflow_.as<uint32_t>();
+    b.overflow = counters_.as<uint32_t>() + kOverflowWord;
 
     return b;
 }
@@ -198,23 +198,27 @@ MCBuffers Engine::buffers() const {
 void Engine::eval_field(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
     const int level = pruning();
+    // one memset for the eval's list lengths, the MC counters and the overflow flags
+    IMPLI_HIP(hipMemsetAsync(counters_.p, 0, kCounterWords * sizeof(uint32_t), s));
+    counters_fresh_ = true;
     mark(0, s);
     if (level > 0) {
         ensure_jit();
         launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, cmodes_.as<uint64_t>(),
-                           ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>() + 13,
+                           ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>() + kCoarseListWord,
                            modes_.as<uint64_t>(), cls_.as<uint8_t>(), s, &jit_iv_);
-        uint32_t* d_count = counters_.as<uint32_t>() + 12;   // brick-list length (count() resets 0..11 only)
-        launch_brick_fill(cls_.as<uint8_t>(), grid_, level >= 2, fill_.as<uint8_t>(), blist_.as<uint32_t>(), d_count,
-                          signs_.as<uint64_t>(), s);
+        uint32_t* d_count = counters_.as<uint32_t>() + kBrickListWord;
+        launch_brick_fill(grid_, ccls_.as<uint8_t>(), cmodes_.as<uint64_t>(), cls_.as<uint8_t>(), modes_.as<uint64_t>(),
+                          level >= 2, fill_.as<uint8_t>(), blist_.as<uint32_t>(), lmodes_.as<uint64_t>(), d_count,
+                          signs_.p, s);
         mark(1, s);
         if (jit_fn_) {
             const float* d_mats = reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
-            TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_), modes_.as<uint64_t>(),
+            TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_), lmodes_.as<uint64_t>(),
                                    blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, eval_bricks_grid(grid_),
                                    s);
         } else {
-            launch_eval_bricks_interp(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, modes_.as<uint64_t>(),
+            launch_eval_bricks_interp(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, lmodes_.as<uint64_t>(),
                                       blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, s);
         }
     } else {
@@ -237,8 +241,11 @@ void Engine::ensure_jit() {   // compile the tree kernels for this shape once (c
 }
 
 void Engine::count(hipStream_t s) {
-    IMPLI_HIP(hipMemsetAsync(counters_.p, 0, 12 * sizeof(uint32_t), s));   // [12] holds the eval's brick-list length
-    IMPLI_HIP(hipMemsetAsync(overflow_.p, 0, 16, s));
+    if (!counters_fresh_) {   // a repeated count: reset the MC counters and overflow flags (eval_field did)
+        IMPLI_HIP(hipMemsetAsync(counters_.p, 0, kBrickListWord * sizeof(uint32_t), s));
+        IMPLI_HIP(hipMemsetAsync(counters_.as<uint32_t>() + kOverflowWord, 0, 4 * sizeof(uint32_t), s));
+    }
+    counters_fresh_ = false;
     MCBuffers b = buffers();
     mark(3, s);
     launch_mc_count(cases_.as<CaseInfo>(), grid_, b, s);
@@ -267,7 +274,7 @@ void Engine::raw_counters(uint32_t out[6], hipStream_t s) {
 SlabCounts Engine::read_counts(hipStream_t s, bool* overflow) {
     uint32_t h[16], of = 0;
     IMPLI_HIP(hipMemcpyAsync(h, counters_.p, sizeof h, hipMemcpyDeviceToHost, s));
-    IMPLI_HIP(hipMemcpyAsync(&of, overflow_.p, sizeof of, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipMemcpyAsync(&of, counters_.as<uint32_t>() + kOverflowWord, sizeof of, hipMemcpyDeviceToHost, s));
     IMPLI_HIP(hipStreamSynchronize(s));
     if (overflow) *overflow = of != 0;
     return SlabCounts{h[2], h[3], h[4], h[5]};
@@ -281,7 +288,7 @@ SlabCounts Engine::marching_cubes(hipStream_t s) {
     SlabCounts c = read_counts(s, &of);
     if (of || ensure_capacity(c)) {
         ensure_capacity(c);
-        IMPLI_HIP(hipMemsetAsync(overflow_.p, 0, 16, s));
+        IMPLI_HIP(hipMemsetAsync(counters_.as<uint32_t>() + kOverflowWord, 0, 4 * sizeof(uint32_t), s));
         emit(nullptr, s);
         c = read_counts(s, &of);
         if (of) throw HipError("marching cubes: output capacity overflow after resize");

@@ -31,6 +31,10 @@ struct SlabCounts {
     uint32_t n_faces() const { return tri_total; }
 };
 
+// counters_ layout (u32 words): [0, 12) marching-cubes counters (mc_types.hpp MCBuffers),
+// [12] brick-list length, [13] mixed coarse-box list length, [16, 20) output overflow flags
+constexpr int kBrickListWord = 12, kCoarseListWord = 13, kOverflowWord = 16, kCounterWords = 32;
+
 class Engine {
 public:
     Engine();
@@ -98,12 +102,13 @@ private:
     Program prog_host_{};
     bool jit_tried_ = false;
     hipFunction_t jit_fn_ = nullptr;
+    bool counters_fresh_ = false;   // eval_field zeroed the counters; the next count() need not
     JitIntervalKernels jit_iv_;
     void ensure_jit();
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, counters_, vid3_, records_, verts_, faces_, overflow_;
+    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, counters_, lmodes_, vid3_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
     hipEvent_t ev_[9] = {};

@@ -63,23 +63,6 @@ __global__ __launch_bounds__(256) void k_coarse_modes(const Program* __restrict_
     coarse_modes_body(InterpIv<D>{prog, tab, tab_range}, g, cg, cmodes, ccls, clist, ccount);
 }
 
-// Bricks of sign-definite coarse boxes inherit the box's modes and class (valid on any sub-box).
-__global__ __launch_bounds__(256) void k_brick_inherit(GridDesc g, BrickGrid bg, BrickGrid cg,
-                                                       const uint64_t* __restrict__ cmodes,
-                                                       const uint8_t* __restrict__ ccls, uint64_t* __restrict__ modes,
-                                                       uint8_t* __restrict__ cls) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= bg.n_bricks) return;
-    int bx, by, bz;
-    brick_of(b, bg, bx, by, bz);
-    const int cb = bx + by * cg.nbx + (bz / kCZ) * cg.nbx * cg.nby;
-    const uint8_t c = ccls[cb];
-    if (c == kBrickMixed) return;   // refined by k_brick_refine
-    modes[b] = cmodes[cb];
-    const BrickBox q = brick_box(g, bx, by, bz, kBZ);
-    cls[b] = sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
-}
-
 template <int D>
 __global__ __launch_bounds__(256) void k_brick_refine(const Program* __restrict__ prog, const float* __restrict__ tab,
                                                       float2 tab_range, GridDesc g, BrickGrid bg, BrickGrid cg,
@@ -109,66 +92,70 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __rest
     eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, list, count, field, signs);
 }
 
-// Neighbour rule per brick (brick_fill_class): fill[b], and the list of bricks to evaluate
-// (mixed, or next to a brick of another class).  Wave-aggregated appends, order irrelevant.
-__global__ __launch_bounds__(256) void k_brick_fill(const uint8_t* __restrict__ cls, BrickGrid bg, int sign_fill,
-                                                    uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
-                                                    uint32_t* __restrict__ count) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    const int lane = threadIdx.x & 63;
+// Per brick: its class (inherited from a sign-definite coarse box, or refined), the neighbour rule
+// (brick_fill_class), fill[b] = class | fill class << 4, and either the constant sign pieces of a
+// sign-filled brick or an entry in the list of bricks to evaluate (with its modes, so the eval
+// kernel reads them in list order).  List appends are aggregated per block: one atomic per 1024
+// bricks.
+constexpr int kFillBlock = 1024;
+__global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid bg, BrickGrid cg,
+                                                           const uint8_t* __restrict__ ccls,
+                                                           const uint64_t* __restrict__ cmodes,
+                                                           const uint8_t* __restrict__ cls,
+                                                           const uint64_t* __restrict__ modes, int sign_fill,
+                                                           uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
+                                                           uint64_t* __restrict__ lmodes, uint32_t* __restrict__ count,
+                                                           sign_piece_t* __restrict__ signs) {
+    __shared__ uint32_t wcnt[kFillBlock / 64], wbase[kFillBlock / 64];
+    const int b = blockIdx.x * kFillBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t fc = kBrickMixed;
-    if (b < bg.n_bricks) {
-        int bx, by, bz;
+    int bx = 0, by = 0, bz = 0, cb = 0;
+    const bool valid = b < bg.n_bricks;
+    if (valid) {
         brick_of(b, bg, bx, by, bz);
-        fc = sign_fill ? brick_fill_class(cls, bg, b, bx, by, bz) : (uint32_t)kBrickMixed;
-        fill[b] = (uint8_t)fc;
+        cb = bx + by * cg.nbx + (bz / kCZ) * cg.nbx * cg.nby;
+        const uint32_t c = brick_class(g, bg, cg, ccls, cls, bx, by, bz);
+        fc = sign_fill ? brick_fill_class(g, bg, cg, ccls, cls, c, bx, by, bz) : (uint32_t)kBrickMixed;
+        fill[b] = (uint8_t)(c | (fc << 4));
     }
-    const bool eval = b < bg.n_bricks && fc == kBrickMixed;
+    const bool eval = valid && fc == kBrickMixed;
     const uint64_t mask = __ballot(eval);
-    uint32_t base = 0;
-    if (lane == __ffsll((unsigned long long)mask) - 1) base = atomicAdd(count, (uint32_t)__popcll(mask));
-    base = __shfl(base, __ffsll((unsigned long long)mask) - 1, 64);
-    if (eval) list[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)b;
-}
-
-// Constant sign bits of the sign-filled bricks: one thread per 64-bit word of the bitmap (pieces
-// of evaluated bricks are rewritten by the eval kernel afterwards).
-__global__ __launch_bounds__(256) void k_sign_fill(GridDesc g, BrickGrid bg, const uint8_t* __restrict__ fill,
-                                                   uint64_t* __restrict__ signs) {
-    const int rw = sign_row_words(g);
-    const int64_t rows = (int64_t)g.n * (g.fz1 - g.fz0);
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= rows * rw) return;
-    const int64_t row = i / rw;
-    const int c = (int)(i - row * rw);
-    const int layer = (int)(row / g.n), y = (int)(row - (int64_t)layer * g.n);
-    constexpr int P = 64 / kBX;   // pieces per word
-    const uint8_t* f = fill + (size_t)((layer / kBZ) * bg.nby + y / kBY) * bg.nbx;
-    uint64_t w = 0;
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int bx = c * P + j;
-        if (bx < bg.nbx && f[bx] == kBrickNeg) w |= (kBX == 64 ? ~0ull : ((1ull << kBX) - 1ull)) << (kBX * j);
+    if (lane == 0) wcnt[w] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < kFillBlock / 64; ++k) { wbase[k] = t; t += wcnt[k]; }
+        const uint32_t base = t ? atomicAdd(count, t) : 0u;
+        for (int k = 0; k < kFillBlock / 64; ++k) wbase[k] += base;
     }
-    signs[i] = w;
+    __syncthreads();
+    if (eval) {
+        const uint32_t i = wbase[w] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        list[i] = (uint32_t)b;
+        lmodes[i] = (ccls[cb] == kBrickMixed) ? modes[b] : cmodes[cb];
+    } else if (valid) {   // sign-filled: constant pieces (all samples of the brick share the sign)
+        const sign_piece_t piece = fc == kBrickNeg ? (sign_piece_t)~(sign_piece_t)0 : (sign_piece_t)0;
+        const int layers = g.fz1 - g.fz0, row_pieces = (64 / kBX) * sign_row_words(g);
+        const int y1 = min(by * kBY + kBY, g.n), z1 = min(bz * kBZ + kBZ, layers);
+        for (int z = bz * kBZ; z < z1; ++z)
+            for (int y = by * kBY; y < y1; ++y) signs[((size_t)z * g.n + y) * row_pieces + bx] = piece;
+    }
 }
 
 // sign bitmap of a fully evaluated field (unpruned path): one thread per 64-bit word
 __global__ __launch_bounds__(256) void k_signs_from_field(GridDesc g, const float* __restrict__ field,
                                                           uint64_t* __restrict__ signs) {
+    // one wave per 64-bit word: lane k reads sample 64 w + k of the row (coalesced 4 B per lane)
     const int rw = sign_row_words(g);
     const int64_t rows = (int64_t)g.n * (g.fz1 - g.fz0);
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= rows * rw) return;
     const int64_t row = i / rw;
-    const int w = (int)(i - row * rw);
-    const float* f = field + row * g.n;
-    uint64_t bits = 0;
-    for (int k = 0; k < 64; ++k) {
-        const int x = 64 * w + k;
-        if (x < g.n && f[x] < 0.f) bits |= 1ull << k;
-    }
-    signs[i] = bits;
+    const int x = 64 * (int)(i - row * rw) + (threadIdx.x & 63);
+    const bool neg = x < g.n && field[row * g.n + x] < 0.f;
+    const uint64_t bits = __ballot(neg);
+    if ((threadIdx.x & 63) == 0) signs[i] = bits;
 }
 
 template <int D>
@@ -237,15 +224,13 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
     BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
-    (void)hipMemsetAsync(d_ccount, 0, sizeof(uint32_t), s);
-    const unsigned tc = (unsigned)((cg.n_bricks + 255) / 256), tb = (unsigned)((bg.n_bricks + 255) / 256);
+    const unsigned tc = (unsigned)((cg.n_bricks + 255) / 256);
     const unsigned tr = (unsigned)std::min<int64_t>(((int64_t)cg.n_bricks * kCZ + 255) / 256, 2048);
     if (jit && jit->coarse && jit->refine) {
         GridDesc gg = g;
         const float* d_mats = reinterpret_cast<const float*>(reinterpret_cast<const char*>(d_prog) + offsetof(Program, mats));
         void* ca[] = {&d_mats, &d_rabbit, &tab_range, &gg, &cg, &d_cmodes, &d_ccls, &d_clist, &d_ccount};
         TreeJit::launch(jit->coarse, tc, ca, s, "impli_coarse_modes");
-        k_brick_inherit<<<tb, 256, 0, s>>>(g, bg, cg, d_cmodes, d_ccls, d_modes, d_cls);
         void* ra[] = {&d_mats, &d_rabbit, &tab_range, &gg, &bg, &cg, &d_cmodes, &d_clist, &d_ccount, &d_modes, &d_cls};
         TreeJit::launch(jit->refine, tr, ra, s, "impli_brick_refine");
         return;
@@ -254,7 +239,6 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
     do {                                                                                                          \
         k_coarse_modes<DD><<<tc, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, cg, d_cmodes, d_ccls, d_clist,     \
                                               d_ccount);                                                          \
-        k_brick_inherit<<<tb, 256, 0, s>>>(g, bg, cg, d_cmodes, d_ccls, d_modes, d_cls);                          \
         k_brick_refine<DD><<<tr, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, cg, d_cmodes, d_clist, d_ccount, \
                                               d_modes, d_cls);                                                    \
     } while (0)
@@ -268,17 +252,17 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
 void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s) {
     const int64_t words = (int64_t)g.n * (g.fz1 - g.fz0) * sign_row_words(g);
     if (words <= 0) return;
-    k_signs_from_field<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(g, d_field, d_signs);
+    k_signs_from_field<<<(unsigned)((words + 3) / 4), 256, 0, s>>>(g, d_field, d_signs);
 }
 
-void launch_brick_fill(const uint8_t* d_cls, const GridDesc& g, int sign_fill, uint8_t* d_fill, uint32_t* d_list,
-                       uint32_t* d_count, uint64_t* d_signs, hipStream_t s) {
-    const BrickGrid bg = brick_grid(g);
+void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t* d_cmodes, const uint8_t* d_cls,
+                       const uint64_t* d_modes, int sign_fill, uint8_t* d_fill, uint32_t* d_list, uint64_t* d_lmodes,
+                       uint32_t* d_count, void* d_signs, hipStream_t s) {
+    const BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0) return;
-    (void)hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
-    k_brick_fill<<<(unsigned)((bg.n_bricks + 255) / 256), 256, 0, s>>>(d_cls, bg, sign_fill, d_fill, d_list, d_count);
-    const int64_t words = (int64_t)g.n * (g.fz1 - g.fz0) * sign_row_words(g);
-    k_sign_fill<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(g, bg, d_fill, d_signs);
+    k_brick_fill<<<(unsigned)((bg.n_bricks + kFillBlock - 1) / kFillBlock), kFillBlock, 0, s>>>(
+        g, bg, cg, d_ccls, d_cmodes, d_cls, d_modes, sign_fill, d_fill, d_list, d_lmodes, d_count,
+        static_cast<sign_piece_t*>(d_signs));
 }
 
 unsigned eval_bricks_grid(const GridDesc& g) {

@@ -35,24 +35,11 @@ __device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, in
     bz = t / bg.nby;
 }
 
-// A brick needs exact values only if one of its samples can be the end of a sign-changing cell
-// edge.  Edges are axis aligned, so that requires the brick or a face neighbour to differ in
-// sign class.  Neighbours outside the stored grid hold no sample any cell of this slab reads.
-__device__ __forceinline__ uint32_t brick_fill_class(const uint8_t* __restrict__ cls, const BrickGrid& bg, int b,
-                                                     int bx, int by, int bz) {
-    const uint32_t cb = cls[b], c = cb & 3u;
-    if (c == kBrickMixed || (cb & kBrickNoFill)) return kBrickMixed;
-    const int sy = bg.nbx, sz = bg.nbx * bg.nby;
-    const uint32_t xm = bx > 0 ? cls[b - 1] & 3u : c, xp = bx + 1 < bg.nbx ? cls[b + 1] & 3u : c;
-    const uint32_t ym = by > 0 ? cls[b - sy] & 3u : c, yp = by + 1 < bg.nby ? cls[b + sy] & 3u : c;
-    const uint32_t zm = bz > 0 ? cls[b - sz] & 3u : c, zp = bz + 1 < bg.nbz ? cls[b + sz] & 3u : c;
-    return (xm == c && xp == c && ym == c && yp == c && zm == c && zp == c) ? c : (uint32_t)kBrickMixed;
-}
-
 // One wave per listed brick (kBX x kBY lanes, kBZ layers each; grid-stride over the list built by
-// k_brick_fill): every sample is evaluated with `ev(modes, x, y, z)`, stored, and its sign bit set
-// (wave ballot: 64 bits = kBY rows x kBX samples).  Sign-filled bricks never reach this kernel --
-// k_sign_fill wrote their constant sign bits.
+// k_brick_fill, modes[i] the listed brick's pruning modes): every sample is evaluated with
+// `ev(modes, x, y, z)`, stored, and its sign bit set (wave ballot: 64 bits = kBY rows x kBX
+// samples).  Sign-filled bricks never reach this kernel -- k_brick_fill wrote their constant sign
+// bits.
 template <class Eval>
 __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
                                                  const uint64_t* __restrict__ modes,
@@ -73,7 +60,7 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
         const bool ok = sx < n && sy < n;
         const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
         float* out = field + (size_t)(ok ? sy : 0) * n + (ok ? sx : 0);
-        const uint64_t m64 = modes[b];
+        const uint64_t m64 = modes[i];
         const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
                            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
         const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);

@@ -29,8 +29,9 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
                         uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_ccount, uint64_t* d_modes,
                         uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit = nullptr);
 // K1b: neighbour rule -> fill[b], the list of bricks to evaluate, constant sign bits of the rest
-void launch_brick_fill(const uint8_t* d_cls, const GridDesc& g, int sign_fill, uint8_t* d_fill, uint32_t* d_list,
-                       uint32_t* d_count, uint64_t* d_signs, hipStream_t s);
+void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t* d_cmodes, const uint8_t* d_cls,
+                       const uint64_t* d_modes, int sign_fill, uint8_t* d_fill, uint32_t* d_list, uint64_t* d_lmodes,
+                       uint32_t* d_count, void* d_signs, hipStream_t s);
 // K1c (interpreter): the listed bricks; the JIT variant is TreeJit::launch_bricks (jit.hpp)
 unsigned eval_bricks_grid(const GridDesc& g);
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
@@ -47,6 +48,6 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 
-inline int64_t n_scan_blocks(const GridDesc& g) { return (n_units(g) + kScanBlock - 1) / kScanBlock; }
+inline int64_t n_scan_blocks(const GridDesc& g) { return n_groups(g); }
 
 }  // namespace impli

@@ -15,12 +15,15 @@
 // Signs come from the eval's sign bitmap (grid.hpp), 64 cells per bit operation; only the ~1 % of
 // non-trivial cells (corner signs not all equal) do per-cell work.  A unit = kUnitRows cell rows.
 //   K2 k_mc_count : per unit the sums of owned edges, triangles, active cells, halo-owned edges.
-//   K2b k_scan_*  : exclusive scan of the unit sums (partial sums, top level, apply).
+//   K2b k_scan_groups : exclusive scan of the group sums (one block, ~1k groups at 512^3); verts
+//                   scans the unit counts of its group.
 //   K3 k_mc_verts : per unit, the non-trivial cells in cell order: owned vertex positions (field
 //                   values read only at crossing edges), the dense vid3[cell][slot] table, records.
 //   K4 k_mc_faces : per active cell, gathers the vertex ids of its triangle corners from vid3 of
 //                   the owner cells.
+#include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "eval_bricks.hpp"
 #include "ifunc_device.hpp"
@@ -65,57 +68,79 @@ void build_case_table(CaseInfo out[256]) {
             if (slot >= 0 && c.rank[slot] < 0) c.rank[slot] = (int8_t)r++;
         }
         c.nown = (uint8_t)r;
+        // k_mc_count relies on two table properties (checked here for every case): the owned
+        // edges a case's triangles use are exactly its crossing owned edges (Bourke edges 5 =
+        // corners 5-6, 6 = 6-7, 10 = 2-6), and every non-trivial case has a triangle.
+        auto neg = [ci](int k) { return (ci >> k) & 1; };
+        const int crossing = (neg(5) ^ neg(6)) + (neg(6) ^ neg(7)) + (neg(2) ^ neg(6));
+        if (crossing != c.nown || (c.ntri > 0) != (ci != 0 && ci != 255))
+            throw std::runtime_error("marching cubes: case table violates the count kernel's assumptions");
         out[ci] = c;
     }
 }
 
 namespace {
 
-// K2: one wave per unit (kUnitRows rows).  Items (row, 64-cell chunk) are spread over the lanes;
-// only non-trivial cells (~1 %) look at the case table.  -> unit_cnt[u] = {own, tri, act, halo own}
-__global__ __launch_bounds__(256) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
-    const int lane = threadIdx.x & 63;
-    const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (u >= n_units(g)) return;
+// K2: one block per group of kGroupUnits units; one lane per item (row, 64-cell chunk) of the
+// group, so every lane has work (a wave per unit would leave 64 - 4 nch lanes idle).  Only
+// non-trivial cells (~1 %) look at the triangle table.  Per-unit sums through LDS atomics.
+//   -> unit_cnt[u] = {own, tri, act, halo own}; scan_blk[c][group] = the group's sums.
+__global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+    __shared__ uint32_t s_u[kGroupUnits][4];
+    __shared__ uint8_t s_ntri[256];
+    const int t = threadIdx.x, nt_ = blockDim.x;
+    for (int k = t; k < 256; k += nt_) s_ntri[k] = cases[k].ntri;
+    for (int k = t; k < 4 * kGroupUnits; k += nt_) (&s_u[0][0])[k] = 0u;
+    __syncthreads();
     const int nch = (g.m + 63) / 64;
-    const int64_t rows = n_rows(g);
-    unsigned own = 0, tri = 0, act = 0, hal = 0;
-    for (int i = lane; i < kUnitRows * nch; i += 64) {
-        const int64_t row = u * kUnitRows + i / nch;
-        if (row >= rows) break;
-        ChunkBits k;
-        load_chunk(g, b.signs, row, i % nch, k);
-        uint64_t nt = k.nt;
-        const bool emit = k.z >= g.cz_emit;
-        while (nt) {
-            const int j = __ffsll((unsigned long long)nt) - 1;
-            nt &= nt - 1;
-            unsigned ntri;
-            const unsigned no = case_counts(cases, chunk_ci(k, j), ntri);
-            own += no;
-            if (emit) { tri += ntri; act += ntri ? 1u : 0u; }
-            else hal += no;
+    const int64_t rows = n_rows(g), nu = n_units(g);
+    const int64_t row0 = (int64_t)blockIdx.x * kGroupUnits * kUnitRows;
+    for (int i = t; i < kGroupUnits * kUnitRows * nch; i += nt_) {
+        const int r = i / nch;
+        const int64_t row = row0 + r;
+        unsigned own = 0, tri = 0, act = 0, hal = 0;
+        if (row < rows) {
+            ChunkBits k;
+            load_chunk(g, b.signs, row, i - r * nch, k);
+            // owned vertices = crossing owned edges (build_case_table checks the identity):
+            // edge 5 = corners 5-6 (t01, t11), 6 = 6-7 (t11, s11), 10 = 2-6 (t10, t11)
+            own = (unsigned)(__popcll((unsigned long long)((k.t01 ^ k.t11) & k.nt)) +
+                             __popcll((unsigned long long)((k.s11 ^ k.t11) & k.nt)) +
+                             __popcll((unsigned long long)((k.t10 ^ k.t11) & k.nt)));
+            if (k.z >= g.cz_emit) {
+                act = (unsigned)__popcll((unsigned long long)k.nt);   // every non-trivial case has a triangle
+                uint64_t nt = k.nt;
+                while (nt) {
+                    const int j = __ffsll((unsigned long long)nt) - 1;
+                    nt &= nt - 1;
+                    tri += s_ntri[chunk_ci(k, j)];
+                }
+            } else {
+                hal = own;
+            }
+        }
+        if (own | tri) {
+            uint32_t* d = s_u[r / kUnitRows];
+            atomicAdd(&d[0], own);
+            if (tri) { atomicAdd(&d[1], tri); atomicAdd(&d[2], act); }
+            if (hal) atomicAdd(&d[3], hal);
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        own += __shfl_down(own, o, 64);
-        tri += __shfl_down(tri, o, 64);
-        act += __shfl_down(act, o, 64);
-        hal += __shfl_down(hal, o, 64);
+    __syncthreads();
+    const int64_t u = (int64_t)blockIdx.x * kGroupUnits + t;
+    if (t < kGroupUnits && u < nu) b.unit_cnt[u] = make_uint4(s_u[t][0], s_u[t][1], s_u[t][2], s_u[t][3]);
+    if (t < 5) {   // blockDim >= 64
+        uint32_t sum = 0;
+        for (int w = 0; w < kGroupUnits; ++w)
+            sum += (t < 4) ? s_u[w][t] : ((s_u[w][0] | s_u[w][1]) ? 1u : 0u);
+        b.scan_blk[(int64_t)t * gridDim.x + blockIdx.x] = sum;
     }
-    if (lane == 0) b.unit_cnt[u] = make_uint4(own, tri, act, hal);
 }
 
-// ---- unit scan: partial sums per scan block, top-level scan, apply ----
+// ---- group scan: one block, exclusive bases of the groups in place, totals to the counters ----
 struct Cnt5 { uint32_t c[5]; };
-__device__ __forceinline__ Cnt5 unit_c5(uint4 v) {
-    Cnt5 r;
-    r.c[0] = v.x; r.c[1] = v.y; r.c[2] = v.z; r.c[3] = v.w; r.c[4] = (v.x | v.y) ? 1u : 0u;
-    return r;
-}
 
-// inclusive block scan (1024 lanes) of 5 components; returns exclusive, fills total
+// block scan (1024 lanes) of 5 components; returns exclusive, fills total
 __device__ __forceinline__ Cnt5 block_scan5(Cnt5 v, Cnt5& total, uint32_t (*s_w)[16]) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     Cnt5 incl;
@@ -141,60 +166,42 @@ __device__ __forceinline__ Cnt5 block_scan5(Cnt5 v, Cnt5& total, uint32_t (*s_w)
     return ex;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_partial(const uint4* __restrict__ cnt, int64_t nu, uint32_t* __restrict__ blk) {
+__global__ __launch_bounds__(1024) void k_scan_groups(uint32_t* __restrict__ blk, int64_t ng,
+                                                      uint32_t* __restrict__ counters) {
     __shared__ uint32_t s_w[5][16];
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanUPT;
-    Cnt5 sum = {{0, 0, 0, 0, 0}};
-    for (int i = 0; i < kScanUPT; ++i)
-        if (base + i < nu) {
-            const Cnt5 c = unit_c5(cnt[base + i]);
-            for (int k = 0; k < 5; ++k) sum.c[k] += c.c[k];
+    Cnt5 carry = {{0, 0, 0, 0, 0}};
+    for (int64_t base0 = 0; base0 < ng; base0 += 1024 * kTopPT) {
+        const int64_t base = base0 + (int64_t)threadIdx.x * kTopPT;
+        Cnt5 sum = {{0, 0, 0, 0, 0}};
+        for (int i = 0; i < kTopPT; ++i)
+            if (base + i < ng)
+#pragma unroll
+                for (int c = 0; c < 5; ++c) sum.c[c] += blk[c * ng + base + i];
+        Cnt5 tot;
+        Cnt5 run = block_scan5(sum, tot, s_w);
+        for (int i = 0; i < kTopPT; ++i) {
+            if (base + i >= ng) break;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) {
+                const uint32_t x = blk[c * ng + base + i];   // this lane's own entries: no race
+                blk[c * ng + base + i] = carry.c[c] + run.c[c];
+                run.c[c] += x;
+            }
         }
-    Cnt5 tot;
-    (void)block_scan5(sum, tot, s_w);
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 5; ++k) blk[8 * blockIdx.x + k] = tot.c[k];
-}
-
-__global__ __launch_bounds__(64) void k_scan_top(uint32_t* __restrict__ blk, int nb, uint32_t* __restrict__ counters) {
-    if (threadIdx.x != 0) return;
-    uint32_t run[5] = {0, 0, 0, 0, 0};
-    for (int b = 0; b < nb; ++b)
-        for (int k = 0; k < 5; ++k) {
-            const uint32_t v = blk[8 * b + k];
-            blk[8 * b + k] = run[k];
-            run[k] += v;
-        }
-    counters[0] = run[4];
-    counters[1] = run[3];
-    counters[2] = run[0];
-    counters[3] = run[1];
-    counters[4] = run[2];
-    counters[5] = run[3];
-}
-
-__global__ __launch_bounds__(1024) void k_scan_apply(uint4* __restrict__ cnt, int64_t nu, const uint32_t* __restrict__ blk) {
-    __shared__ uint32_t s_w[5][16];
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanUPT;
-    uint4 v[kScanUPT];
-    Cnt5 sum = {{0, 0, 0, 0, 0}};
-    for (int i = 0; i < kScanUPT; ++i) {
-        v[i] = (base + i < nu) ? cnt[base + i] : make_uint4(0, 0, 0, 0);
-        const Cnt5 c = unit_c5(v[i]);
-        for (int k = 0; k < 5; ++k) sum.c[k] += c.c[k];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) carry.c[c] += tot.c[c];
     }
-    Cnt5 tot;
-    Cnt5 run = block_scan5(sum, tot, s_w);
-    for (int k = 0; k < 5; ++k) run.c[k] += blk[8 * blockIdx.x + k];
-    for (int i = 0; i < kScanUPT; ++i) {
-        if (base + i >= nu) break;
-        const Cnt5 c = unit_c5(v[i]);
-        cnt[base + i] = make_uint4(run.c[0], run.c[1], run.c[2], run.c[3]);
-        for (int k = 0; k < 5; ++k) run.c[k] += c.c[k];
+    if (threadIdx.x == 0) {
+        counters[0] = carry.c[4];   // non-empty units
+        counters[1] = carry.c[3];   // halo-owned vertices (ids below the slab's first)
+        counters[2] = carry.c[0];   // owned vertices incl. halo
+        counters[3] = carry.c[1];   // triangles
+        counters[4] = carry.c[2];   // active cells (face records)
+        counters[5] = carry.c[3];
     }
 }
 
-__global__ __launch_bounds__(256) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+__global__ __launch_bounds__(64 * kVertsUnits) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     mc_verts_body(cases, g, b);
 }
 
@@ -236,16 +243,16 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
 }  // namespace
 
 void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
-    const int64_t nu = n_units(g);
-    if (nu == 0) return;
-    k_mc_count<<<(unsigned)((nu + 3) / 4), 256, 0, s>>>(d_cases, g, b);
+    const int64_t ng = n_groups(g);
+    if (ng == 0) return;
+    // one lane per item of a group (kGroupUnits kUnitRows rows x nch chunks), whole waves, <= 1024
+    const int items = kGroupUnits * kUnitRows * ((g.m + 63) / 64);
+    const unsigned threads = (unsigned)std::min(1024, (items + 63) / 64 * 64);
+    k_mc_count<<<(unsigned)ng, threads, 0, s>>>(d_cases, g, b);
 }
 
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
-    const int64_t nu = n_units(g), nb = n_scan_blocks(g);
-    if (nb > 0) k_scan_partial<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk);
-    k_scan_top<<<1, 64, 0, s>>>(b.scan_blk, (int)nb, b.counters);
-    if (nb > 0) k_scan_apply<<<(unsigned)nb, 1024, 0, s>>>(b.unit_cnt, nu, b.scan_blk);
+    k_scan_groups<<<1, 1024, 0, s>>>(b.scan_blk, n_groups(g), b.counters);
 }
 
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
@@ -254,7 +261,7 @@ void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
 
 void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     const int64_t nu = n_units(g);
-    if (nu > 0) k_mc_verts<<<(unsigned)((nu + 3) / 4), 256, 0, s>>>(d_cases, g, b);
+    if (nu > 0) k_mc_verts<<<(unsigned)((nu + kVertsUnits - 1) / kVertsUnits), 64 * kVertsUnits, 0, s>>>(d_cases, g, b);
 }
 
 }  // namespace impli

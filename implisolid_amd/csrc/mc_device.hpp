@@ -20,13 +20,6 @@ __device__ __forceinline__ T wave_incl_scan(T x, int lane) {
     return x;
 }
 
-// owned-edge and triangle counts of a cube index
-__device__ __forceinline__ unsigned case_counts(const CaseInfo* __restrict__ cases, unsigned ci, unsigned& ntri) {
-    const uint16_t v = *reinterpret_cast<const uint16_t*>(&cases[ci]);   // {ntri, nown}
-    ntri = v & 255u;
-    return v >> 8;
-}
-
 // 64 consecutive cells of one cell row, as sign bits.  For cell j (x = 64 c + 1 + j) the corners
 // are stored samples x-1 and x of the rows (y, z), (y+1, z), (y, z+1), (y+1, z+1): bit j of s.. and
 // t.. (t = s shifted by one sample).  nt marks the non-trivial cells (corner signs not all equal).
@@ -85,18 +78,36 @@ __device__ __forceinline__ float edge_value(const GridDesc& g, const MCBuffers& 
     return (sealed_xy(g, sx) || sealed_xy(g, sy) || sealed_z(g, sl)) ? kSealed : b.field[sx + sy * g.n + sl * g.n * g.n];
 }
 
+// One block per kVertsUnits units, one wave per unit.  The unit's exclusive bases are its group's
+// (k_scan_groups) plus a scan of the group's kGroupUnits unit counts (one lane each).
 __device__ __forceinline__ void mc_verts_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
+    static_assert(kGroupUnits == 64 && kGroupUnits % kVertsUnits == 0, "one lane per unit of the group");
     __shared__ CaseInfo s_case[256];
-    __shared__ uint32_t s_list[4][kListCap];   // per wave: ci | j << 8 | item << 14
+    __shared__ uint32_t s_list[kVertsUnits][kListCap];   // per wave: ci | j << 8 | item << 14
+    __shared__ uint4 s_base[kVertsUnits];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    s_case[t] = cases[t];
+    if (t < 256) s_case[t] = cases[t];
+    const int64_t u0 = (int64_t)blockIdx.x * kVertsUnits;
+    const int64_t nu = n_units(g);
+    if (wid == 0) {
+        const int64_t grp = u0 / kGroupUnits, ng = n_groups(g);
+        const int64_t uu = grp * kGroupUnits + lane;
+        const uint4 c = (uu < nu) ? b.unit_cnt[uu] : make_uint4(0, 0, 0, 0);
+        // 32-bit scans: a group's prefix can exceed a 16-bit pack4 field
+        const uint32_t ev = wave_incl_scan<uint32_t>(c.x, lane) - c.x;
+        const uint32_t ef = wave_incl_scan<uint32_t>(c.y, lane) - c.y;
+        const uint32_t ea = wave_incl_scan<uint32_t>(c.z, lane) - c.z;
+        const int k = lane - (int)(u0 - grp * kGroupUnits);
+        if (k >= 0 && k < kVertsUnits)
+            s_base[k] = make_uint4(b.scan_blk[grp] + ev, b.scan_blk[ng + grp] + ef, b.scan_blk[2 * ng + grp] + ea, 0u);
+    }
     __syncthreads();
-    const int64_t u = (int64_t)blockIdx.x * 4 + wid;
-    if (u >= n_units(g)) return;
+    const int64_t u = u0 + wid;
+    if (u >= nu) return;
     const uint32_t H = b.counters[1];
     const int nch = (g.m + 63) / 64;
     const int64_t rows = n_rows(g);
-    const uint4 base = b.unit_cnt[u];   // exclusive {vbase, fbase, abase, hbase}
+    const uint4 base = s_base[wid];   // exclusive {vbase, fbase, abase}
     uint32_t vrun0 = base.x, frun0 = base.y, arun0 = base.z;
     uint32_t* list = s_list[wid];
     const int items = kUnitRows * nch;

@@ -19,13 +19,14 @@ static_assert(sizeof(CaseInfo) == 32, "CaseInfo layout");
 // MC pipeline.  Cells are numbered L = row * m + (x - 1), row = (z - cz0) * m + (y - 1); a unit is
 // kUnitRows consecutive rows (contiguous in linear order), processed by one wave.
 constexpr int kUnitRows = 4;
-constexpr int kScanUPT = 8;            // units per lane in the unit scan
-constexpr int kScanBlock = 1024 * kScanUPT;
+constexpr int kGroupUnits = 64;        // units per group: one count block; the group scan's element
+constexpr int kVertsUnits = 16;        // units per verts block (one wave each)
+constexpr int kTopPT = 2;              // groups per lane in one pass of the group scan
 struct MCBuffers {
     const float* field;
     const uint64_t* signs;   // sign bitmap of the stored samples (grid.hpp)
-    uint4* unit_cnt;         // per unit {own, tri, act, halo own}; scanned in place to exclusive bases
-    uint32_t* scan_blk;      // 8 per scan block: partial sums (5 components), then exclusive bases
+    uint4* unit_cnt;         // per unit {own, tri, act, halo own}
+    uint32_t* scan_blk;      // [5][n_groups]: group sums (own, tri, act, halo own, non-empty units), then exclusive bases
     uint32_t* counters;      // [0] unused, [1] halo own, [2..5] totals own/tri/act/halo
     uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
     uint4* records;          // active cells: {L, ci, fbase, 0}
@@ -37,5 +38,6 @@ struct MCBuffers {
 };
 __host__ __device__ inline int64_t n_rows(const GridDesc& g) { return (int64_t)g.m * (g.cz1 - g.cz0); }
 __host__ __device__ inline int64_t n_units(const GridDesc& g) { return (n_rows(g) + kUnitRows - 1) / kUnitRows; }
+__host__ __device__ inline int64_t n_groups(const GridDesc& g) { return (n_units(g) + kGroupUnits - 1) / kGroupUnits; }
 
 }  // namespace impli
