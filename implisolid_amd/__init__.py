@@ -16,7 +16,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libimplisolid_mi355x.so")
-LIB_PATH = os.environ.get("IMPLISOLID_LIB", LIB_PATH)   # experiments: an alternative build
+LIB_PATH = os.environ.get("IMPLISOLID_LIB") or LIB_PATH   # experiments: an alternative build
 
 # every symbol declared in include/implisolid.h
 ABI_SYMBOLS = [

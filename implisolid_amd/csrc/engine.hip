@@ -115,7 +115,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &counters_, &lmodes_, &vid3_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &ulist_, &counters_, &lmodes_, &vid3_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -134,7 +134,6 @@ void Engine::set_object(const Program& prog) {
 void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     const SlabRange sr = slab_partition(R, rank, nranks);   // one halo layer below (owner rule)
     grid_ = make_grid(R, box, sr.z0 - sr.halo, sr.z1, sr.z0);
-    const int64_t nu = n_units(grid_);
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
     cls_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     cmodes_.reserve((size_t)(coarse_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
@@ -144,7 +143,8 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     blist_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     lmodes_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint64_t));
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
-    unit_cnt_.reserve((size_t)(nu + 1) * sizeof(uint4));
+    unit_cnt_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint4));
+    ulist_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint4));
 
     scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
     const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
@@ -180,6 +180,7 @@ MCBuffers Engine::buffers() const {
     b.signs = signs_.as<uint64_t>();
 
     b.unit_cnt = unit_cnt_.as<uint4>();
+    b.ulist = ulist_.as<uint4>();
     b.scan_blk = scan_blk_.as<uint32_t>();
     b.counters = counters_.as<uint32_t>();
     b.vid3 = vid3_.as<uint32_t>();

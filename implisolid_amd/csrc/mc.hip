@@ -15,8 +15,8 @@
 // Signs come from the eval's sign bitmap (grid.hpp), 64 cells per bit operation; only the ~1 % of
 // non-trivial cells (corner signs not all equal) do per-cell work.  A unit = kUnitRows cell rows.
 //   K2 k_mc_count : per unit the sums of owned edges, triangles, active cells, halo-owned edges.
-//   K2b k_scan_groups : exclusive scan of the group sums (one block, ~1k groups at 512^3); verts
-//                   scans the unit counts of its group.
+//   K2b k_scan_groups : exclusive scan of the group sums (one block, ~1k groups at 512^3);
+//       k_unit_flatten: the non-empty units in order with their global bases (one wave per group).
 //   K3 k_mc_verts : per unit, the non-trivial cells in cell order: owned vertex positions (field
 //                   values read only at crossing edges), the dense vid3[cell][slot] table, records.
 //   K4 k_mc_faces : per active cell, gathers the vertex ids of its triangle corners from vid3 of
@@ -84,7 +84,9 @@ namespace {
 // K2: one block per group of kGroupUnits units; one lane per item (row, 64-cell chunk) of the
 // group, so every lane has work (a wave per unit would leave 64 - 4 nch lanes idle).  Only
 // non-trivial cells (~1 %) look at the triangle table.  Per-unit sums through LDS atomics.
-//   -> unit_cnt[u] = {own, tri, act, halo own}; scan_blk[c][group] = the group's sums.
+//   -> unit_cnt[64 group + k] = k-th non-empty unit of the group {unit in group, own / tri / act
+//      exclusive bases in the group}; scan_blk[c][group] = the group's sums (c < 5: own, tri, act,
+//      halo own, non-empty units -- scanned by k_scan_groups), scan_blk[5][group] = non-empty units.
 __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ uint32_t s_u[kGroupUnits][4];
     __shared__ uint8_t s_ntri[256];
@@ -127,13 +129,24 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
         }
     }
     __syncthreads();
-    const int64_t u = (int64_t)blockIdx.x * kGroupUnits + t;
-    if (t < kGroupUnits && u < nu) b.unit_cnt[u] = make_uint4(s_u[t][0], s_u[t][1], s_u[t][2], s_u[t][3]);
-    if (t < 5) {   // blockDim >= 64
-        uint32_t sum = 0;
-        for (int w = 0; w < kGroupUnits; ++w)
-            sum += (t < 4) ? s_u[w][t] : ((s_u[w][0] | s_u[w][1]) ? 1u : 0u);
-        b.scan_blk[(int64_t)t * gridDim.x + blockIdx.x] = sum;
+    if (t < 64) {   // wave 0, one lane per unit of the group (kGroupUnits == 64; blockDim >= 64)
+        const int64_t u = (int64_t)blockIdx.x * kGroupUnits + t;
+        const uint32_t own = s_u[t][0], tri = s_u[t][1], act = s_u[t][2], hal = s_u[t][3];
+        const bool ne = u < nu && (own | tri) != 0;
+        // the group's non-empty units in order, with their exclusive bases inside the group
+        const uint32_t eo = wave_incl_scan<uint32_t>(own, t) - own;
+        const uint32_t et = wave_incl_scan<uint32_t>(tri, t) - tri;
+        const uint32_t ea = wave_incl_scan<uint32_t>(act, t) - act;
+        const uint64_t m = __ballot(ne);
+        const uint32_t pos = (uint32_t)__popcll((unsigned long long)(m & ((1ull << t) - 1ull)));
+        if (ne) b.unit_cnt[(int64_t)blockIdx.x * kGroupUnits + pos] = make_uint4((uint32_t)t, eo, et, ea);
+        const uint32_t sums[5] = {__shfl(eo + own, 63, 64), __shfl(et + tri, 63, 64), __shfl(ea + act, 63, 64),
+                                  wave_incl_scan<uint32_t>(hal, t), (uint32_t)__popcll((unsigned long long)m)};
+        const uint32_t shal = __shfl(sums[3], 63, 64);
+        if (t < 6) {
+            const uint32_t v = t == 0 ? sums[0] : t == 1 ? sums[1] : t == 2 ? sums[2] : t == 3 ? shal : sums[4];
+            b.scan_blk[(int64_t)t * gridDim.x + blockIdx.x] = v;   // row 5: non-empty count, kept unscanned
+        }
     }
 }
 
@@ -201,7 +214,18 @@ __global__ __launch_bounds__(1024) void k_scan_groups(uint32_t* __restrict__ blk
     }
 }
 
-__global__ __launch_bounds__(64 * kVertsUnits) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+// one wave per group: its non-empty units (k_mc_count's in-group list) to their place in the
+// flat ordered list, with global bases
+__global__ __launch_bounds__(64) void k_unit_flatten(GridDesc g, MCBuffers b) {
+    const int64_t G = blockIdx.x, ng = n_groups(g);
+    const uint32_t k = threadIdx.x;
+    if (k >= b.scan_blk[5 * ng + G]) return;
+    const uint4 e = b.unit_cnt[G * kGroupUnits + k];
+    b.ulist[b.scan_blk[4 * ng + G] + k] = make_uint4((uint32_t)(G * kGroupUnits) + e.x, b.scan_blk[G] + e.y,
+                                                     b.scan_blk[ng + G] + e.z, b.scan_blk[2 * ng + G] + e.w);
+}
+
+__global__ __launch_bounds__(64 * kVertsWaves) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     mc_verts_body(cases, g, b);
 }
 
@@ -252,7 +276,10 @@ void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
 }
 
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
-    k_scan_groups<<<1, 1024, 0, s>>>(b.scan_blk, n_groups(g), b.counters);
+    const int64_t ng = n_groups(g);
+    if (ng == 0) return;
+    k_scan_groups<<<1, 1024, 0, s>>>(b.scan_blk, ng, b.counters);
+    k_unit_flatten<<<(unsigned)ng, 64, 0, s>>>(g, b);
 }
 
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
@@ -261,7 +288,9 @@ void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
 
 void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     const int64_t nu = n_units(g);
-    if (nu > 0) k_mc_verts<<<(unsigned)((nu + kVertsUnits - 1) / kVertsUnits), 64 * kVertsUnits, 0, s>>>(d_cases, g, b);
+    if (nu > 0)
+        k_mc_verts<<<(unsigned)std::min<int64_t>((nu + kVertsWaves - 1) / kVertsWaves, kVertsMaxBlocks),
+                     64 * kVertsWaves, 0, s>>>(d_cases, g, b);
 }
 
 }  // namespace impli

@@ -31,18 +31,26 @@ struct ChunkBits {
 __device__ __forceinline__ void load_chunk(const GridDesc& g, const uint64_t* __restrict__ signs, int64_t row, int c,
                                            ChunkBits& k) {
     const int rw = sign_row_words(g);
-    k.y = (int)(row % g.m) + 1;
-    k.z = (int)(row / g.m) + g.cz0;
+    const int r32 = (int)row;   // rows of a slab: m x layers < 2^31 (32-bit division)
+    k.y = r32 % g.m + 1;
+    k.z = r32 / g.m + g.cz0;
     k.x0 = 64 * c + 1;
     const int64_t r00 = ((int64_t)(k.z - g.fz0) * g.n + (k.y - 1)) * rw;   // (layer, stored y) -> word index
     const int64_t rows[4] = {r00, r00 + rw, r00 + (int64_t)g.n * rw, r00 + (int64_t)g.n * rw + rw};
-    uint64_t s[4], t[4];
+    // all eight loads issued before any use (a conditional load becomes a branch with its own
+    // wait, serialising the rows): past a row's last word the next row's first word (or the
+    // bitmap's tail padding) is read and discarded
+    uint64_t w[4], nx[4], s[4], t[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint64_t w = signs[rows[q] + c];
-        const uint64_t nx = (c + 1 < rw) ? signs[rows[q] + c + 1] : 0ull;
-        s[q] = w;
-        t[q] = (w >> 1) | (nx << 63);
+        w[q] = signs[rows[q] + c];
+        nx[q] = signs[rows[q] + c + 1];
+    }
+    const bool last = c + 1 >= rw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        s[q] = w[q];
+        t[q] = (w[q] >> 1) | ((last ? 0ull : nx[q]) << 63);
     }
     k.s00 = s[0]; k.t00 = t[0]; k.s10 = s[1]; k.t10 = t[1]; k.s01 = s[2]; k.t01 = t[2]; k.s11 = s[3]; k.t11 = t[3];
     const uint64_t all = s[0] & t[0] & s[1] & t[1] & s[2] & t[2] & s[3] & t[3];
@@ -78,128 +86,116 @@ __device__ __forceinline__ float edge_value(const GridDesc& g, const MCBuffers& 
     return (sealed_xy(g, sx) || sealed_xy(g, sy) || sealed_z(g, sl)) ? kSealed : b.field[sx + sy * g.n + sl * g.n * g.n];
 }
 
-// One block per kVertsUnits units, one wave per unit.  The unit's exclusive bases are its group's
-// (k_scan_groups) plus a scan of the group's kGroupUnits unit counts (one lane each).
+// Waves take the non-empty units of the flat list (k_unit_flatten) grid-stride, one unit at a time:
+// every resident wave gets an equal share whatever the surface's distribution over groups.
 __device__ __forceinline__ void mc_verts_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
-    static_assert(kGroupUnits == 64 && kGroupUnits % kVertsUnits == 0, "one lane per unit of the group");
     __shared__ CaseInfo s_case[256];
-    __shared__ uint32_t s_list[kVertsUnits][kListCap];   // per wave: ci | j << 8 | item << 14
-    __shared__ uint4 s_base[kVertsUnits];
+    __shared__ uint32_t s_list[kVertsWaves][kListCap];   // per wave: ci | j << 8 | item << 14
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    if (t < 256) s_case[t] = cases[t];
-    const int64_t u0 = (int64_t)blockIdx.x * kVertsUnits;
-    const int64_t nu = n_units(g);
-    if (wid == 0) {
-        const int64_t grp = u0 / kGroupUnits, ng = n_groups(g);
-        const int64_t uu = grp * kGroupUnits + lane;
-        const uint4 c = (uu < nu) ? b.unit_cnt[uu] : make_uint4(0, 0, 0, 0);
-        // 32-bit scans: a group's prefix can exceed a 16-bit pack4 field
-        const uint32_t ev = wave_incl_scan<uint32_t>(c.x, lane) - c.x;
-        const uint32_t ef = wave_incl_scan<uint32_t>(c.y, lane) - c.y;
-        const uint32_t ea = wave_incl_scan<uint32_t>(c.z, lane) - c.z;
-        const int k = lane - (int)(u0 - grp * kGroupUnits);
-        if (k >= 0 && k < kVertsUnits)
-            s_base[k] = make_uint4(b.scan_blk[grp] + ev, b.scan_blk[ng + grp] + ef, b.scan_blk[2 * ng + grp] + ea, 0u);
-    }
+    const uint32_t n_ne = b.counters[0];              // non-empty units
+    const uint32_t w0 = blockIdx.x * kVertsWaves;
+    if (w0 >= n_ne) return;                           // uniform over the block
+    for (int k = t; k < 256; k += blockDim.x) s_case[k] = cases[k];
     __syncthreads();
-    const int64_t u = u0 + wid;
-    if (u >= nu) return;
     const uint32_t H = b.counters[1];
     const int nch = (g.m + 63) / 64;
     const int64_t rows = n_rows(g);
-    const uint4 base = s_base[wid];   // exclusive {vbase, fbase, abase}
-    uint32_t vrun0 = base.x, frun0 = base.y, arun0 = base.z;
     uint32_t* list = s_list[wid];
     const int items = kUnitRows * nch;
-    for (int i0 = 0; i0 < items; i0 += 64) {
-        const int i = i0 + lane;
-        ChunkBits k;
-        k.nt = 0;
-        int64_t row = -1;
-        if (i < items) {
-            row = u * kUnitRows + i / nch;
-            if (row < rows) load_chunk(g, b.signs, row, i % nch, k);
-        }
-        const uint32_t cnt = (uint32_t)__popcll((unsigned long long)k.nt);
-        const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);
-        const uint32_t total = __shfl(incl, 63, 64);
-        for (uint32_t w0 = 0; w0 < total; w0 += kListCap) {
-            // this window's entries, in cell order
-            uint32_t pos = incl - cnt;
-            uint64_t nt = k.nt;
-            while (nt) {
-                const int j = __ffsll((unsigned long long)nt) - 1;
-                nt &= nt - 1;
-                if (pos >= w0 && pos < w0 + kListCap)
-                    list[pos - w0] = chunk_ci(k, j) | ((uint32_t)j << 8) | ((uint32_t)i << 14);
-                ++pos;
+    for (uint32_t e = w0 + wid; e < n_ne; e += gridDim.x * kVertsWaves) {
+        const uint4 ent = b.ulist[e];   // {unit, vbase, fbase, abase}
+        const int64_t u = ent.x;
+        uint32_t vrun0 = ent.y, frun0 = ent.z, arun0 = ent.w;
+        for (int i0 = 0; i0 < items; i0 += 64) {
+            const int i = i0 + lane;
+            ChunkBits k;
+            k.nt = 0;
+            int64_t row = -1;
+            if (i < items) {
+                row = u * kUnitRows + i / nch;
+                if (row < rows) load_chunk(g, b.signs, row, i % nch, k);
             }
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t n_list = (total - w0 < (uint32_t)kListCap) ? total - w0 : (uint32_t)kListCap;
-            for (uint32_t e0 = 0; e0 < n_list; e0 += 64) {
-                const uint32_t e = e0 + (uint32_t)lane;
-                const bool has = e < n_list;
-                const uint32_t ent = has ? list[e] : 0u;
-                const unsigned ci = ent & 255u;
-                const int j = (int)((ent >> 8) & 63u), it = (int)(ent >> 14);
-                const int64_t erow = u * kUnitRows + it / nch;
-                const int x = 64 * (it % nch) + 1 + j;
-                const int y = (int)(erow % g.m) + 1, z = (int)(erow / g.m) + g.cz0;
-                const uint32_t L = (uint32_t)(erow * g.m + (x - 1));
-                const CaseInfo& C = s_case[ci];
-                const bool emit = has && z >= g.cz_emit;
-                const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
-                const unsigned long long p = pack4(own, tri, act, 0u);
-                const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
-                const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
-                // ends of the owned crossing edges: corner 7 (qxyz) and 5 (qxz), 6 (qyz), 3 (qxy)
-                const int sx = x - 1, sy = y - 1, sl = z - g.fz0;   // stored coords of corner 0
-                const bool o5 = own && C.rank[0] >= 0, o6 = own && C.rank[1] >= 0, o10 = own && C.rank[2] >= 0;
-                const float f7 = own ? edge_value(g, b, sx + 1, sy + 1, sl + 1) : 0.f;
-                const float f5 = o5 ? edge_value(g, b, sx + 1, sy, sl + 1) : 0.f;
-                const float f6 = o6 ? edge_value(g, b, sx, sy + 1, sl + 1) : 0.f;
-                const float f3 = o10 ? edge_value(g, b, sx + 1, sy + 1, sl) : 0.f;
-                if (has && own) {
-                    const uint32_t vrun = vrun0 + fld(pre, 0);
-                    const float fx = ((float)x + g.i0[0]) * g.w[0];
-                    const float fy = ((float)y + g.i0[1]) * g.w[1];
-                    const float fz = ((float)z + g.i0[2]) * g.w[2];
-                    const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
-#pragma unroll
-                    for (int slot = 0; slot < 3; ++slot) {
-                        const int r = C.rank[slot];
-                        if (r < 0) continue;
-                        const uint32_t vid = vrun + (uint32_t)r;
-                        b.vid3[(size_t)L * 3 + slot] = vid - H;
-                        if (!emit) continue;
-                        const uint32_t out = vid - H;
-                        if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
-                        float px, py, pz;
-                        if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
-                            const float mu = (0.f - f5) / (f7 - f5);
-                            px = fx2; py = fy + mu * g.w[1]; pz = fz2;
-                        } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
-                            const float mu = (0.f - f6) / (f7 - f6);
-                            px = fx + mu * g.w[0]; py = fy2; pz = fz2;
-                        } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
-                            const float mu = (0.f - f3) / (f7 - f3);
-                            px = fx2; py = fy2; pz = fz + mu * g.w[2];
+            const uint32_t cnt = (uint32_t)__popcll((unsigned long long)k.nt);
+            const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);
+            const uint32_t total = __shfl(incl, 63, 64);
+            for (uint32_t w0 = 0; w0 < total; w0 += kListCap) {
+                // this window's entries, in cell order
+                uint32_t pos = incl - cnt;
+                uint64_t nt = k.nt;
+                while (nt) {
+                    const int j = __ffsll((unsigned long long)nt) - 1;
+                    nt &= nt - 1;
+                    if (pos >= w0 && pos < w0 + kListCap)
+                        list[pos - w0] = chunk_ci(k, j) | ((uint32_t)j << 8) | ((uint32_t)i << 14);
+                    ++pos;
+                }
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t n_list = (total - w0 < (uint32_t)kListCap) ? total - w0 : (uint32_t)kListCap;
+                for (uint32_t e0 = 0; e0 < n_list; e0 += 64) {
+                    const uint32_t e = e0 + (uint32_t)lane;
+                    const bool has = e < n_list;
+                    const uint32_t ent = has ? list[e] : 0u;
+                    const unsigned ci = ent & 255u;
+                    const int j = (int)((ent >> 8) & 63u), it = (int)(ent >> 14);
+                    const int64_t erow = u * kUnitRows + it / nch;
+                    const int x = 64 * (it % nch) + 1 + j;
+                    const int y = (int)erow % g.m + 1, z = (int)erow / g.m + g.cz0;
+                    const uint32_t L = (uint32_t)(erow * g.m + (x - 1));
+                    const CaseInfo& C = s_case[ci];
+                    const bool emit = has && z >= g.cz_emit;
+                    const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
+                    const unsigned long long p = pack4(own, tri, act, 0u);
+                    const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
+                    const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
+                    // ends of the owned crossing edges: corner 7 (qxyz) and 5 (qxz), 6 (qyz), 3 (qxy)
+                    const int sx = x - 1, sy = y - 1, sl = z - g.fz0;   // stored coords of corner 0
+                    const bool o5 = own && C.rank[0] >= 0, o6 = own && C.rank[1] >= 0, o10 = own && C.rank[2] >= 0;
+                    const float f7 = own ? edge_value(g, b, sx + 1, sy + 1, sl + 1) : 0.f;
+                    const float f5 = o5 ? edge_value(g, b, sx + 1, sy, sl + 1) : 0.f;
+                    const float f6 = o6 ? edge_value(g, b, sx, sy + 1, sl + 1) : 0.f;
+                    const float f3 = o10 ? edge_value(g, b, sx + 1, sy + 1, sl) : 0.f;
+                    if (has && own) {
+                        const uint32_t vrun = vrun0 + fld(pre, 0);
+                        const float fx = ((float)x + g.i0[0]) * g.w[0];
+                        const float fy = ((float)y + g.i0[1]) * g.w[1];
+                        const float fz = ((float)z + g.i0[2]) * g.w[2];
+                        const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
+    #pragma unroll
+                        for (int slot = 0; slot < 3; ++slot) {
+                            const int r = C.rank[slot];
+                            if (r < 0) continue;
+                            const uint32_t vid = vrun + (uint32_t)r;
+                            b.vid3[(size_t)L * 3 + slot] = vid - H;
+                            if (!emit) continue;
+                            const uint32_t out = vid - H;
+                            if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
+                            float px, py, pz;
+                            if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
+                                const float mu = (0.f - f5) / (f7 - f5);
+                                px = fx2; py = fy + mu * g.w[1]; pz = fz2;
+                            } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
+                                const float mu = (0.f - f6) / (f7 - f6);
+                                px = fx + mu * g.w[0]; py = fy2; pz = fz2;
+                            } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
+                                const float mu = (0.f - f3) / (f7 - f3);
+                                px = fx2; py = fy2; pz = fz + mu * g.w[2];
+                            }
+                            b.verts[3 * (size_t)out] = px;
+                            b.verts[3 * (size_t)out + 1] = py;
+                            b.verts[3 * (size_t)out + 2] = pz;
                         }
-                        b.verts[3 * (size_t)out] = px;
-                        b.verts[3 * (size_t)out + 1] = py;
-                        b.verts[3 * (size_t)out + 2] = pz;
                     }
+                    if (act) {
+                        const uint32_t arun = arun0 + fld(pre, 2);
+                        if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
+                        else *b.overflow = 1u;
+                    }
+                    vrun0 += fld(tot, 0);
+                    frun0 += fld(tot, 1);
+                    arun0 += fld(tot, 2);
                 }
-                if (act) {
-                    const uint32_t arun = arun0 + fld(pre, 2);
-                    if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
-                    else *b.overflow = 1u;
-                }
-                vrun0 += fld(tot, 0);
-                frun0 += fld(tot, 1);
-                arun0 += fld(tot, 2);
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
         }
     }
 }

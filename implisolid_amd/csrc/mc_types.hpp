@@ -20,14 +20,17 @@ static_assert(sizeof(CaseInfo) == 32, "CaseInfo layout");
 // kUnitRows consecutive rows (contiguous in linear order), processed by one wave.
 constexpr int kUnitRows = 4;
 constexpr int kGroupUnits = 64;        // units per group: one count block; the group scan's element
-constexpr int kVertsUnits = 16;        // units per verts block (one wave each)
+constexpr int kVertsWaves = 4;         // waves per verts block (grid-stride over the unit list)
+constexpr int kVertsMaxBlocks = 2048;  // verts grid: ~ the resident waves of the chip
 constexpr int kTopPT = 2;              // groups per lane in one pass of the group scan
 struct MCBuffers {
     const float* field;
     const uint64_t* signs;   // sign bitmap of the stored samples (grid.hpp)
-    uint4* unit_cnt;         // per unit {own, tri, act, halo own}
-    uint32_t* scan_blk;      // [5][n_groups]: group sums (own, tri, act, halo own, non-empty units), then exclusive bases
-    uint32_t* counters;      // [0] unused, [1] halo own, [2..5] totals own/tri/act/halo
+    uint4* unit_cnt;         // per group, its non-empty units {unit in group, own, tri, act bases} (k_mc_count)
+    uint32_t* scan_blk;      // [6][n_groups]: group sums (own, tri, act, halo own, non-empty units), then
+                             // exclusive bases; row 5: non-empty units (unscanned)
+    uint4* ulist;            // all non-empty units in order: {unit, vbase, fbase, abase} (k_unit_flatten)
+    uint32_t* counters;      // [0] non-empty units, [1] halo own, [2..5] totals own/tri/act/halo
     uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
     uint4* records;          // active cells: {L, ci, fbase, 0}
     float* verts;            // 3 * cap_v
