@@ -6,10 +6,13 @@ config 3's seeded 21-node MP5 CSG tree at R = 512 over the box [-1, 1]^3.  One s
 evaluation of the (R+1)^3 stored samples + marching-cubes count / scan / vertex + face emission,
 with the mesh left resident in HBM (no host copy in the timed region).
 
-N > 1 (torchrun, one process per GPU, RCCL): the cell layers are split into Z-slabs (strong
-scaling, total work fixed).  Each rank recomputes one halo cell layer below its slab; the only
-exchange is an all-gather of the per-slab (vertex, face) counts, which gives every rank its global
-numbering offsets on the device.  The result is byte-identical to one GPU (tests/).
+N > 1 (torchrun, one process per GPU, RCCL): the cell layers are split into Z-slabs.  Weak scaling
+(the default): the grid grows to R_N = R N^(1/3), so every rank's slab holds about R^3 voxels -- the
+one-GPU workload per GPU (R_8 = 1024: 1024 x 1024 x 128 per rank).  Each rank recomputes one halo
+cell layer below its slab; the only exchange is an all-gather of the per-slab (vertex, face) counts,
+which gives every rank its global numbering offsets on the device.  The result is byte-identical
+to one GPU (tests/).  The strong-scaling rate (the R grid itself over N ranks) is reported beside it
+("strong"); --strong makes it the headline value.
 
 Prints ONE JSON line (rank 0).  Extra fields: per-kernel times from HIP events on the launch
 stream, the HBM roofline of the eval+MC kernel sequence (SURVEY.md 8d's algorithmic bytes), and
@@ -77,6 +80,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-256", action="store_true", help="do not also time R=256")
     ap.add_argument("--prune", type=int, default=None, help="pruning level 0/1/2 (default: library default 2)")
+    ap.add_argument("--strong", action="store_true", help="N > 1: the headline is strong scaling of the R grid")
     args = ap.parse_args()
 
     import torch
@@ -92,10 +96,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    torch.cuda.set_device(local)
+    # one GPU per rank; IMPLISOLID_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs
+    backend = os.environ.get("IMPLISOLID_DIST_BACKEND", "nccl")
+    dev_index = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
@@ -103,7 +113,7 @@ def main():
         shape, mc = scene if scene is not None else scenes.config4(R)
         slab = I.Slab(shape, mc, rank, world)
         cnt = torch.zeros(4, dtype=torch.int32, device=dev)
-        offs = torch.zeros(2, dtype=torch.int32, device=dev)
+        gath = torch.zeros(world, 4, dtype=torch.int32, device=dev)
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
 
         def step(e=None):
@@ -113,9 +123,14 @@ def main():
             slab.count(sp)
             if e: e[2].record(stream)
             if world > 1:
+                # the 16 B/rank count all-gather runs while the vertex pass (slab-local ids) does;
+                # the face pass forms this slab's vertex offset from the gathered counts
                 slab.copy_counts(cnt.data_ptr(), sp)
-                D.global_offsets(cnt, rank, world, out=offs)
-                slab.emit(offs.data_ptr(), sp)
+                work = D.gather_counts_async(cnt, gath)
+                slab.emit_verts(sp)
+                if work is not None:
+                    work.wait()
+                slab.emit_faces(0, gath.data_ptr(), rank, sp)
             else:
                 slab.emit(0, sp)
             if e: e[3].record(stream)
@@ -164,10 +179,13 @@ def main():
         slab.close()
         return info
 
-    main_run = run(args.resolution, args.steps, args.warmup)
-    r256 = run(256, args.steps, args.warmup) if (not args.skip_256 and args.resolution != 256) else None
+    weak = world > 1 and not args.strong
+    R_main = int(round(args.resolution * world ** (1.0 / 3.0))) if weak else args.resolution
+    main_run = run(R_main, args.steps, args.warmup)
+    strong_run = run(args.resolution, args.steps, args.warmup) if weak else None
+    r256 = run(256, args.steps, args.warmup) if (not args.skip_256 and args.resolution != 256 and world == 1) else None
     # a dense-surface data point: config 2's scene (sphere u rabbit, ~1.5 M vertices) at the same R
-    rdense = None if args.skip_256 else run(args.resolution, args.steps, args.warmup,
+    rdense = None if (args.skip_256 or world > 1) else run(args.resolution, args.steps, args.warmup,
                                            scene=(scenes.union_sphere_cube(), scenes.mc_settings(args.resolution, 1.0)))
 
     if rank != 0:
@@ -196,7 +214,8 @@ def main():
     # events, 5 extra steps) are reported beside it; the field kernel alone is priced by nothing:
     # it stores exact values only for the listed bricks (the rest are sign-filled), so it is bound
     # by VALU work on those bricks, not by HBM.
-    b_pipe = 8.0 * (R + 1) ** 3 + 12.0 * nv + 12.0 * nf
+    # per GPU: the job's bytes over N ranks, over rank 0's kernel time
+    b_pipe = (8.0 * (R + 1) ** 3 + 12.0 * nv + 12.0 * nf) / world
     t_kern = sum(kms.values()) * 1e-3
     dom = max(kern, key=kern.get)
     traffic = None
@@ -217,16 +236,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
         "config": {
             "workload": "config4: seeded 21-node MP5 CSG tree (scenes.config4, seed 20251015), box [-1,1]^3, "
-                        "R=%d, eval+MC, mesh resident in HBM" % R,
+                        "R=%d, eval+MC, mesh resident in HBM%s" % (
+                            R, (", weak scaling: R = %d N^(1/3), ~%d^3 voxels per rank" % (args.resolution, args.resolution))
+                            if weak else ""),
             "resolution": R, "voxels": R ** 3, "samples": (R + 1) ** 3, "cells": (R + 2) ** 3,
             "verts": nv, "faces": nf, "program_instr": n_instr, "tree_depth": depth,
             "parallelism": "zslab%d" % world,
+            "voxels_per_rank": R ** 3 // world,
         },
         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
         "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
@@ -240,6 +262,10 @@ def main():
                      "dominant_kernel": dom,
                      "kernel_share": {k: round(v / max(1e-9, sum(kern.values())), 3) for k, v in kern.items()}},
     }
+    if strong_run:
+        mss = strong_run["elapsed"] / args.steps * 1e3
+        out["strong"] = {"resolution": args.resolution, "value": round(args.resolution ** 3 / (mss * 1e-3) / 1e6, 2),
+                         "ms_per_step": round(mss, 4), "scaling": "strong"}
     if rdense:
         msd = rdense["elapsed"] / args.steps * 1e3
         out["value_union_scene"] = round(R ** 3 / (msd * 1e-3) / 1e6, 2)

@@ -26,7 +26,7 @@ ABI_SYMBOLS = [
     "get_gradients_size", "get_pointset_ptr", "get_pointset_size", "about", "implisolid_last_error",
     "implisolid_set_error_mode", "implisolid_eval_points", "implisolid_program_info",
     "implisolid_slab_create", "implisolid_slab_destroy", "implisolid_slab_eval", "implisolid_slab_count",
-    "implisolid_slab_emit", "implisolid_slab_counters", "implisolid_slab_counts", "implisolid_slab_grid",
+    "implisolid_slab_emit", "implisolid_slab_emit_verts", "implisolid_slab_emit_faces", "implisolid_slab_counters", "implisolid_slab_counts", "implisolid_slab_grid",
     "implisolid_slab_verts", "implisolid_slab_faces", "implisolid_slab_field", "implisolid_slab_set_offsets",
     "implisolid_slab_download", "implisolid_slab_copy_counts", "implisolid_slab_read_field", "implisolid_set_pruning",
     "implisolid_parse_settings", "implisolid_slab_partition", "implisolid_slab_brick_stats",
@@ -79,6 +79,8 @@ def lib():
         "implisolid_slab_eval": ([c_void_p, c_void_p], c_int),
         "implisolid_slab_count": ([c_void_p, c_void_p], c_int),
         "implisolid_slab_emit": ([c_void_p, c_void_p, c_void_p], c_int),
+        "implisolid_slab_emit_verts": ([c_void_p, c_void_p], c_int),
+        "implisolid_slab_emit_faces": ([c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
         "implisolid_slab_counters": ([c_void_p], c_void_p),
         "implisolid_slab_counts": ([c_void_p, c_void_p, up], c_int),
         "implisolid_slab_grid": ([c_void_p, ip], c_int),
@@ -301,6 +303,16 @@ class Slab:
 
     def emit(self, d_offsets=0, stream=0):
         self._rc(lib().implisolid_slab_emit(self.h, ctypes.c_void_p(d_offsets or None), ctypes.c_void_p(stream)))
+
+    def emit_verts(self, stream=0):
+        """vertex pass alone (slab-local ids, no offsets needed)"""
+        self._rc(lib().implisolid_slab_emit_verts(self.h, ctypes.c_void_p(stream)))
+
+    def emit_faces(self, d_offsets=0, d_gathered=0, rank=0, stream=0):
+        """face pass: offsets from device [Voff, Foff], or from every rank's gathered counts"""
+        self._rc(lib().implisolid_slab_emit_faces(self.h, ctypes.c_void_p(d_offsets or None),
+                                                  ctypes.c_void_p(d_gathered or None), int(rank),
+                                                  ctypes.c_void_p(stream)))
 
     def counters_ptr(self):
         return lib().implisolid_slab_counters(self.h)

@@ -411,6 +411,13 @@ int implisolid_slab_count(implisolid_slab* s, void* stream) { SLAB_TRY(s->engine
 int implisolid_slab_emit(implisolid_slab* s, const uint32_t* d_offsets, void* stream) {
     SLAB_TRY(s->engine.emit(d_offsets, (hipStream_t)stream))
 }
+int implisolid_slab_emit_verts(implisolid_slab* s, void* stream) {
+    SLAB_TRY(s->engine.emit_verts((hipStream_t)stream))
+}
+int implisolid_slab_emit_faces(implisolid_slab* s, const uint32_t* d_offsets, const uint32_t* d_gathered, int rank,
+                               void* stream) {
+    SLAB_TRY(s->engine.emit_faces(d_offsets, d_gathered, rank, (hipStream_t)stream))
+}
 const uint32_t* implisolid_slab_counters(implisolid_slab* s) { return s->engine.d_counters(); }
 int implisolid_slab_counts(implisolid_slab* s, void* stream, uint32_t out[3]) {
     try {

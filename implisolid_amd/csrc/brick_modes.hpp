@@ -58,34 +58,40 @@ __device__ __forceinline__ BrickBox brick_box(const GridDesc& g, int bx, int by,
     return BrickBox{x0, imin(x0 + kBX - 1, g.n - 1), y0, imin(y0 + kBY - 1, g.n - 1), z0, imin(z0 + zlen - 1, layers - 1)};
 }
 
-// class of brick (bx, by, bz): a sign-definite coarse box's class (sealed-adjusted for the
-// brick), or the refined class of a brick of a mixed box
-__device__ __forceinline__ uint32_t brick_class(const GridDesc& g, const BrickGrid& bg, const BrickGrid& cg,
-                                                const uint8_t* __restrict__ ccls, const uint8_t* __restrict__ cls,
-                                                int bx, int by, int bz) {
-    const uint8_t c = ccls[bx + by * cg.nbx + (bz / kCZ) * cg.nbx * cg.nby];
-    if (c == kBrickMixed) return cls[bx + by * bg.nbx + bz * bg.nbx * bg.nby];
+// class of brick (bx, by, bz) from its coarse box's class c and its refined class r: the
+// sign-definite box's class (sealed-adjusted for the brick), or r for a brick of a mixed box
+__device__ __forceinline__ uint32_t brick_class_of(const GridDesc& g, uint8_t c, uint8_t r, int bx, int by, int bz) {
     const BrickBox q = brick_box(g, bx, by, bz, kBZ);
-    return sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
+    return c == kBrickMixed ? (uint32_t)r : (uint32_t)sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
 }
 
-// A brick needs exact values only if one of its samples can be the end of a sign-changing cell
-// edge.  Edges are axis aligned, so that requires the brick or a face neighbour to differ in
-// sign class.  Neighbours outside the stored grid hold no sample any cell of this slab reads.
-// c = the brick's own class (brick_class).
+// The brick's class and its fill class.  A brick needs exact values only if one of its samples can
+// be the end of a sign-changing cell edge.  Edges are axis aligned, so that requires the brick or
+// a face neighbour to differ in sign class.  Neighbours outside the stored grid hold no sample any
+// cell of this slab reads (clamped to the brick itself).  All fourteen class bytes are loaded
+// before any is used: a lookup behind the previous one's branches would wait on its own.
 __device__ __forceinline__ uint32_t brick_fill_class(const GridDesc& g, const BrickGrid& bg, const BrickGrid& cg,
                                                      const uint8_t* __restrict__ ccls, const uint8_t* __restrict__ cls,
-                                                     uint32_t c, int bx, int by, int bz) {
-    if ((c & 3u) == kBrickMixed || (c & kBrickNoFill)) return kBrickMixed;
-    c &= 3u;
+                                                     int bx, int by, int bz, uint32_t& own_class) {
+    const int X[7] = {bx, bx > 0 ? bx - 1 : bx, bx + 1 < bg.nbx ? bx + 1 : bx, bx, bx, bx, bx};
+    const int Y[7] = {by, by, by, by > 0 ? by - 1 : by, by + 1 < bg.nby ? by + 1 : by, by, by};
+    const int Z[7] = {bz, bz, bz, bz, bz, bz > 0 ? bz - 1 : bz, bz + 1 < bg.nbz ? bz + 1 : bz};
+    uint8_t c[7], r[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        c[k] = ccls[X[k] + Y[k] * cg.nbx + (Z[k] / kCZ) * cg.nbx * cg.nby];
+        r[k] = cls[X[k] + Y[k] * bg.nbx + Z[k] * bg.nbx * bg.nby];   // stale unless the box is mixed
+    }
+    uint32_t n[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) n[k] = brick_class_of(g, c[k], r[k], X[k], Y[k], Z[k]);
+    own_class = n[0];
+    if ((n[0] & 3u) == kBrickMixed || (n[0] & kBrickNoFill)) return kBrickMixed;
+    const uint32_t cc = n[0] & 3u;
     bool same = true;
-    if (bx > 0) same &= (brick_class(g, bg, cg, ccls, cls, bx - 1, by, bz) & 3u) == c;
-    if (bx + 1 < bg.nbx) same &= (brick_class(g, bg, cg, ccls, cls, bx + 1, by, bz) & 3u) == c;
-    if (by > 0) same &= (brick_class(g, bg, cg, ccls, cls, bx, by - 1, bz) & 3u) == c;
-    if (by + 1 < bg.nby) same &= (brick_class(g, bg, cg, ccls, cls, bx, by + 1, bz) & 3u) == c;
-    if (bz > 0) same &= (brick_class(g, bg, cg, ccls, cls, bx, by, bz - 1) & 3u) == c;
-    if (bz + 1 < bg.nbz) same &= (brick_class(g, bg, cg, ccls, cls, bx, by, bz + 1) & 3u) == c;
-    return same ? c : (uint32_t)kBrickMixed;
+#pragma unroll
+    for (int k = 1; k < 7; ++k) same &= (n[k] & 3u) == cc;
+    return same ? cc : (uint32_t)kBrickMixed;
 }
 
 // Coarse pass: one thread per coarse box -> modes, sign class; mixed boxes are listed.

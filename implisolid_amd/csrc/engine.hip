@@ -257,11 +257,27 @@ void Engine::count(hipStream_t s) {
 }
 
 void Engine::emit(const uint32_t* d_offsets, hipStream_t s) {
+    emit_verts(s);
+    emit_faces(d_offsets, nullptr, 0, s);
+}
+
+void Engine::emit_verts(hipStream_t s) {   // vertex positions and ids are slab-local: no offsets
     MCBuffers b = buffers();
-    b.offsets = d_offsets ? d_offsets : offsets_.as<uint32_t>();
     mark(6, s);
     launch_mc_verts(cases_.as<CaseInfo>(), grid_, b, s);
     mark(7, s);
+    IMPLI_HIP(hipGetLastError());
+}
+
+void Engine::emit_faces(const uint32_t* d_offsets, const uint32_t* d_gathered, int rank, hipStream_t s) {
+    MCBuffers b = buffers();
+    if (d_gathered) {
+        b.offsets = nullptr;
+        b.gathered = d_gathered;
+        b.rank = rank;
+    } else {
+        b.offsets = d_offsets ? d_offsets : offsets_.as<uint32_t>();
+    }
     launch_mc_faces(cases_.as<CaseInfo>(), grid_, b, s);
     mark(8, s);
     IMPLI_HIP(hipGetLastError());

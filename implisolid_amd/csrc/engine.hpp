@@ -48,6 +48,9 @@ public:
     void eval_field(hipStream_t stream);
     void count(hipStream_t stream);                           // K2 + scan
     void emit(const uint32_t* d_offsets, hipStream_t stream); // K3 + K4 (offsets: [Voff, Foff] or null)
+    void emit_verts(hipStream_t stream);                       // K3 alone (needs no offsets)
+    // K4 alone; d_gathered (all ranks' copy_counts, uint32[world][4]) gives Voff on the device
+    void emit_faces(const uint32_t* d_offsets, const uint32_t* d_gathered, int rank, hipStream_t stream);
     // host-side offsets used when emit() gets no device offsets
     void set_offsets(uint32_t voff, uint32_t foff);
     // blocking copy of this slab's emitted mesh

@@ -95,9 +95,9 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __rest
 // Per brick: its class (inherited from a sign-definite coarse box, or refined), the neighbour rule
 // (brick_fill_class), fill[b] = class | fill class << 4, and either the constant sign pieces of a
 // sign-filled brick or an entry in the list of bricks to evaluate (with its modes, so the eval
-// kernel reads them in list order).  List appends are aggregated per block: one atomic per 1024
+// kernel reads them in list order).  List appends are aggregated per block: one atomic per 256
 // bricks.
-constexpr int kFillBlock = 1024;
+constexpr int kFillBlock = 256;
 __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid bg, BrickGrid cg,
                                                            const uint8_t* __restrict__ ccls,
                                                            const uint64_t* __restrict__ cmodes,
@@ -115,8 +115,9 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
     if (valid) {
         brick_of(b, bg, bx, by, bz);
         cb = bx + by * cg.nbx + (bz / kCZ) * cg.nbx * cg.nby;
-        const uint32_t c = brick_class(g, bg, cg, ccls, cls, bx, by, bz);
-        fc = sign_fill ? brick_fill_class(g, bg, cg, ccls, cls, c, bx, by, bz) : (uint32_t)kBrickMixed;
+        uint32_t c;
+        fc = brick_fill_class(g, bg, cg, ccls, cls, bx, by, bz, c);
+        if (!sign_fill) fc = kBrickMixed;
         fill[b] = (uint8_t)(c | (fc << 4));
     }
     const bool eval = valid && fc == kBrickMixed;
@@ -133,7 +134,8 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
     if (eval) {
         const uint32_t i = wbase[w] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
         list[i] = (uint32_t)b;
-        lmodes[i] = (ccls[cb] == kBrickMixed) ? modes[b] : cmodes[cb];
+        const uint64_t mb = modes[b], mc = cmodes[cb];   // both loaded: no branch around a load
+        lmodes[i] = (ccls[cb] == kBrickMixed) ? mb : mc;
     } else if (valid) {   // sign-filled: constant pieces (all samples of the brick share the sign)
         const sign_piece_t piece = fc == kBrickNeg ? (sign_piece_t)~(sign_piece_t)0 : (sign_piece_t)0;
         const int layers = g.fz1 - g.fz0, row_pieces = (64 / kBX) * sign_row_words(g);

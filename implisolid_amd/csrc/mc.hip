@@ -81,8 +81,8 @@ void build_case_table(CaseInfo out[256]) {
 
 namespace {
 
-// K2: one block per group of kGroupUnits units; one lane per item (row, 64-cell chunk) of the
-// group, so every lane has work (a wave per unit would leave 64 - 4 nch lanes idle).  Only
+// K2: one block per group of kGroupUnits units; lanes take the group's items (row, 64-cell chunk)
+// round robin, so every lane has work (a wave per unit would leave 64 - 4 nch lanes idle).  Only
 // non-trivial cells (~1 %) look at the triangle table.  Per-unit sums through LDS atomics.
 //   -> unit_cnt[64 group + k] = k-th non-empty unit of the group {unit in group, own / tri / act
 //      exclusive bases in the group}; scan_blk[c][group] = the group's sums (c < 5: own, tri, act,
@@ -97,18 +97,33 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
     const int nch = (g.m + 63) / 64;
     const int64_t rows = n_rows(g), nu = n_units(g);
     const int64_t row0 = (int64_t)blockIdx.x * kGroupUnits * kUnitRows;
-    for (int i = t; i < kGroupUnits * kUnitRows * nch; i += nt_) {
-        const int r = i / nch;
-        const int64_t row = row0 + r;
-        unsigned own = 0, tri = 0, act = 0, hal = 0;
-        if (row < rows) {
-            ChunkBits k;
-            load_chunk(g, b.signs, row, i - r * nch, k);
+    // a lane's items are loaded together (kCountBatch at a time), then counted: one memory round
+    // trip per batch instead of one per item
+    constexpr int kCountBatch = 3;
+    const int n_items = kGroupUnits * kUnitRows * nch;
+    for (int i0 = t; i0 < n_items; i0 += kCountBatch * nt_) {
+        ChunkBits kb[kCountBatch];
+        int rb[kCountBatch];
+#pragma unroll
+        for (int q = 0; q < kCountBatch; ++q) {
+            // out-of-range items read a valid chunk (clamped) and drop it: no branch around loads
+            const int i = i0 + q * nt_;
+            const bool ok = i < n_items && row0 + i / nch < rows;
+            const int ic = ok ? i : 0;
+            rb[q] = ic / nch;
+            load_chunk(g, b.signs, row0 + rb[q], ic - rb[q] * nch, kb[q]);
+            if (!ok) kb[q].nt = 0;
+        }
+#pragma unroll
+        for (int q = 0; q < kCountBatch; ++q) {
+            const ChunkBits& k = kb[q];
+            if (!k.nt) continue;
             // owned vertices = crossing owned edges (build_case_table checks the identity):
             // edge 5 = corners 5-6 (t01, t11), 6 = 6-7 (t11, s11), 10 = 2-6 (t10, t11)
-            own = (unsigned)(__popcll((unsigned long long)((k.t01 ^ k.t11) & k.nt)) +
-                             __popcll((unsigned long long)((k.s11 ^ k.t11) & k.nt)) +
-                             __popcll((unsigned long long)((k.t10 ^ k.t11) & k.nt)));
+            const unsigned own = (unsigned)(__popcll((unsigned long long)((k.t01 ^ k.t11) & k.nt)) +
+                                            __popcll((unsigned long long)((k.s11 ^ k.t11) & k.nt)) +
+                                            __popcll((unsigned long long)((k.t10 ^ k.t11) & k.nt)));
+            unsigned tri = 0, act = 0, hal = 0;
             if (k.z >= g.cz_emit) {
                 act = (unsigned)__popcll((unsigned long long)k.nt);   // every non-trivial case has a triangle
                 uint64_t nt = k.nt;
@@ -120,10 +135,8 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
             } else {
                 hal = own;
             }
-        }
-        if (own | tri) {
-            uint32_t* d = s_u[r / kUnitRows];
-            atomicAdd(&d[0], own);
+            uint32_t* d = s_u[rb[q] / kUnitRows];
+            if (own) atomicAdd(&d[0], own);
             if (tri) { atomicAdd(&d[1], tri); atomicAdd(&d[2], act); }
             if (hal) atomicAdd(&d[3], hal);
         }
@@ -249,7 +262,9 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
     __syncthreads();
     const uint32_t n_rec = b.counters[4];
     const uint32_t lim = n_rec < (uint64_t)b.cap_rec ? n_rec : (uint32_t)b.cap_rec;
-    const uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
+    uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
+    if (b.gathered)
+        for (int r = 0; r < b.rank; ++r) Voff += b.gathered[4 * r] - b.gathered[4 * r + 3];
     for (uint32_t i = blockIdx.x * 256 + t; i < lim; i += gridDim.x * 256) {
         const uint4 r = b.records[i];
         const uint32_t L = r.x, ci = r.y, fbase = r.z;
@@ -270,6 +285,7 @@ void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
     const int64_t ng = n_groups(g);
     if (ng == 0) return;
     // one lane per item of a group (kGroupUnits kUnitRows rows x nch chunks), whole waves, <= 1024
+    // (256-lane blocks with 9 items per lane measured slower: 34 vs 28 us at 512^3)
     const int items = kGroupUnits * kUnitRows * ((g.m + 63) / 64);
     const unsigned threads = (unsigned)std::min(1024, (items + 63) / 64 * 64);
     k_mc_count<<<(unsigned)ng, threads, 0, s>>>(d_cases, g, b);

@@ -46,11 +46,13 @@ __device__ __forceinline__ void load_chunk(const GridDesc& g, const uint64_t* __
         w[q] = signs[rows[q] + c];
         nx[q] = signs[rows[q] + c + 1];
     }
-    const bool last = c + 1 >= rw;
+    // arithmetic mask, not a select: a select of a loaded value is turned back into a load under
+    // a branch
+    const uint64_t keep = 0ull - (uint64_t)(c + 1 < rw);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         s[q] = w[q];
-        t[q] = (w[q] >> 1) | ((last ? 0ull : nx[q]) << 63);
+        t[q] = (w[q] >> 1) | ((nx[q] & keep) << 63);
     }
     k.s00 = s[0]; k.t00 = t[0]; k.s10 = s[1]; k.t10 = t[1]; k.s01 = s[2]; k.t01 = t[2]; k.s11 = s[3]; k.t11 = t[3];
     const uint64_t all = s[0] & t[0] & s[1] & t[1] & s[2] & t[2] & s[3] & t[3];

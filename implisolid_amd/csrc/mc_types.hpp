@@ -36,7 +36,9 @@ struct MCBuffers {
     float* verts;            // 3 * cap_v
     int32_t* faces;          // 3 * cap_f
     int64_t cap_v, cap_f, cap_rec;
-    const uint32_t* offsets; // device [Voff, Foff] of this slab in the global numbering
+    const uint32_t* offsets; // device [Voff, Foff] of this slab in the global numbering, or
+    const uint32_t* gathered;  // the all-gathered counts uint32[rank+][4] of the slabs (copy_counts
+    int rank;                  // layout): Voff = sum over lower ranks of (own incl. halo - halo)
     uint32_t* overflow;      // set to 1 if a capacity was exceeded
 };
 __host__ __device__ inline int64_t n_rows(const GridDesc& g) { return (int64_t)g.m * (g.cz1 - g.cz0); }

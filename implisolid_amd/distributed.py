@@ -24,6 +24,18 @@ def gather_counts(local_counts, world, group=None):
     return out
 
 
+def gather_counts_async(local_counts, out, group=None):
+    """Start the all-gather of the per-rank counts into `out` (int32[world, 4], rank order);
+    returns a work handle (wait() orders the caller's stream after it) or None when the backend
+    completed it synchronously.  The face pass reads `out` directly (Slab.emit_faces
+    d_gathered), so the vertex pass can run while the gather is in flight."""
+    if dist.get_backend(group) == "gloo":
+        parts = list(out.unbind(0))
+        dist.all_gather(parts, local_counts, group=group)
+        return None
+    return dist.all_gather_into_tensor(out, local_counts, group=group, async_op=True)
+
+
 def offsets_from_counts(gathered, rank, out=None):
     """Exclusive prefix over ranks: int32 [vertex offset, face offset] for `rank` (on device)."""
     v = gathered[:, 0] - gathered[:, 3]

@@ -117,6 +117,13 @@ int implisolid_slab_count(implisolid_slab* s, void* stream);           /* counts
 /* d_offsets: device uint32[2] = this slab's {vertex, face} offset in the global numbering, or NULL
    for the host-set offsets (implisolid_slab_set_offsets, default 0) */
 int implisolid_slab_emit(implisolid_slab* s, const uint32_t* d_offsets, void* stream);
+/* emit in two halves, so that the count all-gather can overlap the vertex pass: verts needs no
+   offsets (slab-local ids); faces takes d_offsets as above, or d_gathered = every rank's
+   copy_counts (device uint32[nranks][4], rank order) and this slab's rank, from which it forms
+   its vertex offset on the device */
+int implisolid_slab_emit_verts(implisolid_slab* s, void* stream);
+int implisolid_slab_emit_faces(implisolid_slab* s, const uint32_t* d_offsets, const uint32_t* d_gathered, int rank,
+                               void* stream);
 /* device uint32[16]: [2] owned verts incl. halo, [3] faces, [4] active cells, [5] halo verts */
 const uint32_t* implisolid_slab_counters(implisolid_slab* s);
 /* blocking: out[0] = vertices, out[1] = faces of this slab, out[2] = overflow flag; grows the

@@ -24,6 +24,13 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def impli():
+    # torch ships its own HIP runtime under the same soname: let it load (and initialise) first so
+    # both share one runtime, as in bench.py -- the other order leaves torch without devices
+    try:
+        import torch
+        torch.cuda.is_available()
+    except Exception:
+        pass
     import implisolid_amd as I
     if not os.path.exists(I.LIB_PATH):
         I.build()

@@ -286,8 +286,16 @@ def _gloo_worker(rank, world, port, q):
         # places its first owned vertex / first face
         exp_v = int((oz < z0).sum())
         exp_f = int((ci_layers < z0).sum())
+        # the bench's path: async gather into a [world, 4] buffer; the face kernel's vertex offset
+        # is the sum over lower ranks of (own incl. halo - halo) (mc.hip k_mc_faces)
+        g2 = torch.zeros(world, 4, dtype=torch.int32)
+        work = D.gather_counts_async(cnt, g2)
+        if work is not None:
+            work.wait()
+        voff_dev = int(sum(int(g2[r, 0]) - int(g2[r, 3]) for r in range(rank)))
         ok = (int(offs[0]) == exp_v and int(offs[1]) == exp_f and int(gathered[:, 1].sum()) == len(f)
-              and int((gathered[:, 0] - gathered[:, 3]).sum()) == len(v))
+              and int((gathered[:, 0] - gathered[:, 3]).sum()) == len(v) and torch.equal(g2, gathered)
+              and voff_dev == exp_v)
         q.put((rank, ok, [int(offs[0]), int(offs[1])], [exp_v, exp_f]))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent

@@ -191,6 +191,36 @@ def test_zslab_split_identical(impli, oracle, nranks):
     assert np.array_equal(v.view(np.uint32), ref_v.view(np.uint32))
 
 
+@pytest.mark.parametrize("nranks", [2, 5])
+def test_zslab_gathered_counts_identical(impli, oracle, nranks):
+    """The multi-GPU step's emit path: vertex pass, then the face pass taking its vertex offset
+    from every slab's gathered counts on the device == single GPU."""
+    import torch
+    from implisolid_amd import scenes
+    shape, mc = scenes.config3(64)[0], scenes.mc_settings(64, 1.0)
+    ref_v, ref_f = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    slabs = [impli.Slab(shape, mc, r, nranks) for r in range(nranks)]
+    gath = torch.zeros(nranks, 4, dtype=torch.int32, device="cuda")
+    for r, s in enumerate(slabs):
+        s.eval()
+        s.count()
+        s.counts()   # sizes the output buffers
+        s.copy_counts(gath[r].data_ptr())
+    torch.cuda.synchronize()
+    vs, fs = [], []
+    for r, s in enumerate(slabs):
+        s.emit_verts()
+        s.emit_faces(0, gath.data_ptr(), r)
+        nv, nf, of = s.counts()
+        assert not of
+        v, f = s.download(nv, nf)
+        vs.append(v)
+        fs.append(f)
+        s.close()
+    assert np.array_equal(np.concatenate(fs), ref_f)
+    assert np.array_equal(np.concatenate(vs).view(np.uint32), ref_v.view(np.uint32))
+
+
 def _ob02_compare(impli, oracle, shape, mc, exact=True):
     v, f = impli.make_geometry(shape, mc)
     vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
