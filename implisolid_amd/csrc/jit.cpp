@@ -4,6 +4,8 @@
 #include <hip/hiprtc.h>
 
 #include <chrono>
+#include <cmath>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
@@ -72,8 +74,64 @@ const char* prim_call(int t) {
     }
 }
 
+// One row of xform() (matrix_vector_product, basic_functions.hpp:140-177):
+//     ((m0 x + m1 y) + m2 z) + m3
+// specialised on the row's pattern, its values staying data (M + i).  Exact whatever the inputs:
+//   - a coefficient equal to 0 contributes a zero: dropping it can only change the sign of an
+//     intermediate zero, and the row's final + m3 (kept) gives the same result unless m3 is -0
+//     (then the full expression is emitted);
+//   - 1 * v == v exactly;
+//   - an identity row (only 1 * v, m3 == +0) is v itself: coordinates are never -0 (sample
+//     coordinates are a - b differences, every emitted row ends with + m3 != -0), so v + 0 == v.
+std::string xform_row(const float* m, int base, const std::string& x, const std::string& y, const std::string& z) {
+    const std::string v[3] = {x, y, z};
+    auto is_bits = [](float f, uint32_t b) { uint32_t u; std::memcpy(&u, &f, 4); return u == b; };
+    const float t = m[3];
+    auto at = [&](int k) { return "M[" + std::to_string(base + k) + "]"; };
+    if (is_bits(t, 0x80000000u) || !std::isfinite(t))   // -0 (or non-finite) translation: generic
+        return "((" + at(0) + " * " + x + " + " + at(1) + " * " + y + ") + " + at(2) + " * " + z + ") + " + at(3);
+    std::vector<std::string> terms;
+    int ones = 0;
+    for (int k = 0; k < 3; ++k) {
+        if (!std::isfinite(m[k])) return "((" + at(0) + " * " + x + " + " + at(1) + " * " + y + ") + " + at(2) + " * " + z + ") + " + at(3);
+        if (m[k] == 0.f) continue;
+        if (m[k] == 1.f) { terms.push_back(v[k]); ++ones; }
+        else terms.push_back(at(k) + " * " + v[k]);
+    }
+    if (terms.size() == 1 && ones == 1 && is_bits(t, 0u)) return terms[0];   // identity row
+    std::string e;
+    for (size_t k = 0; k < terms.size(); ++k) e = k == 0 ? terms[0] : "(" + e + " + " + terms[k] + ")";
+    return terms.empty() ? "(0.f + " + at(3) + ")" : "(" + e + " + " + at(3) + ")";
+}
+
+// The interval row of xform_iv() (ifunc_interval.hpp), specialised like xform_row(): mulc(v, 1)
+// is v, a zero coefficient adds a [+-0, +-0] term (only zero endpoint signs can differ, which no
+// decision or class depends on), the final ivc(m3) and settle_point stay; an identity row is v.
+std::string xform_iv_row(const float* m, int base, const std::string& p) {
+    const std::string v[3] = {p + ".x", p + ".y", p + ".z"};
+    auto is_bits = [](float f, uint32_t b) { uint32_t u; std::memcpy(&u, &f, 4); return u == b; };
+    auto at = [&](int k) { return "M[" + std::to_string(base + k) + "]"; };
+    const std::string generic = "settle_point(add(add(add(mulc(" + v[0] + ", " + at(0) + "), mulc(" + v[1] + ", " +
+                                at(1) + ")), mulc(" + v[2] + ", " + at(2) + ")), ivc(" + at(3) + ")))";
+    const float t = m[3];
+    if (is_bits(t, 0x80000000u) || !std::isfinite(t)) return generic;
+    std::vector<std::string> terms;
+    int ones = 0;
+    for (int k = 0; k < 3; ++k) {
+        if (!std::isfinite(m[k])) return generic;
+        if (m[k] == 0.f) continue;
+        if (m[k] == 1.f) { terms.push_back(v[k]); ++ones; }
+        else terms.push_back("mulc(" + v[k] + ", " + at(k) + ")");
+    }
+    if (terms.size() == 1 && ones == 1 && is_bits(t, 0u)) return terms[0];
+    std::string e;
+    for (size_t k = 0; k < terms.size(); ++k) e = k == 0 ? terms[0] : "add(" + e + ", " + terms[k] + ")";
+    return terms.empty() ? "settle_point(ivc(" + at(3) + "))" : "settle_point(add(" + e + ", ivc(" + at(3) + ")))";
+}
+
 struct Emitter {
     const std::vector<Node>& nodes;
+    const Program& prog;
     std::ostringstream out;
     int counter = 0;
 
@@ -83,8 +141,11 @@ struct Emitter {
         const int id = counter++;
         const std::string pad(ind, ' ');
         const std::string q = "q" + std::to_string(id), f = "f" + std::to_string(id);
-        // matrix_vector_product (basic_functions.hpp:140-177), same expression order as xform()
-        out << pad << "const V3 " << q << " = xform(M + " << 12 * n.mat << ", " << x << ", " << y << ", " << z << ");\n";
+        // matrix_vector_product (basic_functions.hpp:140-177), rows specialised by xform_row()
+        const float* mm = prog.mats[n.mat];
+        out << pad << "const V3 " << q << " = V3{" << xform_row(mm, 12 * n.mat, x, y, z) << ",\n" << pad << "    "
+            << xform_row(mm + 4, 12 * n.mat + 4, x, y, z) << ",\n" << pad << "    "
+            << xform_row(mm + 8, 12 * n.mat + 8, x, y, z) << "};\n";
         if (n.leaf) {
             out << pad << "const float " << f << " = " << prim_call(n.type) << q << ".x, " << q << ".y, " << q << ".z);\n";
             return f;
@@ -131,6 +192,7 @@ const char* prim_iv_call(int t) {
 // and CSG decisions, so modes and classes are bit-identical to the interpreter's.
 struct IvEmitter {
     const std::vector<Node>& nodes;
+    const Program& prog;
     std::ostringstream out;
     int counter = 0;
 
@@ -139,7 +201,10 @@ struct IvEmitter {
         const int id = counter++;
         const std::string pad(ind, ' ');
         const std::string q = "q" + std::to_string(id), r = "r" + std::to_string(id);
-        out << pad << "const Box " << q << " = xform_iv(M + " << 12 * n.mat << ", " << p << ");\n";
+        const float* mm = prog.mats[n.mat];
+        out << pad << "const Box " << q << " = Box{" << xform_iv_row(mm, 12 * n.mat, p) << ",\n" << pad << "    "
+            << xform_iv_row(mm + 4, 12 * n.mat + 4, p) << ",\n" << pad << "    "
+            << xform_iv_row(mm + 8, 12 * n.mat + 8, p) << "};\n";
         if (n.leaf) {
             out << pad << "const Iv " << r << " = settle(" << prim_iv_call(n.type) << q << "));\n";
             return r;
@@ -187,9 +252,9 @@ std::string TreeJit::kernel_source(const Program& p) {
     int next = 0;
     const int root = parse(p, 0, nodes, next);
     if (next != p.n_instr) throw std::runtime_error("jit: trailing instructions");
-    Emitter em{nodes};
+    Emitter em{nodes, p};
     const std::string f = em.emit(root, "x0", "y0", "z0", 4);
-    IvEmitter iv{nodes};
+    IvEmitter iv{nodes, p};
     const std::string r = iv.emit(root, "p0", 4);
     std::ostringstream s;
     s << kPrelude << "#include \"eval_bricks.hpp\"\n#include \"ifunc_interval.hpp\"\n#include \"brick_modes.hpp\"\n"
