@@ -175,7 +175,7 @@ def main():
         kernel_ms = {k: float(np.mean([p[k] for p in per])) for k in per[0]}
         info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, kernel_ms=kernel_ms,
                     shape=shape, slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats(),
-                    fz=(slab.fz0, slab.fz1), jit=slab.used_jit())
+                    fz=(slab.fz0, slab.fz1), jit=slab.used_jit(), stats=slab.stats())
         slab.close()
         return info
 
@@ -254,7 +254,10 @@ def main():
         "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
         "eval_kernel": "jit" if main_run["jit"] else "interpreter",
         "bricks": {"total": bricks_total, "mixed": bricks_mixed, "sign_filled": bricks_filled,
-                   "evaluated_sample_frac": round(1.0 - bricks_filled / max(1, bricks_total), 4)},
+                   "evaluated_sample_frac": round(1.0 - bricks_filled / max(1, bricks_total), 4),
+                   "mixed_coarse_boxes": main_run["stats"]["mixed_coarse_boxes"]},
+        "mc": {"units": main_run["stats"]["units"], "nonempty_units": main_run["stats"]["nonempty_units"],
+               "active_cells": main_run["stats"]["act"]},
         "roofline": {"bound": "hbm", "kernel": "eval+MC kernel sequence (SURVEY.md 8d)",
                      "achieved": round(b_pipe / t_kern / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(b_pipe / t_kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,

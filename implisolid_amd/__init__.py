@@ -371,10 +371,11 @@ class Slab:
         return dict(zip(self.KERNELS, [float(x) for x in out]))
 
     def stats(self):
-        """After count(): units, active units, owned vertices, triangles, active cells, halo-owned, cells."""
+        """After count(): units, non-empty units, owned vertices, triangles, active cells, halo-owned,
+        cells, mixed coarse boxes."""
         out = (ctypes.c_int64 * 8)()
         self._rc(lib().implisolid_slab_stats(self.h, out))
-        keys = ["units", "unused", "own", "tri", "act", "halo_own", "cells"]
+        keys = ["units", "nonempty_units", "own", "tri", "act", "halo_own", "cells", "mixed_coarse_boxes"]
         return dict(zip(keys, [int(x) for x in out]))
 
     def used_jit(self):

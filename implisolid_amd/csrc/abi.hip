@@ -464,7 +464,7 @@ float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
 
 int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {
     try {
-        uint32_t c[6];
+        uint32_t c[16];
         s->engine.raw_counters(c, 0);
         const GridDesc& g = s->engine.grid();
         out[0] = n_units(g);
@@ -474,7 +474,7 @@ int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {
         out[4] = c[4];
         out[5] = c[5];
         out[6] = g.n_cells;
-        out[7] = 0;
+        out[7] = c[13];   // mixed coarse boxes (interval pass)
     } catch (const std::exception& e) {
         report(e.what(), false);
         return -1;

@@ -283,8 +283,8 @@ void Engine::emit_faces(const uint32_t* d_offsets, const uint32_t* d_gathered, i
     IMPLI_HIP(hipGetLastError());
 }
 
-void Engine::raw_counters(uint32_t out[6], hipStream_t s) {
-    IMPLI_HIP(hipMemcpyAsync(out, counters_.p, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+void Engine::raw_counters(uint32_t out[16], hipStream_t s) {
+    IMPLI_HIP(hipMemcpyAsync(out, counters_.p, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     IMPLI_HIP(hipStreamSynchronize(s));
 }
 

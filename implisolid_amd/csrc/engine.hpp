@@ -92,7 +92,7 @@ public:
     void set_timing(bool on);
     void kernel_times(float out[kTimedKernels]);
     // raw device counters after count(): [active units, halo own, own, tri, act, halo] (blocking)
-    void raw_counters(uint32_t out[6], hipStream_t stream);
+    void raw_counters(uint32_t out[16], hipStream_t stream);
     // brick statistics of the last pruned eval: [bricks, mixed, sign-filled]; blocking
     void brick_stats(int64_t out[3], hipStream_t stream);
 
