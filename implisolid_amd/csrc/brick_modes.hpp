@@ -24,8 +24,9 @@ __device__ __forceinline__ uint8_t sign_class(dev::Iv root) {   // MC sets a cub
 }
 
 // wave-aggregated append of `b` to list (order irrelevant)
+// cap: list capacity (entries past it are dropped -- never reached when the count starts at 0)
 __device__ __forceinline__ void list_append(bool take, uint32_t b, uint32_t* __restrict__ list,
-                                            uint32_t* __restrict__ count) {
+                                            uint32_t* __restrict__ count, uint32_t cap) {
     const int lane = threadIdx.x & 63;
     const uint64_t mask = __ballot(take);
     if (!mask) return;
@@ -33,7 +34,8 @@ __device__ __forceinline__ void list_append(bool take, uint32_t b, uint32_t* __r
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
     base = __shfl(base, leader, 64);
-    if (take) list[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = b;
+    const uint32_t at = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    if (take && at < cap) list[at] = b;
 }
 
 // the brick's class, adjusted for sealed samples (the neighbours' fill test uses it): sealed
@@ -96,10 +98,13 @@ __device__ __forceinline__ uint32_t brick_fill_class(const GridDesc& g, const Br
 
 // Coarse pass: one thread per coarse box -> modes, sign class; mixed boxes are listed.
 // IvEval: Iv operator()(Box p, uint64_t modes_in, uint64_t& modes) const.
+// counters = the engine's counter block (grid.hpp): block 0 clears it except the list length.
 template <class IvEval>
 __device__ __forceinline__ void coarse_modes_body(const IvEval& ev, const GridDesc& g, const BrickGrid& cg,
                                                   uint64_t* __restrict__ cmodes, uint8_t* __restrict__ ccls,
-                                                  uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount) {
+                                                  uint32_t* __restrict__ clist, uint32_t* __restrict__ counters) {
+    uint32_t* ccount = counters + kCoarseListWord;
+    if (blockIdx.x == 0 && threadIdx.x < kCounterWords && threadIdx.x != kCoarseListWord) counters[threadIdx.x] = 0u;
     const int b = blockIdx.x * 256 + threadIdx.x;
     uint8_t c = kBrickPos;
     if (b < cg.n_bricks) {
@@ -111,7 +116,7 @@ __device__ __forceinline__ void coarse_modes_body(const IvEval& ev, const GridDe
         cmodes[b] = m;
         ccls[b] = c;
     }
-    list_append(b < cg.n_bricks && c == kBrickMixed, (uint32_t)b, clist, ccount);
+    list_append(b < cg.n_bricks && c == kBrickMixed, (uint32_t)b, clist, ccount, (uint32_t)cg.n_bricks);
 }
 
 // Bricks of the listed mixed coarse boxes: one thread per (listed box, brick in it).
@@ -121,7 +126,7 @@ __device__ __forceinline__ void brick_refine_body(const IvEval& ev, const GridDe
                                                   const uint32_t* __restrict__ clist,
                                                   const uint32_t* __restrict__ ccount, uint64_t* __restrict__ modes,
                                                   uint8_t* __restrict__ cls) {
-    const uint32_t total = *ccount * kCZ;
+    const uint32_t total = min(*ccount, (uint32_t)cg.n_bricks) * kCZ;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
         const uint32_t cb = clist[i / kCZ];
         int cx, cy, cz;

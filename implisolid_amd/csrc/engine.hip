@@ -80,6 +80,7 @@ Engine::Engine() {
     IMPLI_HIP(hipMemcpy(cases_.p, cases, sizeof cases, hipMemcpyHostToDevice));
     prog_.reserve(sizeof(Program));
     counters_.reserve(kCounterWords * sizeof(uint32_t));
+    IMPLI_HIP(hipMemset(counters_.p, 0, kCounterWords * sizeof(uint32_t)));   // [13] starts at 0 (grid.hpp)
     offsets_.reserve(16);
     IMPLI_HIP(hipMemset(offsets_.p, 0, 16));
 }
@@ -199,14 +200,16 @@ MCBuffers Engine::buffers() const {
 void Engine::eval_field(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
     const int level = pruning();
-    // one memset for the eval's list lengths, the MC counters and the overflow flags
-    IMPLI_HIP(hipMemsetAsync(counters_.p, 0, kCounterWords * sizeof(uint32_t), s));
+    // the counter block (list lengths, MC counters, overflow flags) is cleared by the pruned path's
+    // first kernel (grid.hpp); the dense path clears it with a memset
+    if (level == 0 || brick_grid(grid_).n_bricks <= 0)
+        IMPLI_HIP(hipMemsetAsync(counters_.p, 0, kCounterWords * sizeof(uint32_t), s));
     counters_fresh_ = true;
     mark(0, s);
     if (level > 0) {
         ensure_jit();
         launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, cmodes_.as<uint64_t>(),
-                           ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>() + kCoarseListWord,
+                           ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>(),
                            modes_.as<uint64_t>(), cls_.as<uint8_t>(), s, &jit_iv_);
         uint32_t* d_count = counters_.as<uint32_t>() + kBrickListWord;
         launch_brick_fill(grid_, ccls_.as<uint8_t>(), cmodes_.as<uint64_t>(), cls_.as<uint8_t>(), modes_.as<uint64_t>(),

@@ -31,9 +31,6 @@ struct SlabCounts {
     uint32_t n_faces() const { return tri_total; }
 };
 
-// counters_ layout (u32 words): [0, 12) marching-cubes counters (mc_types.hpp MCBuffers),
-// [12] brick-list length, [13] mixed coarse-box list length, [16, 20) output overflow flags
-constexpr int kBrickListWord = 12, kCoarseListWord = 13, kOverflowWord = 16, kCounterWords = 32;
 
 class Engine {
 public:

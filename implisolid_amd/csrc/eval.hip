@@ -59,8 +59,8 @@ template <int D>
 __global__ __launch_bounds__(256) void k_coarse_modes(const Program* __restrict__ prog, const float* __restrict__ tab,
                                                       float2 tab_range, GridDesc g, BrickGrid cg,
                                                       uint64_t* __restrict__ cmodes, uint8_t* __restrict__ ccls,
-                                                      uint32_t* __restrict__ clist, uint32_t* __restrict__ ccount) {
-    coarse_modes_body(InterpIv<D>{prog, tab, tab_range}, g, cg, cmodes, ccls, clist, ccount);
+                                                      uint32_t* __restrict__ clist, uint32_t* __restrict__ counters) {
+    coarse_modes_body(InterpIv<D>{prog, tab, tab_range}, g, cg, cmodes, ccls, clist, counters);
 }
 
 template <int D>
@@ -105,8 +105,10 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
                                                            const uint64_t* __restrict__ modes, int sign_fill,
                                                            uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
                                                            uint64_t* __restrict__ lmodes, uint32_t* __restrict__ count,
-                                                           sign_piece_t* __restrict__ signs) {
+                                                           sign_piece_t* __restrict__ signs,
+                                                           uint32_t* __restrict__ ccount_reset) {
     __shared__ uint32_t wcnt[kFillBlock / 64], wbase[kFillBlock / 64];
+    if (blockIdx.x == 0 && threadIdx.x == 0) ccount_reset[0] = 0u;   // the refine pass has read it
     const int b = blockIdx.x * kFillBlock + threadIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t fc = kBrickMixed;
@@ -221,17 +223,18 @@ BrickGrid coarse_grid(const GridDesc& g) {
 }
 
 void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
-                        uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_ccount, uint64_t* d_modes,
+                        uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_counters, uint64_t* d_modes,
                         uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit) {
     BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0) return;
+    uint32_t* d_ccount = d_counters + kCoarseListWord;
     depth = eval_depth(depth);
     const unsigned tc = (unsigned)((cg.n_bricks + 255) / 256);
     const unsigned tr = (unsigned)std::min<int64_t>(((int64_t)cg.n_bricks * kCZ + 255) / 256, 2048);
     if (jit && jit->coarse && jit->refine) {
         GridDesc gg = g;
         const float* d_mats = reinterpret_cast<const float*>(reinterpret_cast<const char*>(d_prog) + offsetof(Program, mats));
-        void* ca[] = {&d_mats, &d_rabbit, &tab_range, &gg, &cg, &d_cmodes, &d_ccls, &d_clist, &d_ccount};
+        void* ca[] = {&d_mats, &d_rabbit, &tab_range, &gg, &cg, &d_cmodes, &d_ccls, &d_clist, &d_counters};
         TreeJit::launch(jit->coarse, tc, ca, s, "impli_coarse_modes");
         void* ra[] = {&d_mats, &d_rabbit, &tab_range, &gg, &bg, &cg, &d_cmodes, &d_clist, &d_ccount, &d_modes, &d_cls};
         TreeJit::launch(jit->refine, tr, ra, s, "impli_brick_refine");
@@ -240,7 +243,7 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
 #define IMPLI_MODES(DD)                                                                                           \
     do {                                                                                                          \
         k_coarse_modes<DD><<<tc, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, cg, d_cmodes, d_ccls, d_clist,     \
-                                              d_ccount);                                                          \
+                                              d_counters);                                                        \
         k_brick_refine<DD><<<tr, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, cg, d_cmodes, d_clist, d_ccount, \
                                               d_modes, d_cls);                                                    \
     } while (0)
@@ -264,7 +267,7 @@ void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t*
     if (bg.n_bricks <= 0) return;
     k_brick_fill<<<(unsigned)((bg.n_bricks + kFillBlock - 1) / kFillBlock), kFillBlock, 0, s>>>(
         g, bg, cg, d_ccls, d_cmodes, d_cls, d_modes, sign_fill, d_fill, d_list, d_lmodes, d_count,
-        static_cast<sign_piece_t*>(d_signs));
+        static_cast<sign_piece_t*>(d_signs), d_count - kBrickListWord + kCoarseListWord);
 }
 
 unsigned eval_bricks_grid(const GridDesc& g) {

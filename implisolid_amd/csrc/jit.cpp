@@ -279,8 +279,8 @@ std::string TreeJit::kernel_source(const Program& p) {
       << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, list, count, field, signs);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_coarse_modes(\n"
       << "    const float* M, const float* tab, float2 tab_range, impli::GridDesc g, impli::BrickGrid cg,\n"
-      << "    uint64_t* cmodes, uint8_t* ccls, uint32_t* clist, uint32_t* ccount) {\n"
-      << "    impli::coarse_modes_body(impli::JitIv{M, tab, tab_range}, g, cg, cmodes, ccls, clist, ccount);\n}\n"
+      << "    uint64_t* cmodes, uint8_t* ccls, uint32_t* clist, uint32_t* counters) {\n"
+      << "    impli::coarse_modes_body(impli::JitIv{M, tab, tab_range}, g, cg, cmodes, ccls, clist, counters);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_brick_refine(\n"
       << "    const float* M, const float* tab, float2 tab_range, impli::GridDesc g, impli::BrickGrid bg,\n"
       << "    impli::BrickGrid cg, const uint64_t* cmodes, const uint32_t* clist, const uint32_t* ccount,\n"

@@ -26,7 +26,7 @@ struct JitIntervalKernels {
     hipFunction_t coarse = nullptr, refine = nullptr;
 };
 void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
-                        uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_ccount, uint64_t* d_modes,
+                        uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_counters, uint64_t* d_modes,
                         uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit = nullptr);
 // K1b: neighbour rule -> fill[b], the list of bricks to evaluate, constant sign bits of the rest
 void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t* d_cmodes, const uint8_t* d_cls,
