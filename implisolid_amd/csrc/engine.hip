@@ -116,7 +116,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &ulist_, &counters_, &lmodes_, &vid3_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &ulist_, &umark_, &counters_, &lmodes_, &vid3_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -146,6 +146,9 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
     unit_cnt_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint4));
     ulist_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint4));
+    umark_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint32_t));
+    IMPLI_HIP(hipMemset(umark_.p, 0, (size_t)(n_units(grid_) + 1) * sizeof(uint32_t)));   // ids start at 1
+    marks_valid_ = false;
 
     scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
     const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
@@ -182,6 +185,8 @@ MCBuffers Engine::buffers() const {
 
     b.unit_cnt = unit_cnt_.as<uint4>();
     b.ulist = ulist_.as<uint4>();
+    b.umark = marks_valid_ ? umark_.as<uint32_t>() : nullptr;
+    b.mark_id = mark_id_;
     b.scan_blk = scan_blk_.as<uint32_t>();
     b.counters = counters_.as<uint32_t>();
     b.vid3 = vid3_.as<uint32_t>();
@@ -214,7 +219,8 @@ void Engine::eval_field(hipStream_t s) {
         uint32_t* d_count = counters_.as<uint32_t>() + kBrickListWord;
         launch_brick_fill(grid_, ccls_.as<uint8_t>(), cmodes_.as<uint64_t>(), cls_.as<uint8_t>(), modes_.as<uint64_t>(),
                           level >= 2, fill_.as<uint8_t>(), blist_.as<uint32_t>(), lmodes_.as<uint64_t>(), d_count,
-                          signs_.p, s);
+                          signs_.p, umark_.as<uint32_t>(), ++mark_id_, s);
+        marks_valid_ = true;
         mark(1, s);
         if (jit_fn_) {
             const float* d_mats = reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
@@ -226,6 +232,7 @@ void Engine::eval_field(hipStream_t s) {
                                       blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, s);
         }
     } else {
+        marks_valid_ = false;   // dense field: MC counts every unit
         IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled
         mark(1, s);
         launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);

@@ -103,12 +103,14 @@ private:
     bool jit_tried_ = false;
     hipFunction_t jit_fn_ = nullptr;
     bool counters_fresh_ = false;   // eval_field zeroed the counters; the next count() need not
+    uint32_t mark_id_ = 0;          // id of the last pruned eval's unit marks (umark_)
+    bool marks_valid_ = false;      // the last eval was pruned: count only marked units
     JitIntervalKernels jit_iv_;
     void ensure_jit();
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false;
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, ulist_, counters_, lmodes_, vid3_, records_, verts_, faces_;
+    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, ulist_, umark_, counters_, lmodes_, vid3_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
     hipEvent_t ev_[9] = {};

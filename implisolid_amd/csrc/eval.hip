@@ -106,7 +106,8 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
                                                            uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
                                                            uint64_t* __restrict__ lmodes, uint32_t* __restrict__ count,
                                                            sign_piece_t* __restrict__ signs,
-                                                           uint32_t* __restrict__ ccount_reset) {
+                                                           uint32_t* __restrict__ ccount_reset,
+                                                           uint32_t* __restrict__ umark, uint32_t mark_id) {
     __shared__ uint32_t wcnt[kFillBlock / 64], wbase[kFillBlock / 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) ccount_reset[0] = 0u;   // the refine pass has read it
     const int b = blockIdx.x * kFillBlock + threadIdx.x;
@@ -138,6 +139,12 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
         list[i] = (uint32_t)b;
         const uint64_t mb = modes[b], mc = cmodes[cb];   // both loaded: no branch around a load
         lmodes[i] = (ccls[cb] == kBrickMixed) ? mb : mc;
+        // MC units (kUnitRows cell rows) whose cells have a corner in this brick: cell rows
+        // sy in [by kBY - 1, by kBY + kBY - 1], cell layers lz in [bz kBZ - 1, bz kBZ + kBZ - 1]
+        const int m = g.m, cl = g.cz1 - g.cz0;
+        const int sy0 = max(by * kBY - 1, 0), sy1 = min(by * kBY + kBY - 1, m - 1);
+        for (int lz = max(bz * kBZ - 1, 0); lz <= min(bz * kBZ + kBZ - 1, cl - 1); ++lz)
+            for (int u = (lz * m + sy0) / kUnitRows; u <= (lz * m + sy1) / kUnitRows; ++u) umark[u] = mark_id;
     } else if (valid) {   // sign-filled: constant pieces (all samples of the brick share the sign)
         const sign_piece_t piece = fc == kBrickNeg ? (sign_piece_t)~(sign_piece_t)0 : (sign_piece_t)0;
         const int layers = g.fz1 - g.fz0, row_pieces = (64 / kBX) * sign_row_words(g);
@@ -262,12 +269,12 @@ void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* 
 
 void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t* d_cmodes, const uint8_t* d_cls,
                        const uint64_t* d_modes, int sign_fill, uint8_t* d_fill, uint32_t* d_list, uint64_t* d_lmodes,
-                       uint32_t* d_count, void* d_signs, hipStream_t s) {
+                       uint32_t* d_count, void* d_signs, uint32_t* d_umark, uint32_t mark_id, hipStream_t s) {
     const BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0) return;
     k_brick_fill<<<(unsigned)((bg.n_bricks + kFillBlock - 1) / kFillBlock), kFillBlock, 0, s>>>(
         g, bg, cg, d_ccls, d_cmodes, d_cls, d_modes, sign_fill, d_fill, d_list, d_lmodes, d_count,
-        static_cast<sign_piece_t*>(d_signs), d_count - kBrickListWord + kCoarseListWord);
+        static_cast<sign_piece_t*>(d_signs), d_count - kBrickListWord + kCoarseListWord, d_umark, mark_id);
 }
 
 unsigned eval_bricks_grid(const GridDesc& g) {

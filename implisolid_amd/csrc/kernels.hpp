@@ -31,7 +31,7 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
 // K1b: neighbour rule -> fill[b], the list of bricks to evaluate, constant sign bits of the rest
 void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t* d_cmodes, const uint8_t* d_cls,
                        const uint64_t* d_modes, int sign_fill, uint8_t* d_fill, uint32_t* d_list, uint64_t* d_lmodes,
-                       uint32_t* d_count, void* d_signs, hipStream_t s);
+                       uint32_t* d_count, void* d_signs, uint32_t* d_umark, uint32_t mark_id, hipStream_t s);
 // K1c (interpreter): the listed bricks; the JIT variant is TreeJit::launch_bricks (jit.hpp)
 unsigned eval_bricks_grid(const GridDesc& g);
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,

@@ -73,7 +73,14 @@ void build_case_table(CaseInfo out[256]) {
         // corners 5-6, 6 = 6-7, 10 = 2-6), and every non-trivial case has a triangle.
         auto neg = [ci](int k) { return (ci >> k) & 1; };
         const int crossing = (neg(5) ^ neg(6)) + (neg(6) ^ neg(7)) + (neg(2) ^ neg(6));
-        if (crossing != c.nown || (c.ntri > 0) != (ci != 0 && ci != 255))
+        // ... and the triangle count is E - 2 P (mc_device.hpp chunk_triangles)
+        int ec = 0, ei = 0, v = 0, ff = 0, opp = 0;
+        for (const auto& e : kCubeEdges) { ec += neg(e[0]) ^ neg(e[1]); ei += neg(e[0]) & neg(e[1]); }
+        for (int k = 0; k < 8; ++k) v += neg(k);
+        for (const auto& f : kCubeFaces) ff += neg(f[0]) & neg(f[1]) & neg(f[2]) & neg(f[3]);
+        for (const auto& o : kCubeOpposite) opp += (v == 6 && !neg(o[0]) && !neg(o[1])) ? 1 : 0;
+        const int ntri_formula = (ci == 0 || ci == 255) ? 0 : ec - 2 * (v - ei + ff + 2 * opp);
+        if (crossing != c.nown || (c.ntri > 0) != (ci != 0 && ci != 255) || ntri_formula != c.ntri)
             throw std::runtime_error("marching cubes: case table violates the count kernel's assumptions");
         out[ci] = c;
     }
@@ -83,24 +90,35 @@ namespace {
 
 // K2: one block per group of kGroupUnits units; lanes take the group's items (row, 64-cell chunk)
 // round robin, so every lane has work (a wave per unit would leave 64 - 4 nch lanes idle).  Only
-// non-trivial cells (~1 %) look at the triangle table.  Per-unit sums through LDS atomics.
+// units whose cells touch an evaluated brick are visited (b.umark): all others are trivial.  Owned
+// vertices and triangles of a chunk are popcounts of corner-mask expressions (chunk_triangles).
+// Per-unit sums through LDS atomics.
 //   -> unit_cnt[64 group + k] = k-th non-empty unit of the group {unit in group, own / tri / act
 //      exclusive bases in the group}; scan_blk[c][group] = the group's sums (c < 5: own, tri, act,
 //      halo own, non-empty units -- scanned by k_scan_groups), scan_blk[5][group] = non-empty units.
 __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ uint32_t s_u[kGroupUnits][4];
-    __shared__ uint8_t s_ntri[256];
+    __shared__ uint8_t s_fu[kGroupUnits];   // the group's candidate units, in order
+    __shared__ uint32_t s_nf;
     const int t = threadIdx.x, nt_ = blockDim.x;
-    for (int k = t; k < 256; k += nt_) s_ntri[k] = cases[k].ntri;
+    (void)cases;   // triangle counts come from chunk_triangles (checked against the table)
     for (int k = t; k < 4 * kGroupUnits; k += nt_) (&s_u[0][0])[k] = 0u;
-    __syncthreads();
     const int nch = (g.m + 63) / 64;
     const int64_t rows = n_rows(g), nu = n_units(g);
     const int64_t row0 = (int64_t)blockIdx.x * kGroupUnits * kUnitRows;
+    if (t < 64) {   // candidates: units whose cells touch an evaluated brick (others are all trivial)
+        const int64_t u = (int64_t)blockIdx.x * kGroupUnits + t;
+        const bool cand = u < nu && (!b.umark || b.umark[u] == b.mark_id);
+        const uint64_t m = __ballot(cand);
+        if (cand) s_fu[__popcll((unsigned long long)(m & ((1ull << t) - 1ull)))] = (uint8_t)t;
+        if (t == 0) s_nf = (uint32_t)__popcll((unsigned long long)m);
+    }
+    __syncthreads();
     // a lane's items are loaded together (kCountBatch at a time), then counted: one memory round
     // trip per batch instead of one per item
     constexpr int kCountBatch = 3;
-    const int n_items = kGroupUnits * kUnitRows * nch;
+    const int per_unit = kUnitRows * nch;
+    const int n_items = (int)s_nf * per_unit;
     for (int i0 = t; i0 < n_items; i0 += kCountBatch * nt_) {
         ChunkBits kb[kCountBatch];
         int rb[kCountBatch];
@@ -108,10 +126,11 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
         for (int q = 0; q < kCountBatch; ++q) {
             // out-of-range items read a valid chunk (clamped) and drop it: no branch around loads
             const int i = i0 + q * nt_;
-            const bool ok = i < n_items && row0 + i / nch < rows;
-            const int ic = ok ? i : 0;
-            rb[q] = ic / nch;
-            load_chunk(g, b.signs, row0 + rb[q], ic - rb[q] * nch, kb[q]);
+            const int ic = i < n_items ? i : 0;
+            const int fu = s_fu[ic / per_unit], w = ic - (ic / per_unit) * per_unit;
+            rb[q] = fu * kUnitRows + w / nch;
+            const bool ok = i < n_items && row0 + rb[q] < rows;
+            load_chunk(g, b.signs, ok ? row0 + rb[q] : 0, ok ? w - (w / nch) * nch : 0, kb[q]);
             if (!ok) kb[q].nt = 0;
         }
 #pragma unroll
@@ -126,12 +145,7 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
             unsigned tri = 0, act = 0, hal = 0;
             if (k.z >= g.cz_emit) {
                 act = (unsigned)__popcll((unsigned long long)k.nt);   // every non-trivial case has a triangle
-                uint64_t nt = k.nt;
-                while (nt) {
-                    const int j = __ffsll((unsigned long long)nt) - 1;
-                    nt &= nt - 1;
-                    tri += s_ntri[chunk_ci(k, j)];
-                }
+                tri = chunk_triangles(k);
             } else {
                 hal = own;
             }

@@ -62,6 +62,45 @@ __device__ __forceinline__ void load_chunk(const GridDesc& g, const uint64_t* __
     k.nt = any & ~all & valid;
 }
 
+// Bourke cube edges / faces / opposite corner pairs (corner k = bit k of the cube index)
+constexpr int kCubeEdges[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {4, 5}, {5, 6},
+                                   {6, 7}, {7, 4}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
+constexpr int kCubeFaces[6][4] = {{0, 1, 2, 3}, {4, 5, 6, 7}, {0, 1, 5, 4}, {1, 2, 6, 5}, {2, 3, 7, 6}, {3, 0, 4, 7}};
+constexpr int kCubeOpposite[4][2] = {{0, 6}, {1, 7}, {2, 4}, {3, 5}};
+
+// Triangles of the non-trivial cells of a chunk, all 64 at once.  In the table a case with E
+// crossing edges has E - 2 P triangles, P its polygons: the connected components of its negative
+// corners, V - E_int + F_full (independent cycles of the induced cube subgraph are its full
+// faces), except the four cases with exactly two opposite positive corners, whose six-cycle the
+// table splits into two triangles (P = 2).  Checked for all 256 cases by build_case_table.
+__device__ __forceinline__ unsigned chunk_triangles(const ChunkBits& k) {
+    const uint64_t c[8] = {k.s00, k.t00, k.t10, k.s10, k.s01, k.t01, k.t11, k.s11};   // corner k of each cell
+    const uint64_t nt = k.nt;
+    int ec = 0, ei = 0, v = 0, ff = 0, opp = 0;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+        const uint64_t a = c[kCubeEdges[e][0]], b = c[kCubeEdges[e][1]];
+        ec += __popcll((unsigned long long)((a ^ b) & nt));
+        ei += __popcll((unsigned long long)(a & b & nt));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += __popcll((unsigned long long)(c[q] & nt));
+#pragma unroll
+    for (int f = 0; f < 6; ++f)
+        ff += __popcll((unsigned long long)(c[kCubeFaces[f][0]] & c[kCubeFaces[f][1]] & c[kCubeFaces[f][2]] &
+                                            c[kCubeFaces[f][3]] & nt));
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int a = kCubeOpposite[o][0], b = kCubeOpposite[o][1];
+        uint64_t rest = ~c[a] & ~c[b] & nt;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (q != a && q != b) rest &= c[q];
+        opp += __popcll((unsigned long long)rest);
+    }
+    return (unsigned)(ec - 2 * (v - ei + ff + 2 * opp));
+}
+
 // cube index of cell j of a chunk, corner bits as polygonize_single_cube (:553-560)
 __device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
     return (unsigned)((k.s00 >> j) & 1u) | ((unsigned)((k.t00 >> j) & 1u) << 1) | ((unsigned)((k.s10 >> j) & 1u) << 3) |

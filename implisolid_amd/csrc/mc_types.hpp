@@ -30,6 +30,8 @@ struct MCBuffers {
     uint32_t* scan_blk;      // [6][n_groups]: group sums (own, tri, act, halo own, non-empty units), then
                              // exclusive bases; row 5: non-empty units (unscanned)
     uint4* ulist;            // all non-empty units in order: {unit, vbase, fbase, abase} (k_unit_flatten)
+    const uint32_t* umark;   // units whose cells touch an evaluated brick hold mark_id (k_brick_fill);
+    uint32_t mark_id;        // null: every unit is counted (dense eval)
     uint32_t* counters;      // [0] non-empty units, [1] halo own, [2..5] totals own/tri/act/halo
     uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
     uint4* records;          // active cells: {L, ci, fbase, 0}
