@@ -474,7 +474,7 @@ int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {
         out[4] = c[4];
         out[5] = c[5];
         out[6] = g.n_cells;
-        out[7] = c[13];   // mixed coarse boxes (interval pass)
+        out[7] = c[14];   // mixed coarse boxes of the last eval (the fill kernel's copy of [13])
     } catch (const std::exception& e) {
         report(e.what(), false);
         return -1;

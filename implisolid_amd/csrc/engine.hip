@@ -72,8 +72,22 @@ Engine::Engine() {
         tab_range_.x = v < tab_range_.x ? v : tab_range_.x;
         tab_range_.y = v > tab_range_.y ? v : tab_range_.y;
     }
-    rabbit_.reserve(tab.size() * sizeof(float));
-    IMPLI_HIP(hipMemcpy(rabbit_.p, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
+    // block min / max of the eight reads at every flat index (ifunc_device.hpp kRabbitBlockMinMax)
+    const int sx = IMPLI_RABBIT_NX, sxy = IMPLI_RABBIT_NX * IMPLI_RABBIT_NY;
+    std::vector<float> all(tab);
+    all.resize((size_t)dev::kRabbitPadded * 3, 0.f);
+    for (int b = 0; b < dev::kRabbitPadded; ++b) {
+        float lo = INFINITY, hi = -INFINITY;
+        for (int d : {0, 1, sx, sx + 1, sxy, sxy + 1, sxy + sx, sxy + sx + 1}) {
+            const float v = b + d < dev::kRabbitPadded ? tab[b + d] : 0.f;
+            lo = v < lo ? v : lo;
+            hi = v > hi ? v : hi;
+        }
+        all[dev::kRabbitPadded + 2 * b] = lo;
+        all[dev::kRabbitPadded + 2 * b + 1] = hi;
+    }
+    rabbit_.reserve(all.size() * sizeof(float));
+    IMPLI_HIP(hipMemcpy(rabbit_.p, all.data(), all.size() * sizeof(float), hipMemcpyHostToDevice));
     CaseInfo cases[256];
     build_case_table(cases);
     cases_.reserve(sizeof cases);

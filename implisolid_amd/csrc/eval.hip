@@ -109,7 +109,10 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
                                                            uint32_t* __restrict__ ccount_reset,
                                                            uint32_t* __restrict__ umark, uint32_t mark_id) {
     __shared__ uint32_t wcnt[kFillBlock / 64], wbase[kFillBlock / 64];
-    if (blockIdx.x == 0 && threadIdx.x == 0) ccount_reset[0] = 0u;   // the refine pass has read it
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // the refine pass has read it; kept in [14] for stats
+        ccount_reset[1] = ccount_reset[0];
+        ccount_reset[0] = 0u;
+    }
     const int b = blockIdx.x * kFillBlock + threadIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t fc = kBrickMixed;

@@ -39,7 +39,8 @@ constexpr int kBX = IMPLI_BRICK_X, kBY = IMPLI_BRICK_Y, kBZ = IMPLI_BRICK_Z;
 constexpr int kCZ = 8;
 static_assert(kBX * kBY == 64 && (kBX == 8 || kBX == 16 || kBX == 32), "a brick layer is one wave");
 // the engine's counter block (u32 words): [0, 12) marching-cubes counters (mc_types.hpp),
-// [12] brick-list length, [13] mixed coarse-box list length, [16, 20) output overflow flags.
+// [12] brick-list length, [13] mixed coarse-box list length, [14] its copy for statistics,
+// [16, 20) output overflow flags.
 // The pruned eval zeroes it without a memset: the coarse pass's first block clears every word but
 // [13], which it appends to; the fill kernel clears [13] once the refine pass has read it.
 constexpr int kBrickListWord = 12, kCoarseListWord = 13, kOverflowWord = 16, kCounterWords = 32;

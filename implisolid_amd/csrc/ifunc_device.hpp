@@ -71,7 +71,12 @@ __device__ __forceinline__ V3 egg_g(float x, float y, float z) {
 // The table (+ the object's trailing members and zero padding for out-of-table reads, F8d)
 // is passed as a device pointer; RABBIT_PAD entries are readable.
 constexpr int kRabbitN = IMPLI_RABBIT_NX * IMPLI_RABBIT_NY * IMPLI_RABBIT_NZ;
-constexpr int kRabbitPadded = 9600;   // > max index 23 + 19*22 + 23*396 = 9549
+// readable entries: the point function reads up to 23 + 19*22 + 23*396 = 9549; the interval
+// bound's 2x2x2 blocks (ifunc_interval.hpp cube_iv) start at <= 9549 and read 419 further
+constexpr int kRabbitPadded = 10240;
+// after the table: float2 {min, max} over the eight reads b + {0,1} + {0,sx} + {0,sx*sy} of every
+// flat index b (cube_iv's O(1) range lookups)
+constexpr int kRabbitBlockMinMax = kRabbitPadded;
 
 __device__ __forceinline__ float cube_f(const float* __restrict__ tab, float X, float Y, float Z) {
     const int sx = IMPLI_RABBIT_NX, sy = IMPLI_RABBIT_NY, sz = IMPLI_RABBIT_NZ;

@@ -121,7 +121,19 @@ __device__ __forceinline__ Iv cube_iv(const float* __restrict__ tab, float2 tab_
     const int z0 = (int)((fmax2(p.z.lo, oz) - oz) / gs), z1 = (int)((fmin2(p.z.hi, zm) - oz) / gs);
     float vmin, vmax;
     const int cnt = (x1 - x0 + 2) * (y1 - y0 + 2) * (z1 - z0 + 2);
-    if (cnt > 512 || !(p.x.lo <= p.x.hi)) {
+    if (x1 - x0 <= 1 && y1 - y0 <= 1 && z1 - z0 <= 1 && p.x.lo <= p.x.hi) {
+        // the read range per axis ([x0, x1 + 1], 2 or 3 entries) is covered by the 2-blocks at
+        // x0 and x1: at most eight independent loads of the block min / max table
+        const float2* mm = reinterpret_cast<const float2*>(tab + kRabbitBlockMinMax);
+        vmin = INFINITY; vmax = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int x = (k & 1) ? x1 : x0, y = (k & 2) ? y1 : y0, z = (k & 4) ? z1 : z0;
+            const float2 m = mm[x + y * sx + z * sx * sy];
+            vmin = fmin2(vmin, m.x);
+            vmax = fmax2(vmax, m.y);
+        }
+    } else if (cnt > 512 || !(p.x.lo <= p.x.hi)) {
         vmin = tab_range.x; vmax = tab_range.y;
     } else {
         vmin = INFINITY; vmax = -INFINITY;
