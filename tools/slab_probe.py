@@ -2,7 +2,7 @@
 """Time one rank's slab of config 4 on one GPU (no collectives): the per-rank compute of the
 N-GPU Z-slab run, to see how the kernel sequence scales before any RCCL cost.
 
-    python tools/slab_probe.py [R] [steps]
+    python tools/slab_probe.py [R] [steps] [nranks,...]
 """
 import json
 import os
@@ -22,7 +22,8 @@ def main():
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     out = {}
-    for n in (1, 2, 4, 8):
+    ns = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 2, 4, 8]
+    for n in ns:
         for rank in sorted({0, n // 2, n - 1}):
             s = I.Slab(shape, mc, rank, n)
             for _ in range(3):
