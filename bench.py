@@ -219,8 +219,11 @@ def main():
     t_kern = sum(kms.values()) * 1e-3
     dom = max(kern, key=kern.get)
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "traffic_r01.json")
-    if os.path.exists(tfile):
+    # the newest committed PMC traffic summary (tools/profile_round.sh <tag> -> profiles/traffic_<tag>.json)
+    import glob
+    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
+    tfile = tfiles[-1] if tfiles else None
+    if tfile:
         try:
             tj = json.load(open(tfile))
             if tj.get("workload_R") == R and tj.get("tree_seed") == scenes.CONFIG3_SEED:
