@@ -32,6 +32,7 @@ ABI_SYMBOLS = [
     "implisolid_parse_settings", "implisolid_slab_partition", "implisolid_slab_brick_stats",
     "implisolid_slab_set_timing", "implisolid_slab_kernel_times", "implisolid_jit_compile",
     "implisolid_slab_used_jit", "implisolid_set_jit", "implisolid_slab_stats", "implisolid_slab_read_signs",
+    "implisolid_srand", "implisolid_rand", "implisolid_rand_skip",
 ]
 
 _lib = None
@@ -103,6 +104,9 @@ def lib():
         "implisolid_jit_compile": ([c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)],
                                    ctypes.c_int64),
         "implisolid_slab_kernel_times": ([c_void_p, fp], c_int),
+        "implisolid_srand": ([ctypes.c_uint], None),
+        "implisolid_rand": ([], c_int),
+        "implisolid_rand_skip": ([ctypes.c_uint64], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -171,6 +175,21 @@ def set_pruning(level):
     if level is True:
         level = 2
     lib().implisolid_set_pruning(int(level))
+
+
+def srand(seed):
+    """Seed the library's glibc-compatible rand() (the generator the subdivision noise draws from,
+    randomize_verts basic_functions.hpp:551-557).  Host only."""
+    lib().implisolid_srand(int(seed) & 0xFFFFFFFF)
+
+
+def rand():
+    return int(lib().implisolid_rand())
+
+
+def rand_skip(n):
+    """Discard n draws of the library's rand() (O(log n) jump-ahead)."""
+    lib().implisolid_rand_skip(int(n))
 
 
 def last_error():

@@ -75,9 +75,15 @@ void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.c
         for (int i = 0; i < st.vresampl_iters; ++i) ob.vertex_resampling(st.vresampl_c);   // step 1
         if (st.projection) ob.centroids_projection(st.qem);                             // step 2
         if (st.subdiv && (st.overall_repeats <= 1 || rep == st.overall_repeats - 1)) {
-            report("subdivision (polygonize_step_3) is not implemented by this build; result is unsubdivided", false);
+            // polygonize_step_3 (polygonizer_algorithm_ob02.hpp:119-157): the noise is applied only
+            // on the last repeat, scaled by the constant 10
+            const bool is_last = rep == st.overall_repeats - 1;
+            const float scale_noise = (float)(1.0 * 10.0);
+            ob.subdivide(is_last ? st.post_subdiv_noise * scale_noise : 0.0f);
         }
     }
+    nv = ob.n_verts();
+    nf = ob.n_faces();
     g_state.verts.resize((size_t)nv * 3);
     g_state.faces.resize((size_t)nf * 3);
     ob.fetch(g_state.verts.data(), g_state.faces.data());
@@ -97,6 +103,10 @@ extern "C" {
 
 const char* implisolid_last_error(void) { return g_last_error.c_str(); }
 void implisolid_set_error_mode(int mode) { g_error_mode = mode; }
+
+void implisolid_srand(unsigned seed) { impli::process_rand().seed_(seed); }
+int implisolid_rand(void) { return impli::process_rand().next(); }
+void implisolid_rand_skip(uint64_t n) { impli::process_rand().skip(n); }
 
 void implisolid_set_pruning(int level) { impli::Engine::set_pruning(level); }
 

@@ -272,4 +272,70 @@ SlabRange slab_partition(int R, int rank, int nranks) {
     return r;
 }
 
+void GlibcRand::seed_(unsigned seed) {   // srandom_r (random_r.c:161-196)
+    int32_t word = seed == 0 ? 1 : (int32_t)seed;
+    r_[0] = (uint32_t)word;
+    for (int i = 1; i < 31; ++i) {        // 16807 * word mod (2^31 - 1), Schrage's method
+        const int32_t hi = word / 127773, lo = word % 127773;
+        word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r_[i] = (uint32_t)word;
+    }
+    head_ = 3;                            // fptr = &state[SEP_3] holds the oldest term
+    for (int i = 0; i < 310; ++i) next();
+}
+
+int32_t GlibcRand::next() {               // random_r (random_r.c:353-394): *fptr += *rptr
+    int b = head_ + 28;
+    if (b >= 31) b -= 31;
+    const uint32_t v = r_[head_] + r_[b];
+    r_[head_] = v;
+    if (++head_ == 31) head_ = 0;
+    return (int32_t)(v >> 1);
+}
+
+void GlibcRand::extended_window(uint32_t out[61]) const {
+    for (int j = 0; j < 31; ++j) out[j] = r_[(head_ + j) % 31];
+    for (int j = 31; j < 61; ++j) out[j] = out[j - 31] + out[j - 3];
+}
+
+void GlibcRand::skip(uint64_t n) {
+    uint32_t c[31], x[61];
+    rand_jump_poly(n, c);
+    extended_window(x);
+    for (int j = 0; j < 31; ++j) {
+        uint32_t acc = 0;
+        for (int i = 0; i < 31; ++i) acc += c[i] * x[i + j];
+        r_[j] = acc;
+    }
+    head_ = 0;
+}
+
+void rand_poly_mulmod(const uint32_t a[31], const uint32_t b[31], uint32_t out[31]) {
+    uint32_t p[61] = {};
+    for (int i = 0; i < 31; ++i)
+        for (int j = 0; j < 31; ++j) p[i + j] += a[i] * b[j];
+    for (int k = 60; k >= 31; --k) {      // z^k = z^(k-3) + z^(k-31)
+        p[k - 3] += p[k];
+        p[k - 31] += p[k];
+    }
+    for (int i = 0; i < 31; ++i) out[i] = p[i];
+}
+
+void rand_jump_poly(uint64_t n, uint32_t c[31]) {
+    uint32_t base[31] = {}, r[31] = {};
+    base[1] = 1;   // z
+    r[0] = 1;
+    for (; n; n >>= 1) {
+        if (n & 1) rand_poly_mulmod(r, base, r);
+        rand_poly_mulmod(base, base, base);
+    }
+    for (int i = 0; i < 31; ++i) c[i] = r[i];
+}
+
+GlibcRand& process_rand() {
+    static GlibcRand g(1);
+    return g;
+}
+
 }  // namespace impli

@@ -42,6 +42,35 @@ Program compile_mp5(const Json& shape, bool ignore_root_matrix);
 struct SlabRange { int z0, z1, halo; };
 SlabRange slab_partition(int R, int rank, int nranks);
 
+// glibc rand() / srand() restated (stdlib/random_r.c, TYPE_3: additive feedback
+// x_n = x_{n-3} + x_{n-31} mod 2^32, output x_n >> 1; state seeded by the 16807 LCG, 310 outputs
+// discarded).  randomize_verts (basic_functions.hpp:551-557) draws from the process-global rand() of
+// the native reference build; the library keeps one process-global generator in that state (never
+// seeded = srand(1), implisolid_srand to reseed), advanced only by subdivision.
+//
+// The state is kept as the window of the last 31 terms, so that n draws can be skipped (or handed
+// to GPU lanes) with the polynomial z^n mod P(z), P = z^31 - z^28 - 1 over Z/2^32:
+//   x_{m+n+j} = sum_i c_i x_{m+i+j}  where  z^n = sum_i c_i z^i  (mod P).
+class GlibcRand {
+public:
+    explicit GlibcRand(unsigned seed = 1) { seed_(seed); }
+    void seed_(unsigned seed);
+    int32_t next();
+    void fill(uint32_t* out, int64_t n) { for (int64_t i = 0; i < n; ++i) out[i] = (uint32_t)next(); }
+    // x_m .. x_{m+60}: the window (oldest first) extended by 30 terms; draw k of the future is
+    // produced from x_{m+k} and x_{m+k+28}
+    void extended_window(uint32_t out[61]) const;
+    void skip(uint64_t n);
+private:
+    uint32_t r_[31];
+    int head_ = 0;   // r_[head_] is the oldest term x_{n-31}
+};
+GlibcRand& process_rand();
+
+// z^n mod (z^31 - z^28 - 1), coefficients mod 2^32
+void rand_jump_poly(uint64_t n, uint32_t c[31]);
+void rand_poly_mulmod(const uint32_t a[31], const uint32_t b[31], uint32_t out[31]);
+
 // basic_functions.hpp:77-128 invert_matrix (ublas LU on a float 4x4 with last row 0,0,0,1)
 bool invert_matrix12(const float in[12], float out[12]);
 

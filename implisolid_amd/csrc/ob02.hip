@@ -23,6 +23,16 @@ namespace impli {
 
 using namespace dev;
 
+struct EdgeTab {
+    unsigned long long* key;
+    uint32_t* first;
+    uint32_t* last;
+    uint32_t* cnt;
+    uint32_t* slot_of;   // 3 * nf
+    uint64_t mask;
+};
+
+
 namespace {
 
 constexpr float kRootTol = (float)(0.001 / 10.0);   // configs.hpp:33
@@ -98,14 +108,6 @@ __global__ void k_sort_umbrella(const uint32_t* __restrict__ off, int32_t* __res
     }
 }
 
-struct EdgeTab {
-    unsigned long long* key;
-    uint32_t* first;
-    uint32_t* last;
-    uint32_t* cnt;
-    uint32_t* slot_of;   // 3 * nf
-    uint64_t mask;
-};
 
 __global__ void k_edge_insert(const int32_t* __restrict__ f, int64_t nf, int64_t nv, EdgeTab t) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -135,6 +137,121 @@ __global__ void k_fof(int64_t nf, EdgeTab t, int32_t* __restrict__ fof) {
     const uint32_t fi = (uint32_t)(i / 3);
     const uint32_t first = t.first[s];
     fof[i] = (int32_t)((first != fi) ? first : (t.cnt[s] >= 2 ? t.last[s] : 0u));
+}
+
+// ---- step 3: my_subdiv_ (centroids_projection.cpp:1314-1367) -----------------------------------
+// subdivide_multiple_facets_1to4 (subdiv_1to4.hpp:147-232) numbers midpoints by first appearance of
+// their edge over (face ascending; e01, e12, e20).  The first slot of an edge is in face
+// first[edge], at the lowest k of that face holding the edge.
+__device__ __forceinline__ bool first_slot(const EdgeTab& t, int64_t fi, int k, uint32_t s[3]) {
+    return t.first[s[k]] == (uint32_t)fi && (k < 1 || s[0] != s[k]) && (k < 2 || s[1] != s[k]);
+}
+
+__global__ void k_sub_count(int64_t nf, EdgeTab t, uint32_t* __restrict__ cnt) {
+    const int64_t fi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (fi >= nf) return;
+    uint32_t s[3] = {t.slot_of[3 * fi], t.slot_of[3 * fi + 1], t.slot_of[3 * fi + 2]};
+    cnt[fi] = (uint32_t)first_slot(t, fi, 0, s) + (uint32_t)first_slot(t, fi, 1, s) + (uint32_t)first_slot(t, fi, 2, s);
+}
+
+// new_vert_maker (subdiv_1to4.hpp:277-330): Eigen's lazy 3x3 product reduces a0 + (a1 + a2)
+__device__ __forceinline__ float mid3(float a0, float a1, float a2, float w0, float w1, float w2) {
+    return a0 * w0 + (a1 * w1 + a2 * w2);
+}
+
+__global__ void k_sub_verts(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t nf, int64_t nv, EdgeTab t,
+                            const uint32_t* __restrict__ off, float* __restrict__ vout, uint32_t* __restrict__ tmid) {
+    const int64_t fi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (fi >= nf) return;
+    uint32_t s[3] = {t.slot_of[3 * fi], t.slot_of[3 * fi + 1], t.slot_of[3 * fi + 2]};
+    const float H = 0.5f, O = 0.0f;
+    const float W[3][3] = {{H, H, O}, {O, H, H}, {H, O, H}};   // columns m01, m12, m20 of new_vert_maker
+    const float* p0 = v + 3 * (int64_t)f[3 * fi];
+    const float* p1 = v + 3 * (int64_t)f[3 * fi + 1];
+    const float* p2 = v + 3 * (int64_t)f[3 * fi + 2];
+    uint32_t id = (uint32_t)nv + off[fi];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (!first_slot(t, fi, k, s)) continue;
+        float* o = vout + 3 * (int64_t)id;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) o[r] = mid3(p0[r], p1[r], p2[r], W[k][0], W[k][1], W[k][2]);
+        tmid[s[k]] = id++;
+    }
+}
+
+// subdiv_1to4.hpp:380-470: face fi becomes (m12, m20, m01); nf + 3 fi + {0,1,2} the corner faces
+__global__ void k_sub_faces(const int32_t* __restrict__ f, int64_t nf, EdgeTab t, const uint32_t* __restrict__ tmid,
+                            int32_t* __restrict__ fout) {
+    const int64_t fi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (fi >= nf) return;
+    const int32_t v0 = f[3 * fi], v1 = f[3 * fi + 1], v2 = f[3 * fi + 2];
+    const int32_t m01 = (int32_t)tmid[t.slot_of[3 * fi]], m12 = (int32_t)tmid[t.slot_of[3 * fi + 1]],
+                  m20 = (int32_t)tmid[t.slot_of[3 * fi + 2]];
+    int32_t* o = fout + 3 * fi;
+    o[0] = m12; o[1] = m20; o[2] = m01;
+    o = fout + 3 * (nf + 3 * fi);
+    o[0] = v0; o[1] = m01; o[2] = m20;
+    o[3] = v1; o[4] = m12; o[5] = m01;
+    o[6] = v2; o[7] = m20; o[8] = m12;
+}
+
+// randomize_verts (basic_functions.hpp:551-557) with glibc rand(): lane c produces draws
+// [c L, c L + L) of the sequence from its own window x_{m + cL + j} = sum_i Q_c[i] x_{m+i+j},
+// Q_c = z^(cL) mod P = qlo[c % 64] * qhi[c / 64] (host.hpp GlibcRand).
+constexpr int kRandL = 31 * 8;
+
+__device__ __forceinline__ void poly_mulmod(const uint32_t a[31], const uint32_t b[31], uint32_t out[31]) {
+    uint32_t p[61];
+#pragma unroll
+    for (int k = 0; k < 61; ++k) p[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 31; ++i)
+#pragma unroll
+        for (int j = 0; j < 31; ++j) p[i + j] += a[i] * b[j];
+#pragma unroll
+    for (int k = 60; k >= 31; --k) {
+        p[k - 3] += p[k];
+        p[k - 31] += p[k];
+    }
+#pragma unroll
+    for (int i = 0; i < 31; ++i) out[i] = p[i];
+}
+
+__global__ __launch_bounds__(256) void k_rand_noise(float* __restrict__ v, int64_t n, const uint32_t* __restrict__ xw,
+                                                    const uint32_t* __restrict__ qlo, const uint32_t* __restrict__ qhi,
+                                                    float amplitude) {
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n0 = c * kRandL;
+    if (n0 >= n) return;
+    uint32_t a[31], b[31], q[31], w[31];
+#pragma unroll
+    for (int i = 0; i < 31; ++i) {
+        a[i] = qlo[(c & 63) * 31 + i];
+        b[i] = qhi[(c >> 6) * 31 + i];
+    }
+    poly_mulmod(a, b, q);
+#pragma unroll
+    for (int j = 0; j < 31; ++j) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < 31; ++i) acc += q[i] * xw[i + j];
+        w[j] = acc;
+    }
+    const double amp = (double)amplitude;
+    for (int r = 0; r < kRandL / 31; ++r) {
+#pragma unroll
+        for (int k = 0; k < 31; ++k) {
+            const uint32_t x = w[k] + w[(k + 28) % 31];
+            w[k] = x;
+            const int64_t i = n0 + r * 31 + k;
+            if (i < n) {
+                // (REAL)rand() / (REAL)RAND_MAX - 0.5 (a double literal), times the float amplitude
+                const float u = (float)(int32_t)(x >> 1) / 2147483648.0f;
+                v[i] = (float)((double)v[i] + ((double)u - 0.5) * amp);
+            }
+        }
+    }
 }
 
 // ---- step 1 ----------------------------------------------------------------------------------
@@ -610,7 +727,7 @@ std::vector<float> make_random_pm1(int64_t n, float amplitude) {
 }  // namespace
 
 Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
-    misc_.reserve(64);
+    misc_.reserve(512);
 }
 
 void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_) {
@@ -621,6 +738,24 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     faces_.reserve((size_t)(nf + 1) * 12);
     if (nv) IMPLI_HIP(hipMemcpyAsync(verts_.p, d_verts, (size_t)nv * 12, hipMemcpyDeviceToDevice, s));
     if (nf) IMPLI_HIP(hipMemcpyAsync(faces_.p, d_faces, (size_t)nf * 12, hipMemcpyDeviceToDevice, s));
+    build_topology();
+}
+
+EdgeTab Ob02::edge_table() {
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)(4 * nf + 16)) cap <<= 1;
+    etab_.reserve((size_t)cap * (8 + 12) + (size_t)(3 * nf + 1) * 4);
+    EdgeTab t;
+    t.key = etab_.as<unsigned long long>();
+    t.first = reinterpret_cast<uint32_t*>(t.key + cap);
+    t.last = t.first + cap;
+    t.cnt = t.last + cap;
+    t.slot_of = t.cnt + cap;
+    t.mask = cap - 1;
+    return t;
+}
+
+void Ob02::build_topology() {
     // umbrellas
     deg_.reserve((size_t)(nv + 1) * 4);
     uoff_.reserve((size_t)(nv + 2) * 4);
@@ -633,16 +768,8 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
                                                              deg_.as<uint32_t>(), ulst_.as<int32_t>());
     if (nv) k_sort_umbrella<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), nv);
     // faces of faces
-    uint64_t cap = 1024;
-    while (cap < (uint64_t)(4 * nf + 16)) cap <<= 1;
-    etab_.reserve((size_t)cap * (8 + 12) + (size_t)(3 * nf + 1) * 4);
-    EdgeTab t;
-    t.key = etab_.as<unsigned long long>();
-    t.first = reinterpret_cast<uint32_t*>(t.key + cap);
-    t.last = t.first + cap;
-    t.cnt = t.last + cap;
-    t.slot_of = t.cnt + cap;
-    t.mask = cap - 1;
+    const EdgeTab t = edge_table();
+    const uint64_t cap = t.mask + 1;
     IMPLI_HIP(hipMemsetAsync(t.key, 0xff, (size_t)cap * 8, s));
     IMPLI_HIP(hipMemsetAsync(t.first, 0xff, (size_t)cap * 4, s));
     IMPLI_HIP(hipMemsetAsync(t.last, 0, (size_t)cap * 8, s));   // last + cnt
@@ -655,6 +782,7 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     nrm_.reserve((size_t)(nf + 1) * 12);
     w_.reserve((size_t)(nf + 1) * 4);
     IMPLI_HIP(hipGetLastError());
+    topo_valid_ = true;
 }
 
 void Ob02::store_pointset(const char* key, const float* d, int64_t n, bool keep_first) {
@@ -668,6 +796,7 @@ void Ob02::store_pointset(const char* key, const float* d, int64_t n, bool keep_
 
 void Ob02::vertex_resampling(float c) {
     if (!nf) return;
+    if (!topo_valid_) build_topology();
     store_pointset("pre_resampling_vertices", verts_.as<float>(), nv, true);   // vertex_resampling.hpp:176-180
     DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), verts_.as<float>(),
                  faces_.as<int32_t>(), nf, cen_.as<float>(), nrm_.as<float>());
@@ -692,6 +821,7 @@ float Ob02::average_edge_length() {
 
 void Ob02::centroids_projection(bool enable_qem) {
     if (!nf) return;
+    if (!topo_valid_) build_topology();
     const float avg = average_edge_length();
     avg_edge_ = avg;
     const std::vector<float> alphas = make_alpha_list((float)(avg * 1.0), (float)(0.001 * 1.0), avg, 20);
@@ -748,6 +878,87 @@ void Ob02::centroids_projection(bool enable_qem) {
         IMPLI_HIP(hipGetLastError());
         store_pointset("post_qem_verts", verts_.as<float>(), nv, false);
     }
+}
+
+// z^(kL) mod P for k = 0..63 and z^(64 L h) mod P for h = 0..H-1 (constant tables, grown on demand)
+void Ob02::rand_tables(int64_t lanes) {
+    static std::vector<uint32_t> lo, hi;
+    if (lo.empty()) {
+        uint32_t step[31];
+        rand_jump_poly(kRandL, step);
+        lo.assign(64 * 31, 0u);
+        lo[0] = 1;
+        for (int k = 1; k < 64; ++k) rand_poly_mulmod(&lo[31 * (k - 1)], step, &lo[31 * k]);
+    }
+    const int64_t H = (lanes + 63) / 64;
+    if ((int64_t)hi.size() < 31 * H) {
+        uint32_t step[31];
+        rand_jump_poly((uint64_t)kRandL * 64, step);
+        int64_t h = (int64_t)hi.size() / 31;
+        if (h == 0) {
+            hi.assign(31, 0u);
+            hi[0] = 1;
+            h = 1;
+        }
+        hi.resize((size_t)(31 * H));
+        for (; h < H; ++h) rand_poly_mulmod(&hi[31 * (h - 1)], step, &hi[31 * h]);
+    }
+    if (rand_hi_rows_ < H) {
+        rtab_.reserve((size_t)(64 + H) * 31 * 4);
+        IMPLI_HIP(hipMemcpyAsync(rtab_.p, lo.data(), lo.size() * 4, hipMemcpyHostToDevice, s));
+        IMPLI_HIP(hipMemcpyAsync(rtab_.as<uint32_t>() + 64 * 31, hi.data(), (size_t)H * 31 * 4, hipMemcpyHostToDevice, s));
+        IMPLI_HIP(hipStreamSynchronize(s));   // the host vectors may grow (and move) later
+        rand_hi_rows_ = H;
+    }
+}
+
+void Ob02::add_rand_noise(float amplitude) {
+    const int64_t n = 3 * nv;
+    if (!n) return;
+    GlibcRand& g = process_rand();
+    uint32_t xw[61];
+    g.extended_window(xw);
+    const int64_t lanes = (n + kRandL - 1) / kRandL;
+    rand_tables(lanes);
+    uint32_t* d = misc_.as<uint32_t>() + 16;
+    IMPLI_HIP(hipMemcpyAsync(d, xw, sizeof xw, hipMemcpyHostToDevice, s));
+    k_rand_noise<<<blocks_for(lanes), 256, 0, s>>>(verts_.as<float>(), n, d, rtab_.as<uint32_t>(),
+                                                   rtab_.as<uint32_t>() + 64 * 31, amplitude);
+    IMPLI_HIP(hipGetLastError());
+    g.skip((uint64_t)n);
+    IMPLI_HIP(hipStreamSynchronize(s));   // xw is a stack copy
+}
+
+void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cpp:1314-1367)
+    if (!topo_valid_) build_topology();
+    int64_t added = 0;
+    if (nf) {
+        const EdgeTab t = edge_table();
+        const uint64_t cap = t.mask + 1;
+        DevBuf& cnt = w_;                   // per-face new midpoints (resampling weights are dead here)
+        deg_.reserve((size_t)(nf + 2) * 4);
+        pend_.reserve((size_t)(cap + 1) * 4);
+        k_sub_count<<<blocks_for(nf), 256, 0, s>>>(nf, t, cnt.as<uint32_t>());
+        k_scan_u32<<<1, 1024, 0, s>>>(cnt.as<uint32_t>(), deg_.as<uint32_t>(), nf);
+        uint32_t tot = 0;
+        IMPLI_HIP(hipMemcpyAsync(&tot, deg_.as<uint32_t>() + nf, 4, hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+        added = tot;
+        const int64_t nvt = nv + added;
+        vnew_.reserve((size_t)(nvt + 1) * 12);
+        fnew_.reserve((size_t)(4 * nf + 1) * 12);
+        if (nv) IMPLI_HIP(hipMemcpyAsync(vnew_.p, verts_.p, (size_t)nv * 12, hipMemcpyDeviceToDevice, s));
+        k_sub_verts<<<blocks_for(nf), 256, 0, s>>>(verts_.as<float>(), faces_.as<int32_t>(), nf, nv, t, deg_.as<uint32_t>(),
+                                                   vnew_.as<float>(), pend_.as<uint32_t>());
+        k_sub_faces<<<blocks_for(nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, t, pend_.as<uint32_t>(), fnew_.as<int32_t>());
+        IMPLI_HIP(hipGetLastError());
+        std::swap(verts_, vnew_);
+        std::swap(faces_, fnew_);
+        nv = nvt;
+        nf = 4 * nf;
+        topo_valid_ = false;
+    }
+    add_rand_noise(amplitude);
 }
 
 void Ob02::fetch(float* verts, int32_t* faces) {

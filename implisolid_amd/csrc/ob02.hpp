@@ -1,4 +1,4 @@
-// ob02.hpp -- the Ohtake-Belyaev refinement loop on the GPU (polygonizer steps 1 and 2).
+// ob02.hpp -- the Ohtake-Belyaev refinement loop on the GPU (polygonizer steps 1-3).
 #pragma once
 #include <map>
 #include <string>
@@ -7,6 +7,8 @@
 #include "engine.hpp"
 
 namespace impli {
+
+struct EdgeTab;   // ob02.hip: open-addressed (vmin, vmax) table of the current faces
 
 class Ob02 {
 public:
@@ -17,6 +19,11 @@ public:
     void vertex_resampling(float c);
     // step 2: centroids_projection (centroids_projection.cpp:1219-1311)
     void centroids_projection(bool enable_qem);
+    // step 3: my_subdiv_ (centroids_projection.cpp:1314-1367): 1-to-4 split of every face, then
+    // randomize_verts noise from the process-global glibc rand() (host.hpp GlibcRand)
+    void subdivide(float amplitude);
+    int64_t n_verts() const { return nv; }
+    int64_t n_faces() const { return nf; }
     // blocking copy of the current mesh to host
     void fetch(float* verts, int32_t* faces);
     const std::map<std::string, std::vector<float>>& pointsets() const { return pointsets_; }
@@ -26,13 +33,19 @@ public:
 
 private:
     void store_pointset(const char* key, const float* d, int64_t n, bool keep_first);
+    void build_topology();
+    EdgeTab edge_table();
+    void rand_tables(int64_t lanes);
+    void add_rand_noise(float amplitude);
     float average_edge_length();
 
     Engine& E;
     hipStream_t s;
     int64_t nv = 0, nf = 0;
     DevBuf verts_, faces_, vnew_, cen_, nrm_, w_, fof_, uoff_, ulst_, etab_, deg_, proj_, grad_, fn_, norms_,
-        alphas_, pert_, pend_, misc_;
+        alphas_, pert_, pend_, misc_, fnew_, rtab_;
+    bool topo_valid_ = false;
+    int64_t rand_hi_rows_ = 0;
     float avg_edge_ = 0.f;
     uint32_t cap_hits_ = 0;
     std::map<std::string, std::vector<float>> pointsets_;

@@ -20,16 +20,16 @@ def st(scale, tx, ty, tz):
 
 
 def mc_settings(resolution, box=1.0, *, vresampl_iters=0, vresampl_c=1.0, projection=0, qem=0,
-                overall_repeats=1):
+                overall_repeats=1, subdiv=0, post_subdiv_noise=0):
     return {
         "box": {"xmin": -box, "xmax": box, "ymin": -box, "ymax": box, "zmin": -box, "zmax": box},
         "resolution": resolution,
         "vresampl": {"iters": vresampl_iters, "c": vresampl_c},
         "projection": {"enabled": projection},
         "qem": {"enabled": qem},
-        "subdiv": {"enabled": 0},
+        "subdiv": {"enabled": subdiv},
         "overall_repeats": overall_repeats,
-        "debug": {"post_subdiv_noise": 0},
+        "debug": {"post_subdiv_noise": post_subdiv_noise},
     }
 
 

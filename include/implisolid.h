@@ -86,6 +86,14 @@ void implisolid_set_error_mode(int mode);
  * the mesh is bit-identical). */
 void implisolid_set_pruning(int level);
 
+/* Additive, host only: the library's process-global glibc rand() generator, which the subdivision
+ * noise draws from (randomize_verts, basic_functions.hpp:551-557, calls the C library's rand()).
+ * It starts in glibc's unseeded state (srand(1)); implisolid_srand/implisolid_rand behave as
+ * srand/rand; implisolid_rand_skip(n) discards n draws (jump-ahead, O(log n)). */
+void implisolid_srand(unsigned seed);
+int implisolid_rand(void);
+void implisolid_rand_skip(uint64_t n);
+
 /* Additive, host only: the parsed mc-settings (polygoniser_settings.hpp:147-305 semantics).
  * ints = resolution, ignore_root_matrix, overall_repeats, vresampl.iters, projection, qem, subdiv;
  * floats = vresampl.c, debug.post_subdiv_noise.  0, or -1 with implisolid_last_error() set where

@@ -86,6 +86,11 @@ def lib():
                                            ctypes.c_int64, fp]
         L.or_centroids_projection.argtypes = [npp, ctypes.c_int, fp, ctypes.c_int64, ip, ctypes.c_int64,
                                               ctypes.c_int, fp, fp]
+        L.or_subdivide.argtypes = [fp, ctypes.c_int64, ip, ctypes.c_int64, ctypes.c_float,
+                                   ctypes.POINTER(fp), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ip)]
+        L.or_srand.argtypes = [ctypes.c_uint]
+        L.or_rand.restype = ctypes.c_int
+        L.or_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -264,6 +269,34 @@ def centroids_projection(tree, verts, faces, enable_qem):
     return v, cen, float(avg[0])
 
 
+def srand(seed):
+    """glibc srand() of this process (the state randomize_verts' rand() calls draw from)."""
+    lib().or_srand(int(seed))
+
+
+def rand():
+    return int(lib().or_rand())
+
+
+def subdivide(verts, faces, amplitude):
+    """my_subdiv_ (centroids_projection.cpp:1314-1367): 1-to-4 subdivision + randomize_verts noise
+    drawn from this process's glibc rand()."""
+    v = np.ascontiguousarray(verts, dtype=np.float32)
+    f = np.ascontiguousarray(faces, dtype=np.int32)
+    vo = ctypes.POINTER(ctypes.c_float)()
+    fo = ctypes.POINTER(ctypes.c_int32)()
+    n = ctypes.c_int64(0)
+    if lib().or_subdivide(_fp(v), v.shape[0], _ip(f), f.shape[0], float(np.float32(amplitude)),
+                          ctypes.byref(vo), ctypes.byref(n), ctypes.byref(fo)):
+        raise MemoryError
+    nv, nf = n.value, 4 * f.shape[0]
+    V = np.ctypeslib.as_array(vo, shape=(nv * 3,)).copy().reshape(-1, 3) if nv else np.zeros((0, 3), np.float32)
+    F = np.ctypeslib.as_array(fo, shape=(nf * 3,)).copy().reshape(-1, 3) if nf else np.zeros((0, 3), np.int32)
+    lib().or_free(ctypes.cast(vo, ctypes.c_void_p))
+    lib().or_free(ctypes.cast(fo, ctypes.c_void_p))
+    return V.astype(np.float32), F.astype(np.int32)
+
+
 # ---------------------------------------------------------------------------------------------
 # polygoniser_settings.hpp:147-305 parse_mc_properties_json
 class MCSettings:
@@ -349,7 +382,8 @@ def parse_mc_settings(text):
 
 def polygonize(shape_json, mc_json, taps=None):
     """grand_algorithm (mcc2.cpp:309-444): MC, then overall_repeats x [resampling x iters;
-    projection (+QEM)].  Subdivision (step 3) is outside the implemented scope."""
+    projection (+QEM); subdivision when enabled and (overall_repeats <= 1 or last)].  Subdivision
+    noise draws from this process's glibc rand() (call srand() first for a fixed sequence)."""
     s = parse_mc_settings(mc_json)
     tree = mp5_to_nodes(shape_json, s.ignore_root_matrix)
     v, f = marching_cubes(tree, s.resolution, s.box)
@@ -363,5 +397,9 @@ def polygonize(shape_json, mc_json, taps=None):
             if taps is not None:
                 taps.setdefault("post_p_centroids", []).append(cen)
         if s.subdiv and (s.overall_repeats <= 1 or rep == s.overall_repeats - 1):
-            raise NotImplementedError("subdivision (polygonize_step_3) is outside the implemented scope")
+            # polygonize_step_3 (polygonizer_algorithm_ob02.hpp:119-157): REAL actual_noise =
+            # is_last ? post_subdiv_noise * 10.0f : 0
+            is_last = rep == s.overall_repeats - 1
+            noise = np.float32(s.post_subdiv_noise * np.float32(10.0)) if is_last else np.float32(0)
+            v, f = subdivide(v, f, noise)
     return v, f

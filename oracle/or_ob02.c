@@ -1,5 +1,5 @@
 /*
- * or_ob02.c -- oracle restatement of the Ohtake-Belyaev loop, steps 1 and 2 (TEST INFRA ONLY).
+ * or_ob02.c -- oracle restatement of the Ohtake-Belyaev loop, steps 1-3 (TEST INFRA ONLY).
  *
  *   step 1  apply_vertex_resampling_to_MC_buffers__VMS   apply_v_s_to_mc_buffers.hpp:280-326
  *           -> process2_vertex_resampling_relaxation_v1  vertex_resampling.hpp:152-225
@@ -7,6 +7,9 @@
  *           -> set_centers_on_surface                    centroids_projection.cpp:421-1214
  *           -> bisection                                 polygoniser/bisection.hpp:117-459
  *           -> vertex_apply_qem                          qem.hpp:321-599 (Eigen JacobiSVD restated)
+ *   step 3  my_subdiv_                                   centroids_projection.cpp:1314-1367
+ *           -> subdivide_multiple_facets_1to4            subdivision/subdiv_1to4.hpp:44-488
+ *           -> randomize_verts                           basic_functions.hpp:551-557 (glibc rand())
  *
  * Intended-semantics decisions (documented in DESIGN.md "reference UB"):
  *  - make_edge_lookup (mesh_algorithms.hpp:50-110) inserts its long key through pair<int,int>, so
@@ -496,3 +499,91 @@ done:
     free(C); free(FN); free(P); free(G); free(off); free(lst);
     return rc;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* step 3: my_subdiv_ (centroids_projection.cpp:1314-1367).  subdivide_given_faces
+   (subdivision/do_subdivision.hpp:26-45) requests every face and returns right after the first
+   subdivide_multiple_facets_1to4 (subdiv_1to4.hpp:44-488); randomize_verts (basic_functions.hpp:551-557)
+   then adds glibc rand() noise.  The midpoint map (std::map keyed by easy_edge, mesh_algorithms.hpp:46)
+   assigns new vertex ids in order of first appearance over (face ascending, e01, e12, e20).
+   easy_edge's base 1e6 (configs.hpp:62) makes keys collide beyond 1e6 vertices; the intended
+   (min, max) identity is used. */
+typedef struct { uint64_t key; int32_t vid; } sub_slot;
+
+static int32_t* sub_lookup(sub_slot* tab, uint64_t mask, uint64_t key, int* inserted) {
+    uint64_t s = (key * 0x9E3779B97F4A7C15ull >> 17) & mask;
+    while (tab[s].key != ~0ull && tab[s].key != key) s = (s + 1) & mask;
+    *inserted = tab[s].key == ~0ull;
+    tab[s].key = key;
+    return &tab[s].vid;
+}
+
+/* Eigen 3.3 lazy 3x3 product T * new_vert_maker (subdiv_1to4.hpp:277-330): coefficient sums are
+   reduced as a0 + (a1 + a2) (Redux.h redux_novec_unroller), zero terms included */
+static inline float mid3(float a0, float a1, float a2, float w0, float w1, float w2) {
+    return a0 * w0 + (a1 * w1 + a2 * w2);
+}
+
+int or_subdivide(const float* verts, int64_t nv, const int32_t* faces, int64_t nf, float amplitude,
+                 float** vout, int64_t* nv_out, int32_t** fout) {
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)(4 * nf + 16)) cap <<= 1;
+    sub_slot* tab = (sub_slot*)malloc(sizeof(sub_slot) * cap);
+    int32_t* mids = (int32_t*)malloc(sizeof(int32_t) * (size_t)(3 * nf + 1));
+    unsigned char* ins = (unsigned char*)malloc((size_t)(3 * nf + 1));
+    if (!tab || !mids || !ins) { free(tab); free(mids); free(ins); return -1; }
+    memset(tab, 0xff, sizeof(sub_slot) * cap);
+    int64_t counter = nv;
+    for (int64_t fi = 0; fi < nf; fi++) {          /* subdiv_1to4.hpp:147-232 */
+        for (int k = 0; k < 3; k++) {
+            const uint64_t a = (uint32_t)faces[3 * fi + k], b = (uint32_t)faces[3 * fi + (k + 1) % 3];
+            const uint64_t key = a <= b ? (a << 32 | b) : (b << 32 | a);
+            int inserted;
+            int32_t* vid = sub_lookup(tab, cap - 1, key, &inserted);
+            if (inserted) *vid = (int32_t)counter++;
+            mids[3 * fi + k] = *vid;
+            ins[3 * fi + k] = (unsigned char)inserted;
+        }
+    }
+    float* V = (float*)malloc(sizeof(float) * 3 * (size_t)(counter + 1));
+    int32_t* F = (int32_t*)malloc(sizeof(int32_t) * 3 * (size_t)(4 * nf + 1));
+    if (!V || !F) { free(tab); free(mids); free(ins); free(V); free(F); return -1; }
+    memcpy(V, verts, sizeof(float) * 3 * (size_t)nv);
+    const float H = 0.5f, O = 0.0f;
+    /* new_vert_maker << H,O,H, H,H,O, O,H,H: columns m01 = (H,H,O), m12 = (O,H,H), m20 = (H,O,H) */
+    const float W[3][3] = {{H, H, O}, {O, H, H}, {H, O, H}};
+    int64_t nvt = nv;
+    for (int64_t fi = 0; fi < nf; fi++) {          /* :277-330 */
+        const float* p0 = verts + 3 * faces[3 * fi];
+        const float* p1 = verts + 3 * faces[3 * fi + 1];
+        const float* p2 = verts + 3 * faces[3 * fi + 2];
+        for (int k = 0; k < 3; k++) {
+            if (!ins[3 * fi + k]) continue;
+            for (int r = 0; r < 3; r++) V[3 * nvt + r] = mid3(p0[r], p1[r], p2[r], W[k][0], W[k][1], W[k][2]);
+            nvt++;
+        }
+    }
+    memcpy(F, faces, sizeof(int32_t) * 3 * (size_t)nf);
+    for (int64_t fi = 0; fi < nf; fi++) {          /* :380-470 */
+        const int32_t v0 = faces[3 * fi], v1 = faces[3 * fi + 1], v2 = faces[3 * fi + 2];
+        const int32_t m01 = mids[3 * fi], m12 = mids[3 * fi + 1], m20 = mids[3 * fi + 2];
+        int32_t* o = F + 3 * fi;
+        o[0] = m12; o[1] = m20; o[2] = m01;
+        o = F + 3 * (nf + 3 * fi);
+        o[0] = v0; o[1] = m01; o[2] = m20;
+        o[3] = v1; o[4] = m12; o[5] = m01;
+        o[6] = v2; o[7] = m20; o[8] = m12;
+    }
+    /* randomize_verts (basic_functions.hpp:551-557): REAL is float, the 0.5 literal is double */
+    for (int64_t i = 0; i < 3 * nvt; i++) {
+        const float q = (float)rand() / (float)RAND_MAX;
+        V[i] = (float)((double)V[i] + ((double)q - 0.5) * (double)amplitude);
+    }
+    free(tab); free(mids); free(ins);
+    *vout = V; *fout = F; *nv_out = nvt;
+    return 0;
+}
+
+void or_srand(unsigned seed) { srand(seed); }
+int or_rand(void) { return rand(); }
+void or_free(void* p) { free(p); }

@@ -73,7 +73,7 @@ void or_mesh_free(or_mesh* m);
 /* the sampled field (res^3, sealed) for inspection: res = resolution + 5 */
 int or_mc_field(const or_node* nodes, int root, int resolution, const float box[6], float* field_out);
 
-/* ---- OB02 (polygonizer_algorithm_ob02.hpp steps 1 and 2) ---- */
+/* ---- OB02 (polygonizer_algorithm_ob02.hpp steps 1-3) ---- */
 /* step 1: apply_vertex_resampling_to_MC_buffers__VMS (apply_v_s_to_mc_buffers.hpp:280-326) */
 int or_vertex_resampling(const or_node* nodes, int root, float c,
                          float* verts, int64_t nv, const int32_t* faces, int64_t nf,
@@ -83,6 +83,14 @@ int or_vertex_resampling(const or_node* nodes, int root, float c,
 int or_centroids_projection(const or_node* nodes, int root,
                             float* verts, int64_t nv, const int32_t* faces, int64_t nf,
                             int enable_qem, float* centroids_out, float* avg_edge_out);
+/* step 3: my_subdiv_ (centroids_projection.cpp:1314-1367): 1-to-4 subdivision of every face, then
+   randomize_verts with glibc rand() (process-global state, see or_srand).  *vout / *fout are
+   malloc'ed (free with or_free). */
+int or_subdivide(const float* verts, int64_t nv, const int32_t* faces, int64_t nf, float amplitude,
+                 float** vout, int64_t* nv_out, int32_t** fout);
+void or_srand(unsigned seed);
+int or_rand(void);
+void or_free(void* p);
 
 #ifdef __cplusplus
 }

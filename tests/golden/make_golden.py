@@ -72,6 +72,31 @@ def main():
                         shape=json.dumps(shape), mc=json.dumps(mc),
                         **{"tap_" + k: np.asarray(a) for k, a in taps.items()})
 
+    # 5. subdivision (step 3): config 1 with subdiv on and the default noise 0.01 (x10 on the last
+    #    repeat), rand() seeded with srand(1); and config 2 at R 24 with subdivision after 3 repeats
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    sub = {}
+    for name, (shape, mc) in [("config1", (scenes.config1()[0], scenes.mc_settings(32, 0.6, subdiv=1,
+                                                                                  post_subdiv_noise=0.01))),
+                              ("config2_r24", (scenes.union_sphere_cube(),
+                                               scenes.mc_settings(24, 1.0, vresampl_iters=1, vresampl_c=0.4,
+                                                                  projection=1, qem=1, overall_repeats=3,
+                                                                  subdiv=1, post_subdiv_noise=0.01)))]:
+        oracle.srand(1)
+        v, f = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+        libc.srand(1)
+        sub[name + "_verts"], sub[name + "_faces"] = v, f
+        sub[name + "_shape"], sub[name + "_mc"] = json.dumps(shape), json.dumps(mc)
+    # the numpy restatement agrees on the MC-only case (subdivision of the MC mesh)
+    shape, mc = scenes.config1()
+    v0, f0 = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    libc.srand(1)
+    d = [libc.rand() for _ in range(3 * sub["config1_verts"].shape[0])]
+    v2, f2 = np_restate.subdivide(v0, f0, np.float32(np.float32(0.01) * np.float32(10.0)), d)
+    assert np.array_equal(f2, sub["config1_faces"]) and np.array_equal(v2.view(np.uint32), sub["config1_verts"].view(np.uint32))
+    np.savez_compressed(os.path.join(HERE, "subdiv.npz"), **sub)
+
     # 4. marching-cubes summaries at larger sizes (counts + SHA-256 of the arrays)
     summary = {}
     for name, sh, R, box in [("config2_mc_r128", scenes.union_sphere_cube(), 128, [-1, 1] * 3),

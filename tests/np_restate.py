@@ -293,3 +293,35 @@ def mc_with_codes(F, w, box, R):
     global _LAST_CODES
     v, f = marching_cubes(F, w, box, R)
     return v, f, _LAST_CODES
+
+
+def subdivide(verts, faces, amplitude, draws):
+    """my_subdiv_ (centroids_projection.cpp:1314-1367), vectorised: subdivide_multiple_facets_1to4
+    (subdiv_1to4.hpp:147-470) numbers midpoints by first appearance of their (min, max) edge over
+    (face ascending; e01, e12, e20); randomize_verts (basic_functions.hpp:551-557) adds
+    (draw / RAND_MAX - 0.5) * amplitude with `draws` the rand() outputs (one per coordinate)."""
+    v = np.asarray(verts, np.float32).reshape(-1, 3)
+    f = np.asarray(faces, np.int64).reshape(-1, 3)
+    nv, nf = v.shape[0], f.shape[0]
+    a, b = f, np.roll(f, -1, axis=1)                      # (v0,v1), (v1,v2), (v2,v0)
+    key = (np.minimum(a, b) << 32 | np.maximum(a, b)).reshape(-1)
+    _, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")
+    rank = np.empty_like(order)
+    rank[order] = np.arange(order.size)
+    mid = (nv + rank[inv]).reshape(nf, 3)
+    src = first[order]                                    # first slot of each new vertex
+    fi, k = src // 3, src % 3
+    p = v[f[fi]]                                          # (n, 3 corners, xyz)
+    H, O = np.float32(0.5), np.float32(0)
+    W = np.array([[H, H, O], [O, H, H], [H, O, H]], np.float32)[k]
+    newv = p[:, 0] * W[:, 0:1] + (p[:, 1] * W[:, 1:2] + p[:, 2] * W[:, 2:3])
+    V = np.concatenate([v, newv.astype(np.float32)])
+    m01, m12, m20 = mid[:, 0], mid[:, 1], mid[:, 2]
+    v0, v1, v2 = f[:, 0], f[:, 1], f[:, 2]
+    corner = np.stack([np.stack([v0, m01, m20], 1), np.stack([v1, m12, m01], 1), np.stack([v2, m20, m12], 1)], 1)
+    F = np.concatenate([np.stack([m12, m20, m01], 1), corner.reshape(-1, 3)]).astype(np.int32)
+    d = np.asarray(draws, np.int64)[: V.size].reshape(V.shape)
+    u = d.astype(np.float32) / np.float32(2147483648.0)
+    V = (V.astype(np.float64) + (u.astype(np.float64) - 0.5) * np.float64(np.float32(amplitude))).astype(np.float32)
+    return V, F

@@ -130,6 +130,64 @@ def test_golden_mc_summaries(oracle):
     assert 56684 - 113360 // 2 == 4          # Euler characteristic: two sphere-like components
 
 
+def test_golden_subdivision(oracle):
+    """Step 3 (my_subdiv_) through polygonize with the oracle's glibc rand() seeded by srand(1)."""
+    g = np.load(os.path.join(GOLDEN, "subdiv.npz"))
+    for name in ["config1", "config2_r24"]:
+        oracle.srand(1)
+        v, f = oracle.polygonize(str(g[name + "_shape"]), str(g[name + "_mc"]))
+        assert np.array_equal(f, g[name + "_faces"]) and np.array_equal(_u32(v), _u32(g[name + "_verts"])), name
+    # config 1: V' = V + E, F' = 4F on a closed mesh (E = 3F/2)
+    assert g["config1_verts"].shape == (3318 + 3 * 6632 // 2, 3) and g["config1_faces"].shape == (4 * 6632, 3)
+
+
+def _ragged_mesh(rng, nv=40, nf=90):
+    v = rng.uniform(-1, 1, (nv, 3)).astype(np.float32)
+    f = rng.integers(0, nv, (nf, 3)).astype(np.int32)
+    f[5] = [3, 3, 7]                     # degenerate face: edge (3, 3)
+    f[6] = [7, 3, 3]
+    return v, f
+
+
+@pytest.mark.parametrize("amp", [0.0, 0.1, 3.0])
+def test_subdivide_oracle_matches_numpy(oracle, amp):
+    """The oracle's 1-to-4 subdivision + randomize_verts == the vectorised numpy restatement, on
+    the config-1 mesh and on a ragged mesh (boundary edges, edges in > 2 faces, degenerate faces)."""
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    shape, mc = __import__("implisolid_amd.scenes", fromlist=["x"]).config1()
+    v0, f0 = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    for v, f in [(v0, f0), _ragged_mesh(np.random.default_rng(3))]:
+        oracle.srand(99)
+        V, F = oracle.subdivide(v, f, amp)
+        libc.srand(99)
+        d = [libc.rand() for _ in range(3 * V.shape[0])]
+        V2, F2 = np_restate.subdivide(v, f, amp, d)
+        assert np.array_equal(F, F2) and np.array_equal(_u32(V), _u32(V2))
+    # empty mesh: no faces, the vertices still get their noise
+    oracle.srand(5)
+    V, F = oracle.subdivide(v0[:10], np.zeros((0, 3), np.int32), 1.0)
+    libc.srand(5)
+    V2, _ = np_restate.subdivide(v0[:10], np.zeros((0, 3), np.int32), 1.0, [libc.rand() for _ in range(30)])
+    assert F.shape == (0, 3) and np.array_equal(_u32(V), _u32(V2))
+
+
+def test_library_rand_matches_glibc(impli):
+    """The library's process-global rand() (host.hpp GlibcRand) == glibc rand() after the same
+    srand, including the O(log n) jump-ahead the GPU noise kernel's lanes use."""
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    for seed in [0, 1, 7, 123456789, 0xDEADBEEF]:
+        libc.srand(seed)
+        impli.srand(seed)
+        assert [libc.rand() for _ in range(2000)] == [impli.rand() for _ in range(2000)], seed
+        for n in [1, 30, 31, 62, 248, 15872, 100003]:
+            for _ in range(n):
+                libc.rand()
+            impli.rand_skip(n)
+            assert libc.rand() == impli.rand(), (seed, n)
+
+
 # ---- mesh properties ------------------------------------------------------------------------------
 @pytest.mark.parametrize("name", ["sphere", "union_sphere_cube", "config3_tree"])
 def test_mc_output_is_closed_edge_manifold(oracle, name):

@@ -384,3 +384,64 @@ def test_node_addon_config1_gpu(impli):
         v = np.fromfile(vp, np.float32).reshape(-1, 3)
         f = np.fromfile(fp, np.uint32).reshape(-1, 3).astype(np.int32)
     assert np.array_equal(f, g["faces"]) and np.array_equal(v.view(np.uint32), g["verts"].view(np.uint32))
+
+
+# ---- step 3: subdivision (my_subdiv_, centroids_projection.cpp:1314-1367) -------------------------
+def _subdiv_compare(impli, oracle, shape, mc, seed):
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    impli.srand(seed)
+    v, f = impli.make_geometry(shape, mc)
+    oracle.srand(seed)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    assert np.array_equal(f, fr)
+    bad = np.flatnonzero((v.view(np.uint32) != vr.view(np.uint32)).any(1))
+    assert bad.size == 0, (bad.size, bad[:10], np.abs(v - vr).max())
+    # both generators continue from the same state
+    assert [impli.rand() for _ in range(5)] == [libc.rand() for _ in range(5)]
+    return v, f
+
+
+@pytest.mark.parametrize("noise", [0.0, 0.01, 0.5])
+def test_subdivision_config1(impli, oracle, noise):
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(32, 0.6, subdiv=1, post_subdiv_noise=noise)
+    v, f = _subdiv_compare(impli, oracle, scenes.config1()[0], mc, 1)
+    assert f.shape == (4 * 6632, 3) and v.shape == (3318 + 3 * 6632 // 2, 3)
+
+
+@pytest.mark.parametrize("R", [24, 96])
+def test_subdivision_after_ob02(impli, oracle, R):
+    """config 2's loop with subdivision on the last of 3 repeats (polygonize_step_3, noise x10)."""
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(R, 1.0, vresampl_iters=1, vresampl_c=0.4, projection=1, qem=1, overall_repeats=3,
+                            subdiv=1, post_subdiv_noise=0.01)
+    _subdiv_compare(impli, oracle, scenes.union_sphere_cube(), mc, 20251015)
+
+
+def test_subdivision_mc_only_large_and_empty(impli, oracle):
+    """R 160 (~4k noise lanes: every row of the jump table) and an empty mesh (noise on nothing)."""
+    from implisolid_amd import scenes
+    shape = scenes.union_sphere_cube()
+    _subdiv_compare(impli, oracle, shape, scenes.mc_settings(160, 1.0, subdiv=1, post_subdiv_noise=0.02), 3)
+    far = {"type": "iellipsoid", "matrix": scenes.st(0.25, 5, 5, 5)}
+    v, f = _subdiv_compare(impli, oracle, far, scenes.mc_settings(16, 1.0, subdiv=1, post_subdiv_noise=0.01), 4)
+    assert v.shape[0] == 0 and f.shape[0] == 0
+
+
+def test_subdivision_repeats_without_last(impli, oracle):
+    """overall_repeats 1 subdivides once with noise; default settings (subdiv on) go through it."""
+    from implisolid_amd import scenes
+    shape = scenes.config3(24)[0]
+    mc = scenes.mc_settings(24, 1.0, vresampl_iters=1, vresampl_c=0.4, projection=1, qem=0, overall_repeats=1,
+                            subdiv=1, post_subdiv_noise=0.01)
+    _subdiv_compare(impli, oracle, shape, mc, 77)
+
+
+def test_golden_subdivision_gpu(impli):
+    g = np.load(_golden("subdiv.npz"))
+    for name in ["config1", "config2_r24"]:
+        impli.srand(1)
+        v, f = impli.make_geometry(str(g[name + "_shape"]), str(g[name + "_mc"]))
+        assert np.array_equal(f, g[name + "_faces"]), name
+        assert np.array_equal(v.view(np.uint32), g[name + "_verts"].view(np.uint32)), name
