@@ -150,13 +150,54 @@ struct Builder {
         }
     }
 
+    // raw parameter row (not inverted) for primitives that carry parameters (Instr::prm)
+    int add_params(const float* v, int n) {
+        if (p.n_mats >= kMaxProgram) throw InputError("MP5 tree too large");
+        float row[12] = {};
+        std::memcpy(row, v, sizeof(float) * (size_t)n);
+        std::memcpy(p.mats[p.n_mats], row, sizeof row);
+        return p.n_mats++;
+    }
+
     // A "subtree" pushes exactly one value; it sees the parent's local point on top of the stack.
-    void leaf(NodeType t, const float m[12]) {
+    void leaf(NodeType t, const float m[12], const float* prm = nullptr, int nprm = 0) {
         const int k = add_matrix(m);
+        const int pr = prm ? add_params(prm, nprm) : 0;
         emit(OP_XFORM, t, k);
         push_point();
-        emit(OP_PRIM, t, k);
+        const int pc = emit(OP_PRIM, t, k);
+        p.instr[pc].prm = (int16_t)pr;
         pop_point();
+    }
+
+    // screw::getScrewParameters (screw.hpp:380-470) + constructor (:222-330), in float: outer =
+    // |v| = 1 for v = (0,1,0), inner = outer / delta_ratio, r0 = inner / 2, delta = outer / 2 -
+    // inner / 2, twist_rate = pitch.  ptree get_child/get throw on the missing keys (values unused).
+    static void screw_params(const Json& d, float prm[3]) {
+        for (const char* k : {"matrix", "v", "pitch", "profile", "end_type", "delta_ratio"})
+            if (!d.find(k)) throw InputError(std::string("screw: missing \"") + k + "\"");
+        float pitch, ratio;
+        if (!d.get_float("pitch", &pitch) || !d.get_float("delta_ratio", &ratio))
+            throw InputError("screw: pitch and delta_ratio must be numbers");
+        const float outer = 1.0f, inner = outer / ratio;
+        prm[0] = pitch;
+        prm[1] = inner / 2;
+        prm[2] = outer / 2 - inner / 2;
+    }
+    // half_plane constructor (half_plane.hpp:96-125): plane_vector / |plane_vector| in float, the
+    // norm reduced a0 + (a1 + a2); prm = {unit vector, plane_point}
+    static void half_plane_params(const float pv[3], const float pp[3], float prm[6]) {
+        const float n = std::sqrt(pv[0] * pv[0] + (pv[1] * pv[1] + pv[2] * pv[2]));
+        for (int k = 0; k < 3; ++k) {
+            prm[k] = pv[k] / n;
+            prm[3 + k] = pp[k];
+        }
+    }
+    static void vec3(const Json& d, const char* key, float out[3]) {
+        const Json* a = d.find(key);
+        if (!a || a->kind != Json::Array || a->items.size() < 3) throw InputError(std::string("half_plane: bad \"") + key + "\"");
+        for (int k = 0; k < 3; ++k)
+            if (!a->items[k].second.as_float(&out[k])) throw InputError(std::string("half_plane: bad \"") + key + "\"");
     }
     void push_point() { if (++depth > max_depth) max_depth = depth; if (depth >= kMaxDepth) throw InputError("MP5 tree too deep"); }
     void pop_point() { --depth; }
@@ -223,9 +264,46 @@ struct Builder {
                 [&] { node(ch->items[0].second, false); }, [&] { node(ch->items[1].second, false); });
             return;
         }
-        static const char* unsupported[] = {"tetrahedron", "inf_screw", "screw_diff_two_plane", "screw", "sdf_3d",
-                                            "half_plane", "screw_gradient_wrong", "top_bottom_lid", "rawjscode",
-                                            "meta_balls", "extrusion"};
+        if (t == "screw" || t == "inf_screw" || t == "screw_diff_two_plane") {
+            float prm[3];
+            screw_params(d, prm);
+            matrix12(d, m);
+            if (ignore) std::memcpy(m, eye, sizeof m);
+            if (t == "inf_screw") {   // object_factory.hpp:189-215: the screw under its own matrix
+                leaf(NT_SCREW, m, prm, 3);
+                return;
+            }
+            if (t == "screw") {       // :304-351: subtract(screw(identity), top_bottom_lid)
+                csg(NT_DIFFERENCE, m, [&] { leaf(NT_SCREW, eye, prm, 3); }, [&] { leaf(NT_LID, eye); });
+                return;
+            }
+            // :216-302: subtract(subtract(screw, half_plane z >= 0.25), half_plane z <= -0.25)
+            const float up[3] = {0, 0, 1}, upp[3] = {0, 0, 0.25f}, dn[3] = {0, 0, -1}, dnp[3] = {0, 0, -0.25f};
+            float top[6], bot[6];
+            half_plane_params(up, upp, top);
+            half_plane_params(dn, dnp, bot);
+            csg(NT_DIFFERENCE, m,
+                [&] { csg(NT_DIFFERENCE, eye, [&] { leaf(NT_SCREW, eye, prm, 3); }, [&] { leaf(NT_HALF_PLANE, eye, top, 6); }); },
+                [&] { leaf(NT_HALF_PLANE, eye, bot, 6); });
+            return;
+        }
+        if (t == "top_bottom_lid") {   // :480-506: the matrix is read (get_child) and never applied
+            matrix12(d, m);
+            leaf(NT_LID, eye);
+            return;
+        }
+        if (t == "half_plane") {       // :396-434
+            float pv[3], pp[3], prm[6];
+            vec3(d, "plane_vector", pv);
+            vec3(d, "plane_point", pp);
+            matrix12(d, m);
+            if (ignore) std::memcpy(m, eye, sizeof m);
+            half_plane_params(pv, pp, prm);
+            leaf(NT_HALF_PLANE, m, prm, 6);
+            return;
+        }
+        static const char* unsupported[] = {"tetrahedron", "sdf_3d", "screw_gradient_wrong", "rawjscode", "meta_balls",
+                                            "extrusion"};
         for (auto* u : unsupported)
             if (t == u) throw InputError("MP5 type \"" + t + "\" is outside the implemented node families");
         throw InputError("Invalid object you asked for: \"" + t + "\"");

@@ -211,7 +211,209 @@ __device__ __forceinline__ V3 dm_g(float x, float y, float z) {
     return V3{-2.f * (x - 0.f) / a2, -2.f * (y - 0.f) / b2, 2.f * (z - 0.f) / c2};
 }
 
-__device__ __forceinline__ float prim_f(int t, const float* __restrict__ tab, float x, float y, float z) {
+// ---- glibc 2.35 float math used by the screw family -----------------------------------------
+// sinf: sysdeps/ieee754/flt-32/s_sinf.c + sincosf.h, the x86_64 FMA variant (s_sinf-fma.c, chosen
+// on every FMA-capable host): the double polynomial and the fast reduction are fma-contracted.
+// atanf / atan2f: fdlibm (s_atanf.c, e_atan2f.c).  All three are checked bit-exact against the
+// host libm by the oracle's restatement (or_libm.c; sinf and atanf over all 2^32 patterns).
+__device__ __forceinline__ uint32_t abstop12(float f) { return (__float_as_uint(f) >> 20) & 0x7ffu; }
+
+__device__ __forceinline__ uint32_t inv_pio4(int i) {   // __inv_pio4: 32-bit windows of 2/pi
+    const uint32_t T[24] = {0xa2, 0xa2f9, 0xa2f983, 0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+                            0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd,
+                            0xf534ddc0, 0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43,
+                            0x993c4390, 0x3c439041};
+    return T[i];
+}
+
+// sinf_poly; __sincosf_table[1] (n & 2) is table 0 with the cosine coefficients negated
+__device__ __forceinline__ float sinf_poly(double x, double x2, int n, bool neg) {
+    if ((n & 1) == 0) {
+        const double x3 = x * x2;
+        const double s1 = __fma_rn(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
+        const double x7 = x3 * x2;
+        const double s = __fma_rn(x3, -0x1.555545995a603p-3, x);
+        return (float)__fma_rn(x7, s1, s);
+    }
+    const double k = neg ? -1.0 : 1.0;
+    const double x4 = x2 * x2;
+    const double c2 = __fma_rn(x2, k * 0x1.99343027bf8c3p-16, k * -0x1.6c087e89a359dp-10);
+    const double c1 = __fma_rn(x2, k * -0x1.ffffffd0c621cp-2, k * 0x1p0);
+    const double x6 = x4 * x2;
+    const double c = __fma_rn(x4, k * 0x1.55553e1068f19p-5, c1);
+    return (float)__fma_rn(x6, c2, c);
+}
+
+__device__ __forceinline__ float glibc_sinf(float y) {
+    double x = y;
+    int n;
+    const uint32_t top = abstop12(y);
+    if (top < 0x3f4u) {                                   // |y| < pi/4
+        if (top < 0x398u) return y;                       // |y| < 2^-12
+        return sinf_poly(x, x * x, 0, false);
+    }
+    double s;
+    if (top < 0x42fu) {                                   // |y| < 120: reduce_fast
+        const double r = x * 0x1.45f306dc9c883p+23;
+        n = ((int32_t)r + 0x800000) >> 24;
+        x = __fma_rn(-(double)n, 0x1.921fb54442d18p+0, x);
+        s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+        return sinf_poly(x * s, x * x, n, (n & 2) != 0);
+    }
+    if (top < 0x7f8u) {                                   // reduce_large
+        uint32_t xi = __float_as_uint(y);
+        const int sign = (int)(xi >> 31);
+        const int idx = (int)((xi >> 26) & 15);
+        const int shift = (int)((xi >> 23) & 7);
+        xi = (xi & 0xffffffu) | 0x800000u;
+        xi <<= shift;
+        uint64_t res0 = (uint64_t)(xi * inv_pio4(idx));
+        const uint64_t res1 = (uint64_t)xi * inv_pio4(idx + 4);
+        const uint64_t res2 = (uint64_t)xi * inv_pio4(idx + 8);
+        res0 = (res2 >> 32) | (res0 << 32);
+        res0 += res1;
+        const uint64_t nn = (res0 + (1ull << 61)) >> 62;
+        res0 -= nn << 62;
+        n = (int)nn;
+        x = (double)(int64_t)res0 * 0x1.921fb54442d18p-62;
+        const int q = (n + sign) & 3;
+        s = (q == 1 || q == 2) ? -1.0 : 1.0;
+        return sinf_poly(x * s, x * x, n, (q & 2) != 0);
+    }
+    return (y - y) / (y - y);
+}
+
+__device__ __forceinline__ float glibc_atanf(float x) {
+    const float hi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+    const float lo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const int32_t hx = (int32_t)__float_as_uint(x), ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? hi[3] + lo[3] : -hi[3] - lo[3];
+    }
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000) return x;
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
+            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
+        } else {
+            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
+            else { id = 3; x = -1.0f / x; }
+        }
+    }
+    const float z = x * x, w = z * z;
+    const float s1 = z * (3.3333334327e-01f + w * (1.4285714924e-01f + w * (9.0908870101e-02f +
+                     w * (6.6610731184e-02f + w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
+    const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
+                     w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float h = id == 0 ? hi[0] : id == 1 ? hi[1] : id == 2 ? hi[2] : hi[3];
+    const float l = id == 0 ? lo[0] : id == 1 ? lo[1] : id == 2 ? lo[2] : lo[3];
+    const float r = h - ((x * (s1 + s2) - l) - x);
+    return hx < 0 ? -r : r;
+}
+
+__device__ __forceinline__ float glibc_atan2f(float y, float x) {
+    const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+                pi_lo = -8.7422776573e-08f;
+    const int32_t hx = (int32_t)__float_as_uint(x), ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)__float_as_uint(y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return glibc_atanf(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) return m <= 1 ? y : (m == 2 ? pi + tiny : -pi - tiny);
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000)
+            return m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny : m == 2 ? 3.0f * pi_o_4 + tiny : -3.0f * pi_o_4 - tiny;
+        return m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = glibc_atanf(fabsf(y / x));
+    if (m == 0) return z;
+    if (m == 1) return __uint_as_float(__float_as_uint(z) ^ 0x80000000u);
+    if (m == 2) return pi - (z - pi_lo);
+    return (z - pi_lo) - pi;
+}
+
+// ---- screw, screw.hpp:98-150 at its constructor's constants (u, v, w = the axes, A = (0,0,-0.5),
+//      UVW = I; the factory forces the identity transformation_matrix, object_factory.hpp:304-351).
+//      prm = {twist_rate, r0, delta}.  Eigen orders: GEMV t = (x - A) w into a zeroed result; outer
+//      product p = w t + A; GEMM ab = UVW^-1 (x - p) accumulated from zero; norm a0 + (a1 + a2).
+__device__ __forceinline__ float screw_f(const float* __restrict__ prm, float x, float y, float z) {
+    const float tw = prm[0], r0 = prm[1], delta = prm[2];
+    const float a0 = x - 0.f, a1 = y - 0.f, a2 = z - (-0.5f);
+    const float t = ((0.f + a0 * 0.f) + a1 * 0.f) + a2 * 1.f;
+    const float p0 = 0.f * t + 0.f, p1 = 0.f * t + 0.f, p2 = 1.f * t + (-0.5f);
+    const float d0 = x - p0, d1 = y - p1, d2 = z - p2;
+    const float ab0 = 0.f + (((0.f + 1.f * d0) + 0.f * d1) + 0.f * d2);
+    const float ab1 = 0.f + (((0.f + 0.f * d0) + 1.f * d1) + 0.f * d2);
+    const float theta = glibc_atan2f(ab1, ab0);
+    const float r = sqrtf(d0 * d0 + (d1 * d1 + d2 * d2));
+    const float pi = (float)3.1415926535897, pi2 = pi * 2;   // screw.hpp:20, :140
+    const float ph = t / tw - theta / pi2;
+    return (-r + r0) + delta * glibc_sinf(ph * 2 * pi);       // phi (screw.hpp:29-36)
+}
+// screw.hpp:152-160 (sympy gradient) at the same constants, with the C++ type of every
+// sub-expression: std::pow(float, 2) -> exact double square, atan2(float, float) -> atanf path,
+// cos(double) -> double cos (device libm; the only call not restated bit for bit), M_PI double.
+__device__ __forceinline__ V3 screw_g(const float* __restrict__ prm, float x, float y, float z) {
+    const double kPi = 3.14159265358979323846;
+    const float tw = prm[0], delta = prm[2];
+    const float ax = 0.f, ay = 0.f, az = -0.5f, wx = 0.f, wy = 0.f, wz = 1.f, phi0 = 0.f;
+    const float u00 = 1.f, u01 = 0.f, u02 = 0.f, u10 = 0.f, u11 = 1.f, u12 = 0.f;
+    const float s = (wx * (-ax + x) + wy * (-ay + y)) + wz * (-az + z);
+    const float X1 = (-ax - wx * s) + x, Y1 = (-ay - wy * s) + y, Z1 = (-az - wz * s) + z;
+    const float U0 = (u00 * X1 + u01 * Y1) + u02 * Z1;
+    const float U1 = (u10 * X1 + u11 * Y1) + u12 * Z1;
+    const float nU1 = ((-u10 * X1) - u11 * Y1) - u12 * Z1;
+    const double G = sq_exact(U0) + sq_exact(U1);
+    const double sq = sqrt((sq_exact(X1) + sq_exact(Y1)) + sq_exact(Z1));
+    const float th = glibc_atan2f(U1, U0);
+    const double cv = cos(kPi * (((double)(2 * phi0) - (double)th / kPi) + (double)((2 * s) / tw)));
+    const double wx2 = sq_exact(wx), wy2 = sq_exact(wy), wz2 = sq_exact(wz);
+    const double pd = kPi * (double)delta;
+    const double cAx = ((double)u00 * (-wx2 + 1) - (double)(u01 * wx * wy)) - (double)(u02 * wx * wz);
+    const double cBx = ((double)u10 * (-wx2 + 1) - (double)(u11 * wx * wy)) - (double)(u12 * wx * wz);
+    const double Ax = -(cAx * (double)nU1 / G + (double)U0 * cBx / G) / kPi + (double)(2 * wx / tw);
+    const double Cx = (double)(-wx * wy * Y1 - wx * wz * Z1) + (1.0 / 2.0) * (-2 * wx2 + 2) * (double)X1;
+    const double cAy = ((double)(-u10 * wx * wy) + (double)u11 * (-wy2 + 1)) - (double)(u12 * wy * wz);
+    const double cBy = ((double)(-u00 * wx * wy) + (double)u01 * (-wy2 + 1)) - (double)(u02 * wy * wz);
+    const double Ay = -((double)U0 * cAy / G + (double)nU1 * cBy / G) / kPi + (double)(2 * wy / tw);
+    const double Cy = (double)(-wx * wy * X1 - wy * wz * Z1) + (1.0 / 2.0) * (-2 * wy2 + 2) * (double)Y1;
+    const double cAz = (double)(-u10 * wx * wz - u11 * wy * wz) + (double)u12 * (-wz2 + 1);
+    const double cBz = (double)(-u00 * wx * wz - u01 * wy * wz) + (double)u02 * (-wz2 + 1);
+    const double Az = -((double)U0 * cAz / G + (double)nU1 * cBz / G) / kPi + (double)(2 * wz / tw);
+    const double Cz = (double)(-wx * wz * X1 - wy * wz * Y1) + (1.0 / 2.0) * (-2 * wz2 + 2) * (double)Z1;
+    return V3{(float)(pd * Ax * cv - Cx / sq), (float)(pd * Ay * cv - Cy / sq), (float)(pd * Az * cv - Cz / sq)};
+}
+
+// ---- top_bottom_lid.hpp:117-161: std::max(z - 0.5, (z + 0.5) * -1); gradient always (0,0,1)
+__device__ __forceinline__ float lid_f(float z) {
+    const float a = z - 0.5f, b = (z + 0.5f) * -1.f;
+    return (a < b) ? b : a;
+}
+
+// ---- half_plane.hpp:150-190: GEMV (x - plane_point) . plane_vector; prm = {unit pv, pp}
+__device__ __forceinline__ float hp_f(const float* __restrict__ prm, float x, float y, float z) {
+    const float d0 = x - prm[3], d1 = y - prm[4], d2 = z - prm[5];
+    return ((0.f + d0 * prm[0]) + d1 * prm[1]) + d2 * prm[2];
+}
+__device__ __forceinline__ V3 hp_g(const float* __restrict__ prm, float x, float y, float z) {
+    const float k = hp_f(prm, x, y, z) >= 0 ? -1.f : 1.f;
+    return V3{k * prm[0], k * prm[1], k * prm[2]};
+}
+
+__device__ __forceinline__ float prim_f(int t, const float* __restrict__ tab, const float* __restrict__ prm, float x,
+                                        float y, float z) {
     switch (t) {
         case NT_ELLIPSOID: return egg_f(x, y, z);
         case NT_CUBE: return cube_f(tab, x, y, z);
@@ -219,10 +421,13 @@ __device__ __forceinline__ float prim_f(int t, const float* __restrict__ tab, fl
         case NT_CONE: return cone_f(x, y, z);
         case NT_HEART: return heart_f(x, y, z);
         case NT_TORUS: return torus_f(x, y, z);
+        case NT_SCREW: return screw_f(prm, x, y, z);
+        case NT_LID: return lid_f(z);
+        case NT_HALF_PLANE: return hp_f(prm, x, y, z);
         default: return dm_f(x, y, z);
     }
 }
-__device__ __forceinline__ V3 prim_g(int t, float x, float y, float z) {
+__device__ __forceinline__ V3 prim_g(int t, const float* __restrict__ prm, float x, float y, float z) {
     switch (t) {
         case NT_ELLIPSOID: return egg_g(x, y, z);
         case NT_CUBE: return cube_g(x, y, z);
@@ -230,6 +435,9 @@ __device__ __forceinline__ V3 prim_g(int t, float x, float y, float z) {
         case NT_CONE: return cone_g(x, y, z);
         case NT_HEART: return heart_g(x, y, z);
         case NT_TORUS: return torus_g(x, y, z);
+        case NT_SCREW: return screw_g(prm, x, y, z);
+        case NT_LID: return V3{0.f, 0.f, 1.f};
+        case NT_HALF_PLANE: return hp_g(prm, x, y, z);
         default: return dm_g(x, y, z);
     }
 }
@@ -256,7 +464,7 @@ __device__ __forceinline__ float eval_f(const Program* __restrict__ prog, const 
             ++sp;
             px[sp] = q.x; py[sp] = q.y; pz[sp] = q.z;
         } else if (I.op == OP_PRIM) {
-            vf[vp++] = prim_f(I.type, tab, px[sp], py[sp], pz[sp]);
+            vf[vp++] = prim_f(I.type, tab, prog->mats[I.prm], px[sp], py[sp], pz[sp]);
             --sp;
         } else {
             --sp;
@@ -286,8 +494,8 @@ __device__ __forceinline__ float eval_fg(const Program* __restrict__ prog, const
             ++sp;
             px[sp] = q.x; py[sp] = q.y; pz[sp] = q.z;
         } else if (I.op == OP_PRIM) {
-            const float f = prim_f(I.type, tab, px[sp], py[sp], pz[sp]);
-            V3 g = prim_g(I.type, px[sp], py[sp], pz[sp]);
+            const float f = prim_f(I.type, tab, prog->mats[I.prm], px[sp], py[sp], pz[sp]);
+            V3 g = prim_g(I.type, prog->mats[I.prm], px[sp], py[sp], pz[sp]);
             g = grad_xform(prog->mats[I.mat], g);
             vf[vp] = f; gx[vp] = g.x; gy[vp] = g.y; gz[vp] = g.z;
             ++vp;

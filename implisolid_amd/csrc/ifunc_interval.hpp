@@ -211,7 +211,28 @@ __device__ __forceinline__ Iv dm_iv(Box p) {
     return res;
 }
 
-__device__ __forceinline__ Iv prim_iv(int t, const float* __restrict__ tab, float2 tab_range, Box p) {
+// screw: f = (-r + r0) + delta * sinf(.) with |sinf| <= 1 and r = |(x, y, d2)|, where d2 = z - p2 is
+// the rounding residual of p2 = (z + 0.5) - 0.5: |d2| <= 2^-23 (|z| + 1) (bounded by twice that)
+__device__ __forceinline__ float absmin_iv(Iv a) { return a.lo > 0.f ? a.lo : (a.hi < 0.f ? -a.hi : 0.f); }
+__device__ __forceinline__ float absmax_iv(Iv a) { return fmax2(fabsf(a.lo), fabsf(a.hi)); }
+__device__ __forceinline__ Iv screw_iv(const float* __restrict__ prm, Box p) {
+    const float r0 = prm[1], ad = fabsf(prm[2]);
+    const float ax = absmax_iv(p.x), ay = absmax_iv(p.y), bx = absmin_iv(p.x), by = absmin_iv(p.y);
+    const float dz = (absmax_iv(p.z) + 1.f) * 0x1p-22f;
+    const float rhi = sqrtf(ax * ax + (ay * ay + dz * dz)), rlo = sqrtf(bx * bx + (by * by + 0.f));
+    return Iv{(-rhi + r0) - ad, (-rlo + r0) + ad};
+}
+__device__ __forceinline__ Iv lid_iv(Box p) {
+    const Iv a = sub(p.z, ivc(0.5f)), b = mulc(add(p.z, ivc(0.5f)), -1.f);
+    return Iv{fmax2(a.lo, b.lo), fmax2(a.hi, b.hi)};
+}
+__device__ __forceinline__ Iv hp_iv(const float* __restrict__ prm, Box p) {
+    return add(add(add(ivc(0.f), mulc(sub(p.x, ivc(prm[3])), prm[0])), mulc(sub(p.y, ivc(prm[4])), prm[1])),
+               mulc(sub(p.z, ivc(prm[5])), prm[2]));
+}
+
+__device__ __forceinline__ Iv prim_iv(int t, const float* __restrict__ tab, float2 tab_range,
+                                      const float* __restrict__ prm, Box p) {
     Iv r;
     switch (t) {
         case NT_ELLIPSOID: r = egg_iv(p); break;
@@ -220,6 +241,9 @@ __device__ __forceinline__ Iv prim_iv(int t, const float* __restrict__ tab, floa
         case NT_CONE: r = cone_iv(p); break;
         case NT_HEART: r = heart_iv(p); break;
         case NT_TORUS: r = torus_iv(p); break;
+        case NT_SCREW: r = screw_iv(prm, p); break;
+        case NT_LID: r = lid_iv(p); break;
+        case NT_HALF_PLANE: r = hp_iv(prm, p); break;
         default: r = dm_iv(p); break;
     }
     return settle(r);
@@ -279,7 +303,7 @@ __device__ __forceinline__ Iv eval_iv(const Program* __restrict__ prog, const fl
             ++sp;
             xl[sp] = q.x.lo; xh[sp] = q.x.hi; yl[sp] = q.y.lo; yh[sp] = q.y.hi; zl[sp] = q.z.lo; zh[sp] = q.z.hi;
         } else if (I.op == OP_PRIM) {
-            const Iv r = prim_iv(I.type, tab, tab_range, cur);
+            const Iv r = prim_iv(I.type, tab, tab_range, prog->mats[I.prm], cur);
             vl[vp] = r.lo; vh[vp] = r.hi;
             ++vp;
             --sp;
@@ -330,7 +354,7 @@ __device__ __forceinline__ float eval_f_pruned(const Program* __restrict__ prog,
             ++sp;
             px[sp] = q.x; py[sp] = q.y; pz[sp] = q.z;
         } else if (I.op == OP_PRIM) {
-            vf[vp++] = prim_f(I.type, tab, px[sp], py[sp], pz[sp]);
+            vf[vp++] = prim_f(I.type, tab, prog->mats[I.prm], px[sp], py[sp], pz[sp]);
             --sp;
         } else {
             --sp;

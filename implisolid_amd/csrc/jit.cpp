@@ -35,7 +35,7 @@ typedef unsigned long uint64_t;
 
 struct Node {
     bool leaf = false;
-    int type = 0, mat = 0, csg = -1;
+    int type = 0, mat = 0, csg = -1, prm = 0;
     int child[2] = {-1, -1};
 };
 
@@ -47,6 +47,7 @@ int parse(const Program& p, int pc, std::vector<Node>& nodes, int& next) {
     if (pc + 1 < p.n_instr && p.instr[pc + 1].op == OP_PRIM) {
         n.leaf = true;
         n.type = p.instr[pc + 1].type;
+        n.prm = p.instr[pc + 1].prm;
         next = pc + 2;
     } else {
         int p1 = 0, p2 = 0;
@@ -61,6 +62,13 @@ int parse(const Program& p, int pc, std::vector<Node>& nodes, int& next) {
     return (int)nodes.size() - 1;
 }
 
+// a primitive's parameter row (Instr::prm) is passed as a pointer into the matrix array M
+std::string with_params(const std::string& call, int prm) {
+    const size_t k = call.find("P, ");
+    if (k == std::string::npos) return call;
+    return call.substr(0, k) + "M + " + std::to_string(12 * prm) + ", " + call.substr(k + 3);
+}
+
 const char* prim_call(int t) {
     switch (t) {
         case NT_ELLIPSOID: return "egg_f(";
@@ -70,6 +78,8 @@ const char* prim_call(int t) {
         case NT_HEART: return "heart_f(";
         case NT_TORUS: return "torus_f(";
         case NT_DMUSHROOM: return "dm_f(";
+        case NT_SCREW: return "screw_f(P, ";
+        case NT_HALF_PLANE: return "hp_f(P, ";
         default: throw std::runtime_error("jit: unknown primitive");
     }
 }
@@ -147,7 +157,9 @@ struct Emitter {
             << xform_row(mm + 4, 12 * n.mat + 4, x, y, z) << ",\n" << pad << "    "
             << xform_row(mm + 8, 12 * n.mat + 8, x, y, z) << "};\n";
         if (n.leaf) {
-            out << pad << "const float " << f << " = " << prim_call(n.type) << q << ".x, " << q << ".y, " << q << ".z);\n";
+            std::string call = n.type == NT_LID ? "lid_f(" + q + ".z)"
+                                                : with_params(prim_call(n.type), n.prm) + q + ".x, " + q + ".y, " + q + ".z)";
+            out << pad << "const float " << f << " = " << call << ";\n";
             return f;
         }
         const std::string m = "m" + std::to_string(id), a = "a" + std::to_string(id), b = "b" + std::to_string(id);
@@ -184,6 +196,9 @@ const char* prim_iv_call(int t) {
         case NT_HEART: return "heart_iv(";
         case NT_TORUS: return "torus_iv(";
         case NT_DMUSHROOM: return "dm_iv(";
+        case NT_SCREW: return "screw_iv(P, ";
+        case NT_LID: return "lid_iv(";
+        case NT_HALF_PLANE: return "hp_iv(P, ";
         default: throw std::runtime_error("jit: unknown primitive");
     }
 }
@@ -206,7 +221,7 @@ struct IvEmitter {
             << xform_iv_row(mm + 4, 12 * n.mat + 4, p) << ",\n" << pad << "    "
             << xform_iv_row(mm + 8, 12 * n.mat + 8, p) << "};\n";
         if (n.leaf) {
-            out << pad << "const Iv " << r << " = settle(" << prim_iv_call(n.type) << q << "));\n";
+            out << pad << "const Iv " << r << " = settle(" << with_params(prim_iv_call(n.type), n.prm) << q << "));\n";
             return r;
         }
         const std::string m = "m" + std::to_string(id), a = "a" + std::to_string(id), b = "b" + std::to_string(id);

@@ -9,7 +9,8 @@
 //
 //   XFORM k   push M_k^-1 * top-point            (the node's own inverse matrix)
 //   PRIM t    pop point, push f_t(point)         (egg, rabbit cube, cylinder, cone, heart, torus,
-//                                                 double mushroom)
+//                                                 double mushroom, screw, top/bottom lid, half plane;
+//                                                 parameters in mats[prm])
 //   CSG t     pop point, pop f2, f1, push f1 (op) f2   (Union / Intersection / Difference)
 //
 // With gradients enabled every value slot carries (f, gx, gy, gz) and every XFORM'd node applies
@@ -33,6 +34,9 @@ enum NodeType : int32_t {
     NT_HEART = 7,
     NT_TORUS = 8,
     NT_DMUSHROOM = 9,
+    NT_SCREW = 10,        // screw.hpp (identity transformation_matrix), params {twist, r0, delta}
+    NT_LID = 11,          // top_bottom_lid.hpp
+    NT_HALF_PLANE = 12,   // half_plane.hpp, params {unit plane_vector, plane_point}
 };
 
 enum OpCode : int32_t {
@@ -49,7 +53,7 @@ struct Instr {
     int16_t skip_csg;    // XFORM that starts a CSG operand: that CSG node's index, else -1
     int16_t skip_child;  // ... operand 0 or 1
     int16_t skip_to;     // ... first instruction after the operand's subtree
-    int16_t pad;
+    int16_t prm;         // OP_PRIM: row of mats[] holding the primitive's parameters (raw floats)
 };
 static_assert(sizeof(Instr) == 16, "Instr layout");
 

@@ -64,9 +64,23 @@ def _rabbit_ok(s, t, box):
     return True
 
 
+TWIST_LEAF_TYPES = LEAF_TYPES + ["screw"]
+
+
+def twist(scale, tx, ty, tz, pitch=0.5, delta_ratio=1.5):
+    """The reference's "screw" node (object_factory.hpp:304-351): a sine-profile twisted rod of
+    radius 1/2 cut to |z| <= 1/2 by top_bottom_lid, under the given scale + translation."""
+    return {"type": "screw", "matrix": st(scale, tx, ty, tz), "v": [0, 2, 0], "pitch": pitch, "profile": "sin",
+            "delta_ratio": delta_ratio, "end_type": "0"}
+
+
 def random_leaf(rng, box=1.0, types=LEAF_TYPES):
     while True:
         t = rng.choice(types)
+        if t == "screw":
+            s = rng.choice([0.25, 0.5])
+            tr = [rng.randint(-32, 32) / 64.0 for _ in range(3)]
+            return twist(s, *tr, pitch=rng.choice([0.25, 0.5]))
         s = rng.choice([0.125, 0.25, 0.5])
         tr = [rng.randint(-32, 32) / 64.0 for _ in range(3)]
         if t == "torus" or t == "itorus":
@@ -87,13 +101,17 @@ def _size(node):
     return 1 if "children" not in node else sum(_size(c) for c in node["children"])
 
 
-def random_tree(seed, n_leaves=10, box=1.0):
+def random_tree(seed, n_leaves=10, box=1.0, twist_leaves=False):
     """Random binary CSG tree with n_leaves leaves and n_leaves-1 Union / Difference /
     Intersection nodes.  Subtrees are paired at random from a pool (expected depth O(log n)).
     Difference keeps the larger operand first; Intersection clips with a large ellipsoid leaf so
-    the result stays non-empty; the root is a Union."""
+    the result stays non-empty; the root is a Union.  twist_leaves adds the "screw" node to the
+    leaf types and makes the first leaf one."""
     rng = random.Random(seed)
-    pool = [random_leaf(rng, box) for _ in range(n_leaves)]
+    types = TWIST_LEAF_TYPES if twist_leaves else LEAF_TYPES
+    pool = [random_leaf(rng, box, types) for _ in range(n_leaves)]
+    if twist_leaves and not any(p["type"] == "screw" for p in pool):
+        pool[0] = random_leaf(rng, box, ["screw"])
     while len(pool) > 1:
         i, j = rng.sample(range(len(pool)), 2)
         a, b = pool[i], pool[j]
@@ -115,14 +133,20 @@ def random_tree(seed, n_leaves=10, box=1.0):
 CONFIG3_SEED = 20251015
 
 
+def config3_tree():
+    """~20-node MP5 CSG tree with twist / union / difference (BASELINE.json config 3): 10 leaves
+    including at least one twist ("screw", 3 reference nodes each) and 9 CSG nodes."""
+    return random_tree(CONFIG3_SEED, 10, twist_leaves=True)
+
+
 def config3(resolution=256):
-    return random_tree(CONFIG3_SEED, 10), mc_settings(resolution, 1.0, vresampl_iters=1, vresampl_c=0.4, projection=1,
+    return config3_tree(), mc_settings(resolution, 1.0, vresampl_iters=1, vresampl_c=0.4, projection=1,
                                                       qem=1, overall_repeats=3)
 
 
 def config4(resolution=512):
     """config 3's tree at 512^3, eval + MC (the Z-slab scaling workload)."""
-    return random_tree(CONFIG3_SEED, 10), mc_settings(resolution, 1.0)
+    return config3_tree(), mc_settings(resolution, 1.0)
 
 
 def config5_objects(n=64, resolution=128):

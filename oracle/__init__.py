@@ -26,7 +26,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 
-UNION, INTERSECTION, DIFFERENCE, ELLIPSOID, CUBE, CYLINDER, CONE, HEART, TORUS, DMUSHROOM = range(10)
+UNION, INTERSECTION, DIFFERENCE, ELLIPSOID, CUBE, CYLINDER, CONE, HEART, TORUS, DMUSHROOM, SCREW, LID, HALF_PLANE = range(13)
 
 # MP5 "type" strings accepted by object_factory.hpp:86-653 for the plain-arithmetic node families.
 PRIMITIVE_TYPES = {
@@ -39,14 +39,12 @@ PRIMITIVE_TYPES = {
     "itorus": TORUS,                         # :163-173
 }
 # types the reference knows but this build does not evaluate (Eigen-based or JS callbacks)
-KNOWN_UNSUPPORTED = {"tetrahedron", "inf_screw", "screw_diff_two_plane", "screw", "sdf_3d",
-                     "half_plane", "screw_gradient_wrong", "top_bottom_lid", "rawjscode",
-                     "meta_balls", "extrusion"}
+KNOWN_UNSUPPORTED = {"tetrahedron", "sdf_3d", "screw_gradient_wrong", "rawjscode", "meta_balls", "extrusion"}
 
 
 class OrNode(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("child", ctypes.c_int32 * 2),
-                ("m", ctypes.c_float * 12), ("minv", ctypes.c_float * 12)]
+                ("m", ctypes.c_float * 12), ("minv", ctypes.c_float * 12), ("prm", ctypes.c_float * 8)]
 
 
 class OrMesh(ctypes.Structure):
@@ -79,6 +77,13 @@ def lib():
         L.or_acosf.restype = ctypes.c_float
         L.or_acosf_check.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         L.or_acosf_check.restype = ctypes.c_int64
+        for fn in ("or_sinf", "or_atanf"):
+            getattr(L, fn).argtypes = [ctypes.c_float]
+            getattr(L, fn).restype = ctypes.c_float
+        L.or_atan2f.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.or_atan2f.restype = ctypes.c_float
+        L.or_libm_check.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        L.or_libm_check.restype = ctypes.c_int64
         L.or_marching_cubes.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, ctypes.POINTER(OrMesh)]
         L.or_mesh_free.argtypes = [ctypes.POINTER(OrMesh)]
         L.or_mc_field.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, fp]
@@ -129,12 +134,38 @@ def _matrix12(d):
 EYE12 = [np.float32(v) for v in (1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0)]
 
 
+def _screw_params(d):
+    """screw::getScrewParameters (screw.hpp:380-470) + the constructor (:222-330), in float:
+    outer = |v| = 1 (v = (0,1,0)), inner = outer / delta_ratio, r0 = inner / 2,
+    delta = outer / 2 - inner / 2, twist_rate = pitch.  "matrix", "v", "profile" and "end_type"
+    must be present (ptree get_child / get throw); their values are unused."""
+    for k in ("matrix", "v", "pitch", "profile", "end_type", "delta_ratio"):
+        if k not in d:
+            raise ValueError("screw: missing %r" % k)
+    f = np.float32
+    pitch, ratio = strtof(d["pitch"]), strtof(d["delta_ratio"])
+    outer = f(1.0)
+    inner = f(outer / ratio)
+    r0 = f(inner / f(2))
+    delta = f(f(outer / f(2)) - f(inner / f(2)))
+    return [pitch, r0, delta]
+
+
+def _half_plane_params(pv, pp):
+    """half_plane constructor (half_plane.hpp:96-125): plane_vector / plane_vector.norm() in float,
+    the norm reduced as a0 + (a1 + a2)."""
+    f = np.float32
+    v = [strtof(a) for a in pv]
+    n = np.sqrt(f(v[0] * v[0] + f(v[1] * v[1] + v[2] * v[2])))
+    return [f(a / n) for a in v] + [strtof(a) for a in pp]
+
+
 def mp5_to_nodes(shape, ignore_root_matrix=False):
     """object_factory (object_factory.hpp:56-758) -> flat node list + root index."""
     nodes = []
 
-    def add(t, m, c0=-1, c1=-1):
-        nodes.append((t, (c0, c1), m))
+    def add(t, m, c0=-1, c1=-1, prm=None):
+        nodes.append((t, (c0, c1), m, prm or []))
         return len(nodes) - 1
 
     def build_node(d, ignore):
@@ -169,13 +200,38 @@ def mp5_to_nodes(shape, ignore_root_matrix=False):
             a = build_node(ch[0], False)
             b = build_node(ch[1], False)
             return add(INTERSECTION if t == "Intersection" else DIFFERENCE, m, a, b)
+        if t in ("screw", "inf_screw", "screw_diff_two_plane"):
+            prm = _screw_params(d)
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            if t == "inf_screw":                   # :189-215: the screw under its own matrix
+                return add(SCREW, m, prm=prm)
+            s = add(SCREW, list(EYE12), prm=prm)   # transformation_matrix forced to identity
+            if t == "screw":                       # :304-351: subtract(screw, top_bottom_lid)
+                return add(DIFFERENCE, m, s, add(LID, list(EYE12)))
+            # :216-302: subtract(subtract(screw, half_plane z >= .25), half_plane z <= -.25)
+            top = add(HALF_PLANE, list(EYE12), prm=_half_plane_params(["0", "0", "1"], ["0", "0", "0.25"]))
+            first = add(DIFFERENCE, list(EYE12), s, top)
+            bot = add(HALF_PLANE, list(EYE12), prm=_half_plane_params(["0", "0", "-1"], ["0", "0", "-0.25"]))
+            return add(DIFFERENCE, m, first, bot)
+        if t == "top_bottom_lid":                  # :480-506: the matrix is read, then unused
+            _matrix12(d)
+            return add(LID, list(EYE12))
+        if t == "half_plane":                      # :396-434
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            return add(HALF_PLANE, m, prm=_half_plane_params(d["plane_vector"], d["plane_point"]))
         if t in KNOWN_UNSUPPORTED:
             raise NotImplementedError("MP5 type %r is outside the implemented node families" % t)
         raise ValueError("Invalid object you asked for: %r" % t)   # the reference abort()s
 
     root = build_node(_loads(shape), ignore_root_matrix)
     arr = (OrNode * len(nodes))()
-    for i, (t, (c0, c1), m) in enumerate(nodes):
+    for i, (t, (c0, c1), m, prm) in enumerate(nodes):
+        for k, v in enumerate(prm):
+            arr[i].prm[k] = float(v)
         arr[i].type = t
         arr[i].child[0] = c0
         arr[i].child[1] = c1
@@ -267,6 +323,12 @@ def centroids_projection(tree, verts, faces, enable_qem):
                                      _fp(cen), _fp(avg)):
         raise MemoryError
     return v, cen, float(avg[0])
+
+
+def libm_check(which, start, stride, count):
+    """Mismatches of the restated glibc sinf (0) / atanf (1) over bit patterns start + k*stride,
+    or atan2f (2) over `count` seeded random pairs, against this host's libm."""
+    return int(lib().or_libm_check(int(which), int(start), int(stride), int(count)))
 
 
 def srand(seed):

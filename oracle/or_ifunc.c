@@ -299,6 +299,87 @@ static void dm_g(const float p[3], float g[3]) {
     else { g[0] = -2.f * (x - 0.f) / a2; g[1] = -2.f * (y - 0.f) / b2; g[2] = 2.f * (z - 0.f) / c2; }
 }
 
+/* ---------------- screw.hpp:98-150 (implicitFunction) at the constants its constructor sets:
+   u = (1,0,0), v = (0,1,0), w = (0,0,1), A = (0,0,-slen/2) = (0,0,-0.5), UVW = I (screw.hpp:
+   222-330); the factory forces the identity transformation_matrix (object_factory.hpp:304-351).
+   prm = {twist_rate = pitch, r0 = inner/2, delta = outer/2 - inner/2} (outer = |v| = 1, inner =
+   outer/delta_ratio).  Eigen evaluation orders: t = (x - A) w is a GEMV (columns accumulated into
+   a zeroed result), p = w t^T + A an outer product, ab = UVW^-1 (x - p) a GEMM (depth accumulated
+   from zero, then added to the zeroed destination), |x - p| the 3-term redux a0 + (a1 + a2). */
+static const double OR_M_PI = 3.14159265358979323846;   /* <cmath> M_PI */
+static const float SCREW_PI = (float)3.1415926535897;   /* screw.hpp:20 const REAL pi */
+
+static float screw_f(const float p[3], const float* prm) {
+    const float x = p[0], y = p[1], z = p[2];
+    const float tw = prm[0], r0 = prm[1], delta = prm[2];
+    const float a0 = x - 0.f, a1 = y - 0.f, a2 = z - (-0.5f);
+    const float t = ((0.f + a0 * 0.f) + a1 * 0.f) + a2 * 1.f;
+    const float p0 = 0.f * t + 0.f, p1 = 0.f * t + 0.f, p2 = 1.f * t + (-0.5f);
+    const float d0 = x - p0, d1 = y - p1, d2 = z - p2;
+    const float ab0 = 0.f + (((0.f + 1.f * d0) + 0.f * d1) + 0.f * d2);
+    const float ab1 = 0.f + (((0.f + 0.f * d0) + 1.f * d1) + 0.f * d2);
+    const float theta = or_atan2f(ab1, ab0);
+    const float r = sqrtf(d0 * d0 + (d1 * d1 + d2 * d2));
+    const float pi2 = SCREW_PI * 2;
+    const float ph = t / tw - theta / pi2;
+    return (-r + r0) + delta * or_sinf(ph * 2 * SCREW_PI);   /* phi, screw.hpp:29-36 */
+}
+
+/* screw.hpp:152-160 gradient (sympy expression) at the same constants; the C++ types of each
+   sub-expression are kept: std::pow(float, 2) promotes to an exact double square, atan2 of two
+   floats is atan2f (basic_data_structures.hpp's `using namespace std`), cos of a double is the
+   double cos, M_PI is double. */
+static void screw_g(const float p[3], const float* prm, float g[3]) {
+    const float x = p[0], y = p[1], z = p[2];
+    const float tw = prm[0], delta = prm[2];
+    const float ax = 0.f, ay = 0.f, az = -0.5f, wx = 0.f, wy = 0.f, wz = 1.f, phi0 = 0.f;
+    const float u00 = 1.f, u01 = 0.f, u02 = 0.f, u10 = 0.f, u11 = 1.f, u12 = 0.f;
+    const float s = (wx * (-ax + x) + wy * (-ay + y)) + wz * (-az + z);
+    const float X1 = (-ax - wx * s) + x, Y1 = (-ay - wy * s) + y, Z1 = (-az - wz * s) + z;
+    const float U0 = (u00 * X1 + u01 * Y1) + u02 * Z1;
+    const float U1 = (u10 * X1 + u11 * Y1) + u12 * Z1;
+    const float nU1 = ((-u10 * X1) - u11 * Y1) - u12 * Z1;
+    const double G = sq_exact(U0) + sq_exact(U1);
+    const double sq = sqrt((sq_exact(X1) + sq_exact(Y1)) + sq_exact(Z1));
+    const float th = or_atan2f(U1, U0);
+    const double cv = cos(OR_M_PI * (((double)(2 * phi0) - (double)th / OR_M_PI) + (double)((2 * s) / tw)));
+    const double wx2 = sq_exact(wx), wy2 = sq_exact(wy), wz2 = sq_exact(wz);
+    const double pd = OR_M_PI * (double)delta;
+    const double cAx = ((double)u00 * (-wx2 + 1) - (double)(u01 * wx * wy)) - (double)(u02 * wx * wz);
+    const double cBx = ((double)u10 * (-wx2 + 1) - (double)(u11 * wx * wy)) - (double)(u12 * wx * wz);
+    const double Ax = -(cAx * (double)nU1 / G + (double)U0 * cBx / G) / OR_M_PI + (double)(2 * wx / tw);
+    const double Cx = (double)(-wx * wy * Y1 - wx * wz * Z1) + (1.0 / 2.0) * (-2 * wx2 + 2) * (double)X1;
+    const double cAy = ((double)(-u10 * wx * wy) + (double)u11 * (-wy2 + 1)) - (double)(u12 * wy * wz);
+    const double cBy = ((double)(-u00 * wx * wy) + (double)u01 * (-wy2 + 1)) - (double)(u02 * wy * wz);
+    const double Ay = -((double)U0 * cAy / G + (double)nU1 * cBy / G) / OR_M_PI + (double)(2 * wy / tw);
+    const double Cy = (double)(-wx * wy * X1 - wy * wz * Z1) + (1.0 / 2.0) * (-2 * wy2 + 2) * (double)Y1;
+    const double cAz = (double)(-u10 * wx * wz - u11 * wy * wz) + (double)u12 * (-wz2 + 1);
+    const double cBz = (double)(-u00 * wx * wz - u01 * wy * wz) + (double)u02 * (-wz2 + 1);
+    const double Az = -((double)U0 * cAz / G + (double)nU1 * cBz / G) / OR_M_PI + (double)(2 * wz / tw);
+    const double Cz = (double)(-wx * wz * X1 - wy * wz * Y1) + (1.0 / 2.0) * (-2 * wz2 + 2) * (double)Z1;
+    g[0] = (float)(pd * Ax * cv - Cx / sq);
+    g[1] = (float)(pd * Ay * cv - Cy / sq);
+    g[2] = (float)(pd * Az * cv - Cz / sq);
+}
+
+/* top_bottom_lid.hpp:117-161: max(z - 0.5, (z + 0.5) * -1) (Eigen max = std::max); the gradient's
+   condition `z >= 0.5 && (0.0 > z && z >= -0.5)` never holds, so it is always (0, 0, 1) */
+static float lid_f(const float p[3]) {
+    const float a = p[2] - 0.5f, b = (p[2] + 0.5f) * -1.f;
+    return (a < b) ? b : a;
+}
+
+/* half_plane.hpp:150-190: (x - plane_point) . plane_vector as an Eigen GEMV (zeroed result,
+   columns accumulated in order); gradient -plane_vector where f >= 0, else plane_vector */
+static float hp_f(const float p[3], const float* prm) {
+    const float d0 = p[0] - prm[3], d1 = p[1] - prm[4], d2 = p[2] - prm[5];
+    return ((0.f + d0 * prm[0]) + d1 * prm[1]) + d2 * prm[2];
+}
+static void hp_g(const float p[3], const float* prm, float g[3]) {
+    const float k = hp_f(p, prm) >= 0 ? -1.f : 1.f;   /* exact sign flips of plane_vector */
+    g[0] = k * prm[0]; g[1] = k * prm[1]; g[2] = k * prm[2];
+}
+
 /* ---------------- tree recursion ---------------- */
 static float eval1(const or_node* N, int i, const float p[3]) {
     const or_node* n = &N[i];
@@ -324,6 +405,9 @@ static float eval1(const or_node* N, int i, const float p[3]) {
         case OR_HEART: return heart_f(l);
         case OR_TORUS: return torus_f(l);
         case OR_DMUSHROOM: return dm_f(l);   /* linearly_transformed.hpp:24-33 */
+        case OR_SCREW: return screw_f(l, n->prm);
+        case OR_LID: return lid_f(l);
+        case OR_HALF_PLANE: return hp_f(l, n->prm);
     }
     return NAN;
 }
@@ -352,6 +436,9 @@ static void grad1(const or_node* N, int i, const float p[3], float o[3]) {
         case OR_HEART: heart_g(l, g); break;
         case OR_TORUS: torus_g(l, g); break;
         case OR_DMUSHROOM: dm_g(l, g); break;
+        case OR_SCREW: screw_g(l, n->prm, g); break;
+        case OR_LID: g[0] = 0.f; g[1] = 0.f; g[2] = 1.f; break;
+        case OR_HALF_PLANE: hp_g(l, n->prm, g); break;
         default: g[0] = g[1] = g[2] = NAN;
     }
     grad_xform(n->minv, g, o);

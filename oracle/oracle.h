@@ -35,6 +35,9 @@ enum {
     OR_HEART,          /* heart                     implicit_function/heart.hpp                  */
     OR_TORUS,          /* torus                     implicit_function/torus.hpp                  */
     OR_DMUSHROOM,      /* linearly_transformed(double_mushroom) object_factory.hpp:86-100       */
+    OR_SCREW,          /* screw (identity transformation_matrix)  implicit_function/screw.hpp   */
+    OR_LID,            /* top_bottom_lid            implicit_function/top_bottom_lid.hpp         */
+    OR_HALF_PLANE,     /* half_plane                implicit_function/half_plane.hpp             */
     OR_NTYPES
 };
 
@@ -43,6 +46,8 @@ typedef struct {
     int32_t child[2];   /* node indices, -1 when unused */
     float m[12];        /* transf_matrix, row-major 3x4, as read from the MP5 JSON */
     float minv[12];     /* inv_transf_matrix, filled by or_tree_prepare */
+    float prm[8];       /* primitive parameters: screw {twist_rate, r0, delta};
+                           half_plane {unit plane_vector xyz, plane_point xyz} */
 } or_node;
 
 /* basic_functions.hpp:77-128 invert_matrix (ublas LU in float). returns 1 on success. */
@@ -54,6 +59,12 @@ void or_tree_prepare(or_node* nodes, int n);
 /* implicit_function::eval_implicit / eval_gradient over a batch (implicit_function.hpp:35-36) */
 void or_eval(const or_node* nodes, int root, const float* xyz, int64_t n, float* f_out);
 void or_grad(const or_node* nodes, int root, const float* xyz, int64_t n, float* g_out);
+
+/* glibc-2.35 sinf (x86_64 FMA variant), atanf, atan2f restatements (or_libm.c) */
+float or_sinf(float x);
+float or_atanf(float x);
+float or_atan2f(float y, float x);
+int64_t or_libm_check(int which, uint32_t start, uint32_t stride, uint64_t count);
 
 /* glibc-2.35 acosf restatement (vertex_resampling.hpp:75 calls std::acos(float)) */
 float or_acosf(float x);

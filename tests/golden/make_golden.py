@@ -30,7 +30,7 @@ def point_trees():
     from implisolid_amd import scenes
     out = {"sphere": {"type": "iellipsoid", "matrix": scenes.EYE},
            "union_sphere_cube": scenes.union_sphere_cube(),
-           "config3_tree": scenes.config3()[0]}
+           "config3_tree": scenes.random_tree(scenes.CONFIG3_SEED, 10)}   # the tree without its twist
     for t in ["iellipsoid", "icylinder", "icone", "itorus", "implicit_double_mushroom", "iheart", "cube"]:
         out["leaf_" + t] = {"type": t, "matrix": scenes.st(0.5, 0.125, -0.0625, 0.03125)}
     return out
@@ -61,6 +61,13 @@ def main():
         fn = np_restate.evaluate(sh, pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy())
         assert np.array_equal(fo.view(np.uint32), fn.view(np.uint32)), name
         arrays["f_" + name] = fo
+        arrays["g_" + name] = oracle.eval_gradient(tree, pts)
+    # the twist family (oracle only: the numpy restatement has no glibc sinf / atan2f)
+    for name, sh in {"twist": scenes.twist(1, 0, 0, 0), "twist_small_pitch": scenes.twist(0.5, 0.125, 0, 0.0625, pitch=0.0625),
+                     "config3_twist_tree": scenes.config3_tree()}.items():
+        trees[name] = sh
+        tree = oracle.mp5_to_nodes(json.dumps(sh))
+        arrays["f_" + name] = oracle.eval_implicit(tree, pts)
         arrays["g_" + name] = oracle.eval_gradient(tree, pts)
     np.savez_compressed(os.path.join(HERE, "points_eval.npz"), trees=json.dumps(trees), **arrays)
 

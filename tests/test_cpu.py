@@ -59,7 +59,7 @@ def _trees():
     from implisolid_amd import scenes
     t = {"sphere": ({"type": "iellipsoid", "matrix": scenes.EYE}, [-0.6, 0.6] * 3, 32),
          "union_sphere_cube": (scenes.union_sphere_cube(), [-1, 1] * 3, 40),
-         "config3_tree": (scenes.config3()[0], [-1, 1] * 3, 40),
+         "config3_tree": (scenes.random_tree(scenes.CONFIG3_SEED, 10), [-1, 1] * 3, 40),   # without twists
          "anisotropic": (scenes.union_sphere_cube(), [-0.7, 0.9, -1.1, 0.6, -0.55, 0.8], 36)}
     for seed in (7, 11, 13, 101, 102):
         t["random_%d" % seed] = (scenes.random_tree(seed, 3 + seed % 10), [-1, 1] * 3, 40)
@@ -188,6 +188,69 @@ def test_library_rand_matches_glibc(impli):
             assert libc.rand() == impli.rand(), (seed, n)
 
 
+# ---- glibc float math of the screw family (or_libm.c; the device copies are compared on the GPU) ---
+def test_libm_restatements_match_glibc_strided(oracle):
+    # screw.hpp: std::sin(float) (x86_64 FMA variant of sinf) and std::atan2(float, float)
+    assert oracle.libm_check(0, 0, 61, (1 << 32) // 61) == 0      # sinf, every 61st pattern
+    assert oracle.libm_check(1, 7, 61, (1 << 32) // 61) == 0      # atanf
+    assert oracle.libm_check(2, 1, 1, 2_000_000) == 0             # atan2f, seeded pairs
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not os.environ.get("IMPLISOLID_SLOW"), reason="exhaustive (~2 min): set IMPLISOLID_SLOW=1")
+def test_libm_restatements_match_glibc_exhaustive(oracle):
+    assert oracle.libm_check(0, 0, 1, 1 << 32) == 0
+    assert oracle.libm_check(1, 0, 1, 1 << 32) == 0
+    assert oracle.libm_check(2, 2, 1, 100_000_000) == 0
+
+
+def _screw_family():
+    from implisolid_amd import scenes
+    tw = scenes.twist(1, 0, 0, 0)
+    return {"screw": tw, "screw_diff_two_plane": dict(tw, type="screw_diff_two_plane"),
+            "inf_screw": dict(tw, type="inf_screw", pitch=0.25),
+            "half_plane": {"type": "Intersection", "matrix": scenes.EYE, "children": [
+                {"type": "iellipsoid", "matrix": scenes.EYE},
+                {"type": "half_plane", "matrix": scenes.st(0.5, 0, 0.125, 0), "plane_vector": [0, 1, 2],
+                 "plane_point": [0, 0, 0.25]}]},
+            "lid": {"type": "Intersection", "matrix": scenes.EYE, "children": [
+                {"type": "icylinder", "matrix": scenes.st(1, 0, 0, 0.5)},
+                {"type": "top_bottom_lid", "matrix": scenes.st(1, 0, 0, 0)}]},
+            "config3_twist": scenes.config3_tree()}
+
+
+@pytest.mark.parametrize("name", sorted(_screw_family()))
+def test_screw_family_oracle_meshes_closed(oracle, name):
+    """The twist (screw), lid and half-plane nodes give closed edge-manifold MC meshes."""
+    shape = _screw_family()[name]
+    v, f = oracle.marching_cubes(oracle.mp5_to_nodes(json.dumps(shape)), 48, [-0.7, 0.7] * 3)
+    assert len(f) > 1000
+    _, cnt = mesh_edges(f)
+    assert (cnt == 2).all()
+
+
+def test_screw_values_follow_the_reference_formula(oracle):
+    """Spot values of screw.hpp's field at its constants: f = r0 + delta sin(2 pi (t/pitch) - theta)
+    - r, with r0 = 1/3, delta = 1/6 (delta_ratio 1.5), t = z + 1/2; the lid cuts |z| > 1/2."""
+    from implisolid_amd import scenes
+    tree = oracle.mp5_to_nodes(json.dumps(dict(scenes.twist(1, 0, 0, 0), type="inf_screw")))
+    rng = np.random.default_rng(4)
+    p = rng.uniform(-0.6, 0.6, (2000, 3)).astype(np.float32)
+    f = oracle.eval_implicit(tree, p).astype(np.float64)
+    x, y, z = p[:, 0].astype(np.float64), p[:, 1].astype(np.float64), p[:, 2].astype(np.float64)
+    ref = 1 / 3 + (1 / 6) * np.sin(2 * np.pi * ((z + 0.5) / 0.5) - np.arctan2(y, x)) - np.hypot(x, y)
+    assert np.abs(f - ref).max() < 2e-6
+
+
+def test_screw_factory_errors(impli):
+    from implisolid_amd import scenes
+    bad = dict(scenes.twist(1, 0, 0, 0))
+    del bad["v"]
+    with pytest.raises(impli.ImplisolidError, match="missing"):
+        impli.program_info(bad)
+    assert impli.program_info(scenes.twist(1, 0, 0, 0))[:3] == (6, 3, 4)   # XFORM Diff + 2 leaves, 1 param row
+
+
 # ---- mesh properties ------------------------------------------------------------------------------
 @pytest.mark.parametrize("name", ["sphere", "union_sphere_cube", "config3_tree"])
 def test_mc_output_is_closed_edge_manifold(oracle, name):
@@ -264,7 +327,8 @@ def test_program_compiles_reference_factory_semantics(impli):
     n_instr, depth, n_mats, _ = impli.program_info(u3)
     assert n_instr == 3 * 2 + 2 * 2     # 3 leaves (XFORM + PRIM) + 2 unions (XFORM + CSG)
     for bad, msg in [({"type": "bogus", "matrix": scenes.EYE}, "Invalid"),
-                     ({"type": "screw", "matrix": scenes.EYE}, "outside the implemented"),
+                     ({"type": "screw", "matrix": scenes.EYE}, "missing"),
+                     ({"type": "meta_balls", "matrix": scenes.EYE}, "outside the implemented"),
                      ({"type": "iellipsoid"}, "matrix")]:
         with pytest.raises(Exception) as e:
             impli.program_info(bad)

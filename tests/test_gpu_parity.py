@@ -27,9 +27,33 @@ def _trees():
         {"type": "icylinder", "matrix": scenes.st(0.5, 0, 0, 0)}, {"type": "iellipsoid", "matrix": scenes.st(0.5, 0.25, 0, 0)}]}
     out["intersection"] = {"type": "Intersection", "matrix": scenes.EYE, "children": [
         {"type": "itorus", "matrix": scenes.st(0.25, 0, 0, 0)}, {"type": "icone", "matrix": scenes.st(1, 0, 0, -0.25)}]}
+    out.update(SCREW_TREES)
     return out
 
 
+def _screw_trees():
+    from implisolid_amd import scenes
+    tw = scenes.twist(1, 0, 0, 0)
+    return {
+        "twist": tw,
+        "twist_small_pitch": scenes.twist(0.5, 0.125, 0, 0.0625, pitch=0.0625),   # sinf arguments > 120
+        "twist_two_plane": dict(tw, type="screw_diff_two_plane"),
+        "twist_inf": dict(scenes.twist(0.5, 0, 0.25, 0), type="inf_screw", pitch=0.25),
+        "half_plane": {"type": "Intersection", "matrix": scenes.EYE, "children": [
+            {"type": "iellipsoid", "matrix": scenes.EYE},
+            {"type": "half_plane", "matrix": scenes.st(0.5, 0, 0.125, 0), "plane_vector": [0, 1, 2],
+             "plane_point": [0, 0, 0.25]}]},
+        "lid": {"type": "Intersection", "matrix": scenes.EYE, "children": [
+            {"type": "icylinder", "matrix": scenes.st(1, 0, 0, 0.5)},
+            {"type": "top_bottom_lid", "matrix": scenes.st(1, 0, 0, 0)}]},
+    }
+
+
+# the screw gradient (screw.hpp:152-160) calls the double cos, which is the device libm's here and
+# glibc's in the oracle (both within an ulp of cos): gradients of trees holding a twist are compared
+# to a tolerance, everything else (values, meshes) bit for bit
+SCREW_TREES = _screw_trees()
+GRAD_TOL = 2e-6
 TREES = _trees()
 
 
@@ -46,7 +70,18 @@ def test_eval_points_bit_exact(impli, oracle, name):
         f2 = svc.eval(pts)
     assert np.array_equal(f.view(np.uint32), f_ref.view(np.uint32)), np.flatnonzero(f != f_ref)[:10]
     assert np.array_equal(f2.view(np.uint32), f_ref.view(np.uint32))
-    assert np.array_equal(g.view(np.uint32), g_ref.view(np.uint32)), np.flatnonzero((g != g_ref).any(1))[:10]
+    if _has_twist(shape):
+        ok = np.isfinite(g_ref).all(1)
+        scale = np.maximum(np.abs(g_ref[ok]), 1.0)
+        assert (np.abs(g[ok] - g_ref[ok]) <= GRAD_TOL * scale).all()
+        assert np.array_equal(np.isfinite(g).all(1), ok)
+        assert (g == g_ref).all(1).mean() > 0.999          # bit-identical except where cos rounds apart
+    else:
+        assert np.array_equal(g.view(np.uint32), g_ref.view(np.uint32)), np.flatnonzero((g != g_ref).any(1))[:10]
+
+
+def _has_twist(shape):
+    return "screw" in json.dumps(shape)
 
 
 def test_direct_eval_abi_matches_reference_semantics(impli, oracle):
@@ -103,6 +138,21 @@ def test_union_sphere_cube_mc(impli, oracle, R):
 def test_random_tree_mc(impli, oracle, seed):
     from implisolid_amd import scenes
     _mc_compare(impli, oracle, scenes.random_tree(seed, 10), scenes.mc_settings(48, 1.0))
+
+
+@pytest.mark.parametrize("name", sorted(SCREW_TREES))
+def test_screw_family_mc(impli, oracle, name):
+    """Twist / lid / half-plane trees: field values are bit-exact (glibc sinf / atan2f restated),
+    so the meshes are too."""
+    from implisolid_amd import scenes
+    for R in (40, 97):
+        _mc_compare(impli, oracle, SCREW_TREES[name], scenes.mc_settings(R, 0.7))
+
+
+def test_config3_twist_tree_mc(impli, oracle):
+    from implisolid_amd import scenes
+    for R in (48, 128):
+        _mc_compare(impli, oracle, scenes.config3_tree(), scenes.mc_settings(R, 1.0))
 
 
 def test_anisotropic_box_mc(impli, oracle):
@@ -221,13 +271,19 @@ def test_zslab_gathered_counts_identical(impli, oracle, nranks):
     assert np.array_equal(np.concatenate(vs).view(np.uint32), ref_v.view(np.uint32))
 
 
-def _ob02_compare(impli, oracle, shape, mc, exact=True):
+def _ob02_compare(impli, oracle, shape, mc, exact=None):
+    """Faces bit-exact; vertices bit-exact, or (trees with a twist, whose gradient goes through the
+    double cos) within 1e-5 -- the north-star vertex tolerance."""
+    if exact is None:
+        exact = not _has_twist(shape)
     v, f = impli.make_geometry(shape, mc)
     vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
     assert np.array_equal(f, fr)
+    bad = np.flatnonzero((v != vr).any(1))
     if exact:
-        bad = np.flatnonzero((v != vr).any(1))
         assert bad.size == 0, (bad.size, bad[:10], np.abs(v - vr).max())
+    else:
+        assert np.abs(v - vr).max() < 1e-5, (bad.size, np.abs(v - vr).max())
     return v, vr
 
 
@@ -251,6 +307,13 @@ def test_ob02_full_config2_shape(impli, oracle, R):
     from implisolid_amd import scenes
     shape, mc = scenes.config2(R)
     _ob02_compare(impli, oracle, shape, mc)
+
+
+@pytest.mark.parametrize("name", ["twist", "twist_two_plane", "half_plane"])
+def test_ob02_screw_family(impli, oracle, name):
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(40, 0.7, vresampl_iters=1, vresampl_c=0.4, projection=1, qem=1, overall_repeats=2)
+    _ob02_compare(impli, oracle, SCREW_TREES[name], mc)
 
 
 def test_ob02_config3_tree_small(impli, oracle):
@@ -338,7 +401,12 @@ def test_golden_points_gpu(impli):
         with impli.ImplicitService(sh) as svc:
             f, gr = svc.eval(g["points"], gradient=True)
         assert np.array_equal(f.view(np.uint32), g["f_" + name].view(np.uint32)), name
-        assert np.array_equal(gr.view(np.uint32), g["g_" + name].view(np.uint32)), name
+        if _has_twist(sh):
+            ref = g["g_" + name]
+            ok = np.isfinite(ref).all(1)
+            assert (np.abs(gr[ok] - ref[ok]) <= GRAD_TOL * np.maximum(np.abs(ref[ok]), 1.0)).all(), name
+        else:
+            assert np.array_equal(gr.view(np.uint32), g["g_" + name].view(np.uint32)), name
 
 
 def test_golden_config2_ob02_gpu(impli):
