@@ -32,7 +32,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 # algorithmic FP ops per sample for one instruction of the node program
-OP_FLOPS = {"xform": 18, "csg": 2, 3: 9, 4: 45, 5: 24, 6: 20, 7: 24, 8: 14, 9: 12}
+OP_FLOPS = {"xform": 18, "csg": 2, 3: 9, 4: 45, 5: 24, 6: 20, 7: 24, 8: 14, 9: 12,
+            10: 90, 11: 3, 12: 8}   # 10 screw (atan2f + sinf + 25), 11 lid, 12 half plane
 
 
 def program_flops(shape):
@@ -45,6 +46,13 @@ def program_flops(shape):
             kids = d["children"]
             n = len(kids) - 1 if t == "Union" else 1
             return OP_FLOPS["csg"] * n + OP_FLOPS["xform"] * n + sum(walk(c) for c in (kids if t == "Union" else kids[:2]))
+        x, c = OP_FLOPS["xform"], OP_FLOPS["csg"]
+        composite = {"screw": (c + x) + (x + OP_FLOPS[10]) + (x + OP_FLOPS[11]),
+                     "inf_screw": x + OP_FLOPS[10],
+                     "screw_diff_two_plane": 2 * (c + x) + (x + OP_FLOPS[10]) + 2 * (x + OP_FLOPS[12]),
+                     "top_bottom_lid": x + OP_FLOPS[11], "half_plane": x + OP_FLOPS[12]}
+        if t in composite:
+            return composite[t]
         code = {"iellipsoid": 3, "ellipsoid": 3, "cube": 4, "icube": 4, "icylinder": 5, "cylinder": 5, "icone": 6,
                 "cone": 6, "iheart": 7, "itorus": 8, "implicit_double_mushroom": 9}[t]
         return OP_FLOPS["xform"] + OP_FLOPS[code]
@@ -81,6 +89,8 @@ def main():
     ap.add_argument("--skip-256", action="store_true", help="do not also time R=256")
     ap.add_argument("--prune", type=int, default=None, help="pruning level 0/1/2 (default: library default 2)")
     ap.add_argument("--strong", action="store_true", help="N > 1: the headline is strong scaling of the R grid")
+    ap.add_argument("--skip-config5", action="store_true", help="do not time the 64-object stream (config 5)")
+    ap.add_argument("--config5-streams", type=int, default=8)
     args = ap.parse_args()
 
     import torch
@@ -188,6 +198,36 @@ def main():
     rdense = None if (args.skip_256 or world > 1) else run(args.resolution, args.steps, args.warmup,
                                            scene=(scenes.union_sphere_cube(), scenes.mc_settings(args.resolution, 1.0)))
 
+    # config 5: a stream of 64 seeded random MP5 objects at 128^3, eval + MC, each object's
+    # pipeline captured once in a hipGraph and replayed (objects round-robin over a few streams)
+    c5 = None
+    if world == 1 and not args.skip_config5:
+        objs = scenes.config5_objects(64, 128)
+        t0 = time.perf_counter()
+        batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=args.config5_streams)
+        setup_s = time.perf_counter() - t0
+        for _ in range(max(1, args.warmup)):
+            batch.run(sp)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            batch.run(sp)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        tv = tf = 0
+        for i in range(batch.n):
+            a, b_, of = batch.counts(i)
+            if of:
+                raise RuntimeError("config 5: object %d overflowed" % i)
+            tv, tf = tv + a, tf + b_
+        ms5 = el / args.steps * 1e3
+        c5 = {"workload": "config5: 64 seeded random MP5 objects (scenes.config5_objects, 1-12 leaves) at 128^3, "
+                          "eval+MC, hipGraph per object, %d streams" % batch.n_streams,
+              "objects_per_s": round(batch.n / (ms5 * 1e-3), 1), "value": round(batch.n * 128 ** 3 / (ms5 * 1e-3) / 1e6, 2),
+              "unit": "Mvoxels/s", "ms_per_stream": round(ms5, 4), "graphs": batch.graphs,
+              "verts": tv, "faces": tf, "setup_s": round(setup_s, 2), "jit_compile_s": round(batch.jit_seconds, 2)}
+        batch.close()
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -244,7 +284,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": "config4: seeded 21-node MP5 CSG tree (scenes.config4, seed 20251015), box [-1,1]^3, "
+            "workload": "config4: seeded ~20-node MP5 CSG tree with twist/union/difference (scenes.config4, seed 20251015), box [-1,1]^3, "
                         "R=%d, eval+MC, mesh resident in HBM%s" % (
                             R, (", weak scaling: R = %d N^(1/3), ~%d^3 voxels per rank" % (args.resolution, args.resolution))
                             if weak else ""),
@@ -282,6 +322,8 @@ def main():
         ms256 = r256["elapsed"] / args.steps * 1e3
         out["value_256"] = round(256 ** 3 / (ms256 * 1e-3) / 1e6, 2)
         out["ms_per_step_256"] = round(ms256, 4)
+    if c5:
+        out["config5"] = c5
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(main_run["shape"])
     else:

@@ -33,6 +33,8 @@ ABI_SYMBOLS = [
     "implisolid_slab_set_timing", "implisolid_slab_kernel_times", "implisolid_jit_compile",
     "implisolid_slab_used_jit", "implisolid_set_jit", "implisolid_slab_stats", "implisolid_slab_read_signs",
     "implisolid_srand", "implisolid_rand", "implisolid_rand_skip",
+    "implisolid_batch_create", "implisolid_batch_run", "implisolid_batch_info", "implisolid_batch_counts",
+    "implisolid_batch_download", "implisolid_batch_destroy",
 ]
 
 _lib = None
@@ -107,6 +109,12 @@ def lib():
         "implisolid_srand": ([ctypes.c_uint], None),
         "implisolid_rand": ([], c_int),
         "implisolid_rand_skip": ([ctypes.c_uint64], None),
+        "implisolid_batch_create": ([ctypes.POINTER(c_char_p), c_int, c_char_p, c_int], c_void_p),
+        "implisolid_batch_run": ([c_void_p, c_void_p], c_int),
+        "implisolid_batch_info": ([c_void_p, ip, ctypes.POINTER(ctypes.c_double)], c_int),
+        "implisolid_batch_counts": ([c_void_p, c_int, up], c_int),
+        "implisolid_batch_download": ([c_void_p, c_int, fp, ip], c_int),
+        "implisolid_batch_destroy": ([c_void_p], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -438,3 +446,51 @@ class Slab:
             self.close()
         except Exception:
             pass
+
+
+class Batch:
+    """A stream of objects polygonised with one mc-settings dict (BASELINE config 5): every
+    object's eval + count + emit is captured in a hipGraph on creation; run() replays them all
+    (asynchronously, on `stream`), counts()/download() block."""
+
+    def __init__(self, shapes, mc_settings, n_streams=4):
+        L = lib()
+        enc = [_s(sh) for sh in shapes]
+        arr = (ctypes.c_char_p * len(enc))(*enc)
+        self.h = L.implisolid_batch_create(arr, len(enc), _s(mc_settings), int(n_streams))
+        if not self.h:
+            raise ImplisolidError(last_error() or "implisolid_batch_create failed")
+        info = (ctypes.c_int32 * 4)()
+        secs = ctypes.c_double(0)
+        L.implisolid_batch_info(self.h, info, ctypes.byref(secs))
+        self.n, self.n_streams, self.graphs, self.jit_seconds = int(info[0]), int(info[1]), bool(info[2]), secs.value
+
+    def run(self, stream=None):
+        if lib().implisolid_batch_run(self.h, stream) != 0:
+            raise ImplisolidError(last_error())
+
+    def counts(self, i):
+        out = (ctypes.c_uint32 * 3)()
+        if lib().implisolid_batch_counts(self.h, int(i), out) != 0:
+            raise ImplisolidError(last_error())
+        return int(out[0]), int(out[1]), bool(out[2])
+
+    def download(self, i):
+        nv, nf, of = self.counts(i)
+        v = np.empty((nv, 3), np.float32)
+        f = np.empty((nf, 3), np.int32)
+        if lib().implisolid_batch_download(self.h, int(i), v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                           f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))) != 0:
+            raise ImplisolidError(last_error())
+        return v, f
+
+    def close(self):
+        if self.h:
+            lib().implisolid_batch_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -544,4 +544,158 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
     }
 }
 
+// ---- object stream (config 5): one engine per object, each object's eval + count + emit captured
+//      once in a hipGraph and replayed; objects spread over a few streams ----------------------------
+struct implisolid_batch {
+    std::vector<std::unique_ptr<Engine>> engines;
+    std::vector<hipGraphExec_t> execs;   // empty when capture is unavailable (direct launches)
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> events;      // fork (0) and one join event per stream
+    double jit_seconds = 0;
+};
+
+implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, const char* mc_json, int n_streams) {
+    g_last_error.clear();
+    auto* b = new implisolid_batch();
+    try {
+        if (n <= 0) throw InputError("implisolid_batch_create: no objects");
+        const MCSettings st = parse_mc_settings(mc_json);
+        std::vector<Program> progs;
+        for (int i = 0; i < n; ++i) progs.push_back(compile_mp5(shapes[i], st.ignore_root_matrix));
+        const auto t0 = std::chrono::steady_clock::now();
+        if (Engine::pruning() > 0) TreeJit::instance().precompile(progs, 16);
+        b->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        const int ns = std::max(1, std::min(n_streams, 8));
+        for (int k = 0; k < ns; ++k) {
+            hipStream_t q;
+            IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+            b->streams.push_back(q);
+        }
+        for (int k = 0; k <= ns; ++k) {
+            hipEvent_t e;
+            IMPLI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            b->events.push_back(e);
+        }
+        hipStream_t s0 = b->streams[0];
+        for (int i = 0; i < n; ++i) {   // warm run: JIT lookup, output capacities from the real counts
+            b->engines.emplace_back(new Engine());
+            Engine& E = *b->engines.back();
+            E.set_object(progs[(size_t)i]);
+            E.set_grid(st.resolution, st.box, 0, 1);
+            E.marching_cubes(s0);
+        }
+        bool graphs = !std::getenv("IMPLISOLID_NO_GRAPH");
+        for (int i = 0; i < n && graphs; ++i) {
+            hipGraph_t g = nullptr;
+            hipGraphExec_t x = nullptr;
+            if (hipStreamBeginCapture(s0, hipStreamCaptureModeRelaxed) != hipSuccess) { graphs = false; break; }
+            bool ok = true;
+            try {
+                b->engines[(size_t)i]->eval_field(s0);
+                b->engines[(size_t)i]->count(s0);
+                b->engines[(size_t)i]->emit(nullptr, s0);
+            } catch (const std::exception&) {
+                ok = false;
+            }
+            const hipError_t ec = hipStreamEndCapture(s0, &g);
+            if (!ok || ec != hipSuccess || !g || hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                (void)hipGetLastError();
+                graphs = false;
+                break;
+            }
+            (void)hipGraphDestroy(g);
+            b->execs.push_back(x);
+        }
+        if (!graphs) {
+            for (auto x : b->execs) (void)hipGraphExecDestroy(x);
+            b->execs.clear();
+            std::fprintf(stderr, "implisolid: stream capture unavailable, the batch launches directly\n");
+        }
+        IMPLI_HIP(hipStreamSynchronize(s0));
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        implisolid_batch_destroy(b);
+        return nullptr;
+    }
+    return b;
+}
+
+int implisolid_batch_run(implisolid_batch* b, void* stream) {
+    try {
+        hipStream_t s = (hipStream_t)stream;
+        const int ns = (int)b->streams.size();
+        IMPLI_HIP(hipEventRecord(b->events[0], s));
+        for (int k = 0; k < ns; ++k) IMPLI_HIP(hipStreamWaitEvent(b->streams[(size_t)k], b->events[0], 0));
+        for (size_t i = 0; i < b->engines.size(); ++i) {
+            hipStream_t q = b->streams[i % (size_t)ns];
+            if (!b->execs.empty()) {
+                IMPLI_HIP(hipGraphLaunch(b->execs[i], q));
+            } else {
+                b->engines[i]->eval_field(q);
+                b->engines[i]->count(q);
+                b->engines[i]->emit(nullptr, q);
+            }
+        }
+        for (int k = 0; k < ns; ++k) {
+            IMPLI_HIP(hipEventRecord(b->events[(size_t)k + 1], b->streams[(size_t)k]));
+            IMPLI_HIP(hipStreamWaitEvent(s, b->events[(size_t)k + 1], 0));
+        }
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
+int implisolid_batch_info(implisolid_batch* b, int32_t out[4], double* jit_seconds) {
+    out[0] = (int32_t)b->engines.size();
+    out[1] = (int32_t)b->streams.size();
+    out[2] = b->execs.empty() ? 0 : 1;
+    out[3] = 0;
+    if (jit_seconds) *jit_seconds = b->jit_seconds;
+    return 0;
+}
+
+int implisolid_batch_counts(implisolid_batch* b, int i, uint32_t out[3]) {
+    try {
+        if (i < 0 || i >= (int)b->engines.size()) throw InputError("implisolid_batch_counts: bad index");
+        for (auto q : b->streams) IMPLI_HIP(hipStreamSynchronize(q));
+        bool of = false;
+        const SlabCounts c = b->engines[(size_t)i]->read_counts(b->streams[0], &of);
+        out[0] = c.n_verts();
+        out[1] = c.n_faces();
+        out[2] = of ? 1u : 0u;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
+int implisolid_batch_download(implisolid_batch* b, int i, float* verts, int32_t* faces) {
+    try {
+        if (i < 0 || i >= (int)b->engines.size()) throw InputError("implisolid_batch_download: bad index");
+        for (auto q : b->streams) IMPLI_HIP(hipStreamSynchronize(q));
+        bool of = false;
+        Engine& E = *b->engines[(size_t)i];
+        const SlabCounts c = E.read_counts(b->streams[0], &of);
+        if (of) throw HipError("batch object overflowed its output capacity");
+        E.download(verts, faces, c, b->streams[0]);
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
+void implisolid_batch_destroy(implisolid_batch* b) {
+    if (!b) return;
+    for (auto q : b->streams) (void)hipStreamSynchronize(q);
+    for (auto x : b->execs) (void)hipGraphExecDestroy(x);
+    for (auto e : b->events) (void)hipEventDestroy(e);
+    for (auto q : b->streams) (void)hipStreamDestroy(q);
+    delete b;
+}
+
 }  // extern "C"

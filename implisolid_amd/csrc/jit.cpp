@@ -8,8 +8,11 @@
 #include <cstring>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
+#include <set>
 #include <sstream>
 #include <stdexcept>
+#include <thread>
 #include <vector>
 
 #include "generated/jit_headers.inc"
@@ -370,6 +373,59 @@ TreeJit::Kernels TreeJit::kernels(const Program& p) {
     if (ent.k.bricks) ++n_compiled_;
     cache_.emplace(src, ent);
     return ent.k;
+}
+
+void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
+    if (!enabled_) return;
+    std::vector<std::string> srcs;
+    {
+        std::set<std::string> seen;
+        std::lock_guard<std::mutex> lock(mu_);
+        for (const Program& p : progs) {
+            std::string src;
+            try {
+                src = kernel_source(p);
+            } catch (const std::exception&) {
+                continue;   // kernels() logs and falls back for this shape
+            }
+            if (!cache_.count(src) && seen.insert(src).second) srcs.push_back(std::move(src));
+        }
+    }
+    if (srcs.empty()) return;
+    std::vector<std::vector<char>> codes(srcs.size());
+    std::vector<std::string> errs(srcs.size());
+    std::atomic<size_t> next{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    auto work = [&] {
+        for (size_t i; (i = next++) < srcs.size();) {
+            try {
+                codes[i] = compile(srcs[i]);
+            } catch (const std::exception& e) {
+                errs[i] = e.what();
+            }
+        }
+    };
+    const int nt = std::max(1, std::min<int>(threads, (int)srcs.size()));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    std::lock_guard<std::mutex> lock(mu_);
+    for (size_t i = 0; i < srcs.size(); ++i) {
+        Entry ent;
+        if (!codes[i].empty() && hipModuleLoadData(&ent.mod, codes[i].data()) == hipSuccess &&
+            hipModuleGetFunction(&ent.k.bricks, ent.mod, "impli_eval_bricks") == hipSuccess &&
+            hipModuleGetFunction(&ent.k.coarse, ent.mod, "impli_coarse_modes") == hipSuccess &&
+            hipModuleGetFunction(&ent.k.refine, ent.mod, "impli_brick_refine") == hipSuccess) {
+            ++n_compiled_;
+        } else {
+            std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n",
+                         errs[i].empty() ? "module load failed" : errs[i].substr(0, 400).c_str());
+            ent.k = Kernels{};
+        }
+        cache_.emplace(srcs[i], ent);
+    }
+    compile_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,

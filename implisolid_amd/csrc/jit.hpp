@@ -39,6 +39,10 @@ public:
     };
     Kernels kernels(const Program& p);
 
+    // compile the kernels of many shapes on up to `threads` host threads (hipRTC runs outside the
+    // cache lock); shapes already cached are skipped.  kernels() then finds them cached.
+    void precompile(const std::vector<Program>& progs, int threads);
+
     // launch the compiled brick kernel (same contract as launch_eval_field_pruned's 2nd kernel)
     static void launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
                               const BrickGrid& bg, const uint64_t* d_modes, const uint32_t* d_list,
