@@ -69,7 +69,9 @@ void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.c
     E.set_grid(st.resolution, st.box, 0, 1);
     SlabCounts c = E.marching_cubes(s);   // polygonize_step_0
     int64_t nv = c.n_verts(), nf = c.n_faces();
-    Ob02 ob(E, s);
+    static std::unique_ptr<Ob02> ob_ptr;   // one refinement state, its buffers reused by every build
+    if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+    Ob02& ob = *ob_ptr;
     ob.load_mesh(E.d_verts(), nv, E.d_faces(), nf);
     for (int rep = 0; rep < st.overall_repeats; ++rep) {
         for (int i = 0; i < st.vresampl_iters; ++i) ob.vertex_resampling(st.vresampl_c);   // step 1

@@ -86,6 +86,60 @@ __global__ __launch_bounds__(1024) void k_scan_u32(const uint32_t* __restrict__ 
     if (t == 0) out[n] = tot;
 }
 
+// multi-block exclusive scan: tiles of 256 x 16 values -> tile sums -> one-block scan of the sums
+// (k_scan_u32) -> tiles re-scanned with their offsets.  out[n] = total.
+constexpr int kScanPer = 16, kScanTile = 256 * kScanPer;
+
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* s_w, uint32_t& total) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    uint32_t v = x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) s_w[wid] = v;
+    __syncthreads();
+    uint32_t pre = 0;
+    total = 0;
+    for (int w = 0; w < 4; ++w) {
+        pre += (w < wid) ? s_w[w] : 0u;
+        total += s_w[w];
+    }
+    __syncthreads();
+    return pre + v - x;
+}
+
+__global__ __launch_bounds__(256) void k_scan_tile_sums(const uint32_t* __restrict__ in, int64_t n, uint32_t* __restrict__ sums) {
+    __shared__ uint32_t s_w[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
+    uint32_t a = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) a += (base + k < n) ? in[base + k] : 0u;
+    uint32_t total;
+    (void)block_excl_scan256(a, s_w, total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_scan_tiles(const uint32_t* __restrict__ in, int64_t n, const uint32_t* __restrict__ offs,
+                                                    uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_w[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
+    uint32_t v[kScanPer], a = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        v[k] = (base + k < n) ? in[base + k] : 0u;
+        a += v[k];
+    }
+    uint32_t total;
+    uint32_t run = offs[blockIdx.x] + block_excl_scan256(a, s_w, total);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = offs[blockIdx.x] + total;
+}
+
 __global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const uint32_t* __restrict__ off,
                                 uint32_t* __restrict__ fill, int32_t* __restrict__ lst) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -733,6 +787,11 @@ Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
 void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_) {
     nv = nv_;
     nf = nf_;
+    for (auto& kv : snaps_) kv.second.buf.release();
+    snaps_.clear();
+    pointsets_.clear();
+    cap_hits_ = 0;
+    avg_edge_ = 0.f;
     verts_.reserve((size_t)(nv + 1) * 12);
     vnew_.reserve((size_t)(nv + 1) * 12);
     faces_.reserve((size_t)(nf + 1) * 12);
@@ -762,7 +821,7 @@ void Ob02::build_topology() {
     ulst_.reserve((size_t)(3 * nf + 1) * 4);
     IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
     if (nf) k_degree<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
-    k_scan_u32<<<1, 1024, 0, s>>>(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv);
+    scan(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv);
     IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
     if (nf) k_fill_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(),
                                                              deg_.as<uint32_t>(), ulst_.as<int32_t>());
@@ -785,13 +844,47 @@ void Ob02::build_topology() {
     topo_valid_ = true;
 }
 
+void Ob02::scan(const uint32_t* in, uint32_t* out, int64_t n) {
+    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles <= 1) {
+        k_scan_u32<<<1, 1024, 0, s>>>(in, out, n);
+        return;
+    }
+    scan_tmp_.reserve((size_t)(2 * tiles + 2) * 4);
+    uint32_t* sums = scan_tmp_.as<uint32_t>();
+    uint32_t* offs = sums + tiles + 1;
+    k_scan_tile_sums<<<(unsigned)tiles, 256, 0, s>>>(in, n, sums);
+    k_scan_u32<<<1, 1024, 0, s>>>(sums, offs, tiles);
+    k_scan_tiles<<<(unsigned)tiles, 256, 0, s>>>(in, n, offs, out);
+}
+
+// STORE_POINTSET: a device snapshot now (stream-ordered, no host sync), copied to the host only
+// when pointsets() is asked for
 void Ob02::store_pointset(const char* key, const float* d, int64_t n, bool keep_first) {
     if (!capture_pointsets) return;
-    if (keep_first && pointsets_.count(key)) return;
-    std::vector<float> h((size_t)n * 3);
-    if (n) IMPLI_HIP(hipMemcpyAsync(h.data(), d, (size_t)n * 12, hipMemcpyDeviceToHost, s));
+    if (keep_first && snaps_.count(key)) return;
+    Snapshot& e = snaps_[key];
+    e.buf.reserve((size_t)(n + 1) * 12);
+    e.n = n;
+    if (n) IMPLI_HIP(hipMemcpyAsync(e.buf.p, d, (size_t)n * 12, hipMemcpyDeviceToDevice, s));
+}
+
+const std::map<std::string, std::vector<float>>& Ob02::pointsets() {
+    pointsets_.clear();
+    for (auto& kv : snaps_) {
+        std::vector<float>& h = pointsets_[kv.first];
+        h.resize((size_t)kv.second.n * 3);
+        if (kv.second.n) IMPLI_HIP(hipMemcpyAsync(h.data(), kv.second.buf.p, (size_t)kv.second.n * 12, hipMemcpyDeviceToHost, s));
+    }
     IMPLI_HIP(hipStreamSynchronize(s));
-    pointsets_[key] = std::move(h);
+    return pointsets_;
+}
+
+Ob02::~Ob02() {
+    for (DevBuf* b : {&verts_, &faces_, &vnew_, &cen_, &nrm_, &w_, &fof_, &uoff_, &ulst_, &etab_, &deg_, &proj_, &grad_,
+                      &fn_, &norms_, &alphas_, &pert_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_})
+        b->release();
+    for (auto& kv : snaps_) kv.second.buf.release();
 }
 
 void Ob02::vertex_resampling(float c) {
@@ -939,7 +1032,7 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
         deg_.reserve((size_t)(nf + 2) * 4);
         pend_.reserve((size_t)(cap + 1) * 4);
         k_sub_count<<<blocks_for(nf), 256, 0, s>>>(nf, t, cnt.as<uint32_t>());
-        k_scan_u32<<<1, 1024, 0, s>>>(cnt.as<uint32_t>(), deg_.as<uint32_t>(), nf);
+        scan(cnt.as<uint32_t>(), deg_.as<uint32_t>(), nf);
         uint32_t tot = 0;
         IMPLI_HIP(hipMemcpyAsync(&tot, deg_.as<uint32_t>() + nf, 4, hipMemcpyDeviceToHost, s));
         IMPLI_HIP(hipStreamSynchronize(s));

@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""End-to-end build_geometry timings (host-resident result, PCIe included) for the OB02 configs:
+config 2 (union sphere+rabbit, 128^3, MC + 3 x [resample, project, QEM]) and config 3 (twist tree,
+256^3, same loop), plus MC-only and subdivision variants.  usage: python tools/ob02_probe.py [reps]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    import implisolid_amd as I
+    from implisolid_amd import scenes
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    torch.cuda.init()
+    cases = [("config2 R128 MC only", scenes.union_sphere_cube(), scenes.mc_settings(128, 1.0)),
+             ("config2 R128 MC+3xOB02", *scenes.config2(128)),
+             ("config3 R256 MC only", scenes.config3_tree(), scenes.mc_settings(256, 1.0)),
+             ("config3 R256 MC+3xOB02", *scenes.config3(256))]
+    sub = dict(scenes.config2(128)[1])
+    sub["subdiv"] = {"enabled": 1}
+    sub["debug"] = {"post_subdiv_noise": 0.01}
+    cases.append(("config2 R128 MC+3xOB02+subdiv", scenes.union_sphere_cube(), sub))
+    for name, shape, mc in cases:
+        I.make_geometry(shape, mc)   # warm (JIT, buffers)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            v, f = I.make_geometry(shape, mc)
+            ts.append(time.perf_counter() - t0)
+        print("%-32s V %8d F %8d  build_geometry %.2f ms (min of %d)" % (name, len(v), len(f), min(ts) * 1e3, reps),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
