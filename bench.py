@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--strong", action="store_true", help="N > 1: the headline is strong scaling of the R grid")
     ap.add_argument("--skip-config5", action="store_true", help="do not time the 64-object stream (config 5)")
     ap.add_argument("--config5-streams", type=int, default=8)
+    ap.add_argument("--skip-ob02", action="store_true", help="do not time build_geometry with the OB02 loop")
     args = ap.parse_args()
 
     import torch
@@ -228,6 +229,28 @@ def main():
               "verts": tv, "faces": tf, "setup_s": round(setup_s, 2), "jit_compile_s": round(batch.jit_seconds, 2)}
         batch.close()
 
+    # configs 2 and 3 through the C ABI: build_geometry (MC + 3 x [resample, project, QEM]) to a
+    # host-resident mesh, PCIe included; the oracle times config 2 on one host core beside it
+    ob02 = None
+    if world == 1 and not args.skip_ob02:
+        ob02 = {}
+        for key, (shape, mc) in (("config2_r128", scenes.config2(128)), ("config3_r256", scenes.config3(256))):
+            I.make_geometry(shape, mc)
+            ts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                v, f = I.make_geometry(shape, mc)
+                ts.append(time.perf_counter() - t0)
+            ob02[key] = {"build_geometry_ms": round(min(ts) * 1e3, 3), "verts": int(len(v)), "faces": int(len(f)),
+                         "steps": "MC + 3 x [vertex resampling, centroid projection, QEM]"}
+        if not args.no_cpu_baseline:
+            import oracle
+            oracle.build()
+            shape, mc = scenes.config2(128)
+            t0 = time.perf_counter()
+            oracle.polygonize(json.dumps(shape), json.dumps(mc))
+            ob02["config2_r128"]["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -324,6 +347,8 @@ def main():
         out["ms_per_step_256"] = round(ms256, 4)
     if c5:
         out["config5"] = c5
+    if ob02:
+        out["ob02"] = ob02
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(main_run["shape"])
     else:
