@@ -1,6 +1,7 @@
 // host.cpp -- mc-settings parser, MP5-JSON -> node-program compiler, float LU inverse.
 #include "host.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -150,13 +151,19 @@ struct Builder {
         }
     }
 
-    // raw parameter row (not inverted) for primitives that carry parameters (Instr::prm)
+    // raw parameters (not inverted) for primitives that carry them (Instr::prm): ceil(n / 12)
+    // consecutive rows of mats[], read as one float array
     int add_params(const float* v, int n) {
-        if (p.n_mats >= kMaxProgram) throw InputError("MP5 tree too large");
-        float row[12] = {};
-        std::memcpy(row, v, sizeof(float) * (size_t)n);
-        std::memcpy(p.mats[p.n_mats], row, sizeof row);
-        return p.n_mats++;
+        const int rows = (n + 11) / 12;
+        if (p.n_mats + rows > kMaxProgram) throw InputError("MP5 tree too large");
+        const int first = p.n_mats;
+        for (int r = 0; r < rows; ++r) {
+            float row[12] = {};
+            const int k = std::min(12, n - 12 * r);
+            std::memcpy(row, v + 12 * r, sizeof(float) * (size_t)k);
+            std::memcpy(p.mats[p.n_mats++], row, sizeof row);
+        }
+        return first;
     }
 
     // A "subtree" pushes exactly one value; it sees the parent's local point on top of the stack.
@@ -193,6 +200,95 @@ struct Builder {
             prm[3 + k] = pp[k];
         }
     }
+    // tetrahedron (tetrahedron.hpp:20-128; getCorners object_factory.hpp:32-45, a missing corner
+    // stays 0): corners moved by the forward node matrix (matrix_vector_product,
+    // basic_functions.hpp:140-177), the four calculatePlaneCoefficients planes, each multiplied by
+    // the sign (ROOT_TOLERANCE, configs.hpp:33) of its value at the opposite corner
+    static void tetra_params(const Json& d, const float m[12], float out[16]) {
+        float c[4][3] = {};
+        if (const Json* cs = d.find("corners")) {
+            if (cs->kind != Json::Array) throw InputError("tetrahedron: \"corners\" must be an array");
+            for (size_t i = 0; i < cs->items.size() && i < 4; ++i) {
+                const Json& cj = cs->items[i].second;
+                for (size_t j = 0; j < cj.items.size() && j < 3; ++j)
+                    if (!cj.items[j].second.as_float(&c[i][j])) throw InputError("tetrahedron: bad corner");
+            }
+        } else {
+            throw InputError("tetrahedron: missing \"corners\"");
+        }
+        float p[4][3];
+        for (int i = 0; i < 4; ++i)
+            for (int r = 0; r < 3; ++r)
+                p[i][r] = m[4 * r] * c[i][0] + m[4 * r + 1] * c[i][1] + m[4 * r + 2] * c[i][2] + m[4 * r + 3];
+        auto coef = [](const float* P1, const float* P2, const float* P3, float* o) {
+            const float x1 = P1[0], y1 = P1[1], z1 = P1[2], x2 = P2[0], y2 = P2[1], z2 = P2[2], x3 = P3[0], y3 = P3[1],
+                        z3 = P3[2];
+            o[0] = y1 * z2 - y1 * z3 - y2 * z1 + y2 * z3 + y3 * z1 - y3 * z2;
+            o[1] = x1 * z3 - x1 * z2 + x2 * z1 - x2 * z3 - x3 * z1 + x3 * z2;
+            o[2] = x1 * y2 - x1 * y3 - x2 * y1 + x2 * y3 + x3 * y1 - x3 * y2;
+            o[3] = x1 * y3 * z2 - x1 * y2 * z3 + x2 * y1 * z3 - x2 * y3 * z1 - x3 * y1 * z2 + x3 * y2 * z1;
+        };
+        coef(p[1], p[2], p[3], out);
+        coef(p[0], p[2], p[3], out + 4);
+        coef(p[0], p[1], p[3], out + 8);
+        coef(p[0], p[1], p[2], out + 12);
+        const float tol = (float)(0.001 / 10.0);
+        for (int k = 0; k < 4; ++k) {
+            float* P = out + 4 * k;
+            const float v = P[0] * p[k][0] + P[1] * p[k][1] + P[2] * p[k][2] + P[3];
+            const float sg = (v > +tol) ? 1.0f : (v < -tol) ? -1.0f : 0.0f;   // sign(), basic_functions.hpp:22-31
+            for (int j = 0; j < 4; ++j) P[j] *= sg;
+        }
+    }
+    // meta_ball_Rydgard (meta_balls_Rydgard.hpp:27-60): 4 blobs, scale 1; ball centres in double
+    // (libm sin / cos) stored to float; strength 1.2 / ((sqrt(4) - 1) / 4 + 1), subtract 12
+    static void metaball_params(const Json& d, float out[20]) {
+        float time = 0.1f;   // get<REAL>("time", 0.1)
+        if (d.find("time") && !d.get_float("time", &time)) throw InputError("meta_balls: bad \"time\"");
+        const int numblobs = 4;
+        for (int i = 0; i < numblobs; ++i) {
+            const float x0 = 0.5f, y0 = 0.5f, z0 = 0.5f, D = 1;
+            const float ballx = (float)(std::sin(i + 1.26 * time * (1.03 + 0.5 * std::cos(0.21 * i))) * 0.27 * D + 0.5 - x0);
+            const float bally = (float)(std::abs(std::cos(i + 1.12 * time * std::cos(1.22 + 0.1424 * i))) * 0.77 * D - y0);
+            const float ballz = (float)(std::cos(i + 1.32 * time * 0.1 * std::sin((0.92 + 0.53 * i))) * 0.27 * D + 0.5 - z0);
+            const float subtract = 12;
+            const float strength = (float)(1.2 / ((std::sqrt((double)numblobs) - 1) / 4 + 1));
+            const float v[5] = {ballx, bally, ballz, strength, subtract};
+            std::memcpy(out + 5 * i, v, sizeof v);
+        }
+    }
+    // extrusion(eye, size) (extrusion.hpp:61-94) with convex_polygon::update_inner_data
+    // (2d/GDT/convex_polygon.hpp:77-93): regular size-gon of radius 0.5 from (0, 0.5),
+    // polarToCartesian (basic_functions.hpp:33-36) through std::cos/sin(float); 1/d in double
+    static int extrusion_params(const Json& d, float* out) {
+        float fs;
+        if (!d.get_float("size", &fs)) throw InputError("extrusion: missing \"size\"");
+        const int size = (int)fs;
+        if (size < 3) throw InputError("extrusion: Invalid size");
+        if (size > 40) throw InputError("extrusion: size above 40 is not supported");
+        const float PI = (float)3.141592653589793238463;   // basic_functions.hpp:8
+        const float rot = 2 * PI / size;
+        std::vector<float> cx{0.f}, cy{0.5f};
+        const float radius = 0.5f;
+        for (int i = 1; i < size; ++i) {
+            const float theta = (float)(PI / 2.0 + i * rot);
+            cx.push_back(radius * std::cos(theta));
+            cy.push_back(radius * std::sin(theta));
+        }
+        out[0] = (float)size;
+        for (int i = 0; i < size; ++i) {
+            const int j = (i < size - 1) ? i + 1 : 0;
+            const float dx = cx[j] - cx[i], dy = cy[j] - cy[i];
+            const float dd = std::sqrt(dx * dx + dy * dy);
+            const float dinv = (float)((dd > 0.00000001) ? 1.0 / dd : 0.0);
+            const float nx = +dy * dinv, ny = -dx * dinv;
+            out[1 + 3 * i] = nx;
+            out[2 + 3 * i] = ny;
+            out[3 + 3 * i] = cx[i] * nx + cy[i] * ny;
+        }
+        return 1 + 3 * size;
+    }
+
     static void vec3(const Json& d, const char* key, float out[3]) {
         const Json* a = d.find(key);
         if (!a || a->kind != Json::Array || a->items.size() < 3) throw InputError(std::string("half_plane: bad \"") + key + "\"");
@@ -302,8 +398,31 @@ struct Builder {
             leaf(NT_HALF_PLANE, m, prm, 6);
             return;
         }
-        static const char* unsupported[] = {"tetrahedron", "sdf_3d", "screw_gradient_wrong", "rawjscode", "meta_balls",
-                                            "extrusion"};
+        if (t == "tetrahedron") {      // :175-188: the corners are moved, the object itself is not
+            float prm[16];
+            matrix12(d, m);
+            if (ignore) std::memcpy(m, eye, sizeof m);
+            tetra_params(d, m, prm);
+            leaf(NT_TETRA, eye, prm, 16);
+            return;
+        }
+        if (t == "meta_balls") {       // :654-673
+            float prm[20];
+            matrix12(d, m);
+            if (ignore) std::memcpy(m, eye, sizeof m);
+            metaball_params(d, prm);
+            leaf(NT_METABALLS, m, prm, 20);
+            return;
+        }
+        if (t == "extrusion") {        // :674-731: subtract(extrusion(eye, size), top_bottom_lid)
+            float prm[1 + 3 * 40];
+            matrix12(d, m);
+            if (ignore) std::memcpy(m, eye, sizeof m);
+            const int n = extrusion_params(d, prm);
+            csg(NT_DIFFERENCE, m, [&] { leaf(NT_EXTRUSION, eye, prm, n); }, [&] { leaf(NT_LID, eye); });
+            return;
+        }
+        static const char* unsupported[] = {"sdf_3d", "screw_gradient_wrong", "rawjscode"};
         for (auto* u : unsupported)
             if (t == u) throw InputError("MP5 type \"" + t + "\" is outside the implemented node families");
         throw InputError("Invalid object you asked for: \"" + t + "\"");

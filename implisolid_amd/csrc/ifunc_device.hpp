@@ -412,6 +412,82 @@ __device__ __forceinline__ V3 hp_g(const float* __restrict__ prm, float x, float
     return V3{k * prm[0], k * prm[1], k * prm[2]};
 }
 
+// ---- tetrahedron.hpp:129-178: min of four oriented planes (std::min); gradient of the first
+//      minimal plane.  The planes (getPlanes :20-120, corners moved by the node matrix) are host data.
+__device__ __forceinline__ float tet_plane(const float* __restrict__ P, int k, float x, float y, float z) {
+    return ((P[4 * k] * x + P[4 * k + 1] * y) + P[4 * k + 2] * z) + P[4 * k + 3];
+}
+__device__ __forceinline__ float tet_f(const float* __restrict__ P, float x, float y, float z) {
+    return stdmin(tet_plane(P, 0, x, y, z), stdmin(tet_plane(P, 1, x, y, z), stdmin(tet_plane(P, 2, x, y, z), tet_plane(P, 3, x, y, z))));
+}
+__device__ __forceinline__ V3 tet_g(const float* __restrict__ P, float x, float y, float z) {
+    int index = 0;
+    float mn = tet_plane(P, 0, x, y, z);
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+        const float v = tet_plane(P, i, x, y, z);
+        if (v < mn) { index = i; mn = v; }
+    }
+    return V3{P[4 * index], P[4 * index + 1], P[4 * index + 2]};
+}
+
+// ---- meta_balls_Rydgard.hpp:80-124 (4 balls): sum of (strength / h - subtract) / 100, 1/h a
+//      double division stored to float; the gradient's h is summed in double (its 1e-6 literal)
+__device__ __forceinline__ float meta_f(const float* __restrict__ P, float x, float y, float z) {
+    float out = 0.0f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const float* B = P + 5 * b;
+        const float fx = x - B[0], fx2 = fx * fx;
+        const float fy = y - B[1], fy2 = fy * fy;
+        const float fz = z - B[2], fz2 = fz * fz;
+        const float h = (((float)0.000001 + fx2) + fy2) + fz2;
+        const float hinv = (float)(1.0 / (double)h);
+        const float val = B[3] * hinv - B[4];
+        out += val / 100;
+    }
+    return out;
+}
+__device__ __forceinline__ V3 meta_g(const float* __restrict__ P, float x, float y, float z) {
+    float gx = 0, gy = 0, gz = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const float* B = P + 5 * b;
+        const float fz = z - B[2], fz2 = fz * fz;
+        const float fy = y - B[1], fy2 = fy * fy;
+        const float fx = x - B[0], fx2 = fx * fx;
+        const float h = (float)(((0.000001 + (double)fx2) + (double)fy2) + (double)fz2);
+        const float hinv = (float)(1.0 / (double)h);
+        gx += B[3] * (-2 * fx * hinv * hinv) / 100;
+        gy += B[3] * (-2 * fy * hinv * hinv) / 100;
+        gz += B[3] * (-2 * fz * hinv * hinv) / 100;
+    }
+    return V3{gx, gy, gz};
+}
+
+// ---- extrusion.hpp:103-118 over convex_polygon (2d/GDT/convex_polygon.hpp:97-140): min over edges
+//      of -(x nx + y ny - n0), first minimal edge on ties; gradient (-nx, -ny, 0)
+__device__ __forceinline__ float extr_eval(const float* __restrict__ P, float x, float y, int& which) {
+    const int n = (int)P[0];
+    float minv = 0.f;
+    int w = -1;
+    for (int j = 0; j < n; ++j) {
+        const float v = -((x * P[1 + 3 * j] + y * P[2 + 3 * j]) - P[3 + 3 * j]);
+        if (v < minv || w < 0) { minv = v; w = j; }
+    }
+    which = w;
+    return minv;
+}
+__device__ __forceinline__ float extr_f(const float* __restrict__ P, float x, float y) {
+    int w;
+    return extr_eval(P, x, y, w);
+}
+__device__ __forceinline__ V3 extr_g(const float* __restrict__ P, float x, float y) {
+    int w;
+    extr_eval(P, x, y, w);
+    return V3{-P[1 + 3 * w], -P[2 + 3 * w], 0.f};
+}
+
 __device__ __forceinline__ float prim_f(int t, const float* __restrict__ tab, const float* __restrict__ prm, float x,
                                         float y, float z) {
     switch (t) {
@@ -424,6 +500,9 @@ __device__ __forceinline__ float prim_f(int t, const float* __restrict__ tab, co
         case NT_SCREW: return screw_f(prm, x, y, z);
         case NT_LID: return lid_f(z);
         case NT_HALF_PLANE: return hp_f(prm, x, y, z);
+        case NT_TETRA: return tet_f(prm, x, y, z);
+        case NT_METABALLS: return meta_f(prm, x, y, z);
+        case NT_EXTRUSION: return extr_f(prm, x, y);
         default: return dm_f(x, y, z);
     }
 }
@@ -438,6 +517,9 @@ __device__ __forceinline__ V3 prim_g(int t, const float* __restrict__ prm, float
         case NT_SCREW: return screw_g(prm, x, y, z);
         case NT_LID: return V3{0.f, 0.f, 1.f};
         case NT_HALF_PLANE: return hp_g(prm, x, y, z);
+        case NT_TETRA: return tet_g(prm, x, y, z);
+        case NT_METABALLS: return meta_g(prm, x, y, z);
+        case NT_EXTRUSION: return extr_g(prm, x, y);
         default: return dm_g(x, y, z);
     }
 }

@@ -231,6 +231,36 @@ __device__ __forceinline__ Iv hp_iv(const float* __restrict__ prm, Box p) {
                mulc(sub(p.z, ivc(prm[5])), prm[2]));
 }
 
+__device__ __forceinline__ Iv tet_iv(const float* __restrict__ P, Box p) {
+    Iv r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        r[k] = add(add(add(mulc(p.x, P[4 * k]), mulc(p.y, P[4 * k + 1])), mulc(p.z, P[4 * k + 2])), ivc(P[4 * k + 3]));
+    return stdmin_iv(r[0], stdmin_iv(r[1], stdmin_iv(r[2], r[3])));
+}
+// each ball's term is monotone decreasing in h, h monotone in each square; 1/h rounds monotonely
+__device__ __forceinline__ Iv meta_iv(const float* __restrict__ P, Box p) {
+    Iv out = ivc(0.0f);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const float* B = P + 5 * b;
+        const Iv h = add(add(add(ivc((float)0.000001), sqr(sub(p.x, ivc(B[0])))), sqr(sub(p.y, ivc(B[1])))),
+                         sqr(sub(p.z, ivc(B[2]))));
+        const Iv hinv{(float)(1.0 / (double)h.hi), (float)(1.0 / (double)h.lo)};
+        out = add(out, divc(sub(mulc(hinv, B[3]), ivc(B[4])), 100.f));
+    }
+    return out;
+}
+__device__ __forceinline__ Iv extr_iv(const float* __restrict__ P, Box p) {
+    const int n = (int)P[0];
+    Iv r{INFINITY, INFINITY};
+    for (int j = 0; j < n; ++j) {
+        const Iv v = neg(sub(add(mulc(p.x, P[1 + 3 * j]), mulc(p.y, P[2 + 3 * j])), ivc(P[3 + 3 * j])));
+        r = min_iv(r, v);
+    }
+    return r;
+}
+
 __device__ __forceinline__ Iv prim_iv(int t, const float* __restrict__ tab, float2 tab_range,
                                       const float* __restrict__ prm, Box p) {
     Iv r;
@@ -244,6 +274,9 @@ __device__ __forceinline__ Iv prim_iv(int t, const float* __restrict__ tab, floa
         case NT_SCREW: r = screw_iv(prm, p); break;
         case NT_LID: r = lid_iv(p); break;
         case NT_HALF_PLANE: r = hp_iv(prm, p); break;
+        case NT_TETRA: r = tet_iv(prm, p); break;
+        case NT_METABALLS: r = meta_iv(prm, p); break;
+        case NT_EXTRUSION: r = extr_iv(prm, p); break;
         default: r = dm_iv(p); break;
     }
     return settle(r);

@@ -83,6 +83,8 @@ const char* prim_call(int t) {
         case NT_DMUSHROOM: return "dm_f(";
         case NT_SCREW: return "screw_f(P, ";
         case NT_HALF_PLANE: return "hp_f(P, ";
+        case NT_TETRA: return "tet_f(P, ";
+        case NT_METABALLS: return "meta_f(P, ";
         default: throw std::runtime_error("jit: unknown primitive");
     }
 }
@@ -160,8 +162,9 @@ struct Emitter {
             << xform_row(mm + 4, 12 * n.mat + 4, x, y, z) << ",\n" << pad << "    "
             << xform_row(mm + 8, 12 * n.mat + 8, x, y, z) << "};\n";
         if (n.leaf) {
-            std::string call = n.type == NT_LID ? "lid_f(" + q + ".z)"
-                                                : with_params(prim_call(n.type), n.prm) + q + ".x, " + q + ".y, " + q + ".z)";
+            std::string call = n.type == NT_LID         ? "lid_f(" + q + ".z)"
+                               : n.type == NT_EXTRUSION ? with_params("extr_f(P, ", n.prm) + q + ".x, " + q + ".y)"
+                                                        : with_params(prim_call(n.type), n.prm) + q + ".x, " + q + ".y, " + q + ".z)";
             out << pad << "const float " << f << " = " << call << ";\n";
             return f;
         }
@@ -202,6 +205,9 @@ const char* prim_iv_call(int t) {
         case NT_SCREW: return "screw_iv(P, ";
         case NT_LID: return "lid_iv(";
         case NT_HALF_PLANE: return "hp_iv(P, ";
+        case NT_TETRA: return "tet_iv(P, ";
+        case NT_METABALLS: return "meta_iv(P, ";
+        case NT_EXTRUSION: return "extr_iv(P, ";
         default: throw std::runtime_error("jit: unknown primitive");
     }
 }

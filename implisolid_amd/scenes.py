@@ -74,6 +74,22 @@ def twist(scale, tx, ty, tz, pitch=0.5, delta_ratio=1.5):
             "delta_ratio": delta_ratio, "end_type": "0"}
 
 
+def tetrahedron(scale=1.0, t=(0, 0, 0)):
+    """tetrahedron.hpp: corners moved by the node matrix."""
+    return {"type": "tetrahedron", "matrix": st(scale, *t),
+            "corners": [[-0.5, -0.375, -0.25], [0.5, -0.25, -0.375], [0, 0.5, -0.25], [0.125, 0, 0.5]]}
+
+
+def meta_balls(scale=1.0, t=(0, 0, 0), time=0.1):
+    """meta_balls_Rydgard.hpp: 4 moving blobs at `time`."""
+    return {"type": "meta_balls", "matrix": st(scale, *t), "time": time}
+
+
+def extrusion(size=6, scale=1.0, t=(0, 0, 0)):
+    """extrusion.hpp: a regular size-gon prism of radius 1/2, cut to |z| <= 1/2."""
+    return {"type": "extrusion", "matrix": st(scale, *t), "size": size}
+
+
 def random_leaf(rng, box=1.0, types=LEAF_TYPES):
     while True:
         t = rng.choice(types)

@@ -26,7 +26,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 
-UNION, INTERSECTION, DIFFERENCE, ELLIPSOID, CUBE, CYLINDER, CONE, HEART, TORUS, DMUSHROOM, SCREW, LID, HALF_PLANE = range(13)
+(UNION, INTERSECTION, DIFFERENCE, ELLIPSOID, CUBE, CYLINDER, CONE, HEART, TORUS, DMUSHROOM, SCREW, LID, HALF_PLANE,
+ TETRA, METABALLS, EXTRUSION) = range(16)
 
 # MP5 "type" strings accepted by object_factory.hpp:86-653 for the plain-arithmetic node families.
 PRIMITIVE_TYPES = {
@@ -39,12 +40,12 @@ PRIMITIVE_TYPES = {
     "itorus": TORUS,                         # :163-173
 }
 # types the reference knows but this build does not evaluate (Eigen-based or JS callbacks)
-KNOWN_UNSUPPORTED = {"tetrahedron", "sdf_3d", "screw_gradient_wrong", "rawjscode", "meta_balls", "extrusion"}
+KNOWN_UNSUPPORTED = {"sdf_3d", "screw_gradient_wrong", "rawjscode"}
 
 
 class OrNode(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("child", ctypes.c_int32 * 2),
-                ("m", ctypes.c_float * 12), ("minv", ctypes.c_float * 12), ("prm", ctypes.c_float * 8)]
+                ("m", ctypes.c_float * 12), ("minv", ctypes.c_float * 12), ("prm", ctypes.c_float * 128)]
 
 
 class OrMesh(ctypes.Structure):
@@ -160,6 +161,97 @@ def _half_plane_params(pv, pp):
     return [f(a / n) for a in v] + [strtof(a) for a in pp]
 
 
+_libm = ctypes.CDLL("libm.so.6")
+for _fn, _t in (("sin", ctypes.c_double), ("cos", ctypes.c_double), ("sqrt", ctypes.c_double),
+                ("sinf", ctypes.c_float), ("cosf", ctypes.c_float)):
+    getattr(_libm, _fn).argtypes = [_t]
+    getattr(_libm, _fn).restype = _t
+
+
+def _tetra_params(d, m12):
+    """tetrahedron (tetrahedron.hpp:20-128): the corners (getCorners, object_factory.hpp:32-45; a
+    missing corner stays 0) moved by the forward matrix (matrix_vector_product, basic_functions.hpp:
+    140-177), the four planes of calculatePlaneCoefficients, each multiplied by the sign (tolerance
+    ROOT_TOLERANCE, configs.hpp:33) of its value at the opposite corner."""
+    f = np.float32
+    c = [[f(0)] * 3 for _ in range(4)]
+    for i, corner in enumerate(d.get("corners", [])[:4]):
+        for j, v in enumerate(corner[:3]):
+            c[i][j] = strtof(v)
+    m = [f(v) for v in m12]
+    p = [[f(f(f(f(m[4 * r] * q[0]) + f(m[4 * r + 1] * q[1])) + f(m[4 * r + 2] * q[2])) + m[4 * r + 3]) for r in range(3)]
+         for q in c]
+
+    def coef(P1, P2, P3):
+        x1, y1, z1 = P1
+        x2, y2, z2 = P2
+        x3, y3, z3 = P3
+        a = f(f(f(f(f(y1 * z2) - f(y1 * z3)) - f(y2 * z1)) + f(y2 * z3)) + f(y3 * z1)) - f(y3 * z2)
+        b = f(f(f(f(f(x1 * z3) - f(x1 * z2)) + f(x2 * z1)) - f(x2 * z3)) - f(x3 * z1)) + f(x3 * z2)
+        cc = f(f(f(f(f(x1 * y2) - f(x1 * y3)) - f(x2 * y1)) + f(x2 * y3)) + f(x3 * y1)) - f(x3 * y2)
+        dd = f(f(f(f(f(f(x1 * y3) * z2) - f(f(x1 * y2) * z3)) + f(f(x2 * y1) * z3)) - f(f(x2 * y3) * z1))
+               - f(f(x3 * y1) * z2)) + f(f(x3 * y2) * z1)
+        return [a, b, cc, dd]
+
+    planes = [coef(p[1], p[2], p[3]), coef(p[0], p[2], p[3]), coef(p[0], p[1], p[3]), coef(p[0], p[1], p[2])]
+    tol = f(0.001 / 10.0)
+    out = []
+    for k in range(4):
+        a, b, cc, dd = planes[k]
+        v = f(f(f(f(a * p[k][0]) + f(b * p[k][1])) + f(cc * p[k][2])) + dd)
+        sg = f(1) if v > tol else (f(-1) if v < -tol else f(0))
+        out += [f(a * sg), f(b * sg), f(cc * sg), f(dd * sg)]
+    return out
+
+
+def _metaball_params(d):
+    """meta_ball_Rydgard (meta_balls_Rydgard.hpp:27-60) with 4 blobs, scale 1 and `time` (default
+    0.1): the ball centres in double (libm sin / cos) stored to float; strength 1.2 / ((sqrt(4) - 1)
+    / 4 + 1), subtract 12."""
+    f = np.float32
+    time = strtof(d["time"]) if "time" in d else f(0.1)
+    t, D, half = float(time), float(f(1)), float(f(0.5))
+    out = []
+    for i in range(4):
+        bx = _libm.sin(i + 1.26 * t * (1.03 + 0.5 * _libm.cos(0.21 * i))) * 0.27 * D + 0.5 - half
+        by = abs(_libm.cos(i + 1.12 * t * _libm.cos(1.22 + 0.1424 * i))) * 0.77 * D - half
+        bz = _libm.cos(i + 1.32 * t * 0.1 * _libm.sin(0.92 + 0.53 * i)) * 0.27 * D + 0.5 - half
+        strength = 1.2 / ((_libm.sqrt(4) - 1) / 4 + 1)
+        out += [f(bx), f(by), f(bz), f(strength), f(12)]
+    return out
+
+
+def _extrusion_params(d):
+    """extrusion(eye, size) (extrusion.hpp:61-94): a regular `size`-gon of radius 0.5 starting at
+    (0, 0.5), counter-clockwise, corners from polarToCartesian (basic_functions.hpp:33-36: cosf /
+    sinf of a float angle); convex_polygon::update_inner_data (:77-93) edge normals in float with
+    1/d divided in double."""
+    f = np.float32
+    if "size" not in d:
+        raise ValueError("extrusion: missing 'size'")
+    size = int(strtof(d["size"]))
+    if size < 3:
+        raise ValueError("extrusion: Invalid size")
+    if size > 40:
+        raise ValueError("extrusion: size above 40 is not supported")
+    PI = f(3.141592653589793238463)
+    rot = f(f(2 * PI) / f(size))
+    cx, cy = [f(0)], [f(0.5)]
+    for i in range(1, size):
+        theta = f(float(PI) / 2.0 + float(f(f(i) * rot)))
+        cx.append(f(f(0.5) * f(_libm.cosf(theta))))
+        cy.append(f(f(0.5) * f(_libm.sinf(theta))))
+    out = [f(size)]
+    for i in range(size):
+        j = i + 1 if i < size - 1 else 0
+        dx, dy = f(cx[j] - cx[i]), f(cy[j] - cy[i])
+        dd = np.sqrt(f(f(dx * dx) + f(dy * dy)))
+        dinv = f(1.0 / float(dd)) if dd > 0.00000001 else f(0)
+        nx, ny = f(dy * dinv), f(-dx * dinv)
+        out += [nx, ny, f(f(cx[i] * nx) + f(cy[i] * ny))]
+    return out
+
+
 def mp5_to_nodes(shape, ignore_root_matrix=False):
     """object_factory (object_factory.hpp:56-758) -> flat node list + root index."""
     nodes = []
@@ -223,6 +315,22 @@ def mp5_to_nodes(shape, ignore_root_matrix=False):
             if ignore:
                 m = list(EYE12)
             return add(HALF_PLANE, m, prm=_half_plane_params(d["plane_vector"], d["plane_point"]))
+        if t == "tetrahedron":                     # :175-188
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            return add(TETRA, list(EYE12), prm=_tetra_params(d, m))
+        if t == "meta_balls":                      # :654-673
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            return add(METABALLS, m, prm=_metaball_params(d))
+        if t == "extrusion":                       # :674-731: subtract(extrusion(eye, size), lid)
+            m = _matrix12(d)
+            if ignore:
+                m = list(EYE12)
+            e = add(EXTRUSION, list(EYE12), prm=_extrusion_params(d))
+            return add(DIFFERENCE, m, e, add(LID, list(EYE12)))
         if t in KNOWN_UNSUPPORTED:
             raise NotImplementedError("MP5 type %r is outside the implemented node families" % t)
         raise ValueError("Invalid object you asked for: %r" % t)   # the reference abort()s

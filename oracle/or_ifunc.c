@@ -380,6 +380,79 @@ static void hp_g(const float p[3], const float* prm, float g[3]) {
     g[0] = k * prm[0]; g[1] = k * prm[1]; g[2] = k * prm[2];
 }
 
+/* ---------------- tetrahedron.hpp:129-150: min of the four oriented planes (std::min); the
+   gradient is the first minimal plane's normal (:152-178).  Planes: getPlanes (:20-120) on the
+   corners transformed by the node matrix, computed on the host (oracle/__init__.py). */
+static inline float tet_plane(const float* P, int k, const float p[3]) {
+    return ((P[4 * k] * p[0] + P[4 * k + 1] * p[1]) + P[4 * k + 2] * p[2]) + P[4 * k + 3];
+}
+static float tet_f(const float p[3], const float* P) {
+    return stdmin(tet_plane(P, 0, p), stdmin(tet_plane(P, 1, p), stdmin(tet_plane(P, 2, p), tet_plane(P, 3, p))));
+}
+static void tet_g(const float p[3], const float* P, float g[3]) {
+    int index = 0;
+    float mn = tet_plane(P, 0, p);
+    for (int i = 1; i < 4; i++) {
+        const float v = tet_plane(P, i, p);
+        if (v < mn) { index = i; mn = v; }
+    }
+    g[0] = P[4 * index]; g[1] = P[4 * index + 1]; g[2] = P[4 * index + 2];
+}
+
+/* ---------------- meta_balls_Rydgard.hpp: 4 balls, f = sum (strength/h - subtract)/100 with
+   h = 1e-6f + fx^2 + fy^2 + fz^2 (implicit_ball :80-98); the gradient's h sums in double from the
+   double literal (gradient_ball :99-124).  1/h is a double division stored to float. */
+static float meta_f(const float p[3], const float* P) {
+    float out = 0.0f;
+    for (int b = 0; b < 4; b++) {
+        const float* B = P + 5 * b;
+        const float fx = p[0] - B[0], fx2 = fx * fx;
+        const float fy = p[1] - B[1], fy2 = fy * fy;
+        const float fz = p[2] - B[2], fz2 = fz * fz;
+        const float h = (((float)0.000001 + fx2) + fy2) + fz2;
+        const float hinv = (float)(1.0 / (double)h);
+        const float val = B[3] * hinv - B[4];
+        out += val / 100;
+    }
+    return out;
+}
+static void meta_g(const float p[3], const float* P, float g[3]) {
+    float gx = 0, gy = 0, gz = 0;
+    for (int b = 0; b < 4; b++) {
+        const float* B = P + 5 * b;
+        const float fz = p[2] - B[2], fz2 = fz * fz;
+        const float fy = p[1] - B[1], fy2 = fy * fy;
+        const float fx = p[0] - B[0], fx2 = fx * fx;
+        const float h = (float)(((0.000001 + (double)fx2) + (double)fy2) + (double)fz2);
+        const float hinv = (float)(1.0 / (double)h);
+        gx += B[3] * (-2 * fx * hinv * hinv) / 100;
+        gy += B[3] * (-2 * fy * hinv * hinv) / 100;
+        gz += B[3] * (-2 * fz * hinv * hinv) / 100;
+    }
+    g[0] = gx; g[1] = gy; g[2] = gz;
+}
+
+/* ---------------- extrusion.hpp:103-118 -> convex_polygon (2d/GDT/convex_polygon.hpp:97-140):
+   f = min_j -(x nx_j + y ny_j - n0_j), first minimal edge on ties; gradient (-nx_w, -ny_w, 0) (the
+   2-D gradient leaves the zero-initialised z component) */
+static float extr_eval(const float p[3], const float* P, int* which) {
+    const int n = (int)P[0];
+    float minv = 0.f;
+    int w = -1;
+    for (int j = 0; j < n; j++) {
+        const float v = -((p[0] * P[1 + 3 * j] + p[1] * P[2 + 3 * j]) - P[3 + 3 * j]);
+        if (v < minv || w < 0) { minv = v; w = j; }
+    }
+    *which = w;
+    return minv;
+}
+static float extr_f(const float p[3], const float* P) { int w; return extr_eval(p, P, &w); }
+static void extr_g(const float p[3], const float* P, float g[3]) {
+    int w;
+    extr_eval(p, P, &w);
+    g[0] = -P[1 + 3 * w]; g[1] = -P[2 + 3 * w]; g[2] = 0.f;
+}
+
 /* ---------------- tree recursion ---------------- */
 static float eval1(const or_node* N, int i, const float p[3]) {
     const or_node* n = &N[i];
@@ -408,6 +481,9 @@ static float eval1(const or_node* N, int i, const float p[3]) {
         case OR_SCREW: return screw_f(l, n->prm);
         case OR_LID: return lid_f(l);
         case OR_HALF_PLANE: return hp_f(l, n->prm);
+        case OR_TETRA: return tet_f(l, n->prm);
+        case OR_METABALLS: return meta_f(l, n->prm);
+        case OR_EXTRUSION: return extr_f(l, n->prm);
     }
     return NAN;
 }
@@ -439,6 +515,9 @@ static void grad1(const or_node* N, int i, const float p[3], float o[3]) {
         case OR_SCREW: screw_g(l, n->prm, g); break;
         case OR_LID: g[0] = 0.f; g[1] = 0.f; g[2] = 1.f; break;
         case OR_HALF_PLANE: hp_g(l, n->prm, g); break;
+        case OR_TETRA: tet_g(l, n->prm, g); break;
+        case OR_METABALLS: meta_g(l, n->prm, g); break;
+        case OR_EXTRUSION: extr_g(l, n->prm, g); break;
         default: g[0] = g[1] = g[2] = NAN;
     }
     grad_xform(n->minv, g, o);

@@ -38,6 +38,9 @@ enum {
     OR_SCREW,          /* screw (identity transformation_matrix)  implicit_function/screw.hpp   */
     OR_LID,            /* top_bottom_lid            implicit_function/top_bottom_lid.hpp         */
     OR_HALF_PLANE,     /* half_plane                implicit_function/half_plane.hpp             */
+    OR_TETRA,          /* tetrahedron               implicit_function/tetrahedron.hpp            */
+    OR_METABALLS,      /* meta_ball_Rydgard         implicit_function/meta_balls_Rydgard.hpp     */
+    OR_EXTRUSION,      /* extrusion (convex n-gon)  implicit_function/extrusion.hpp + 2d/GDT/convex_polygon.hpp */
     OR_NTYPES
 };
 
@@ -46,8 +49,10 @@ typedef struct {
     int32_t child[2];   /* node indices, -1 when unused */
     float m[12];        /* transf_matrix, row-major 3x4, as read from the MP5 JSON */
     float minv[12];     /* inv_transf_matrix, filled by or_tree_prepare */
-    float prm[8];       /* primitive parameters: screw {twist_rate, r0, delta};
-                           half_plane {unit plane_vector xyz, plane_point xyz} */
+    float prm[128];     /* primitive parameters: screw {twist_rate, r0, delta};
+                           half_plane {unit plane_vector xyz, plane_point xyz};
+                           tetrahedron {a, b, c, d} x 4 planes; meta_balls {x, y, z, strength,
+                           subtract} x 4 balls; extrusion {n, (nx, ny, n0) x n edges} */
 } or_node;
 
 /* basic_functions.hpp:77-128 invert_matrix (ublas LU in float). returns 1 on success. */

@@ -216,7 +216,9 @@ def _screw_family():
             "lid": {"type": "Intersection", "matrix": scenes.EYE, "children": [
                 {"type": "icylinder", "matrix": scenes.st(1, 0, 0, 0.5)},
                 {"type": "top_bottom_lid", "matrix": scenes.st(1, 0, 0, 0)}]},
-            "config3_twist": scenes.config3_tree()}
+            "config3_twist": scenes.config3_tree(),
+            "tetrahedron": scenes.tetrahedron(), "meta_balls": scenes.meta_balls(), "extrusion": scenes.extrusion(6),
+            "extrusion_tri": scenes.extrusion(3, scale=0.5)}
 
 
 @pytest.mark.parametrize("name", sorted(_screw_family()))
@@ -328,7 +330,7 @@ def test_program_compiles_reference_factory_semantics(impli):
     assert n_instr == 3 * 2 + 2 * 2     # 3 leaves (XFORM + PRIM) + 2 unions (XFORM + CSG)
     for bad, msg in [({"type": "bogus", "matrix": scenes.EYE}, "Invalid"),
                      ({"type": "screw", "matrix": scenes.EYE}, "missing"),
-                     ({"type": "meta_balls", "matrix": scenes.EYE}, "outside the implemented"),
+                     ({"type": "sdf_3d", "matrix": scenes.EYE}, "outside the implemented"),
                      ({"type": "iellipsoid"}, "matrix")]:
         with pytest.raises(Exception) as e:
             impli.program_info(bad)

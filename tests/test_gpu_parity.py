@@ -46,6 +46,12 @@ def _screw_trees():
         "lid": {"type": "Intersection", "matrix": scenes.EYE, "children": [
             {"type": "icylinder", "matrix": scenes.st(1, 0, 0, 0.5)},
             {"type": "top_bottom_lid", "matrix": scenes.st(1, 0, 0, 0)}]},
+        "tetrahedron": scenes.tetrahedron(),
+        "meta_balls": scenes.meta_balls(),
+        "meta_balls_t": scenes.meta_balls(0.5, (0.125, 0, 0), time=2.5),
+        "extrusion": scenes.extrusion(6),
+        "extrusion_tri": {"type": "Union", "matrix": scenes.EYE, "children": [
+            scenes.extrusion(3, 0.5, (0.25, 0, 0)), scenes.tetrahedron(0.5, (-0.25, 0, 0))]},
     }
 
 
@@ -309,7 +315,7 @@ def test_ob02_full_config2_shape(impli, oracle, R):
     _ob02_compare(impli, oracle, shape, mc)
 
 
-@pytest.mark.parametrize("name", ["twist", "twist_two_plane", "half_plane"])
+@pytest.mark.parametrize("name", ["twist", "twist_two_plane", "half_plane", "tetrahedron", "meta_balls", "extrusion"])
 def test_ob02_screw_family(impli, oracle, name):
     from implisolid_amd import scenes
     mc = scenes.mc_settings(40, 0.7, vresampl_iters=1, vresampl_c=0.4, projection=1, qem=1, overall_repeats=2)
