@@ -281,6 +281,7 @@ std::string TreeJit::kernel_source(const Program& p) {
     IvEmitter iv{nodes, p};
     const std::string r = iv.emit(root, "p0", 4);
     std::ostringstream s;
+    if (const char* e = std::getenv("IMPLISOLID_EVAL_PAIR")) s << "#define IMPLI_EVAL_PAIR " << (e[0] == '1' ? 1 : 0) << "\n";
     s << kPrelude << "#include \"eval_bricks.hpp\"\n#include \"ifunc_interval.hpp\"\n#include \"brick_modes.hpp\"\n"
       << "namespace impli {\nusing namespace dev;\n"
       << "__device__ __forceinline__ float tree_f(const float* __restrict__ M, const float* __restrict__ tab,\n"

@@ -279,17 +279,26 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
     uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
     if (b.gathered)
         for (int r = 0; r < b.rank; ++r) Voff += b.gathered[4 * r] - b.gathered[4 * r + 3];
+    const uint32_t* __restrict__ vid3 = b.vid3;
     for (uint32_t i = blockIdx.x * 256 + t; i < lim; i += gridDim.x * 256) {
         const uint4 r = b.records[i];
         const uint32_t L = r.x, ci = r.y, fbase = r.z;
         const CaseInfo& C = s_case[ci];
+        const int n3 = 3 * C.ntri;
         if (fbase + C.ntri > (uint64_t)b.cap_f) { *b.overflow = 1u; continue; }
-        int32_t* out = b.faces + 3 * (size_t)fbase;
-        for (int k = 0; k < 3 * C.ntri; ++k) {
-            const int e = C.tri[k];
-            const uint32_t owner = L - (uint32_t)s_off[e];
-            out[k] = (int32_t)(Voff + b.vid3[(size_t)owner * 3 + s_slot[e]]);
+        // all corner ids gathered before any store: unconditional loads (corners past the case's
+        // triangles re-read corner 0), so the 15 round trips overlap instead of queueing behind
+        // the stores (faces and vid3 may alias for the compiler)
+        uint32_t v[15];
+#pragma unroll
+        for (int k = 0; k < 15; ++k) {
+            const int e = C.tri[k < n3 ? k : 0];
+            v[k] = vid3[(size_t)(L - (uint32_t)s_off[e]) * 3 + s_slot[e]];
         }
+        int32_t* out = b.faces + 3 * (size_t)fbase;
+#pragma unroll
+        for (int k = 0; k < 15; ++k)
+            if (k < n3) out[k] = (int32_t)(Voff + v[k]);
     }
 }
 

@@ -190,11 +190,19 @@ __device__ __forceinline__ void mc_verts_body(const CaseInfo* __restrict__ cases
                     const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
                     // ends of the owned crossing edges: corner 7 (qxyz) and 5 (qxz), 6 (qyz), 3 (qxy)
                     const int sx = x - 1, sy = y - 1, sl = z - g.fz0;   // stored coords of corner 0
-                    const bool o5 = own && C.rank[0] >= 0, o6 = own && C.rank[1] >= 0, o10 = own && C.rank[2] >= 0;
-                    const float f7 = own ? edge_value(g, b, sx + 1, sy + 1, sl + 1) : 0.f;
-                    const float f5 = o5 ? edge_value(g, b, sx + 1, sy, sl + 1) : 0.f;
-                    const float f6 = o6 ? edge_value(g, b, sx, sy + 1, sl + 1) : 0.f;
-                    const float f3 = o10 ? edge_value(g, b, sx + 1, sy + 1, sl) : 0.f;
+                    // the four corner loads are issued unconditionally (lanes without a cell read
+                    // sample 0): a load under a divergent branch waits on its own
+                    const int n_ = g.n;
+                    const int64_t base = has ? (int64_t)sx + (int64_t)sy * n_ + (int64_t)sl * n_ * n_ : 0;
+                    const int64_t dx = has ? 1 : 0, dy = has ? n_ : 0, dz = has ? (int64_t)n_ * n_ : 0;
+                    const float r7 = b.field[base + dx + dy + dz], r5 = b.field[base + dx + dz];
+                    const float r6 = b.field[base + dy + dz], r3 = b.field[base + dx + dy];
+                    const bool sx1 = sealed_xy(g, sx + 1), sy1 = sealed_xy(g, sy + 1), sz1 = sealed_z(g, sl + 1);
+                    const bool sx0 = sealed_xy(g, sx), sy0 = sealed_xy(g, sy), sz0 = sealed_z(g, sl);
+                    const float f7 = (sx1 || sy1 || sz1) ? kSealed : r7;
+                    const float f5 = (sx1 || sy0 || sz1) ? kSealed : r5;
+                    const float f6 = (sx0 || sy1 || sz1) ? kSealed : r6;
+                    const float f3 = (sx1 || sy1 || sz0) ? kSealed : r3;
                     if (has && own) {
                         const uint32_t vrun = vrun0 + fld(pre, 0);
                         const float fx = ((float)x + g.i0[0]) * g.w[0];
