@@ -76,7 +76,37 @@ def cpu_baseline(shape, target_s=20.0):
     dt = time.perf_counter() - t0
     return {"value": R ** 3 / dt / 1e6, "unit": "Mvoxels/s", "cores": 1, "kind": "port",
             "sample": "oracle restatement (C, 1 thread) eval+MC of the same tree at %d^3 on this host (%.1f s, %d faces)"
-                      % (R, dt, f.shape[0])}
+                      % (R, dt, f.shape[0])}, (R, v, f)
+
+
+def mesh_parity(v, f, v_ref, f_ref):
+    """max|v - v_ref| over the vertices and whether the face arrays are identical (the metric's
+    max|v-v_ref|)."""
+    same_shape = v.shape == v_ref.shape and f.shape == f_ref.shape
+    diff = None
+    if same_shape:
+        diff = float(np.abs(v.astype(np.float64) - v_ref).max()) if v.size else 0.0
+    return {"verts": int(v_ref.shape[0]), "faces": int(f_ref.shape[0]),
+            "faces_identical": bool(same_shape and np.array_equal(f, f_ref)), "max_abs_v_diff": diff}
+
+
+def copy_attainable(dev, nbytes=1 << 30, reps=10):
+    """Measured device-to-device copy rate (GB/s, read + write bytes): the attainable HBM figure
+    SURVEY.md 8d asks to report beside the 8 TB/s peak."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    return round(gbs, 1)
 
 
 def main():
@@ -244,12 +274,16 @@ def main():
             ob02[key] = {"build_geometry_ms": round(min(ts) * 1e3, 3), "verts": int(len(v)), "faces": int(len(f)),
                          "steps": "MC + 3 x [vertex resampling, centroid projection, QEM]"}
         if not args.no_cpu_baseline:
+            # the oracle runs both configurations on this host: its time on one core, and max|v - v_ref|
+            # and face identity of the GPU result against it
             import oracle
             oracle.build()
-            shape, mc = scenes.config2(128)
-            t0 = time.perf_counter()
-            oracle.polygonize(json.dumps(shape), json.dumps(mc))
-            ob02["config2_r128"]["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+            for key, (shape, mc) in (("config2_r128", scenes.config2(128)), ("config3_r256", scenes.config3(256))):
+                v, f = I.make_geometry(shape, mc)
+                t0 = time.perf_counter()
+                v_ref, f_ref = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+                ob02[key]["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+                ob02[key]["parity"] = mesh_parity(v, f, v_ref, f_ref)
 
     if rank != 0:
         if world > 1:
@@ -350,9 +384,14 @@ def main():
     if ob02:
         out["ob02"] = ob02
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(main_run["shape"])
+        out["cpu_baseline"], (Rs, v_ref, f_ref) = cpu_baseline(main_run["shape"])
+        # the GPU mesh of the same tree at the sample's resolution against the oracle's
+        v, f = I.make_geometry(main_run["shape"], scenes.mc_settings(Rs, 1.0))
+        out["parity"] = dict(mesh_parity(v, f, v_ref, f_ref), resolution=Rs,
+                             workload="config4 tree, eval+MC: GPU (build_geometry) vs the oracle")
     else:
         out["cpu_baseline"] = None
+    out["roofline"]["copy_attainable"] = copy_attainable(dev)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -159,12 +159,12 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     lmodes_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint64_t));
     field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
     unit_cnt_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint4));
+    scan_blk_.reserve((size_t)(n_groups(grid_) + 1) * kScanParts * sizeof(uint32_t));
     ulist_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint4));
     umark_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint32_t));
     IMPLI_HIP(hipMemset(umark_.p, 0, (size_t)(n_units(grid_) + 1) * sizeof(uint32_t)));   // ids start at 1
     marks_valid_ = false;
 
-    scan_blk_.reserve((size_t)(n_scan_blocks(grid_) + 1) * 8 * sizeof(uint32_t));
     const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
     signs_.reserve(sign_bytes + 64);
     // the pieces past the last brick of a row are never written by the pruned path: keep them 0
@@ -198,10 +198,10 @@ MCBuffers Engine::buffers() const {
     b.signs = signs_.as<uint64_t>();
 
     b.unit_cnt = unit_cnt_.as<uint4>();
+    b.scan_blk = scan_blk_.as<uint32_t>();
     b.ulist = ulist_.as<uint4>();
     b.umark = marks_valid_ ? umark_.as<uint32_t>() : nullptr;
     b.mark_id = mark_id_;
-    b.scan_blk = scan_blk_.as<uint32_t>();
     b.counters = counters_.as<uint32_t>();
     b.vid3 = vid3_.as<uint32_t>();
     b.records = records_.as<uint4>();

@@ -58,15 +58,24 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
     const int layers = g.fz1 - g.fz0;
     const size_t plane = (size_t)n * n;
     const int row_pieces = (64 / kBX) * sign_row_words(g);
-    for (uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); i < nb; i += gridDim.x * 4) {
-        const int b = __builtin_amdgcn_readfirstlane((int)list[i]);
+    const uint32_t stride = gridDim.x * 4;
+    uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    // the next brick's list entry and modes are loaded while this brick is evaluated
+    uint32_t b_next = i < nb ? list[i] : 0u;
+    uint64_t m_next = i < nb ? modes[i] : 0ull;
+    for (; i < nb; i += stride) {
+        const int b = __builtin_amdgcn_readfirstlane((int)b_next);
+        const uint64_t m64 = m_next;
+        if (i + stride < nb) {
+            b_next = list[i + stride];
+            m_next = modes[i + stride];
+        }
         int bx, by, bz;
         brick_of(b, bg, bx, by, bz);
         const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
         const bool ok = sx < n && sy < n;
         const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
         float* out = field + (size_t)(ok ? sy : 0) * n + (ok ? sx : 0);
-        const uint64_t m64 = modes[i];
         const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
                            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
         const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);

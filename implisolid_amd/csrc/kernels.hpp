@@ -42,12 +42,11 @@ void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* 
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
                         float* d_f, float* d_grad /* nullable: values only */, hipStream_t s);
 
+// K2 (count per group) and K2b (group bases + flat list of non-empty units)
 void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s);
 // K3 and K4
 void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
-
-inline int64_t n_scan_blocks(const GridDesc& g) { return n_groups(g); }
 
 }  // namespace impli

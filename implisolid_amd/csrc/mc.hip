@@ -15,8 +15,8 @@
 // Signs come from the eval's sign bitmap (grid.hpp), 64 cells per bit operation; only the ~1 % of
 // non-trivial cells (corner signs not all equal) do per-cell work.  A unit = kUnitRows cell rows.
 //   K2 k_mc_count : per unit the sums of owned edges, triangles, active cells, halo-owned edges.
-//   K2b k_scan_groups : exclusive scan of the group sums (one block, ~1k groups at 512^3);
-//       k_unit_flatten: the non-empty units in order with their global bases (one wave per group).
+//   K2b k_unit_scan: per group, its global bases (sum of the groups before it) and its non-empty
+//       units in order in the flat list.
 //   K3 k_mc_verts : per unit, the non-trivial cells in cell order: owned vertex positions (field
 //                   values read only at crossing edges), the dense vid3[cell][slot] table, records.
 //   K4 k_mc_faces : per active cell, gathers the vertex ids of its triangle corners from vid3 of
@@ -88,14 +88,20 @@ void build_case_table(CaseInfo out[256]) {
 
 namespace {
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
 // K2: one block per group of kGroupUnits units; lanes take the group's items (row, 64-cell chunk)
 // round robin, so every lane has work (a wave per unit would leave 64 - 4 nch lanes idle).  Only
 // units whose cells touch an evaluated brick are visited (b.umark): all others are trivial.  Owned
 // vertices and triangles of a chunk are popcounts of corner-mask expressions (chunk_triangles).
 // Per-unit sums through LDS atomics.
 //   -> unit_cnt[64 group + k] = k-th non-empty unit of the group {unit in group, own / tri / act
-//      exclusive bases in the group}; scan_blk[c][group] = the group's sums (c < 5: own, tri, act,
-//      halo own, non-empty units -- scanned by k_scan_groups), scan_blk[5][group] = non-empty units.
+//      exclusive bases in the group}; scan_blk[c][group] = the group's sums (own, tri, act, halo
+//      own, non-empty units), read by k_unit_scan.
 __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ uint32_t s_u[kGroupUnits][4];
     __shared__ uint8_t s_fu[kGroupUnits];   // the group's candidate units, in order
@@ -103,11 +109,12 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
     const int t = threadIdx.x, nt_ = blockDim.x;
     (void)cases;   // triangle counts come from chunk_triangles (checked against the table)
     for (int k = t; k < 4 * kGroupUnits; k += nt_) (&s_u[0][0])[k] = 0u;
+    const int64_t G = blockIdx.x;
     const int nch = (g.m + 63) / 64;
     const int64_t rows = n_rows(g), nu = n_units(g);
-    const int64_t row0 = (int64_t)blockIdx.x * kGroupUnits * kUnitRows;
+    const int64_t row0 = G * kGroupUnits * kUnitRows;
     if (t < 64) {   // candidates: units whose cells touch an evaluated brick (others are all trivial)
-        const int64_t u = (int64_t)blockIdx.x * kGroupUnits + t;
+        const int64_t u = G * kGroupUnits + t;
         const bool cand = u < nu && (!b.umark || b.umark[u] == b.mark_id);
         const uint64_t m = __ballot(cand);
         if (cand) s_fu[__popcll((unsigned long long)(m & ((1ull << t) - 1ull)))] = (uint8_t)t;
@@ -157,7 +164,7 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
     }
     __syncthreads();
     if (t < 64) {   // wave 0, one lane per unit of the group (kGroupUnits == 64; blockDim >= 64)
-        const int64_t u = (int64_t)blockIdx.x * kGroupUnits + t;
+        const int64_t u = G * kGroupUnits + t;
         const uint32_t own = s_u[t][0], tri = s_u[t][1], act = s_u[t][2], hal = s_u[t][3];
         const bool ne = u < nu && (own | tri) != 0;
         // the group's non-empty units in order, with their exclusive bases inside the group
@@ -166,90 +173,62 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
         const uint32_t ea = wave_incl_scan<uint32_t>(act, t) - act;
         const uint64_t m = __ballot(ne);
         const uint32_t pos = (uint32_t)__popcll((unsigned long long)(m & ((1ull << t) - 1ull)));
-        if (ne) b.unit_cnt[(int64_t)blockIdx.x * kGroupUnits + pos] = make_uint4((uint32_t)t, eo, et, ea);
-        const uint32_t sums[5] = {__shfl(eo + own, 63, 64), __shfl(et + tri, 63, 64), __shfl(ea + act, 63, 64),
-                                  wave_incl_scan<uint32_t>(hal, t), (uint32_t)__popcll((unsigned long long)m)};
-        const uint32_t shal = __shfl(sums[3], 63, 64);
-        if (t < 6) {
-            const uint32_t v = t == 0 ? sums[0] : t == 1 ? sums[1] : t == 2 ? sums[2] : t == 3 ? shal : sums[4];
-            b.scan_blk[(int64_t)t * gridDim.x + blockIdx.x] = v;   // row 5: non-empty count, kept unscanned
+        if (ne) b.unit_cnt[G * kGroupUnits + pos] = make_uint4((uint32_t)t, eo, et, ea);
+        const uint32_t sums[kScanParts] = {__shfl(eo + own, 63, 64), __shfl(et + tri, 63, 64),
+                                           __shfl(ea + act, 63, 64), wave_sum(hal),
+                                           (uint32_t)__popcll((unsigned long long)m)};
+        if (t < kScanParts) {
+            const uint32_t v = t == 0 ? sums[0] : t == 1 ? sums[1] : t == 2 ? sums[2] : t == 3 ? sums[3] : sums[4];
+            b.scan_blk[(int64_t)t * gridDim.x + G] = v;
         }
     }
 }
 
-// ---- group scan: one block, exclusive bases of the groups in place, totals to the counters ----
-struct Cnt5 { uint32_t c[5]; };
-
-// block scan (1024 lanes) of 5 components; returns exclusive, fills total
-__device__ __forceinline__ Cnt5 block_scan5(Cnt5 v, Cnt5& total, uint32_t (*s_w)[16]) {
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    Cnt5 incl;
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-        incl.c[c] = wave_incl_scan<uint32_t>(v.c[c], lane);
-        if (lane == 63) s_w[c][wid] = incl.c[c];
-    }
-    __syncthreads();
-    Cnt5 ex;
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-        uint32_t pre = 0, tt = 0;
-        for (int w = 0; w < 16; ++w) {
-            const uint32_t x = s_w[c][w];
-            if (w < wid) pre += x;
-            tt += x;
-        }
-        ex.c[c] = pre + incl.c[c] - v.c[c];
-        total.c[c] = tt;
-    }
-    __syncthreads();
-    return ex;
-}
-
-__global__ __launch_bounds__(1024) void k_scan_groups(uint32_t* __restrict__ blk, int64_t ng,
-                                                      uint32_t* __restrict__ counters) {
-    __shared__ uint32_t s_w[5][16];
-    Cnt5 carry = {{0, 0, 0, 0, 0}};
-    for (int64_t base0 = 0; base0 < ng; base0 += 1024 * kTopPT) {
-        const int64_t base = base0 + (int64_t)threadIdx.x * kTopPT;
-        Cnt5 sum = {{0, 0, 0, 0, 0}};
-        for (int i = 0; i < kTopPT; ++i)
-            if (base + i < ng)
-#pragma unroll
-                for (int c = 0; c < 5; ++c) sum.c[c] += blk[c * ng + base + i];
-        Cnt5 tot;
-        Cnt5 run = block_scan5(sum, tot, s_w);
-        for (int i = 0; i < kTopPT; ++i) {
-            if (base + i >= ng) break;
-#pragma unroll
-            for (int c = 0; c < 5; ++c) {
-                const uint32_t x = blk[c * ng + base + i];   // this lane's own entries: no race
-                blk[c * ng + base + i] = carry.c[c] + run.c[c];
-                run.c[c] += x;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < 5; ++c) carry.c[c] += tot.c[c];
-    }
-    if (threadIdx.x == 0) {
-        counters[0] = carry.c[4];   // non-empty units
-        counters[1] = carry.c[3];   // halo-owned vertices (ids below the slab's first)
-        counters[2] = carry.c[0];   // owned vertices incl. halo
-        counters[3] = carry.c[1];   // triangles
-        counters[4] = carry.c[2];   // active cells (face records)
-        counters[5] = carry.c[3];
-    }
-}
-
-// one wave per group: its non-empty units (k_mc_count's in-group list) to their place in the
-// flat ordered list, with global bases
-__global__ __launch_bounds__(64) void k_unit_flatten(GridDesc g, MCBuffers b) {
+// K2b: one block per group.  Its global bases are the sums of the groups before it, read straight
+// from L2 (kScanParts x G words, all loads in flight together; nothing waits on another block), then
+// its non-empty units go to their place in the flat ordered list.  Groups without non-empty units
+// exit at once; the last group writes the totals.  (A single-block scan plus a flatten kernel took
+// 7.3 + 4.5 us at 512^3; a decoupled look-back inside k_mc_count, 28 us more: its status words
+// cross the XCDs' L2s at memory latency, one round trip per 64 groups walked.)
+constexpr int kScanBlock = 256;
+__global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) {
+    __shared__ uint32_t s_part[kScanBlock / 64][kScanParts];
+    __shared__ uint32_t s_base[kScanParts];
     const int64_t G = blockIdx.x, ng = n_groups(g);
-    const uint32_t k = threadIdx.x;
-    if (k >= b.scan_blk[5 * ng + G]) return;
-    const uint4 e = b.unit_cnt[G * kGroupUnits + k];
-    b.ulist[b.scan_blk[4 * ng + G] + k] = make_uint4((uint32_t)(G * kGroupUnits) + e.x, b.scan_blk[G] + e.y,
-                                                     b.scan_blk[ng + G] + e.z, b.scan_blk[2 * ng + G] + e.w);
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const bool last = G == ng - 1;
+    const uint32_t nne = b.scan_blk[4 * ng + G];
+    if (nne == 0 && !last) return;   // uniform
+    const uint4 e = b.unit_cnt[G * kGroupUnits + (t < (int)nne ? t : 0)];
+    uint32_t acc[kScanParts] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll 4
+    for (int64_t i = t; i < G; i += kScanBlock)
+#pragma unroll
+        for (int c = 0; c < kScanParts; ++c) acc[c] += b.scan_blk[c * ng + i];
+#pragma unroll
+    for (int c = 0; c < kScanParts; ++c) {
+        const uint32_t s = wave_sum(acc[c]);
+        if (lane == 0) s_part[wid][c] = s;
+    }
+    __syncthreads();
+    if (t < kScanParts) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < kScanBlock / 64; ++w) s += s_part[w][t];
+        s_base[t] = s;
+    }
+    __syncthreads();
+    if (t < (int)nne)
+        b.ulist[s_base[4] + t] = make_uint4((uint32_t)(G * kGroupUnits) + e.x, s_base[0] + e.y, s_base[1] + e.z,
+                                            s_base[2] + e.w);
+    if (last && t == 0) {
+        b.counters[0] = s_base[4] + nne;                           // non-empty units
+        b.counters[1] = s_base[3] + b.scan_blk[3 * ng + G];       // halo-owned vertices (ids below the slab's first)
+        b.counters[2] = s_base[0] + b.scan_blk[G];                // owned vertices incl. halo
+        b.counters[3] = s_base[1] + b.scan_blk[ng + G];           // triangles
+        b.counters[4] = s_base[2] + b.scan_blk[2 * ng + G];       // active cells (face records)
+        b.counters[5] = s_base[3] + b.scan_blk[3 * ng + G];
+    }
 }
 
 __global__ __launch_bounds__(64 * kVertsWaves) void k_mc_verts(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
@@ -316,9 +295,7 @@ void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
 
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     const int64_t ng = n_groups(g);
-    if (ng == 0) return;
-    k_scan_groups<<<1, 1024, 0, s>>>(b.scan_blk, ng, b.counters);
-    k_unit_flatten<<<(unsigned)ng, 64, 0, s>>>(g, b);
+    if (ng > 0) k_unit_scan<<<(unsigned)ng, kScanBlock, 0, s>>>(g, b);
 }
 
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {

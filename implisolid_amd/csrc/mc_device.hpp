@@ -127,7 +127,7 @@ __device__ __forceinline__ float edge_value(const GridDesc& g, const MCBuffers& 
     return (sealed_xy(g, sx) || sealed_xy(g, sy) || sealed_z(g, sl)) ? kSealed : b.field[sx + sy * g.n + sl * g.n * g.n];
 }
 
-// Waves take the non-empty units of the flat list (k_unit_flatten) grid-stride, one unit at a time:
+// Waves take the non-empty units of the flat list (k_unit_scan) grid-stride, one unit at a time:
 // every resident wave gets an equal share whatever the surface's distribution over groups.
 __device__ __forceinline__ void mc_verts_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
     __shared__ CaseInfo s_case[256];

@@ -22,14 +22,13 @@ constexpr int kUnitRows = 4;
 constexpr int kGroupUnits = 64;        // units per group: one count block; the group scan's element
 constexpr int kVertsWaves = 4;         // waves per verts block (grid-stride over the unit list)
 constexpr int kVertsMaxBlocks = 2048;  // verts grid: ~ the resident waves of the chip
-constexpr int kTopPT = 2;              // groups per lane in one pass of the group scan
+constexpr int kScanParts = 5;          // group sums: own, tri, act, halo own, non-empty units
 struct MCBuffers {
     const float* field;
     const uint64_t* signs;   // sign bitmap of the stored samples (grid.hpp)
     uint4* unit_cnt;         // per group, its non-empty units {unit in group, own, tri, act bases} (k_mc_count)
-    uint32_t* scan_blk;      // [6][n_groups]: group sums (own, tri, act, halo own, non-empty units), then
-                             // exclusive bases; row 5: non-empty units (unscanned)
-    uint4* ulist;            // all non-empty units in order: {unit, vbase, fbase, abase} (k_unit_flatten)
+    uint32_t* scan_blk;      // [kScanParts][n_groups]: group sums (own, tri, act, halo own, non-empty units)
+    uint4* ulist;            // all non-empty units in order: {unit, vbase, fbase, abase} (k_unit_scan)
     const uint32_t* umark;   // units whose cells touch an evaluated brick hold mark_id (k_brick_fill);
     uint32_t mark_id;        // null: every unit is counted (dense eval)
     uint32_t* counters;      // [0] non-empty units, [1] halo own, [2..5] totals own/tri/act/halo
