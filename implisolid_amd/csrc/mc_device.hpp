@@ -109,29 +109,39 @@ __device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
            ((unsigned)((k.t11 >> j) & 1u) << 6);
 }
 
-// K3: one wave per unit.  Lanes find the non-trivial cells of their (row, chunk) items; a wave scan
-// orders them (cell order) into an LDS list, processed 64 at a time: a second wave scan of (owned
-// edges, triangles, active) gives every cell its vertex / face / record base, all written in
-// parallel.  Corner values are read from the field only for owned crossing edges.
+// K3a: one wave per unit.  Lanes find the non-trivial cells of their (row, chunk) items; the cells
+// are then taken in cell order, 64 at a time: a wave scan of (owned
+// edges, triangles, active) gives every cell its vertex / face / record base.  Active cells get a
+// record {L, ci, face base, vertex base}; halo cells (below the slab's first emitted layer) write
+// their owned ids into vid3 -- no field value is read here, so a unit with hundreds of cells costs
+// a few ALU passes, not a memory round trip per 64 cells.  K3b (mc_vpos_body) then places the
+// vertices, one lane per active cell.
 __device__ __forceinline__ unsigned long long pack4(unsigned a, unsigned b, unsigned c, unsigned d) {
     return (unsigned long long)a | ((unsigned long long)b << 16) | ((unsigned long long)c << 32) |
            ((unsigned long long)d << 48);
 }
 __device__ __forceinline__ unsigned fld(unsigned long long p, int i) { return (unsigned)(p >> (16 * i)) & 0xffffu; }
 
-constexpr int kListCap = 1024;   // LDS list entries per wave (a window; larger units loop)
-
-// Field value of stored sample (sx, sy, sl) at the end of a sign-changing edge (never in a
-// sign-filled brick, eval_bricks.hpp); sealed samples are the constant.
-__device__ __forceinline__ float edge_value(const GridDesc& g, const MCBuffers& b, int sx, int sy, int sl) {
-    return (sealed_xy(g, sx) || sealed_xy(g, sy) || sealed_z(g, sl)) ? kSealed : b.field[sx + sy * g.n + sl * g.n * g.n];
+// position of the r-th set bit of x (r < popcount(x))
+__device__ __forceinline__ int select_bit(uint64_t x, uint32_t r) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) {
+        const uint32_t c = (uint32_t)__popcll((unsigned long long)(x & ((1ull << w) - 1ull)));
+        if (r >= c) { r -= c; x >>= w; pos += w; }
+    }
+    return pos;
 }
 
 // Waves take the non-empty units of the flat list (k_unit_scan) grid-stride, one unit at a time:
-// every resident wave gets an equal share whatever the surface's distribution over groups.
-__device__ __forceinline__ void mc_verts_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
+// every resident wave gets an equal share whatever the surface's distribution over groups.  A
+// unit's items (row, 64-cell chunk) go to LDS with their exclusive cell counts; each lane then
+// finds its own cell -- the item by binary search, the cell by selecting the bit -- so cells are
+// listed in cell order 64 at a time, with no lane looping over a dense chunk's bits.
+__device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
     __shared__ CaseInfo s_case[256];
-    __shared__ uint32_t s_list[kVertsWaves][kListCap];   // per wave: ci | j << 8 | item << 14
+    __shared__ uint64_t s_bits[kVertsWaves][9][64];   // per wave and item: the 8 corner words + nt
+    __shared__ uint32_t s_excl[kVertsWaves][64];      // per wave and item: cells in the items before it
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t n_ne = b.counters[0];              // non-empty units
     const uint32_t w0 = blockIdx.x * kVertsWaves;
@@ -141,7 +151,8 @@ __device__ __forceinline__ void mc_verts_body(const CaseInfo* __restrict__ cases
     const uint32_t H = b.counters[1];
     const int nch = (g.m + 63) / 64;
     const int64_t rows = n_rows(g);
-    uint32_t* list = s_list[wid];
+    uint64_t(*bits)[64] = s_bits[wid];
+    uint32_t* excl = s_excl[wid];
     const int items = kUnitRows * nch;
     for (uint32_t e = w0 + wid; e < n_ne; e += gridDim.x * kVertsWaves) {
         const uint4 ent = b.ulist[e];   // {unit, vbase, fbase, abase}
@@ -151,103 +162,121 @@ __device__ __forceinline__ void mc_verts_body(const CaseInfo* __restrict__ cases
             const int i = i0 + lane;
             ChunkBits k;
             k.nt = 0;
-            int64_t row = -1;
             if (i < items) {
-                row = u * kUnitRows + i / nch;
+                const int64_t row = u * kUnitRows + i / nch;
                 if (row < rows) load_chunk(g, b.signs, row, i % nch, k);
             }
             const uint32_t cnt = (uint32_t)__popcll((unsigned long long)k.nt);
             const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);
             const uint32_t total = __shfl(incl, 63, 64);
-            for (uint32_t w0 = 0; w0 < total; w0 += kListCap) {
-                // this window's entries, in cell order
-                uint32_t pos = incl - cnt;
-                uint64_t nt = k.nt;
-                while (nt) {
-                    const int j = __ffsll((unsigned long long)nt) - 1;
-                    nt &= nt - 1;
-                    if (pos >= w0 && pos < w0 + kListCap)
-                        list[pos - w0] = chunk_ci(k, j) | ((uint32_t)j << 8) | ((uint32_t)i << 14);
-                    ++pos;
+            __builtin_amdgcn_wave_barrier();   // the previous batch's LDS reads are done
+            bits[0][lane] = k.s00; bits[1][lane] = k.t00; bits[2][lane] = k.s10; bits[3][lane] = k.t10;
+            bits[4][lane] = k.s01; bits[5][lane] = k.t01; bits[6][lane] = k.s11; bits[7][lane] = k.t11;
+            bits[8][lane] = k.nt;
+            excl[lane] = incl - cnt;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t e0 = 0; e0 < total; e0 += 64) {
+                const uint32_t ce = e0 + (uint32_t)lane;
+                const bool has = ce < total;
+                // the item holding cell ce: the last item whose exclusive count is <= ce (items
+                // without cells share the next one's count, so the last such item has cells)
+                int q = 0;
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1)
+                    if (excl[q + step] <= ce) q += step;
+                const int j = has ? select_bit(bits[8][q], ce - excl[q]) : 0;
+                const unsigned ci =
+                    has ? (unsigned)((bits[0][q] >> j) & 1u) | ((unsigned)((bits[1][q] >> j) & 1u) << 1) |
+                              ((unsigned)((bits[3][q] >> j) & 1u) << 2) | ((unsigned)((bits[2][q] >> j) & 1u) << 3) |
+                              ((unsigned)((bits[4][q] >> j) & 1u) << 4) | ((unsigned)((bits[5][q] >> j) & 1u) << 5) |
+                              ((unsigned)((bits[7][q] >> j) & 1u) << 6) | ((unsigned)((bits[6][q] >> j) & 1u) << 7)
+                        : 0u;   // chunk_ci of item q, cell j
+                const int it = i0 + q;
+                const int64_t erow = u * kUnitRows + it / nch;
+                const int x = 64 * (it % nch) + 1 + j;
+                const int z = (int)erow / g.m + g.cz0;
+                const uint32_t L = (uint32_t)(erow * g.m + (x - 1));
+                const CaseInfo& C = s_case[ci];
+                const bool emit = has && z >= g.cz_emit;
+                const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
+                const unsigned long long p = pack4(own, tri, act, 0u);
+                const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
+                const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
+                const uint32_t vrun = vrun0 + fld(pre, 0);
+                if (own && !emit) {   // halo cell: the slab below emits its vertices; ids only
+#pragma unroll
+                    for (int slot = 0; slot < 3; ++slot)
+                        if (C.rank[slot] >= 0) b.vid3[(size_t)L * 3 + slot] = vrun + (uint32_t)C.rank[slot] - H;
                 }
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t n_list = (total - w0 < (uint32_t)kListCap) ? total - w0 : (uint32_t)kListCap;
-                for (uint32_t e0 = 0; e0 < n_list; e0 += 64) {
-                    const uint32_t e = e0 + (uint32_t)lane;
-                    const bool has = e < n_list;
-                    const uint32_t ent = has ? list[e] : 0u;
-                    const unsigned ci = ent & 255u;
-                    const int j = (int)((ent >> 8) & 63u), it = (int)(ent >> 14);
-                    const int64_t erow = u * kUnitRows + it / nch;
-                    const int x = 64 * (it % nch) + 1 + j;
-                    const int y = (int)erow % g.m + 1, z = (int)erow / g.m + g.cz0;
-                    const uint32_t L = (uint32_t)(erow * g.m + (x - 1));
-                    const CaseInfo& C = s_case[ci];
-                    const bool emit = has && z >= g.cz_emit;
-                    const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
-                    const unsigned long long p = pack4(own, tri, act, 0u);
-                    const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
-                    const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
-                    // ends of the owned crossing edges: corner 7 (qxyz) and 5 (qxz), 6 (qyz), 3 (qxy)
-                    const int sx = x - 1, sy = y - 1, sl = z - g.fz0;   // stored coords of corner 0
-                    // the four corner loads are issued unconditionally (lanes without a cell read
-                    // sample 0): a load under a divergent branch waits on its own
-                    const int n_ = g.n;
-                    const int64_t base = has ? (int64_t)sx + (int64_t)sy * n_ + (int64_t)sl * n_ * n_ : 0;
-                    const int64_t dx = has ? 1 : 0, dy = has ? n_ : 0, dz = has ? (int64_t)n_ * n_ : 0;
-                    const float r7 = b.field[base + dx + dy + dz], r5 = b.field[base + dx + dz];
-                    const float r6 = b.field[base + dy + dz], r3 = b.field[base + dx + dy];
-                    const bool sx1 = sealed_xy(g, sx + 1), sy1 = sealed_xy(g, sy + 1), sz1 = sealed_z(g, sl + 1);
-                    const bool sx0 = sealed_xy(g, sx), sy0 = sealed_xy(g, sy), sz0 = sealed_z(g, sl);
-                    const float f7 = (sx1 || sy1 || sz1) ? kSealed : r7;
-                    const float f5 = (sx1 || sy0 || sz1) ? kSealed : r5;
-                    const float f6 = (sx0 || sy1 || sz1) ? kSealed : r6;
-                    const float f3 = (sx1 || sy1 || sz0) ? kSealed : r3;
-                    if (has && own) {
-                        const uint32_t vrun = vrun0 + fld(pre, 0);
-                        const float fx = ((float)x + g.i0[0]) * g.w[0];
-                        const float fy = ((float)y + g.i0[1]) * g.w[1];
-                        const float fz = ((float)z + g.i0[2]) * g.w[2];
-                        const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
-    #pragma unroll
-                        for (int slot = 0; slot < 3; ++slot) {
-                            const int r = C.rank[slot];
-                            if (r < 0) continue;
-                            const uint32_t vid = vrun + (uint32_t)r;
-                            b.vid3[(size_t)L * 3 + slot] = vid - H;
-                            if (!emit) continue;
-                            const uint32_t out = vid - H;
-                            if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
-                            float px, py, pz;
-                            if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
-                                const float mu = (0.f - f5) / (f7 - f5);
-                                px = fx2; py = fy + mu * g.w[1]; pz = fz2;
-                            } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
-                                const float mu = (0.f - f6) / (f7 - f6);
-                                px = fx + mu * g.w[0]; py = fy2; pz = fz2;
-                            } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
-                                const float mu = (0.f - f3) / (f7 - f3);
-                                px = fx2; py = fy2; pz = fz + mu * g.w[2];
-                            }
-                            b.verts[3 * (size_t)out] = px;
-                            b.verts[3 * (size_t)out + 1] = py;
-                            b.verts[3 * (size_t)out + 2] = pz;
-                        }
-                    }
-                    if (act) {
-                        const uint32_t arun = arun0 + fld(pre, 2);
-                        if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
-                        else *b.overflow = 1u;
-                    }
-                    vrun0 += fld(tot, 0);
-                    frun0 += fld(tot, 1);
-                    arun0 += fld(tot, 2);
+                if (act) {
+                    const uint32_t arun = arun0 + fld(pre, 2);
+                    if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), vrun);
+                    else *b.overflow = 1u;
                 }
-                __builtin_amdgcn_wave_barrier();
+                vrun0 += fld(tot, 0);
+                frun0 += fld(tot, 1);
+                arun0 += fld(tot, 2);
             }
         }
     }
 }
 
+// K3b: one lane per active cell (its record): the owned vertices' ids into vid3 and their
+// positions from the owner cell's fx/fy/fz (the reference's first emission).  Corner values are
+// read from the field only at owned crossing edges (never in a sign-filled brick).
+__device__ __forceinline__ void mc_vpos_body(const CaseInfo* __restrict__ s_case, const GridDesc& g, const MCBuffers& b) {
+    const uint32_t n_rec = b.counters[4];
+    const uint32_t lim = n_rec < (uint64_t)b.cap_rec ? n_rec : (uint32_t)b.cap_rec;
+    const uint32_t H = b.counters[1];
+    const uint32_t m = (uint32_t)g.m;
+    const int n_ = g.n;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gridDim.x * blockDim.x) {
+        const uint4 r = b.records[i];   // {L, ci, fbase, vbase}
+        const uint32_t L = r.x;
+        const CaseInfo& C = s_case[r.y];
+        if (!C.nown) continue;
+        const uint32_t row = L / m;
+        const int x = (int)(L - row * m) + 1, y = (int)(row % m) + 1, z = (int)(row / m) + g.cz0;
+        // ends of the owned crossing edges: corner 7 (qxyz) and 5 (qxz), 6 (qyz), 3 (qxy); the four
+        // loads are issued together
+        const int sx = x - 1, sy = y - 1, sl = z - g.fz0;   // stored coords of corner 0
+        const int64_t base = (int64_t)sx + (int64_t)sy * n_ + (int64_t)sl * n_ * n_;
+        const int64_t dy = n_, dz = (int64_t)n_ * n_;
+        const float r7 = b.field[base + 1 + dy + dz], r5 = b.field[base + 1 + dz];
+        const float r6 = b.field[base + dy + dz], r3 = b.field[base + 1 + dy];
+        const bool sx1 = sealed_xy(g, sx + 1), sy1 = sealed_xy(g, sy + 1), sz1 = sealed_z(g, sl + 1);
+        const bool sx0 = sealed_xy(g, sx), sy0 = sealed_xy(g, sy), sz0 = sealed_z(g, sl);
+        const float f7 = (sx1 || sy1 || sz1) ? kSealed : r7;
+        const float f5 = (sx1 || sy0 || sz1) ? kSealed : r5;
+        const float f6 = (sx0 || sy1 || sz1) ? kSealed : r6;
+        const float f3 = (sx1 || sy1 || sz0) ? kSealed : r3;
+        const float fx = ((float)x + g.i0[0]) * g.w[0];
+        const float fy = ((float)y + g.i0[1]) * g.w[1];
+        const float fz = ((float)z + g.i0[2]) * g.w[2];
+        const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
+#pragma unroll
+        for (int slot = 0; slot < 3; ++slot) {
+            const int rk = C.rank[slot];
+            if (rk < 0) continue;
+            const uint32_t out = r.w + (uint32_t)rk - H;
+            b.vid3[(size_t)L * 3 + slot] = out;
+            if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
+            float px, py, pz;
+            if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
+                const float mu = (0.f - f5) / (f7 - f5);
+                px = fx2; py = fy + mu * g.w[1]; pz = fz2;
+            } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
+                const float mu = (0.f - f6) / (f7 - f6);
+                px = fx + mu * g.w[0]; py = fy2; pz = fz2;
+            } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
+                const float mu = (0.f - f3) / (f7 - f3);
+                px = fx2; py = fy2; pz = fz + mu * g.w[2];
+            }
+            b.verts[3 * (size_t)out] = px;
+            b.verts[3 * (size_t)out + 1] = py;
+            b.verts[3 * (size_t)out + 2] = pz;
+        }
+    }
+}
 
 }  // namespace impli
