@@ -17,10 +17,9 @@
 //   K2 k_mc_count : per unit the sums of owned edges, triangles, active cells, halo-owned edges.
 //   K2b k_unit_scan: per group, its global bases (sum of the groups before it) and its non-empty
 //       units in order in the flat list.
-//   K3a k_mc_cells : per unit, the non-trivial cells in cell order: records {cell, case, face base,
-//                    vertex base} of the active cells (vid3 of the halo cells).
-//   K3b k_mc_vpos : per active cell, owned vertex positions (field values read only at crossing
-//                   edges) and the dense vid3[cell][slot] table.
+//   K3 k_mc_cells : per unit, the non-trivial cells in cell order (selected in parallel): owned
+//                   vertex positions (field values read only at crossing edges), the dense
+//                   vid3[cell][slot] table, records {cell, case, face base} of the active cells.
 //   K4 k_mc_faces : per active cell, gathers the vertex ids of its triangle corners from vid3 of
 //                   the owner cells.
 #include <algorithm>
@@ -237,13 +236,6 @@ __global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells(const CaseInfo* _
     mc_cells_body(cases, g, b);
 }
 
-__global__ __launch_bounds__(256) void k_mc_vpos(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
-    __shared__ CaseInfo s_case[256];
-    s_case[threadIdx.x] = cases[threadIdx.x];
-    __syncthreads();
-    mc_vpos_body(s_case, g, b);
-}
-
 // owner offset (dx, dy, dz subtracted) and owned slot of each Bourke edge
 __constant__ int8_t c_edge_owner[12][4] = {
     {0, 1, 1, 1}, {0, 0, 1, 0}, {0, 0, 1, 1}, {1, 0, 1, 0}, {0, 1, 0, 1}, {0, 0, 0, 0},
@@ -316,7 +308,6 @@ void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
     if (nu > 0) {
         k_mc_cells<<<(unsigned)std::min<int64_t>((nu + kVertsWaves - 1) / kVertsWaves, kVertsMaxBlocks),
                      64 * kVertsWaves, 0, s>>>(d_cases, g, b);
-        k_mc_vpos<<<(unsigned)std::min<int64_t>((b.cap_rec + 255) / 256, 2048), 256, 0, s>>>(d_cases, g, b);
     }
 }
 

@@ -109,13 +109,12 @@ __device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
            ((unsigned)((k.t11 >> j) & 1u) << 6);
 }
 
-// K3a: one wave per unit.  Lanes find the non-trivial cells of their (row, chunk) items; the cells
-// are then taken in cell order, 64 at a time: a wave scan of (owned
-// edges, triangles, active) gives every cell its vertex / face / record base.  Active cells get a
-// record {L, ci, face base, vertex base}; halo cells (below the slab's first emitted layer) write
-// their owned ids into vid3 -- no field value is read here, so a unit with hundreds of cells costs
-// a few ALU passes, not a memory round trip per 64 cells.  K3b (mc_vpos_body) then places the
-// vertices, one lane per active cell.
+// K3: one wave per unit.  Lanes find the non-trivial cells of their (row, chunk) items; the cells
+// are then taken in cell order, 64 at a time: a wave scan of (owned edges, triangles, active)
+// gives every cell its vertex / face / record base; owned vertices are
+// placed from the owner cell's fx/fy/fz (the reference's first emission), their ids go to vid3
+// (halo cells, below the slab's first emitted layer: ids only), active cells get a record
+// {L, ci, face base}.  (A separate one-lane-per-active-cell position pass measured 2 us slower.)
 __device__ __forceinline__ unsigned long long pack4(unsigned a, unsigned b, unsigned c, unsigned d) {
     return (unsigned long long)a | ((unsigned long long)b << 16) | ((unsigned long long)c << 32) |
            ((unsigned long long)d << 48);
@@ -203,78 +202,50 @@ __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases
                 const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
                 const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
                 const uint32_t vrun = vrun0 + fld(pre, 0);
-                if (own && !emit) {   // halo cell: the slab below emits its vertices; ids only
+                {
+                    const int y = (int)erow % g.m + 1;
+                    const int sx = x - 1, sy = y - 1, sl = z - g.fz0;
+                    const int n_ = g.n;
+                    const int64_t base = has ? (int64_t)sx + (int64_t)sy * n_ + (int64_t)sl * n_ * n_ : 0;
+                    const int64_t dx = has ? 1 : 0, dy = has ? n_ : 0, dz = has ? (int64_t)n_ * n_ : 0;
+                    const float r7 = b.field[base + dx + dy + dz], r5 = b.field[base + dx + dz];
+                    const float r6 = b.field[base + dy + dz], r3 = b.field[base + dx + dy];
+                    const bool sx1 = sealed_xy(g, sx + 1), sy1 = sealed_xy(g, sy + 1), sz1 = sealed_z(g, sl + 1);
+                    const bool sx0 = sealed_xy(g, sx), sy0 = sealed_xy(g, sy), sz0 = sealed_z(g, sl);
+                    const float f7 = (sx1 || sy1 || sz1) ? kSealed : r7;
+                    const float f5 = (sx1 || sy0 || sz1) ? kSealed : r5;
+                    const float f6 = (sx0 || sy1 || sz1) ? kSealed : r6;
+                    const float f3 = (sx1 || sy1 || sz0) ? kSealed : r3;
+                    if (has && own) {
+                        const float fx = ((float)x + g.i0[0]) * g.w[0];
+                        const float fy = ((float)y + g.i0[1]) * g.w[1];
+                        const float fz = ((float)z + g.i0[2]) * g.w[2];
+                        const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
 #pragma unroll
-                    for (int slot = 0; slot < 3; ++slot)
-                        if (C.rank[slot] >= 0) b.vid3[(size_t)L * 3 + slot] = vrun + (uint32_t)C.rank[slot] - H;
+                        for (int slot = 0; slot < 3; ++slot) {
+                            const int r = C.rank[slot];
+                            if (r < 0) continue;
+                            const uint32_t out = vrun + (uint32_t)r - H;
+                            b.vid3[(size_t)L * 3 + slot] = out;
+                            if (!emit) continue;
+                            if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
+                            float px, py, pz;
+                            if (slot == 0) { const float mu = (0.f - f5) / (f7 - f5); px = fx2; py = fy + mu * g.w[1]; pz = fz2; }
+                            else if (slot == 1) { const float mu = (0.f - f6) / (f7 - f6); px = fx + mu * g.w[0]; py = fy2; pz = fz2; }
+                            else { const float mu = (0.f - f3) / (f7 - f3); px = fx2; py = fy2; pz = fz + mu * g.w[2]; }
+                            b.verts[3 * (size_t)out] = px; b.verts[3 * (size_t)out + 1] = py; b.verts[3 * (size_t)out + 2] = pz;
+                        }
+                    }
                 }
                 if (act) {
                     const uint32_t arun = arun0 + fld(pre, 2);
-                    if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), vrun);
+                    if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
                     else *b.overflow = 1u;
                 }
                 vrun0 += fld(tot, 0);
                 frun0 += fld(tot, 1);
                 arun0 += fld(tot, 2);
             }
-        }
-    }
-}
-
-// K3b: one lane per active cell (its record): the owned vertices' ids into vid3 and their
-// positions from the owner cell's fx/fy/fz (the reference's first emission).  Corner values are
-// read from the field only at owned crossing edges (never in a sign-filled brick).
-__device__ __forceinline__ void mc_vpos_body(const CaseInfo* __restrict__ s_case, const GridDesc& g, const MCBuffers& b) {
-    const uint32_t n_rec = b.counters[4];
-    const uint32_t lim = n_rec < (uint64_t)b.cap_rec ? n_rec : (uint32_t)b.cap_rec;
-    const uint32_t H = b.counters[1];
-    const uint32_t m = (uint32_t)g.m;
-    const int n_ = g.n;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gridDim.x * blockDim.x) {
-        const uint4 r = b.records[i];   // {L, ci, fbase, vbase}
-        const uint32_t L = r.x;
-        const CaseInfo& C = s_case[r.y];
-        if (!C.nown) continue;
-        const uint32_t row = L / m;
-        const int x = (int)(L - row * m) + 1, y = (int)(row % m) + 1, z = (int)(row / m) + g.cz0;
-        // ends of the owned crossing edges: corner 7 (qxyz) and 5 (qxz), 6 (qyz), 3 (qxy); the four
-        // loads are issued together
-        const int sx = x - 1, sy = y - 1, sl = z - g.fz0;   // stored coords of corner 0
-        const int64_t base = (int64_t)sx + (int64_t)sy * n_ + (int64_t)sl * n_ * n_;
-        const int64_t dy = n_, dz = (int64_t)n_ * n_;
-        const float r7 = b.field[base + 1 + dy + dz], r5 = b.field[base + 1 + dz];
-        const float r6 = b.field[base + dy + dz], r3 = b.field[base + 1 + dy];
-        const bool sx1 = sealed_xy(g, sx + 1), sy1 = sealed_xy(g, sy + 1), sz1 = sealed_z(g, sl + 1);
-        const bool sx0 = sealed_xy(g, sx), sy0 = sealed_xy(g, sy), sz0 = sealed_z(g, sl);
-        const float f7 = (sx1 || sy1 || sz1) ? kSealed : r7;
-        const float f5 = (sx1 || sy0 || sz1) ? kSealed : r5;
-        const float f6 = (sx0 || sy1 || sz1) ? kSealed : r6;
-        const float f3 = (sx1 || sy1 || sz0) ? kSealed : r3;
-        const float fx = ((float)x + g.i0[0]) * g.w[0];
-        const float fy = ((float)y + g.i0[1]) * g.w[1];
-        const float fz = ((float)z + g.i0[2]) * g.w[2];
-        const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
-#pragma unroll
-        for (int slot = 0; slot < 3; ++slot) {
-            const int rk = C.rank[slot];
-            if (rk < 0) continue;
-            const uint32_t out = r.w + (uint32_t)rk - H;
-            b.vid3[(size_t)L * 3 + slot] = out;
-            if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
-            float px, py, pz;
-            if (slot == 0) {        // edge 5: VIntY at qxz, (fx2, fy + mu*dy, fz2), field5 -> field7
-                const float mu = (0.f - f5) / (f7 - f5);
-                px = fx2; py = fy + mu * g.w[1]; pz = fz2;
-            } else if (slot == 1) { // edge 6: VIntX at qyz, (fx + mu*dx, fy2, fz2), field6 -> field7
-                const float mu = (0.f - f6) / (f7 - f6);
-                px = fx + mu * g.w[0]; py = fy2; pz = fz2;
-            } else {                // edge 10: VIntZ at qxy, (fx2, fy2, fz + mu*dz), field3 -> field7
-                const float mu = (0.f - f3) / (f7 - f3);
-                px = fx2; py = fy2; pz = fz + mu * g.w[2];
-            }
-            b.verts[3 * (size_t)out] = px;
-            b.verts[3 * (size_t)out + 1] = py;
-            b.verts[3 * (size_t)out + 2] = pz;
         }
     }
 }
