@@ -23,18 +23,25 @@ __device__ __forceinline__ uint8_t sign_class(dev::Iv root) {   // MC sets a cub
     return (root.lo >= 0.f) ? kBrickPos : (root.hi < 0.f) ? kBrickNeg : kBrickMixed;
 }
 
-// wave-aggregated append of `b` to list (order irrelevant)
+// block-aggregated append of `b` to list (order irrelevant): one atomic per block -- same-address
+// atomics serialise (per-wave appends measured slower).  Every thread of the block must call it.
 // cap: list capacity (entries past it are dropped -- never reached when the count starts at 0)
-__device__ __forceinline__ void list_append(bool take, uint32_t b, uint32_t* __restrict__ list,
-                                            uint32_t* __restrict__ count, uint32_t cap) {
-    const int lane = threadIdx.x & 63;
+template <int kBlock>
+__device__ __forceinline__ void block_append(bool take, uint32_t b, uint32_t* __restrict__ list,
+                                             uint32_t* __restrict__ count, uint32_t cap) {
+    __shared__ uint32_t s_cnt[kBlock / 64], s_base[kBlock / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t mask = __ballot(take);
-    if (!mask) return;
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader, 64);
-    const uint32_t at = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    if (lane == 0) s_cnt[w] = (uint32_t)__popcll((unsigned long long)mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < kBlock / 64; ++k) { s_base[k] = t; t += s_cnt[k]; }
+        const uint32_t base = t ? atomicAdd(count, t) : 0u;
+        for (int k = 0; k < kBlock / 64; ++k) s_base[k] += base;
+    }
+    __syncthreads();
+    const uint32_t at = s_base[w] + (uint32_t)__popcll((unsigned long long)(mask & ((1ull << lane) - 1ull)));
     if (take && at < cap) list[at] = b;
 }
 
@@ -116,7 +123,7 @@ __device__ __forceinline__ void coarse_modes_body(const IvEval& ev, const GridDe
         cmodes[b] = m;
         ccls[b] = c;
     }
-    list_append(b < cg.n_bricks && c == kBrickMixed, (uint32_t)b, clist, ccount, (uint32_t)cg.n_bricks);
+    block_append<256>(b < cg.n_bricks && c == kBrickMixed, (uint32_t)b, clist, ccount, (uint32_t)cg.n_bricks);
 }
 
 // Bricks of the listed mixed coarse boxes: one thread per (listed box, brick in it).
