@@ -122,6 +122,9 @@ def main():
     ap.add_argument("--skip-config5", action="store_true", help="do not time the 64-object stream (config 5)")
     ap.add_argument("--config5-streams", type=int, default=8)
     ap.add_argument("--skip-ob02", action="store_true", help="do not time build_geometry with the OB02 loop")
+    ap.add_argument("--graph", action="store_true",
+                    help="N = 1: replay the step as a hipGraph (measured no faster than direct launches: "
+                         "0.176 vs 0.172 ms at 512^3)")
     args = ap.parse_args()
 
     import torch
@@ -183,12 +186,40 @@ def main():
         if grew:
             step()
         torch.cuda.synchronize(dev)
+        # --graph (one GPU): the step's launches are captured once as a hipGraph and replayed --
+        # every replay recomputes everything; the graph only changes how the kernels are launched
+        graph = None
+        if world == 1 and args.graph:
+            try:
+                graph = torch.cuda.CUDAGraph()
+                cs = torch.cuda.Stream(dev)
+                cs.wait_stream(stream)
+                with torch.cuda.stream(cs):
+                    graph.capture_begin()
+                    slab.eval(cs.cuda_stream)
+                    slab.count(cs.cuda_stream)
+                    slab.emit(0, cs.cuda_stream)
+                    graph.capture_end()
+                stream.wait_stream(cs)
+                for _ in range(2):
+                    graph.replay()
+                torch.cuda.synchronize(dev)
+            except Exception as exc:   # capture unavailable: direct launches
+                print("bench: hipGraph capture failed (%s); launching directly" % exc, file=sys.stderr)
+                graph = None
+                torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for k in range(steps):
-            step(ev[k])
+        if graph is not None:
+            for k in range(steps):
+                ev[k][0].record(stream)
+                graph.replay()
+                ev[k][3].record(stream)
+        else:
+            for k in range(steps):
+                step(ev[k])
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -202,9 +233,12 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot)
         el = float(t.item())
-        kms = {"eval": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
-               "mc_count_scan": float(np.mean([e[1].elapsed_time(e[2]) for e in ev])),
-               "mc_emit": float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))}
+        if graph is not None:   # one interval per replay: eval + count + scan + emit
+            kms = {"step_graph": float(np.mean([e[0].elapsed_time(e[3]) for e in ev]))}
+        else:
+            kms = {"eval": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
+                   "mc_count_scan": float(np.mean([e[1].elapsed_time(e[2]) for e in ev])),
+                   "mc_emit": float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))}
         # per-kernel durations: HIP events recorded by the engine between its launches on this
         # stream, over a few extra steps after the timed region (so it is not perturbed)
         slab.set_timing(True)
@@ -216,6 +250,7 @@ def main():
         kernel_ms = {k: float(np.mean([p[k] for p in per])) for k in per[0]}
         info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, kernel_ms=kernel_ms,
                     shape=shape, slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats(),
+                    graph=graph is not None,
                     fz=(slab.fz0, slab.fz1), jit=slab.used_jit(), stats=slab.stats())
         slab.close()
         return info
@@ -353,6 +388,7 @@ def main():
         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
         "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
         "eval_kernel": "jit" if main_run["jit"] else "interpreter",
+        "launch": "hipGraph replay of the step" if main_run["graph"] else "direct launches",
         "bricks": {"total": bricks_total, "mixed": bricks_mixed, "sign_filled": bricks_filled,
                    "evaluated_sample_frac": round(1.0 - bricks_filled / max(1, bricks_total), 4),
                    "mixed_coarse_boxes": main_run["stats"]["mixed_coarse_boxes"]},
