@@ -81,13 +81,20 @@ def cpu_baseline(shape, target_s=20.0):
 
 def mesh_parity(v, f, v_ref, f_ref):
     """max|v - v_ref| over the vertices and whether the face arrays are identical (the metric's
-    max|v-v_ref|)."""
+    max|v-v_ref|).  Non-finite reference vertices (OB02 on a tree whose singular
+    point lands on a grid sample: a zero gradient that normalize_1111 divides by)
+    must be non-finite at the same rows; the difference is taken over the finite ones."""
     same_shape = v.shape == v_ref.shape and f.shape == f_ref.shape
-    diff = None
+    out = {"verts": int(v_ref.shape[0]), "faces": int(f_ref.shape[0]),
+           "faces_identical": bool(same_shape and np.array_equal(f, f_ref)), "max_abs_v_diff": None}
     if same_shape:
-        diff = float(np.abs(v.astype(np.float64) - v_ref).max()) if v.size else 0.0
-    return {"verts": int(v_ref.shape[0]), "faces": int(f_ref.shape[0]),
-            "faces_identical": bool(same_shape and np.array_equal(f, f_ref)), "max_abs_v_diff": diff}
+        fin, fin_ref = np.isfinite(v).all(1), np.isfinite(v_ref).all(1)
+        both = fin & fin_ref
+        out["max_abs_v_diff"] = float(np.abs(v[both].astype(np.float64) - v_ref[both]).max()) if both.any() else 0.0
+        if not fin_ref.all():
+            out["nonfinite_ref_verts"] = int((~fin_ref).sum())
+            out["nonfinite_rows_identical"] = bool(np.array_equal(fin, fin_ref))
+    return out
 
 
 def copy_attainable(dev, nbytes=1 << 30, reps=10):

@@ -27,8 +27,8 @@ KERNELS = {   # substring of the demangled name -> engine phase (Engine::kernel_
     "k_brick_refine": "brick_modes", "k_brick_fill": "brick_modes",
     "impli_eval_bricks": "eval_field", "k_eval_field_pruned": "eval_field", "k_eval_field": "eval_field",
     "k_signs_from_field": "eval_field",
-    "k_mc_count": "mc_count", "k_scan_groups": "mc_scan", "k_unit_flatten": "mc_scan",
-    "k_mc_verts": "mc_verts", "k_mc_faces": "mc_faces",
+    "k_mc_count": "mc_count", "k_scan_groups": "mc_scan", "k_unit_flatten": "mc_scan", "k_unit_scan": "mc_scan",
+    "k_mc_verts": "mc_verts", "k_mc_cells": "mc_verts", "k_mc_faces": "mc_faces",
 }
 
 
