@@ -480,7 +480,7 @@ int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {
         s->engine.raw_counters(c, 0);
         const GridDesc& g = s->engine.grid();
         out[0] = n_units(g);
-        out[1] = c[0];
+        out[1] = c[6];   // non-empty units (c[0] counts their parts)
         out[2] = c[2];
         out[3] = c[3];
         out[4] = c[4];

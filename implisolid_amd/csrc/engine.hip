@@ -130,7 +130,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &ulist_, &umark_, &counters_, &lmodes_, &vid3_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &vid3_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -157,10 +157,16 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     blist_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     lmodes_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint64_t));
-    field_.reserve((size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float));
+    const size_t field_bytes = (size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float);
+    field_.reserve(field_bytes);
+    // the pruned eval writes only the listed bricks: the rest of the field reads as 0, not as
+    // whatever the allocation held (deterministic read_field; nothing on the path reads it)
+    IMPLI_HIP(hipMemset(field_.p, 0, field_bytes));
     unit_cnt_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint4));
-    scan_blk_.reserve((size_t)(n_groups(grid_) + 1) * kScanParts * sizeof(uint32_t));
-    ulist_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint4));
+    unit_part_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint32_t));
+    scan_blk_.reserve((size_t)(n_groups(grid_) + 1) * (kScanParts + 1) * sizeof(uint32_t));
+    ulist_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint4));
+    upart_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint32_t));
     umark_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint32_t));
     IMPLI_HIP(hipMemset(umark_.p, 0, (size_t)(n_units(grid_) + 1) * sizeof(uint32_t)));   // ids start at 1
     marks_valid_ = false;
@@ -198,8 +204,10 @@ MCBuffers Engine::buffers() const {
     b.signs = signs_.as<uint64_t>();
 
     b.unit_cnt = unit_cnt_.as<uint4>();
+    b.unit_part = unit_part_.as<uint32_t>();
     b.scan_blk = scan_blk_.as<uint32_t>();
     b.ulist = ulist_.as<uint4>();
+    b.upart = upart_.as<uint32_t>();
     b.umark = marks_valid_ ? umark_.as<uint32_t>() : nullptr;
     b.mark_id = mark_id_;
     b.counters = counters_.as<uint32_t>();

@@ -174,12 +174,19 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
         const uint32_t ea = wave_incl_scan<uint32_t>(act, t) - act;
         const uint64_t m = __ballot(ne);
         const uint32_t pos = (uint32_t)__popcll((unsigned long long)(m & ((1ull << t) - 1ull)));
-        if (ne) b.unit_cnt[G * kGroupUnits + pos] = make_uint4((uint32_t)t, eo, et, ea);
-        const uint32_t sums[kScanParts] = {__shfl(eo + own, 63, 64), __shfl(et + tri, 63, 64),
-                                           __shfl(ea + act, 63, 64), wave_sum(hal),
-                                           (uint32_t)__popcll((unsigned long long)m)};
-        if (t < kScanParts) {
-            const uint32_t v = t == 0 ? sums[0] : t == 1 ? sums[1] : t == 2 ? sums[2] : t == 3 ? sums[3] : sums[4];
+        // parts: a unit's active cells split into runs of kPartCells for separate waves
+        const uint32_t parts = ne ? min((uint32_t)kMaxParts, max(1u, (act + kPartCells - 1) / kPartCells)) : 0u;
+        const uint32_t ep = wave_incl_scan<uint32_t>(parts, t) - parts;
+        if (ne) {
+            b.unit_cnt[G * kGroupUnits + pos] = make_uint4((uint32_t)t, eo, et, ea);
+            b.unit_part[G * kGroupUnits + pos] = ep | (parts << 16);
+        }
+        const uint32_t sums[kScanParts + 1] = {__shfl(eo + own, 63, 64), __shfl(et + tri, 63, 64),
+                                               __shfl(ea + act, 63, 64), wave_sum(hal), __shfl(ep + parts, 63, 64),
+                                               (uint32_t)__popcll((unsigned long long)m)};
+        if (t <= kScanParts) {
+            const uint32_t v = t == 0 ? sums[0] : t == 1 ? sums[1] : t == 2 ? sums[2] : t == 3 ? sums[3]
+                             : t == 4 ? sums[4] : sums[5];
             b.scan_blk[(int64_t)t * gridDim.x + G] = v;
         }
     }
@@ -192,43 +199,51 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
 // 7.3 + 4.5 us at 512^3; a decoupled look-back inside k_mc_count, 28 us more: its status words
 // cross the XCDs' L2s at memory latency, one round trip per 64 groups walked.)
 constexpr int kScanBlock = 256;
+constexpr int kScanRows = kScanParts + 1;   // + the non-empty unit counts (summed for statistics)
 __global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) {
-    __shared__ uint32_t s_part[kScanBlock / 64][kScanParts];
-    __shared__ uint32_t s_base[kScanParts];
+    __shared__ uint32_t s_part[kScanBlock / 64][kScanRows];
+    __shared__ uint32_t s_base[kScanRows];
     const int64_t G = blockIdx.x, ng = n_groups(g);
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const bool last = G == ng - 1;
-    const uint32_t nne = b.scan_blk[4 * ng + G];
+    const uint32_t nne = b.scan_blk[5 * ng + G];   // non-empty units of the group
     if (nne == 0 && !last) return;   // uniform
     const uint4 e = b.unit_cnt[G * kGroupUnits + (t < (int)nne ? t : 0)];
-    uint32_t acc[kScanParts] = {0u, 0u, 0u, 0u, 0u};
+    const uint32_t pp = b.unit_part[G * kGroupUnits + (t < (int)nne ? t : 0)];
+    uint32_t acc[kScanRows] = {0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll 4
     for (int64_t i = t; i < G; i += kScanBlock)
 #pragma unroll
-        for (int c = 0; c < kScanParts; ++c) acc[c] += b.scan_blk[c * ng + i];
+        for (int c = 0; c < kScanRows; ++c) acc[c] += b.scan_blk[c * ng + i];
 #pragma unroll
-    for (int c = 0; c < kScanParts; ++c) {
+    for (int c = 0; c < kScanRows; ++c) {
         const uint32_t s = wave_sum(acc[c]);
         if (lane == 0) s_part[wid][c] = s;
     }
     __syncthreads();
-    if (t < kScanParts) {
+    if (t < kScanRows) {
         uint32_t s = 0;
 #pragma unroll
         for (int w = 0; w < kScanBlock / 64; ++w) s += s_part[w][t];
         s_base[t] = s;
     }
     __syncthreads();
-    if (t < (int)nne)
-        b.ulist[s_base[4] + t] = make_uint4((uint32_t)(G * kGroupUnits) + e.x, s_base[0] + e.y, s_base[1] + e.z,
-                                            s_base[2] + e.w);
+    if (t < (int)nne) {
+        const uint4 ent = make_uint4((uint32_t)(G * kGroupUnits) + e.x, s_base[0] + e.y, s_base[1] + e.z, s_base[2] + e.w);
+        const uint32_t P = pp >> 16, at = s_base[4] + (pp & 0xffffu);
+        for (uint32_t q = 0; q < P; ++q) {
+            b.ulist[at + q] = ent;
+            b.upart[at + q] = q | (P << 8);
+        }
+    }
     if (last && t == 0) {
-        b.counters[0] = s_base[4] + nne;                           // non-empty units
+        b.counters[0] = s_base[4] + b.scan_blk[4 * ng + G];       // unit parts
         b.counters[1] = s_base[3] + b.scan_blk[3 * ng + G];       // halo-owned vertices (ids below the slab's first)
         b.counters[2] = s_base[0] + b.scan_blk[G];                // owned vertices incl. halo
         b.counters[3] = s_base[1] + b.scan_blk[ng + G];           // triangles
         b.counters[4] = s_base[2] + b.scan_blk[2 * ng + G];       // active cells (face records)
         b.counters[5] = s_base[3] + b.scan_blk[3 * ng + G];
+        b.counters[6] = s_base[5] + nne;                          // non-empty units (statistics)
     }
 }
 

@@ -132,8 +132,10 @@ __device__ __forceinline__ int select_bit(uint64_t x, uint32_t r) {
     return pos;
 }
 
-// Waves take the non-empty units of the flat list (k_unit_scan) grid-stride, one unit at a time:
-// every resident wave gets an equal share whatever the surface's distribution over groups.  A
+// Waves take the parts of the non-empty units from the flat list (k_unit_scan) grid-stride: every
+// resident wave gets an equal share whatever the surface's distribution over groups, and a heavy
+// unit (up to ~2000 cells) is spread over up to kMaxParts waves instead of serialising its 64-cell
+// windows, each with a field round trip, on one.  A
 // unit's items (row, 64-cell chunk) go to LDS with their exclusive cell counts; each lane then
 // finds its own cell -- the item by binary search, the cell by selecting the bit -- so cells are
 // listed in cell order 64 at a time, with no lane looping over a dense chunk's bits.
@@ -155,8 +157,11 @@ __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases
     const int items = kUnitRows * nch;
     for (uint32_t e = w0 + wid; e < n_ne; e += gridDim.x * kVertsWaves) {
         const uint4 ent = b.ulist[e];   // {unit, vbase, fbase, abase}
+        const uint32_t up = b.upart[e];   // part | parts << 8: this wave emits windows w % parts == part
+        const uint32_t part = up & 255u, parts = up >> 8;
         const int64_t u = ent.x;
         uint32_t vrun0 = ent.y, frun0 = ent.z, arun0 = ent.w;
+        uint32_t win = 0;   // 64-cell window index within the unit
         for (int i0 = 0; i0 < items; i0 += 64) {
             const int i = i0 + lane;
             ChunkBits k;
@@ -174,7 +179,8 @@ __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases
             bits[8][lane] = k.nt;
             excl[lane] = incl - cnt;
             __builtin_amdgcn_wave_barrier();
-            for (uint32_t e0 = 0; e0 < total; e0 += 64) {
+            for (uint32_t e0 = 0; e0 < total; e0 += 64, ++win) {
+                const bool mine = win % parts == part;   // uniform: other windows only advance the bases
                 const uint32_t ce = e0 + (uint32_t)lane;
                 const bool has = ce < total;
                 // the item holding cell ce: the last item whose exclusive count is <= ce (items
@@ -202,7 +208,7 @@ __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases
                 const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
                 const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
                 const uint32_t vrun = vrun0 + fld(pre, 0);
-                {
+                if (mine) {
                     const int y = (int)erow % g.m + 1;
                     const int sx = x - 1, sy = y - 1, sl = z - g.fz0;
                     const int n_ = g.n;
@@ -237,7 +243,7 @@ __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases
                         }
                     }
                 }
-                if (act) {
+                if (mine && act) {
                     const uint32_t arun = arun0 + fld(pre, 2);
                     if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
                     else *b.overflow = 1u;

@@ -22,16 +22,23 @@ constexpr int kUnitRows = 4;
 constexpr int kGroupUnits = 64;        // units per group: one count block; the group scan's element
 constexpr int kVertsWaves = 4;         // waves per verts block (grid-stride over the unit list)
 constexpr int kVertsMaxBlocks = 2048;  // verts grid: ~ the resident waves of the chip
-constexpr int kScanParts = 5;          // group sums: own, tri, act, halo own, non-empty units
+constexpr int kScanParts = 5;          // group sums scanned: own, tri, act, halo own, unit parts
+// A non-empty unit with many active cells is handed to several waves ("parts"): part p of P takes
+// the unit's 64-cell windows w with w % P == p (the other windows only advance its bases).
+constexpr int kPartCells = 128;        // active cells per part
+constexpr int kMaxParts = 8;
 struct MCBuffers {
     const float* field;
     const uint64_t* signs;   // sign bitmap of the stored samples (grid.hpp)
     uint4* unit_cnt;         // per group, its non-empty units {unit in group, own, tri, act bases} (k_mc_count)
-    uint32_t* scan_blk;      // [kScanParts][n_groups]: group sums (own, tri, act, halo own, non-empty units)
-    uint4* ulist;            // all non-empty units in order: {unit, vbase, fbase, abase} (k_unit_scan)
+    uint32_t* unit_part;     // ... and their parts: in-group part base | part count << 16
+    uint32_t* scan_blk;      // [kScanParts + 1][n_groups]: group sums (own, tri, act, halo own, parts),
+                             // then the group's non-empty unit count (not scanned)
+    uint4* ulist;            // all parts of the non-empty units in order: {unit, vbase, fbase, abase}
+    uint32_t* upart;         // ... part index | part count << 8 (k_unit_scan)
     const uint32_t* umark;   // units whose cells touch an evaluated brick hold mark_id (k_brick_fill);
     uint32_t mark_id;        // null: every unit is counted (dense eval)
-    uint32_t* counters;      // [0] non-empty units, [1] halo own, [2..5] totals own/tri/act/halo
+    uint32_t* counters;      // [0] unit parts, [1] halo own, [2..5] totals own/tri/act/halo, [6] non-empty units
     uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
     uint4* records;          // active cells: {L, ci, fbase, 0}
     float* verts;            // 3 * cap_v
