@@ -74,34 +74,10 @@ __device__ __forceinline__ uint32_t brick_class_of(const GridDesc& g, uint8_t c,
     return c == kBrickMixed ? (uint32_t)r : (uint32_t)sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
 }
 
-// The brick's class and its fill class.  A brick needs exact values only if one of its samples can
-// be the end of a sign-changing cell edge.  Edges are axis aligned, so that requires the brick or
-// a face neighbour to differ in sign class.  Neighbours outside the stored grid hold no sample any
-// cell of this slab reads (clamped to the brick itself).  All fourteen class bytes are loaded
-// before any is used: a lookup behind the previous one's branches would wait on its own.
-__device__ __forceinline__ uint32_t brick_fill_class(const GridDesc& g, const BrickGrid& bg, const BrickGrid& cg,
-                                                     const uint8_t* __restrict__ ccls, const uint8_t* __restrict__ cls,
-                                                     int bx, int by, int bz, uint32_t& own_class) {
-    const int X[7] = {bx, bx > 0 ? bx - 1 : bx, bx + 1 < bg.nbx ? bx + 1 : bx, bx, bx, bx, bx};
-    const int Y[7] = {by, by, by, by > 0 ? by - 1 : by, by + 1 < bg.nby ? by + 1 : by, by, by};
-    const int Z[7] = {bz, bz, bz, bz, bz, bz > 0 ? bz - 1 : bz, bz + 1 < bg.nbz ? bz + 1 : bz};
-    uint8_t c[7], r[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        c[k] = ccls[X[k] + Y[k] * cg.nbx + (Z[k] / kCZ) * cg.nbx * cg.nby];
-        r[k] = cls[X[k] + Y[k] * bg.nbx + Z[k] * bg.nbx * bg.nby];   // stale unless the box is mixed
-    }
-    uint32_t n[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) n[k] = brick_class_of(g, c[k], r[k], X[k], Y[k], Z[k]);
-    own_class = n[0];
-    if ((n[0] & 3u) == kBrickMixed || (n[0] & kBrickNoFill)) return kBrickMixed;
-    const uint32_t cc = n[0] & 3u;
-    bool same = true;
-#pragma unroll
-    for (int k = 1; k < 7; ++k) same &= (n[k] & 3u) == cc;
-    return same ? cc : (uint32_t)kBrickMixed;
-}
+// The neighbour rule (k_brick_fill, eval.hip): a brick needs exact values only if one of its
+// samples can be the end of a sign-changing cell edge.  Edges are axis aligned, so that requires the
+// brick or a face neighbour to differ in sign class.  Neighbours outside the stored grid hold no
+// sample any cell of this slab reads (clamped to the brick itself).
 
 // Coarse pass: one thread per coarse box -> modes, sign class; mixed boxes are listed.
 // IvEval: Iv operator()(Box p, uint64_t modes_in, uint64_t& modes) const.

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __rest
 }
 
 // Per brick: its class (inherited from a sign-definite coarse box, or refined), the neighbour rule
-// (brick_fill_class), fill[b] = class | fill class << 4, and either the constant sign pieces of a
+// (brick_modes.hpp), fill[b] = class | fill class << 4, and either the constant sign pieces of a
 // sign-filled brick or an entry in the list of bricks to evaluate (with its modes, so the eval
 // kernel reads them in list order).  List appends are aggregated per block: one atomic per
 // block (same-address atomics serialise: a wave-level append measured +30 us).
@@ -109,22 +109,60 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
                                                            uint32_t* __restrict__ ccount_reset,
                                                            uint32_t* __restrict__ umark, uint32_t mark_id) {
     __shared__ uint32_t wcnt[kFillBlock / 64], wbase[kFillBlock / 64];
+    __shared__ uint8_t s_cls[kFillBlock];   // the block's bricks' classes (its x / y neighbours mostly)
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // the refine pass has read it; kept in [14] for stats
         ccount_reset[1] = ccount_reset[0];
         ccount_reset[0] = 0u;
     }
-    const int b = blockIdx.x * kFillBlock + threadIdx.x;
+    const int b0 = blockIdx.x * kFillBlock, b = b0 + threadIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t fc = kBrickMixed;
     int bx = 0, by = 0, bz = 0, cb = 0;
     const bool valid = b < bg.n_bricks;
+    // the neighbour rule (brick_modes.hpp): the brick and its six face neighbours share a definite
+    // class.  Its own and its z neighbours' class bytes (other brick layers) are loaded together;
+    // x / y neighbours come from LDS when they belong to this block.  Neighbours outside the grid
+    // are the brick itself.
+    uint32_t own = kBrickMixed;
+    int zl = 0, zh = 0;
+    uint8_t czl = 0, rzl = 0, czh = 0, rzh = 0;
+    const int plane = bg.nbx * bg.nby, cplane = cg.nbx * cg.nby;
     if (valid) {
         brick_of(b, bg, bx, by, bz);
-        cb = bx + by * cg.nbx + (bz / kCZ) * cg.nbx * cg.nby;
-        uint32_t c;
-        fc = brick_fill_class(g, bg, cg, ccls, cls, bx, by, bz, c);
+        cb = bx + by * cg.nbx + (bz / kCZ) * cplane;
+        zl = bz > 0 ? bz - 1 : bz;
+        zh = bz + 1 < bg.nbz ? bz + 1 : bz;
+        const uint8_t c0 = ccls[cb], r0 = cls[b];
+        czl = ccls[bx + by * cg.nbx + (zl / kCZ) * cplane];
+        rzl = cls[b + (zl - bz) * plane];
+        czh = ccls[bx + by * cg.nbx + (zh / kCZ) * cplane];
+        rzh = cls[b + (zh - bz) * plane];
+        own = brick_class_of(g, c0, r0, bx, by, bz);
+    }
+    s_cls[threadIdx.x] = (uint8_t)own;
+    __syncthreads();
+    if (valid) {
+        const int nx[4] = {bx > 0 ? bx - 1 : bx, bx + 1 < bg.nbx ? bx + 1 : bx, bx, bx};
+        const int ny[4] = {by, by, by > 0 ? by - 1 : by, by + 1 < bg.nby ? by + 1 : by};
+        uint32_t n[6];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int bn = b + (nx[k] - bx) + (ny[k] - by) * bg.nbx, tn = bn - b0;
+            n[k] = (tn >= 0 && tn < kFillBlock)
+                       ? (uint32_t)s_cls[tn]
+                       : brick_class_of(g, ccls[nx[k] + ny[k] * cg.nbx + (bz / kCZ) * cplane], cls[bn], nx[k], ny[k], bz);
+        }
+        n[4] = brick_class_of(g, czl, rzl, bx, by, zl);
+        n[5] = brick_class_of(g, czh, rzh, bx, by, zh);
+        fc = kBrickMixed;
+        if ((own & 3u) != kBrickMixed && !(own & kBrickNoFill)) {
+            bool same = true;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) same &= (n[k] & 3u) == (own & 3u);
+            if (same) fc = own & 3u;
+        }
         if (!sign_fill) fc = kBrickMixed;
-        fill[b] = (uint8_t)(c | (fc << 4));
+        fill[b] = (uint8_t)(own | (fc << 4));
     }
     const bool eval = valid && fc == kBrickMixed;
     const uint64_t mask = __ballot(eval);
