@@ -103,7 +103,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 //   -> unit_cnt[64 group + k] = k-th non-empty unit of the group {unit in group, own / tri / act
 //      exclusive bases in the group}; scan_blk[c][group] = the group's sums (own, tri, act, halo
 //      own, non-empty units), read by k_unit_scan.
-__global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+__global__ __launch_bounds__(512) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ uint32_t s_u[kGroupUnits][4];
     __shared__ uint8_t s_fu[kGroupUnits];   // the group's candidate units, in order
     __shared__ uint32_t s_nf;
@@ -122,9 +122,9 @@ __global__ __launch_bounds__(1024) void k_mc_count(const CaseInfo* __restrict__ 
         if (t == 0) s_nf = (uint32_t)__popcll((unsigned long long)m);
     }
     __syncthreads();
-    // a lane's items are loaded together (kCountBatch at a time), then counted: one memory round
-    // trip per batch instead of one per item
-    constexpr int kCountBatch = 3;
+    // a lane's items are loaded kCountBatch at a time, then counted (1 with 512-lane blocks: 14.8 us
+    // at 512^3; 3 items with 1024 lanes: 24.5 us; 1 with 1024: 16.4; 1 with 256: 15.7)
+    constexpr int kCountBatch = 1;
     const int per_unit = kUnitRows * nch;
     const int n_items = (int)s_nf * per_unit;
     for (int i0 = t; i0 < n_items; i0 += kCountBatch * nt_) {
@@ -302,10 +302,10 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
 void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
     const int64_t ng = n_groups(g);
     if (ng == 0) return;
-    // one lane per item of a group (kGroupUnits kUnitRows rows x nch chunks), whole waves, <= 1024
-    // (256-lane blocks with 9 items per lane measured slower: 34 vs 28 us at 512^3)
+    // lanes over the items of a group (kGroupUnits kUnitRows rows x nch chunks), whole waves, at
+    // most 512: twice the resident groups of 1024-lane blocks
     const int items = kGroupUnits * kUnitRows * ((g.m + 63) / 64);
-    const unsigned threads = (unsigned)std::min(1024, (items + 63) / 64 * 64);
+    const unsigned threads = (unsigned)std::min(512, (items + 63) / 64 * 64);
     k_mc_count<<<(unsigned)ng, threads, 0, s>>>(d_cases, g, b);
 }
 
