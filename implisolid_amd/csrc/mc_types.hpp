@@ -21,7 +21,7 @@ static_assert(sizeof(CaseInfo) == 32, "CaseInfo layout");
 constexpr int kUnitRows = 4;
 constexpr int kGroupUnits = 64;        // units per group: one count block; the group scan's element
 constexpr int kVertsWaves = 4;         // waves per verts block (grid-stride over the unit list)
-constexpr int kVertsMaxBlocks = 2048;  // verts grid: ~ the resident waves of the chip
+constexpr int kVertsMaxBlocks = 4096;  // cells grid cap (2048: +1 us at 512^3)
 constexpr int kScanParts = 5;          // group sums scanned: own, tri, act, halo own, unit parts
 // A non-empty unit with many active cells is handed to several waves ("parts"): part p of P takes
 // the unit's 64-cell windows w with w % P == p (the other windows only advance its bases).
