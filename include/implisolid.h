@@ -154,8 +154,8 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
  * count / emit calls; kernel_times blocks and returns milliseconds of the last timed calls for
  * [brick pass, field eval, MC count, unit scan, vertex emission, face emission] */
 int implisolid_slab_set_timing(implisolid_slab* s, int on);
-/* after count: [units, active units, owned vertices (incl. halo), triangles, active cells,
- * halo-owned vertices, cells, 0] (blocking) */
+/* after count: [units, non-empty units, owned vertices (incl. halo), triangles, active cells,
+ * halo-owned vertices, cells, mixed coarse boxes of the last eval] (blocking) */
 int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]);
 /* 1 if the slab's last eval ran the JIT-compiled tree kernel, 0 if the interpreter */
 int implisolid_slab_used_jit(implisolid_slab* s);
