@@ -318,10 +318,11 @@ void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t*
         static_cast<sign_piece_t*>(d_signs), d_count - kBrickListWord + kCoarseListWord, d_umark, mark_id);
 }
 
-unsigned eval_bricks_grid(const GridDesc& g) {
+unsigned eval_bricks_grid(const GridDesc& g) {   // blocks of kEvalBlock lanes, one brick per wave
     const int nb = brick_grid(g).n_bricks;
-    const unsigned want = (unsigned)((nb + 3) / 4);
-    return want < 4096u ? (want ? want : 1u) : 4096u;   // grid-stride over the list
+    const unsigned wpb = kEvalBlock / 64, cap = 16384u / wpb;
+    const unsigned want = (unsigned)((nb + wpb - 1) / wpb);
+    return want < cap ? (want ? want : 1u) : cap;   // grid-stride over the list
 }
 
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
@@ -331,10 +332,10 @@ void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
     const unsigned eb = eval_bricks_grid(g);
-    if (depth <= 4) k_eval_field_pruned<4><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
-    else if (depth <= 8) k_eval_field_pruned<8><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
-    else if (depth <= 12) k_eval_field_pruned<12><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
-    else k_eval_field_pruned<16><<<eb, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    if (depth <= 4) k_eval_field_pruned<4><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    else if (depth <= 8) k_eval_field_pruned<8><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    else if (depth <= 12) k_eval_field_pruned<12><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    else k_eval_field_pruned<16><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
 }
 
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,

@@ -58,8 +58,9 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
     const int layers = g.fz1 - g.fz0;
     const size_t plane = (size_t)n * n;
     const int row_pieces = (64 / kBX) * sign_row_words(g);
-    const uint32_t stride = gridDim.x * 4;
-    uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint32_t wpb = blockDim.x >> 6;   // waves per block
+    const uint32_t stride = gridDim.x * wpb;
+    uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
     // the next brick's list entry and modes are loaded while this brick is evaluated
     uint32_t b_next = i < nb ? list[i] : 0u;
     uint64_t m_next = i < nb ? modes[i] : 0ull;

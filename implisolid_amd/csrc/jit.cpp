@@ -1,5 +1,6 @@
 // jit.cpp -- code generation and hipRTC compilation of tree kernels (see jit.hpp).
 #include "jit.hpp"
+#include "kernels.hpp"
 
 #include <hip/hiprtc.h>
 
@@ -443,7 +444,7 @@ void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* 
     BrickGrid bb = bg;
     void* args[] = {(void*)&d_mats, (void*)&d_rabbit, (void*)&gg, (void*)&bb, (void*)&d_modes,
                     (void*)&d_list, (void*)&d_count, (void*)&d_field, (void*)&d_signs};
-    if (hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, args, nullptr) != hipSuccess)
+    if (hipModuleLaunchKernel(fn, blocks, 1, 1, kEvalBlock, 1, 1, 0, s, args, nullptr) != hipSuccess)
         throw std::runtime_error("hipModuleLaunchKernel(impli_eval_bricks) failed");
 }
 

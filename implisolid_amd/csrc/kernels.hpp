@@ -33,6 +33,7 @@ void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t*
                        const uint64_t* d_modes, int sign_fill, uint8_t* d_fill, uint32_t* d_list, uint64_t* d_lmodes,
                        uint32_t* d_count, void* d_signs, uint32_t* d_umark, uint32_t mark_id, hipStream_t s);
 // K1c (interpreter): the listed bricks; the JIT variant is TreeJit::launch_bricks (jit.hpp)
+constexpr int kEvalBlock = 256;   // lanes per block of the brick eval kernels
 unsigned eval_bricks_grid(const GridDesc& g);
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint32_t* d_list, const uint32_t* d_count,
