@@ -275,7 +275,11 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
     if (b.gathered)
         for (int r = 0; r < b.rank; ++r) Voff += b.gathered[4 * r] - b.gathered[4 * r + 3];
     const uint32_t* __restrict__ vid3 = b.vid3;
-    for (uint32_t i = blockIdx.x * 256 + t; i < lim; i += gridDim.x * 256) {
+    // XCD-aware: the dispatcher puts block b on XCD b % 8, so XCD x takes the x-th eighth of the
+    // records (cell order): the owner cells a face gathers from stay in that XCD's L2
+    const uint32_t nb = gridDim.x, lb = (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u;
+    const uint32_t per = (lim + nb - 1u) / nb, i_end = min(lim, (lb + 1u) * per);
+    for (uint32_t i = lb * per + t; i < i_end; i += 256) {
         const uint4 r = b.records[i];
         const uint32_t L = r.x, ci = r.y, fbase = r.z;
         const CaseInfo& C = s_case[ci];
