@@ -399,10 +399,11 @@ class Slab:
 
     def stats(self):
         """After count(): units, non-empty units, owned vertices, triangles, active cells, halo-owned,
-        cells, mixed coarse boxes."""
-        out = (ctypes.c_int64 * 8)()
+        cells, mixed coarse boxes, halo-owned as the vertex pass reads it, unit parts."""
+        out = (ctypes.c_int64 * 10)()
         self._rc(lib().implisolid_slab_stats(self.h, out))
-        keys = ["units", "nonempty_units", "own", "tri", "act", "halo_own", "cells", "mixed_coarse_boxes"]
+        keys = ["units", "nonempty_units", "own", "tri", "act", "halo_own", "cells", "mixed_coarse_boxes",
+                "halo_own_verts_pass", "unit_parts"]
         return dict(zip(keys, [int(x) for x in out]))
 
     def used_jit(self):

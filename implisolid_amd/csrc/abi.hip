@@ -474,7 +474,7 @@ float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
 int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
 float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
 
-int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {
+int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]) {
     try {
         uint32_t c[16];
         s->engine.raw_counters(c, 0);
@@ -487,6 +487,8 @@ int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {
         out[5] = c[5];
         out[6] = g.n_cells;
         out[7] = c[14];   // mixed coarse boxes of the last eval (the fill kernel's copy of [13])
+        out[8] = c[1];    // the vertex pass's copy of the halo count (mc_types.hpp counters)
+        out[9] = c[0];    // unit parts
     } catch (const std::exception& e) {
         report(e.what(), false);
         return -1;

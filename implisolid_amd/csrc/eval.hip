@@ -83,7 +83,7 @@ struct InterpEval {   // the node-program interpreter with per-brick operand ski
 };
 
 template <int D>
-__global__ __launch_bounds__(256) void k_eval_field_pruned(const Program* __restrict__ prog,
+__global__ __launch_bounds__(kEvalBlock) void k_eval_field_pruned(const Program* __restrict__ prog,
                                                            const float* __restrict__ tab, GridDesc g, BrickGrid bg,
                                                            const uint64_t* __restrict__ modes,
                                                            const uint32_t* __restrict__ list,

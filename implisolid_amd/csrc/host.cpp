@@ -458,15 +458,26 @@ Program compile_mp5(const char* shape_json, bool ignore_root_matrix) {
     return compile_mp5(d, ignore_root_matrix);
 }
 
+SlabRange slab_range(int R, int z0, int z1) {
+    const int layers = (R + 5) - 3;   // cell layers 1 .. res-3
+    if (R < 1 || z0 < 1 || z1 <= z0 || z1 > layers + 1) throw InputError("slab_range: bad layer range");
+    SlabRange r{z0, z1, z0 > 1 ? 1 : 0};
+    // 32-bit indexing of one slab (mc_types.hpp / mc_device.hpp): the cell id L of a slab's cells
+    // (halo layer included) is a uint32, and so are vertex ids, face rows and the MC counters.
+    const int64_t m = (int64_t)R + 2, cells = m * m * (int64_t)(z1 - z0 + r.halo);
+    if (cells >= (int64_t)1 << 32)
+        throw InputError("slab of " + std::to_string(cells) + " cells exceeds the 2^32-cell limit of one slab (R = " +
+                         std::to_string(R) + "): split the grid over more Z-slabs");
+    return r;
+}
+
 SlabRange slab_partition(int R, int rank, int nranks) {
     if (R < 1 || nranks < 1 || rank < 0 || rank >= nranks) throw InputError("slab_partition: bad arguments");
     const int layers = (R + 5) - 3;   // cell layers 1 .. res-3
+    if (nranks > layers) throw InputError("slab_partition: more slabs than cell layers");
     const int base = layers / nranks, extra = layers % nranks;
-    SlabRange r;
-    r.z0 = 1 + rank * base + (rank < extra ? rank : extra);
-    r.z1 = r.z0 + base + (rank < extra ? 1 : 0);
-    r.halo = (rank > 0) ? 1 : 0;
-    return r;
+    const int z0 = 1 + rank * base + (rank < extra ? rank : extra);
+    return slab_range(R, z0, z0 + base + (rank < extra ? 1 : 0));
 }
 
 void GlibcRand::seed_(unsigned seed) {   // srandom_r (random_r.c:161-196)

@@ -41,6 +41,8 @@ Program compile_mp5(const Json& shape, bool ignore_root_matrix);
 // layers [z0, z1) and recomputes `halo` (0 or 1) layer below z0 (owner rule).
 struct SlabRange { int z0, z1, halo; };
 SlabRange slab_partition(int R, int rank, int nranks);
+// the slab of cell layers [z0, z1); throws if its cells overflow the kernels' 32-bit cell ids
+SlabRange slab_range(int R, int z0, int z1);
 
 // glibc rand() / srand() restated (stdlib/random_r.c, TYPE_3: additive feedback
 // x_n = x_{n-3} + x_{n-31} mod 2^32, output x_n >> 1; state seeded by the 16807 LCG, 310 outputs

@@ -299,7 +299,7 @@ std::string TreeJit::kernel_source(const Program& p) {
       << "    __device__ __forceinline__ Iv operator()(Box p, uint64_t mi, uint64_t& m) const {\n"
       << "        return tree_iv(M, tab, tab_range, p, mi, m);\n    }\n};\n"
       << "}  // namespace impli\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void impli_eval_bricks(\n"
+      << "extern \"C\" __global__ __launch_bounds__(" << kEvalBlock << ") void impli_eval_bricks(\n"
       << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
       << "    const uint32_t* list, const uint32_t* count, float* field, void* signs) {\n"
       << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, list, count, field, signs);\n}\n"

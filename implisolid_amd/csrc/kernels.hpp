@@ -34,6 +34,8 @@ void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t*
                        uint32_t* d_count, void* d_signs, uint32_t* d_umark, uint32_t mark_id, hipStream_t s);
 // K1c (interpreter): the listed bricks; the JIT variant is TreeJit::launch_bricks (jit.hpp)
 constexpr int kEvalBlock = 256;   // lanes per block of the brick eval kernels
+// whole waves (a partial wave would share the next block's brick index), within __launch_bounds__
+static_assert(kEvalBlock % 64 == 0 && kEvalBlock <= 256, "kEvalBlock: whole waves, at most 256 lanes");
 unsigned eval_bricks_grid(const GridDesc& g);
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint32_t* d_list, const uint32_t* d_count,

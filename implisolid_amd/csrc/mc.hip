@@ -242,7 +242,8 @@ __global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers 
         b.counters[2] = s_base[0] + b.scan_blk[G];                // owned vertices incl. halo
         b.counters[3] = s_base[1] + b.scan_blk[ng + G];           // triangles
         b.counters[4] = s_base[2] + b.scan_blk[2 * ng + G];       // active cells (face records)
-        b.counters[5] = s_base[3] + b.scan_blk[3 * ng + G];
+        b.counters[5] = s_base[3] + b.scan_blk[3 * ng + G];       // = [1]: [2, 6) is the totals block
+                                                                  // copy_counts / read_counts take whole
         b.counters[6] = s_base[5] + nne;                          // non-empty units (statistics)
     }
 }
@@ -256,6 +257,10 @@ __constant__ int8_t c_edge_owner[12][4] = {
     {0, 1, 1, 1}, {0, 0, 1, 0}, {0, 0, 1, 1}, {1, 0, 1, 0}, {0, 1, 0, 1}, {0, 0, 0, 0},
     {0, 0, 0, 1}, {1, 0, 0, 0}, {1, 1, 0, 2}, {0, 1, 0, 2}, {0, 0, 0, 2}, {1, 0, 0, 2},
 };
+
+// The face grid: the XCD remap below is a permutation of the blocks only when it is a multiple of 8.
+constexpr unsigned kFacesBlocks = 2048;
+static_assert(kFacesBlocks % 8 == 0, "k_mc_faces' XCD remap needs a multiple of 8 blocks");
 
 __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ CaseInfo s_case[256];
@@ -319,7 +324,7 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
 }
 
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {
-    k_mc_faces<<<2048, 256, 0, s>>>(d_cases, g, b);
+    k_mc_faces<<<kFacesBlocks, 256, 0, s>>>(d_cases, g, b);
 }
 
 void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s) {

@@ -6,10 +6,6 @@
 
 namespace impli {
 
-// stored sample (sx, sy, sz) -- sample indices in [1, res-2], the sealed ring included
-__device__ __forceinline__ int sample_index(const GridDesc& g, int sx, int sy, int sz) {
-    return (sx - 1) + (sy - 1) * g.n + (sz - g.fz0) * g.n * g.n;   // the field is < 2^31 elements
-}
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T x, int lane) {
 #pragma unroll
@@ -31,7 +27,7 @@ struct ChunkBits {
 __device__ __forceinline__ void load_chunk(const GridDesc& g, const uint64_t* __restrict__ signs, int64_t row, int c,
                                            ChunkBits& k) {
     const int rw = sign_row_words(g);
-    const int r32 = (int)row;   // rows of a slab: m x layers < 2^31 (32-bit division)
+    const int r32 = (int)row;   // rows of a slab: m x layers < 2^31 (cells < 2^32, slab_range)
     k.y = r32 % g.m + 1;
     k.z = r32 / g.m + g.cz0;
     k.x0 = 64 * c + 1;

@@ -38,7 +38,8 @@ struct MCBuffers {
     uint32_t* upart;         // ... part index | part count << 8 (k_unit_scan)
     const uint32_t* umark;   // units whose cells touch an evaluated brick hold mark_id (k_brick_fill);
     uint32_t mark_id;        // null: every unit is counted (dense eval)
-    uint32_t* counters;      // [0] unit parts, [1] halo own, [2..5] totals own/tri/act/halo, [6] non-empty units
+    uint32_t* counters;      // [0] unit parts, [1] halo own (read by the vertex pass), [2..5] totals
+                             // own/tri/act/halo (copied as one block; [5] == [1]), [6] non-empty units
     uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
     uint4* records;          // active cells: {L, ci, fbase, 0}
     float* verts;            // 3 * cap_v

@@ -155,8 +155,9 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
  * [brick pass, field eval, MC count, unit scan, vertex emission, face emission] */
 int implisolid_slab_set_timing(implisolid_slab* s, int on);
 /* after count: [units, non-empty units, owned vertices (incl. halo), triangles, active cells,
- * halo-owned vertices, cells, mixed coarse boxes of the last eval] (blocking) */
-int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]);
+ * halo-owned vertices, cells, mixed coarse boxes of the last eval, halo-owned vertices as the
+ * vertex pass reads them (counter word 1, must equal [5]), unit parts] (blocking) */
+int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]);
 /* 1 if the slab's last eval ran the JIT-compiled tree kernel, 0 if the interpreter */
 int implisolid_slab_used_jit(implisolid_slab* s);
 /* process-wide: compile tree kernels with hipRTC for objects set from now on (default on;

@@ -15,6 +15,14 @@
  *  - make_edge_lookup (mesh_algorithms.hpp:50-110) inserts its long key through pair<int,int>, so
  *    keys >= 2^31 (meshes with more than ~53k faces) are truncated and never found again, which
  *    leads to out-of-bounds writes.  We implement the intended lookup (first/last face per edge).
+ *  - the same function stores the int edge id in edges_of_faces, a multi_array of short_edge_type
+ *    = short int (basic_data_structures.hpp:196-197; mesh_algorithms.hpp:92,100).  Edge ids >= 2^15
+ *    wrap: ids 32768..65535 become negative, 65536..98303 alias edges 0..32767, and so on.
+ *    build_faces_of_faces (mesh_algorithms.hpp:111-131) then indexes faces_of_edges with the wrapped
+ *    id -- an out-of-bounds read (negative) or another edge's faces (aliased).  Any mesh with more
+ *    than 32767 edges, i.e. F > 21845 faces, is affected (config 2 at R = 128: F = 113 360; config 3
+ *    at R = 256: F = 179 656).  We keep the full int edge id.  OB02 parity for such meshes is parity
+ *    against the reference's intended semantics, not against what its binary would compute.
  *  - compute_average_edge_length starts from an uninitialised float (centroids_projection.cpp:72);
  *    we start from 0.
  *  - create_directions_bundle slices alpha_list_full.begin()+10 even when the list is shorter

@@ -376,6 +376,19 @@ def test_slab_partition_covers_all_layers(impli):
             assert [h for (_, _, h) in parts] == [0] + [1] * (n - 1)
 
 
+def test_slab_32bit_cell_limit(impli):
+    """A slab's cell ids, vertex ids and face rows are 32-bit: one slab may hold < 2^32 cells
+    (halo layer included).  R = 1623 fits one GPU (1625^3 cells); R = 1624 and R = 2000 must be
+    split, and 2 slabs of R = 2000 (2002^2 x 1002 cells each) fit."""
+    assert impli.slab_partition(1623, 0, 1) == (1, 1626, 0)
+    for R in (1624, 2000):
+        with pytest.raises(impli.ImplisolidError, match="2\\^32"):
+            impli.slab_partition(R, 0, 1)
+    assert impli.slab_partition(2000, 1, 2)[2] == 1
+    with pytest.raises(impli.ImplisolidError):
+        impli.slab_partition(2000, 0, 3000)   # more slabs than layers
+
+
 # ---- multi-rank numbering exchange (gloo, CPU) -----------------------------------------------------
 def _slab_counts(codes, faces_cell_z, R, z0, z1, halo):
     """counts int32[4] a rank's Slab.count() produces: own vertices incl. halo, faces, -, halo."""
@@ -491,3 +504,15 @@ def test_jit_tree_kernels_compile_for_gfx950(impli):
         n, secs, src = impli.jit_compile(shape)
         assert n > 1000 and "impli_eval_bricks" in src, src[:500]
         assert "impli_coarse_modes" in src and "impli_brick_refine" in src
+
+
+def test_headline_summary_oracle_regression(oracle):
+    """The cheapest headline fixture (config 2, R 128, 3 OB02 repeats; tests/golden/make_headline.py)
+    still reproduces from the oracle -- the GPU tests compare against these summaries."""
+    import hashlib
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "headline_summaries.json")))
+    s = d["config2_ob02_r128"]
+    v, f = oracle.polygonize(json.dumps(s["shape"]), json.dumps(s["mc"]))
+    assert (len(v), len(f)) == (s["n_verts"], s["n_faces"])
+    assert hashlib.sha256(np.ascontiguousarray(f).tobytes()).hexdigest() == s["sha256_faces"]
+    assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"]

@@ -231,7 +231,7 @@ def test_zslab_split_identical(impli, oracle, nranks):
         counts.append(s.counts()[:2])
     voff = np.concatenate([[0], np.cumsum([c[0] for c in counts])])
     foff = np.concatenate([[0], np.cumsum([c[1] for c in counts])])
-    vs, fs = [], []
+    vs, fs, st = [], [], []
     for r, s in enumerate(slabs):
         s.set_offsets(int(voff[r]), int(foff[r]))
         s.emit()
@@ -240,11 +240,25 @@ def test_zslab_split_identical(impli, oracle, nranks):
         v, f = s.download(nv, nf)
         vs.append(v)
         fs.append(f)
+        st.append(s.stats())
         s.close()
     v = np.concatenate(vs)
     f = np.concatenate(fs)
     assert np.array_equal(f, ref_f)
     assert np.array_equal(v.view(np.uint32), ref_v.view(np.uint32))
+    # every counter slot: the halo count the vertex pass reads is the totals block's; the slabs'
+    # owned-minus-halo vertices, triangles and active cells add up to the oracle's mesh
+    for k, c in enumerate(st):
+        assert c["halo_own"] == c["halo_own_verts_pass"], k
+        assert (c["halo_own"] == 0) == (k == 0), k
+        assert c["unit_parts"] >= c["nonempty_units"] > 0, k
+    assert sum(c["own"] - c["halo_own"] for c in st) == len(ref_v)
+    assert sum(c["tri"] for c in st) == len(ref_f)
+    one = impli.Slab(shape, mc, 0, 1)
+    one.eval()
+    one.count()
+    assert sum(c["act"] for c in st) == one.stats()["act"]
+    one.close()
 
 
 @pytest.mark.parametrize("nranks", [2, 5])
@@ -550,3 +564,38 @@ def test_batch_stream_matches_oracle(impli, oracle):
                 vr, fr = oracle.marching_cubes(oracle.mp5_to_nodes(json.dumps(sh)), 56, [-1, 1] * 3)
                 assert np.array_equal(f, fr), (rep, i)
                 assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), (rep, i)
+
+
+# ---- the bench's own workloads at their full sizes (tests/golden/make_headline.py) -----------------
+_HEADLINE = None
+
+
+def _headline():
+    global _HEADLINE
+    if _HEADLINE is None:
+        _HEADLINE = (json.load(open(_golden("headline_summaries.json"))), np.load(_golden("headline_samples.npz")))
+    return _HEADLINE
+
+
+@pytest.mark.parametrize("name", ["config4_mc_r512", "config4_mc_r256", "config3_ob02_r256", "config2_ob02_r128"])
+def test_headline_against_oracle_summary(impli, name):
+    """The exact meshes bench.py times (config 4's tree at 512^3 and 256^3, eval + MC) and the OB02
+    legs it reports (config 3 at 256^3, config 2 at 128^3, 3 repeats of resample + project + QEM),
+    against the oracle's summaries: faces byte-identical (SHA-256); vertices bit-identical where the
+    tree has no twist, else every sampled row within the north star's 1e-5 and the finite-vertex
+    sum within 1e-5 per vertex; the reference's non-finite rows at the same rows."""
+    import hashlib
+    summ, samples = _headline()
+    s = summ[name]
+    v, f = impli.make_geometry(s["shape"], s["mc"])
+    assert (len(v), len(f)) == (s["n_verts"], s["n_faces"])
+    assert hashlib.sha256(np.ascontiguousarray(f).tobytes()).hexdigest() == s["sha256_faces"]
+    fin = np.isfinite(v).all(1)
+    assert np.flatnonzero(~fin).tolist() == s["nonfinite_rows"]
+    idx, vs = samples[name + "_idx"], samples[name + "_v"]
+    if not _has_twist(s["shape"]) or "_mc_" in name:   # MC vertices are bit-exact for every tree
+        assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"]
+    ok = np.isfinite(vs).all(1)
+    assert np.abs(v[idx][ok].astype(np.float64) - vs[ok]).max(initial=0.0) < 1e-5
+    tot = v[fin].astype(np.float64).sum(0)
+    assert np.abs(tot - np.array(s["finite_sum"])).max() < 1e-5 * max(1, fin.sum())
