@@ -6,13 +6,14 @@ config 3's seeded 21-node MP5 CSG tree at R = 512 over the box [-1, 1]^3.  One s
 evaluation of the (R+1)^3 stored samples + marching-cubes count / scan / vertex + face emission,
 with the mesh left resident in HBM (no host copy in the timed region).
 
-N > 1 (torchrun, one process per GPU, RCCL): the cell layers are split into Z-slabs.  Weak scaling
-(the default): the grid grows to R_N = R N^(1/3), so every rank's slab holds about R^3 voxels -- the
-one-GPU workload per GPU (R_8 = 1024: 1024 x 1024 x 128 per rank).  Each rank recomputes one halo
-cell layer below its slab; the only exchange is an all-gather of the per-slab (vertex, face) counts,
-which gives every rank its global numbering offsets on the device.  The result is byte-identical
-to one GPU (tests/).  The strong-scaling rate (the R grid itself over N ranks) is reported beside it
-("strong"); --strong makes it the headline value.
+N > 1 (torchrun, one process per GPU, RCCL): the cell layers are split into Z-slabs at balanced
+cuts (one interval pass of the whole grid, computed alike by every rank).  The headline is strong
+scaling of BASELINE config 4 -- the R = 512 grid over N GPUs.  Each rank recomputes one halo cell
+layer below its slab; the only exchange in the step is an all-gather of the per-slab (vertex, face)
+counts, overlapped with the vertex pass, which gives every rank its global numbering offsets on the
+device.  After the timed steps the mesh is gathered to rank 0 (distributed.gather_mesh, timed as
+"gather_ms") and checked against the oracle's summary of the same workload.  Weak scaling (the grid
+grown to R_N = R N^(1/3), ~R^3 voxels per rank) is reported beside it; --weak swaps the two.
 
 Prints ONE JSON line (rank 0).  Extra fields: per-kernel times from HIP events on the launch
 stream, the HBM roofline of the eval+MC kernel sequence (SURVEY.md 8d's algorithmic bytes), and
@@ -30,6 +31,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# kernel (profile short name) -> the engine's timed phase (Slab.KERNELS; tools/pmc_traffic.py)
+KERNEL_PHASE = {"impli_coarse_modes": "brick_modes", "impli_brick_refine": "brick_modes", "k_brick_fill": "brick_modes",
+                "impli_eval_bricks": "eval_field", "k_eval_field_pruned": "eval_field", "k_mc_count": "mc_count",
+                "k_unit_scan": "mc_scan", "k_mc_cells": "mc_verts", "k_mc_faces": "mc_faces"}
 
 # algorithmic FP ops per sample for one instruction of the node program
 OP_FLOPS = {"xform": 18, "csg": 2, 3: 9, 4: 45, 5: 24, 6: 20, 7: 24, 8: 14, 9: 12,
@@ -76,7 +81,27 @@ def cpu_baseline(shape, target_s=20.0):
     dt = time.perf_counter() - t0
     return {"value": R ** 3 / dt / 1e6, "unit": "Mvoxels/s", "cores": 1, "kind": "port",
             "sample": "oracle restatement (C, 1 thread) eval+MC of the same tree at %d^3 on this host (%.1f s, %d faces)"
-                      % (R, dt, f.shape[0])}, (R, v, f)
+                      % (R, dt, f.shape[0]), "host": host_info()}, (R, v, f)
+
+
+def host_info():
+    """The host the CPU baseline ran on: logical CPUs (nproc), the CPUs this process may use, and
+    the model name (lscpu) -- SURVEY.md 8d asks for the core count beside the one-thread figure."""
+    import subprocess
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except Exception:
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core"):
+                info[k.strip().lower().replace(" ", "_").replace("(s)", "s")] = v.strip()
+    except Exception:
+        pass
+    return info
 
 
 def mesh_parity(v, f, v_ref, f_ref):
@@ -95,6 +120,21 @@ def mesh_parity(v, f, v_ref, f_ref):
             out["nonfinite_ref_verts"] = int((~fin_ref).sum())
             out["nonfinite_rows_identical"] = bool(np.array_equal(fin, fin_ref))
     return out
+
+
+def headline_parity(name, v, f):
+    """The whole mesh against the oracle's committed summary of the same workload
+    (tests/golden/headline_summaries.json, made by tests/golden/make_headline.py), if there is one."""
+    import hashlib
+    path = os.path.join(ROOT, "tests", "golden", "headline_summaries.json")
+    try:
+        s = json.load(open(path))[name]
+    except Exception:
+        return {"checked": False, "why": "no oracle summary for " + name}
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+    return {"checked": True, "against": "oracle summary " + name, "verts": int(len(v)), "faces": int(len(f)),
+            "faces_identical": sha(f) == s["sha256_faces"], "verts_identical": sha(v) == s["sha256_verts"],
+            "max_abs_v_diff": 0.0 if sha(v) == s["sha256_verts"] else None}
 
 
 def copy_attainable(dev, nbytes=1 << 30, reps=10):
@@ -125,10 +165,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-256", action="store_true", help="do not also time R=256")
     ap.add_argument("--prune", type=int, default=None, help="pruning level 0/1/2 (default: library default 2)")
-    ap.add_argument("--strong", action="store_true", help="N > 1: the headline is strong scaling of the R grid")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: the headline is weak scaling (R N^(1/3)); default strong scaling of the R grid")
+    ap.add_argument("--equal-slabs", action="store_true", help="N > 1: equal-layer slabs instead of balanced cuts")
     ap.add_argument("--skip-config5", action="store_true", help="do not time the 64-object stream (config 5)")
     ap.add_argument("--config5-streams", type=int, default=8)
     ap.add_argument("--skip-ob02", action="store_true", help="do not time build_geometry with the OB02 loop")
+    ap.add_argument("--bake", type=int, default=None, help="1: tree modules with the matrices baked in (per object)")
     ap.add_argument("--graph", action="store_true",
                     help="N = 1: replay the step as a hipGraph (measured no faster than direct launches: "
                          "0.176 vs 0.172 ms at 512^3)")
@@ -142,6 +185,8 @@ def main():
 
     if args.prune is not None:
         I.set_pruning(args.prune)
+    if args.bake is not None:
+        I.set_jit_bake(bool(args.bake))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -160,9 +205,17 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
-    def run(R, steps, warmup, scene=None):
+    def run(R, steps, warmup, scene=None, gather=False):
         shape, mc = scene if scene is not None else scenes.config4(R)
-        slab = I.Slab(shape, mc, rank, world)
+        # N > 1: balanced Z-slab cuts from one interval pass of the whole grid, computed by every
+        # rank alike (no exchange; implisolid_slab_balance), unless --equal-slabs
+        cuts = None
+        t_cut = 0.0
+        if world > 1 and not args.equal_slabs:
+            t0 = time.perf_counter()
+            cuts = D.balanced_cuts(shape, mc, world)
+            t_cut = time.perf_counter() - t0
+        slab = I.Slab(shape, mc, rank, world, cuts=cuts)
         cnt = torch.zeros(4, dtype=torch.int32, device=dev)
         gath = torch.zeros(world, 4, dtype=torch.int32, device=dev)
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
@@ -186,7 +239,11 @@ def main():
                 slab.emit(0, sp)
             if e: e[3].record(stream)
 
-        # warmup (first call sizes the output buffers)
+        # warmup (first call sizes the output buffers); the tree module compiles in the background
+        # meanwhile (async JIT) -- wait for it, so the timed steps run the compiled kernels
+        for _ in range(max(1, warmup)):
+            step()
+        I.jit_wait()
         for _ in range(max(1, warmup)):
             step()
         nv, nf, grew = slab.counts(sp)
@@ -257,28 +314,54 @@ def main():
         kernel_ms = {k: float(np.mean([p[k] for p in per])) for k in per[0]}
         info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, kernel_ms=kernel_ms,
                     shape=shape, slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats(),
-                    graph=graph is not None,
+                    graph=graph is not None, cuts=cuts, cut_s=t_cut,
                     fz=(slab.fz0, slab.fz1), jit=slab.used_jit(), stats=slab.stats())
+        if world > 1:
+            # every rank's own step time (the max over ranks is the headline's): the balance
+            rt = torch.tensor([el], dtype=torch.float64, device=dev)
+            allt = [torch.zeros_like(rt) for _ in range(world)]
+            dist.all_gather(allt, rt)
+            info["rank_ms"] = [round(float(x.item()) / steps * 1e3, 4) for x in allt]
+        if gather and world > 1:
+            # the output gather to rank 0 (the C ABI's host-resident result; outside the timed step):
+            # then parity of the whole N-GPU mesh against the oracle's summary of the same workload
+            step()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            res = D.gather_mesh(slab, gath, rank, world)
+            info["gather_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+            if rank == 0:
+                info["parity"] = headline_parity("config4_mc_r%d" % R, *res)
         slab.close()
         return info
 
-    weak = world > 1 and not args.strong
-    R_main = int(round(args.resolution * world ** (1.0 / 3.0))) if weak else args.resolution
-    main_run = run(R_main, args.steps, args.warmup)
-    strong_run = run(args.resolution, args.steps, args.warmup) if weak else None
+    # N > 1: the headline is strong scaling of config 4 (the R grid over N GPUs, BASELINE config 4);
+    # weak scaling (R_N = R N^(1/3), ~R^3 voxels per rank) is reported beside it (--weak swaps them)
+    weak = world > 1 and args.weak
+    R_weak = int(round(args.resolution * world ** (1.0 / 3.0)))
+    main_run = run(R_weak if weak else args.resolution, args.steps, args.warmup, gather=not weak)
+    side_run = None
+    if world > 1:
+        side_run = run(args.resolution if weak else R_weak, args.steps, args.warmup)
     r256 = run(256, args.steps, args.warmup) if (not args.skip_256 and args.resolution != 256 and world == 1) else None
     # a dense-surface data point: config 2's scene (sphere u rabbit, ~1.5 M vertices) at the same R
     rdense = None if (args.skip_256 or world > 1) else run(args.resolution, args.steps, args.warmup,
                                            scene=(scenes.union_sphere_cube(), scenes.mc_settings(args.resolution, 1.0)))
 
     # config 5: a stream of 64 seeded random MP5 objects at 128^3, eval + MC, each object's
-    # pipeline captured once in a hipGraph and replayed (objects round-robin over a few streams)
-    c5 = None
-    if world == 1 and not args.skip_config5:
-        objs = scenes.config5_objects(64, 128)
-        t0 = time.perf_counter()
-        batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=args.config5_streams)
-        setup_s = time.perf_counter() - t0
+    # pipeline captured once in a hipGraph and replayed (objects round-robin over a few streams).
+    # Headline: the interpreter kernels (no per-object compilation, so nothing is left out of the
+    # rate); beside it the JIT tier, whose hipRTC time for the 64 shapes is reported and folded
+    # into an objects/s over one pass that includes it.
+    def run_batch(objs, jit_mode):
+        I.set_jit(jit_mode)
+        try:
+            t0 = time.perf_counter()
+            batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=args.config5_streams)
+            setup_s = time.perf_counter() - t0
+        finally:
+            I.set_jit(2)
         for _ in range(max(1, args.warmup)):
             batch.run(sp)
         torch.cuda.synchronize(dev)
@@ -294,12 +377,61 @@ def main():
                 raise RuntimeError("config 5: object %d overflowed" % i)
             tv, tf = tv + a, tf + b_
         ms5 = el / args.steps * 1e3
-        c5 = {"workload": "config5: 64 seeded random MP5 objects (scenes.config5_objects, 1-12 leaves) at 128^3, "
-                          "eval+MC, hipGraph per object, %d streams" % batch.n_streams,
-              "objects_per_s": round(batch.n / (ms5 * 1e-3), 1), "value": round(batch.n * 128 ** 3 / (ms5 * 1e-3) / 1e6, 2),
-              "unit": "Mvoxels/s", "ms_per_stream": round(ms5, 4), "graphs": batch.graphs,
-              "verts": tv, "faces": tf, "setup_s": round(setup_s, 2), "jit_compile_s": round(batch.jit_seconds, 2)}
+        res = {"objects_per_s": round(batch.n / (ms5 * 1e-3), 1), "value": round(batch.n * 128 ** 3 / (ms5 * 1e-3) / 1e6, 2),
+               "unit": "Mvoxels/s", "ms_per_stream": round(ms5, 4), "graphs": batch.graphs, "verts": tv, "faces": tf,
+               "setup_s": round(setup_s, 2), "jit_compile_s": round(batch.jit_seconds, 2),
+               "objects_per_s_incl_setup": round(batch.n / (ms5 * 1e-3 + setup_s), 1)}
+        n_streams = batch.n_streams
         batch.close()
+        return res, n_streams
+
+    c5 = None
+    if world == 1 and not args.skip_config5:
+        objs = scenes.config5_objects(64, 128)
+        c5, ns5 = run_batch(objs, 0)
+        c5["workload"] = ("config5: 64 seeded random MP5 objects (scenes.config5_objects, 1-12 leaves) at 128^3, eval+MC, "
+                          "interpreter kernels (no per-object compilation), hipGraph per object, %d streams" % ns5)
+        c5["jit"], _ = run_batch(objs, 1)
+
+    # First-call latency of a never-seen shape (async JIT: the interpreter kernels run at once, the
+    # module compiles in the background): build_geometry (eval + MC, host-resident result) of fresh
+    # random trees at R 32 and 128, against the oracle on one host core for the same call
+    first = None
+    if world == 1 and not args.skip_ob02:
+        import oracle
+        oracle.build()
+        first = {}
+        for k, Rf in enumerate((32, 128)):
+            shape = scenes.random_tree(990001 + k, 10)
+            mc = scenes.mc_settings(Rf, 1.0)
+            t0 = time.perf_counter()
+            v, f = I.make_geometry(shape, mc)
+            t_gpu = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+            t_cpu = time.perf_counter() - t0
+            first["r%d" % Rf] = {"gpu_first_call_ms": round(t_gpu * 1e3, 3), "cpu_oracle_ms": round(t_cpu * 1e3, 3),
+                                 "faces_identical": bool(np.array_equal(f, fr)),
+                                 "verts_identical": bool(np.array_equal(v.view(np.uint32), vr.view(np.uint32)))}
+        I.jit_wait()
+        first["jit"] = I.jit_stats()
+
+    # end-to-end build_geometry of the config-4 tree (eval + MC) through the C ABI,
+    # to a host-resident mesh (PCIe included), at 256^3 and 512^3 -- the reference's unit of work
+    e2e = None
+    if world == 1 and not args.skip_ob02:
+        e2e = {}
+        for Re in (256, 512):
+            shape, mc = scenes.config4(Re)
+            I.make_geometry(shape, mc)
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                v, f = I.make_geometry(shape, mc)
+                ts.append(time.perf_counter() - t0)
+            e2e["r%d" % Re] = {"build_geometry_ms": round(min(ts) * 1e3, 3), "median_ms": round(float(np.median(ts)) * 1e3, 3),
+                               "mvoxels_per_s": round(Re ** 3 / min(ts) / 1e6, 1), "verts": int(len(v)), "faces": int(len(f)),
+                               "parity": headline_parity("config4_mc_r%d" % Re, v, f)}
 
     # configs 2 and 3 through the C ABI: build_geometry (MC + 3 x [resample, project, QEM]) to a
     # host-resident mesh, PCIe included; the oracle times config 2 on one host core beside it
@@ -357,18 +489,55 @@ def main():
     b_pipe = (8.0 * (R + 1) ** 3 + 12.0 * nv + 12.0 * nf) / world
     t_kern = sum(kms.values()) * 1e-3
     dom = max(kern, key=kern.get)
-    traffic = None
-    # the newest committed PMC traffic summary (tools/profile_round.sh <tag> -> profiles/traffic_<tag>.json)
+    # the newest committed PMC summaries (tools/profile_round.sh <tag> -> profiles/traffic_<tag>.json,
+    # profiles/valu_<tag>.json), if they were taken on this workload
     import glob
-    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
-    tfile = tfiles[-1] if tfiles else None
-    if tfile:
+
+    def newest(pattern):
+        fs = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+        if not fs:
+            return None, None
         try:
-            tj = json.load(open(tfile))
-            if tj.get("workload_R") == R and tj.get("tree_seed") == scenes.CONFIG3_SEED:
-                traffic = tj.get("pipeline_bytes")
+            return os.path.basename(fs[-1]), json.load(open(fs[-1]))
         except Exception:
-            traffic = None
+            return None, None
+    tname, tj = newest("traffic_r*.json")
+    if not (tj and tj.get("workload_R") == R and tj.get("tree_seed") == scenes.CONFIG3_SEED):
+        tname, tj = None, None
+    vname, vj = newest("valu_r*.json")
+    traffic = tj.get("pipeline_bytes") if tj else None
+    phase_traffic = tj.get("phase_bytes", {}) if tj else {}
+    valu_phase = {}
+    if vj:
+        for k, v in vj.get("kernels", {}).items():
+            ph = KERNEL_PHASE.get(k)
+            if ph:   # the phase's busiest kernel
+                valu_phase[ph] = max(valu_phase.get(ph, 0.0), v["valu_busy"])
+    # Per-kernel roofline table (per launch, this slab): time from the engine's HIP events, HBM
+    # bytes from the PMC summary, achieved GB/s and fraction of the 8 TB/s peak, VALU busy.  The
+    # field kernel's algorithmic bytes (per evaluated sample: one 4 B store) use the
+    # samples it actually evaluates: the listed bricks x kBX kBY kBZ = 128 samples.
+    evaluated = (bricks_total - bricks_filled) * 128
+    alg_phase = {"eval_field": 4.0 * evaluated}
+    per_kernel = {}
+    for k, ms_k in kern.items():
+        row = {"ms": round(ms_k, 4)}
+        if k in phase_traffic:
+            row["traffic"] = phase_traffic[k]
+            row["achieved_gbs"] = round(phase_traffic[k] / (ms_k * 1e-3) / 1e9, 1)
+            row["frac"] = round(row["achieved_gbs"] / HBM_PEAK_GBS, 4)
+        if k in alg_phase:
+            row["alg_bytes"] = alg_phase[k]
+            row["alg_gbs"] = round(alg_phase[k] / (ms_k * 1e-3) / 1e9, 1)
+            row["alg_frac"] = round(row["alg_gbs"] / HBM_PEAK_GBS, 4)
+        if k in valu_phase:
+            row["valu_busy"] = valu_phase[k]
+        per_kernel[k] = row
+    # The pass: the counter-measured HBM bytes over the kernel sequence's time (what the hardware
+    # moved), next to SURVEY.md 8d's dense-equivalent bytes B = 8 (R+1)^3 + 12 V + 12 F (what a
+    # dense eval + MC would move; "effective").  No kernel is HBM-bound: the
+    # pass waits on memory round trips and dependency chains, hence bound = "latency".
+    achieved = traffic / t_kern / 1e9 if traffic else None
     out = {
         "metric": "Mvoxels/s (eval+MC) at 256^3 & 512^3",
         "value": round(value, 2),
@@ -386,7 +555,7 @@ def main():
             "workload": "config4: seeded ~20-node MP5 CSG tree with twist/union/difference (scenes.config4, seed 20251015), box [-1,1]^3, "
                         "R=%d, eval+MC, mesh resident in HBM%s" % (
                             R, (", weak scaling: R = %d N^(1/3), ~%d^3 voxels per rank" % (args.resolution, args.resolution))
-                            if weak else ""),
+                            if weak else (", strong scaling: the grid over %d balanced Z-slabs" % world) if world > 1 else ""),
             "resolution": R, "voxels": R ** 3, "samples": (R + 1) ** 3, "cells": (R + 2) ** 3,
             "verts": nv, "faces": nf, "program_instr": n_instr, "tree_depth": depth,
             "parallelism": "zslab%d" % world,
@@ -401,17 +570,31 @@ def main():
                    "mixed_coarse_boxes": main_run["stats"]["mixed_coarse_boxes"]},
         "mc": {"units": main_run["stats"]["units"], "nonempty_units": main_run["stats"]["nonempty_units"],
                "active_cells": main_run["stats"]["act"]},
-        "roofline": {"bound": "hbm", "kernel": "eval+MC kernel sequence (SURVEY.md 8d)",
-                     "achieved": round(b_pipe / t_kern / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(b_pipe / t_kern / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "roofline": {"bound": "latency", "kernel": "eval+MC kernel sequence (SURVEY.md 8d)",
+                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
+                     "traffic_source": tname, "valu_source": vname,
+                     "effective_achieved": round(b_pipe / t_kern / 1e9, 1),
+                     "effective_frac": round(b_pipe / t_kern / 1e9 / HBM_PEAK_GBS, 4),
                      "alg_bytes_per_launch": b_pipe, "launch_ms": round(t_kern * 1e3, 4),
-                     "dominant_kernel": dom,
+                     "dominant_kernel": dom, "dominant": dict(per_kernel[dom], kernel=dom),
+                     "per_kernel": per_kernel,
                      "kernel_share": {k: round(v / max(1e-9, sum(kern.values())), 3) for k, v in kern.items()}},
     }
-    if strong_run:
-        mss = strong_run["elapsed"] / args.steps * 1e3
-        out["strong"] = {"resolution": args.resolution, "value": round(args.resolution ** 3 / (mss * 1e-3) / 1e6, 2),
-                         "ms_per_step": round(mss, 4), "scaling": "strong"}
+    if world > 1:
+        out["slabs"] = {"cuts": main_run["cuts"], "balanced": main_run["cuts"] is not None,
+                        "cut_probe_s": round(main_run["cut_s"], 4), "rank_ms": main_run.get("rank_ms"),
+                        "max_over_min": round(max(main_run["rank_ms"]) / max(1e-9, min(main_run["rank_ms"])), 3)}
+        if "gather_ms" in main_run:
+            out["gather_ms"] = main_run["gather_ms"]
+        if "parity" in main_run:
+            out["parity"] = main_run["parity"]
+    if side_run:
+        mss = side_run["elapsed"] / args.steps * 1e3
+        out["strong" if weak else "weak"] = {
+            "resolution": side_run["R"], "value": round(side_run["R"] ** 3 / (mss * 1e-3) / 1e6, 2),
+            "ms_per_step": round(mss, 4), "scaling": "strong" if weak else "weak",
+            "rank_ms": side_run.get("rank_ms"), "cuts": side_run["cuts"]}
     if rdense:
         msd = rdense["elapsed"] / args.steps * 1e3
         out["value_union_scene"] = round(R ** 3 / (msd * 1e-3) / 1e6, 2)
@@ -426,6 +609,11 @@ def main():
         out["config5"] = c5
     if ob02:
         out["ob02"] = ob02
+    if e2e:
+        out["end_to_end"] = dict(e2e, workload="config4 tree, build_geometry (eval + MC) to host-resident verts/faces")
+    if first:
+        out["first_call"] = dict(first, workload="never-seen random 10-leaf trees, build_geometry eval+MC, "
+                                                 "async JIT (interpreter kernels on the first call)")
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], (Rs, v_ref, f_ref) = cpu_baseline(main_run["shape"])
         # the GPU mesh of the same tree at the sample's resolution against the oracle's

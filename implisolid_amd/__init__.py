@@ -35,6 +35,8 @@ ABI_SYMBOLS = [
     "implisolid_srand", "implisolid_rand", "implisolid_rand_skip",
     "implisolid_batch_create", "implisolid_batch_run", "implisolid_batch_info", "implisolid_batch_counts",
     "implisolid_batch_download", "implisolid_batch_destroy",
+    "implisolid_slab_create_range", "implisolid_slab_balance", "implisolid_cuts_from_layer_work", "implisolid_set_devices",
+    "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
 ]
 
 _lib = None
@@ -115,6 +117,14 @@ def lib():
         "implisolid_batch_counts": ([c_void_p, c_int, up], c_int),
         "implisolid_batch_download": ([c_void_p, c_int, fp, ip], c_int),
         "implisolid_batch_destroy": ([c_void_p], None),
+        "implisolid_slab_create_range": ([c_char_p, c_char_p, c_int, c_int], c_void_p),
+        "implisolid_slab_balance": ([c_char_p, c_char_p, c_int, ip], c_int),
+        "implisolid_cuts_from_layer_work": ([ctypes.POINTER(ctypes.c_int64), c_int, ctypes.c_int64, c_int, c_int, ip], c_int),
+        "implisolid_set_devices": ([ip, c_int], c_int),
+        "implisolid_slab_copy_mesh": ([c_void_p, c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, c_void_p], c_int),
+        "implisolid_set_jit_bake": ([c_int], None),
+        "implisolid_jit_wait": ([], None),
+        "implisolid_jit_stats": ([ip, ctypes.POINTER(ctypes.c_double)], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -161,9 +171,56 @@ def slab_partition(R, rank, nranks):
     return int(out[0]), int(out[1]), int(out[2])
 
 
-def set_jit(on):
-    """Compile tree kernels with hipRTC for objects set from now on (default on)."""
-    lib().implisolid_set_jit(1 if on else 0)
+def slab_balance(shape, mc_settings, nranks):
+    """Balanced Z-slab cuts [1, ..., R + 3] (nranks + 1 cell-layer boundaries) from one interval
+    pass of the whole grid on the current device; rank r owns layers [cuts[r], cuts[r + 1])."""
+    out = (ctypes.c_int32 * (int(nranks) + 1))()
+    if lib().implisolid_slab_balance(_s(shape), _s(mc_settings), int(nranks), out) != 0:
+        raise ImplisolidError(last_error())
+    return [int(x) for x in out]
+
+
+def cuts_from_layer_work(listed, bricks_per_layer, R, nranks):
+    """Host only: the balanced cuts from per-sample-layer listed-brick counts (R + 3 layers)."""
+    a = np.ascontiguousarray(listed, dtype=np.int64)
+    out = (ctypes.c_int32 * (int(nranks) + 1))()
+    if lib().implisolid_cuts_from_layer_work(a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(a),
+                                             int(bricks_per_layer), int(R), int(nranks), out) != 0:
+        raise ImplisolidError(last_error())
+    return [int(x) for x in out]
+
+
+def set_devices(ids):
+    """The HIP devices build_geometry's marching cubes runs on (balanced Z-slabs, slab r on
+    ids[r]; a device may repeat).  None or one device: the current device only."""
+    ids = list(ids or [])
+    arr = (ctypes.c_int32 * max(1, len(ids)))(*ids)
+    if lib().implisolid_set_devices(arr if ids else None, len(ids)) != 0:
+        raise ImplisolidError(last_error())
+
+
+def set_jit(mode):
+    """Tree-kernel JIT mode for objects set from now on: False/0 off (interpreter), True/1 sync
+    (compile before the first eval), 2 async (the library default: compile in the background, the
+    interpreter meanwhile)."""
+    lib().implisolid_set_jit(int(mode))
+
+
+def set_jit_bake(on):
+    """Bake each object's matrices into its tree module (one module per object) or not (per shape)."""
+    lib().implisolid_set_jit_bake(1 if on else 0)
+
+
+def jit_wait():
+    """Block until every scheduled tree-kernel compilation has finished."""
+    lib().implisolid_jit_wait()
+
+
+def jit_stats():
+    out = (ctypes.c_int32 * 4)()
+    secs = ctypes.c_double(0)
+    lib().implisolid_jit_stats(out, ctypes.byref(secs))
+    return {"mode": out[0], "bake": bool(out[1]), "compiled": out[2], "disk_hits": out[3], "compile_s": secs.value}
 
 
 def jit_compile(shape):
@@ -310,8 +367,15 @@ def program_info(shape, ignore_root_matrix=False):
 class Slab:
     """One Z-slab of one object on the current device.  Stream = a hipStream_t handle (int)."""
 
-    def __init__(self, shape, mc_settings, rank=0, nranks=1):
-        self.h = lib().implisolid_slab_create(_s(shape), _s(mc_settings), int(rank), int(nranks))
+    def __init__(self, shape, mc_settings, rank=0, nranks=1, cuts=None):
+        """cuts: nranks + 1 cell-layer boundaries (slab_balance) -- rank r takes [cuts[r], cuts[r+1]);
+        None: the equal-layer split (slab_partition)."""
+        if cuts is not None:
+            if len(cuts) != nranks + 1:
+                raise ImplisolidError("Slab: cuts must hold nranks + 1 boundaries")
+            self.h = lib().implisolid_slab_create_range(_s(shape), _s(mc_settings), int(cuts[rank]), int(cuts[rank + 1]))
+        else:
+            self.h = lib().implisolid_slab_create(_s(shape), _s(mc_settings), int(rank), int(nranks))
         if not self.h:
             raise ImplisolidError(last_error())
         g = (ctypes.c_int32 * 8)()
@@ -352,6 +416,11 @@ class Slab:
     def copy_counts(self, d_dst, stream=0):
         """async: counters [own incl. halo, faces, active, halo] -> device uint32[4] at d_dst"""
         self._rc(lib().implisolid_slab_copy_counts(self.h, ctypes.c_void_p(d_dst), ctypes.c_void_p(stream)))
+
+    def copy_mesh(self, d_verts, d_faces, nv, nf, stream=0):
+        """async device-to-device copy of the emitted mesh into caller-owned device buffers"""
+        self._rc(lib().implisolid_slab_copy_mesh(self.h, ctypes.c_void_p(d_verts or None), ctypes.c_void_p(d_faces or None),
+                                                 int(nv), int(nf), ctypes.c_void_p(stream)))
 
     def set_offsets(self, voff, foff):
         self._rc(lib().implisolid_slab_set_offsets(self.h, int(voff), int(foff)))

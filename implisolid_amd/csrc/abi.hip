@@ -57,6 +57,92 @@ hipStream_t abi_stream() {
     return s;
 }
 
+// ---- build_geometry over several devices (implisolid_set_devices) -------------------------------
+std::vector<int> g_devices;   // empty: the current device only
+
+struct DeviceGuard {          // restores the caller's current device
+    int prev = 0;
+    DeviceGuard() { (void)hipGetDevice(&prev); }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+struct SlabEngine {           // one slab's engine and stream on its device, kept across builds
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::unique_ptr<Engine> engine;
+    ~SlabEngine() {
+        if (stream) {
+            (void)hipSetDevice(device);
+            engine.reset();
+            (void)hipStreamDestroy(stream);
+        }
+    }
+};
+std::vector<std::unique_ptr<SlabEngine>> g_slab_engines;
+
+// polygonize_step_0 on g_devices: balanced cuts (cached per object and grid), every slab evaluated
+// and counted on its device concurrently, vertex / face offsets from the counts (host), emission,
+// and the slabs' meshes copied into the host result at their offsets -- byte-identical to one GPU.
+void multi_device_mc(const Program& prog, const MCSettings& st, std::vector<float>& verts, std::vector<int32_t>& faces) {
+    DeviceGuard guard;
+    const int n = (int)g_devices.size();
+    while ((int)g_slab_engines.size() < n) {
+        const int d = g_devices[g_slab_engines.size()];
+        IMPLI_HIP(hipSetDevice(d));
+        std::unique_ptr<SlabEngine> se(new SlabEngine());
+        se->device = d;
+        IMPLI_HIP(hipStreamCreateWithFlags(&se->stream, hipStreamNonBlocking));
+        se->engine.reset(new Engine());
+        g_slab_engines.push_back(std::move(se));
+    }
+    static std::string cut_key;
+    static std::vector<int> cuts;
+    std::string key((const char*)&prog, sizeof(Program));
+    key.append((const char*)&st.resolution, sizeof st.resolution).append((const char*)st.box, sizeof st.box);
+    key.append((const char*)&n, sizeof n);
+    if (key != cut_key) {
+        IMPLI_HIP(hipSetDevice(g_devices[0]));
+        cuts = balance_cuts(prog, st.resolution, st.box, n, g_slab_engines[0]->stream);
+        cut_key = key;
+    }
+    for (int r = 0; r < n; ++r) {   // eval + count, all devices in flight
+        SlabEngine& se = *g_slab_engines[(size_t)r];
+        IMPLI_HIP(hipSetDevice(se.device));
+        se.engine->set_object(prog);
+        se.engine->set_slab(st.resolution, st.box, SlabRange{cuts[(size_t)r], cuts[(size_t)r + 1], 0});
+        se.engine->eval_field(se.stream);
+        se.engine->count(se.stream);
+    }
+    std::vector<SlabCounts> c((size_t)n);
+    std::vector<int64_t> voff((size_t)n + 1, 0), foff((size_t)n + 1, 0);
+    for (int r = 0; r < n; ++r) {
+        SlabEngine& se = *g_slab_engines[(size_t)r];
+        IMPLI_HIP(hipSetDevice(se.device));
+        c[(size_t)r] = se.engine->read_counts(se.stream, nullptr);
+        se.engine->ensure_capacity(c[(size_t)r]);
+        voff[(size_t)r + 1] = voff[(size_t)r] + c[(size_t)r].n_verts();
+        foff[(size_t)r + 1] = foff[(size_t)r] + c[(size_t)r].n_faces();
+    }
+    if (voff[(size_t)n] >= ((int64_t)1 << 31) || foff[(size_t)n] >= ((int64_t)1 << 31))
+        throw InputError("build_geometry: the mesh exceeds 2^31 vertices or faces");
+    for (int r = 0; r < n; ++r) {
+        SlabEngine& se = *g_slab_engines[(size_t)r];
+        IMPLI_HIP(hipSetDevice(se.device));
+        se.engine->set_offsets((uint32_t)voff[(size_t)r], (uint32_t)foff[(size_t)r]);
+        se.engine->emit(nullptr, se.stream);
+    }
+    verts.resize((size_t)voff[(size_t)n] * 3);
+    faces.resize((size_t)foff[(size_t)n] * 3);
+    for (int r = 0; r < n; ++r) {
+        SlabEngine& se = *g_slab_engines[(size_t)r];
+        IMPLI_HIP(hipSetDevice(se.device));
+        bool of = false;
+        const SlabCounts cr = se.engine->read_counts(se.stream, &of);
+        if (of) throw HipError("build_geometry: slab output overflow after sizing");
+        se.engine->download(verts.data() + 3 * voff[(size_t)r], faces.data() + 3 * foff[(size_t)r], cr, se.stream);
+    }
+}
+
 void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.cpp:309-444
     if (g_state.active) {
         report("build_geometry() called in a bad state.", false);
@@ -66,13 +152,35 @@ void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.c
     Engine& E = engine();
     hipStream_t s = abi_stream();
     E.set_object(prog);
-    E.set_grid(st.resolution, st.box, 0, 1);
-    SlabCounts c = E.marching_cubes(s);   // polygonize_step_0
-    int64_t nv = c.n_verts(), nf = c.n_faces();
+    int64_t nv = 0, nf = 0;
     static std::unique_ptr<Ob02> ob_ptr;   // one refinement state, its buffers reused by every build
-    if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+    if (!g_devices.empty()) {
+        // polygonize_step_0 over several devices: balanced Z-slabs, concatenated on the host
+        multi_device_mc(prog, st, g_state.verts, g_state.faces);
+        nv = (int64_t)g_state.verts.size() / 3;
+        nf = (int64_t)g_state.faces.size() / 3;
+        const bool refine = st.overall_repeats > 0 && (st.vresampl_iters > 0 || st.projection || st.subdiv);
+        if (!refine) {
+            g_state.active = true;
+            return;
+        }
+        DevBuf& dv = E.scratch(8);
+        DevBuf& df = E.scratch(9);
+        dv.reserve((size_t)nv * 12 + 16);
+        df.reserve((size_t)nf * 12 + 16);
+        IMPLI_HIP(hipMemcpyAsync(dv.p, g_state.verts.data(), (size_t)nv * 12, hipMemcpyHostToDevice, s));
+        IMPLI_HIP(hipMemcpyAsync(df.p, g_state.faces.data(), (size_t)nf * 12, hipMemcpyHostToDevice, s));
+        if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+        ob_ptr->load_mesh(dv.as<float>(), nv, df.as<int32_t>(), nf);
+    } else {
+        E.set_grid(st.resolution, st.box, 0, 1);
+        SlabCounts c = E.marching_cubes(s);   // polygonize_step_0
+        nv = c.n_verts();
+        nf = c.n_faces();
+        if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+        ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf);
+    }
     Ob02& ob = *ob_ptr;
-    ob.load_mesh(E.d_verts(), nv, E.d_faces(), nf);
     for (int rep = 0; rep < st.overall_repeats; ++rep) {
         for (int i = 0; i < st.vresampl_iters; ++i) ob.vertex_resampling(st.vresampl_c);   // step 1
         if (st.projection) ob.centroids_projection(st.qem);                             // step 2
@@ -393,6 +501,68 @@ struct implisolid_slab {
     Engine engine;
 };
 
+implisolid_slab* implisolid_slab_create_range(const char* shape_json, const char* mc_json, int z0, int z1) {
+    g_last_error.clear();
+    try {
+        MCSettings st = parse_mc_settings(mc_json);
+        Program p = compile_mp5(shape_json, st.ignore_root_matrix);
+        auto* s = new implisolid_slab();
+        s->engine.set_object(p);
+        s->engine.set_slab(st.resolution, st.box, SlabRange{z0, z1, 0});
+        return s;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return nullptr;
+    }
+}
+
+int implisolid_slab_balance(const char* shape_json, const char* mc_json, int nranks, int32_t* cuts) {
+    g_last_error.clear();
+    try {
+        const MCSettings st = parse_mc_settings(mc_json);
+        const Program p = compile_mp5(shape_json, st.ignore_root_matrix);
+        const std::vector<int> c = balance_cuts(p, st.resolution, st.box, nranks, nullptr);
+        for (size_t k = 0; k < c.size(); ++k) cuts[k] = c[k];
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
+int implisolid_cuts_from_layer_work(const int64_t* listed, int n_layers, int64_t bricks_per_layer, int R, int nranks,
+                                    int32_t* cuts) {
+    g_last_error.clear();
+    try {
+        const std::vector<int> c =
+            cuts_from_layer_work(std::vector<int64_t>(listed, listed + n_layers), bricks_per_layer, R, nranks);
+        for (size_t k = 0; k < c.size(); ++k) cuts[k] = c[k];
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
+int implisolid_set_devices(const int32_t* ids, int n) {
+    g_last_error.clear();
+    try {
+        std::vector<int> d;
+        int count = 0;
+        if (ids && n > 0) IMPLI_HIP(hipGetDeviceCount(&count));
+        for (int k = 0; ids && k < n; ++k) {
+            if (ids[k] < 0 || ids[k] >= count) throw InputError("implisolid_set_devices: no HIP device " + std::to_string(ids[k]));
+            d.push_back(ids[k]);
+        }
+        g_devices = d.size() > 1 ? d : std::vector<int>{};
+        g_slab_engines.clear();
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
 implisolid_slab* implisolid_slab_create(const char* shape_json, const char* mc_json, int rank, int nranks) {
     g_last_error.clear();
     try {
@@ -455,6 +625,11 @@ int implisolid_slab_copy_counts(implisolid_slab* s, uint32_t* d_dst, void* strea
     SLAB_TRY(IMPLI_HIP(hipMemcpyAsync(d_dst, s->engine.d_counters() + 2, 4 * sizeof(uint32_t), hipMemcpyDeviceToDevice,
                                       (hipStream_t)stream)))
 }
+int implisolid_slab_copy_mesh(implisolid_slab* s, float* d_verts, int32_t* d_faces, int64_t nv, int64_t nf, void* stream) {
+    SLAB_TRY(
+        if (nv > 0) IMPLI_HIP(hipMemcpyAsync(d_verts, s->engine.d_verts(), (size_t)nv * 12, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+        if (nf > 0) IMPLI_HIP(hipMemcpyAsync(d_faces, s->engine.d_faces(), (size_t)nf * 12, hipMemcpyDeviceToDevice, (hipStream_t)stream)))
+}
 int implisolid_slab_set_offsets(implisolid_slab* s, uint32_t voff, uint32_t foff) {
     SLAB_TRY(s->engine.set_offsets(voff, foff))
 }
@@ -497,7 +672,17 @@ int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]) {
 }
 
 int implisolid_slab_used_jit(implisolid_slab* s) { return s->engine.used_jit() ? 1 : 0; }
-void implisolid_set_jit(int on) { TreeJit::instance().set_enabled(on != 0); }
+void implisolid_set_jit(int mode) { TreeJit::instance().set_mode(mode); }
+void implisolid_set_jit_bake(int on) { TreeJit::instance().set_bake(on != 0); }
+void implisolid_jit_wait(void) { TreeJit::instance().wait_idle(); }
+void implisolid_jit_stats(int32_t out[4], double* compile_seconds) {
+    TreeJit& j = TreeJit::instance();
+    out[0] = j.mode();
+    out[1] = j.bake() ? 1 : 0;
+    out[2] = j.compiled();
+    out[3] = j.disk_hits();
+    if (compile_seconds) *compile_seconds = j.compile_seconds();
+}
 
 int implisolid_slab_set_timing(implisolid_slab* s, int on) { SLAB_TRY(s->engine.set_timing(on != 0)) }
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]) { SLAB_TRY(s->engine.kernel_times(ms)) }

@@ -141,14 +141,20 @@ void Engine::set_object(const Program& prog) {
     depth_ = prog.max_depth;
     n_csg_ = prog.n_csg;
     prog_host_ = prog;
-    jit_tried_ = false;
+    jit_requested_ = false;
+    jit_slot_ = nullptr;
     jit_fn_ = nullptr;
     have_object_ = true;
 }
 
 void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
-    const SlabRange sr = slab_partition(R, rank, nranks);   // one halo layer below (owner rule)
+    set_slab(R, box, slab_partition(R, rank, nranks));   // one halo layer below (owner rule)
+}
+
+void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool probe_only) {
+    const SlabRange sr = slab_range(R, sr_in.z0, sr_in.z1);   // validated, 32-bit limits checked
     grid_ = make_grid(R, box, sr.z0 - sr.halo, sr.z1, sr.z0);
+    probe_only_ = probe_only;
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
     cls_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     cmodes_.reserve((size_t)(coarse_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
@@ -157,6 +163,17 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     blist_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     lmodes_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint64_t));
+    umark_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint32_t));
+    IMPLI_HIP(hipMemset(umark_.p, 0, (size_t)(n_units(grid_) + 1) * sizeof(uint32_t)));   // ids start at 1
+    marks_valid_ = false;
+    const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
+    signs_.reserve(sign_bytes + 64);
+    // the pieces past the last brick of a row are never written by the pruned path: keep them 0
+    IMPLI_HIP(hipMemset(signs_.p, 0, sign_bytes + 64));
+    if (probe_only) {   // interval_pass / listed_per_layer only
+        have_grid_ = true;
+        return;
+    }
     const size_t field_bytes = (size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float);
     field_.reserve(field_bytes);
     // the pruned eval writes only the listed bricks: the rest of the field reads as 0, not as
@@ -167,14 +184,6 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     scan_blk_.reserve((size_t)(n_groups(grid_) + 1) * (kScanParts + 1) * sizeof(uint32_t));
     ulist_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint4));
     upart_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint32_t));
-    umark_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint32_t));
-    IMPLI_HIP(hipMemset(umark_.p, 0, (size_t)(n_units(grid_) + 1) * sizeof(uint32_t)));   // ids start at 1
-    marks_valid_ = false;
-
-    const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
-    signs_.reserve(sign_bytes + 64);
-    // the pieces past the last brick of a row are never written by the pruned path: keep them 0
-    IMPLI_HIP(hipMemset(signs_.p, 0, sign_bytes + 64));
     vid3_.reserve((size_t)grid_.n_cells * 3 * sizeof(uint32_t));
     const int64_t m2 = (int64_t)grid_.m * grid_.m;
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
@@ -226,6 +235,7 @@ MCBuffers Engine::buffers() const {
 
 void Engine::eval_field(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before eval");
+    if (probe_only_) throw InputError("engine: a probe slab has no field (interval_pass only)");
     const int level = pruning();
     // the counter block (list lengths, MC counters, overflow flags) is cleared by the pruned path's
     // first kernel (grid.hpp); the dense path clears it with a memset
@@ -264,13 +274,86 @@ void Engine::eval_field(hipStream_t s) {
     IMPLI_HIP(hipGetLastError());
 }
 
-void Engine::ensure_jit() {   // compile the tree kernels for this shape once (cached by shape)
-    if (jit_tried_) return;
-    const TreeJit::Kernels k = TreeJit::instance().kernels(prog_host_);
-    jit_fn_ = k.bricks;
-    jit_iv_.coarse = k.coarse;
-    jit_iv_.refine = k.refine;
-    jit_tried_ = true;
+void Engine::interval_pass(hipStream_t s) {
+    if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before the interval pass");
+    if (brick_grid(grid_).n_bricks <= 0) return;
+    ensure_jit();
+    launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, cmodes_.as<uint64_t>(),
+                       ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>(), modes_.as<uint64_t>(),
+                       cls_.as<uint8_t>(), s, &jit_iv_);
+    launch_brick_fill(grid_, ccls_.as<uint8_t>(), cmodes_.as<uint64_t>(), cls_.as<uint8_t>(), modes_.as<uint64_t>(),
+                      1, fill_.as<uint8_t>(), blist_.as<uint32_t>(), lmodes_.as<uint64_t>(),
+                      counters_.as<uint32_t>() + kBrickListWord, signs_.p, umark_.as<uint32_t>(), ++mark_id_, s);
+    marks_valid_ = false;   // no field behind these marks
+    counters_fresh_ = true;
+    IMPLI_HIP(hipGetLastError());
+}
+
+std::vector<int64_t> Engine::listed_per_layer(hipStream_t s) {
+    const BrickGrid bg = brick_grid(grid_);
+    const int layers = grid_.fz1 - grid_.fz0;
+    std::vector<int64_t> out((size_t)layers, 0);
+    if (bg.n_bricks <= 0) return out;
+    std::vector<uint8_t> f((size_t)bg.n_bricks);   // fill[b] = class | fill class << 4 (k_brick_fill)
+    IMPLI_HIP(hipStreamSynchronize(s));
+    IMPLI_HIP(hipMemcpy(f.data(), fill_.p, f.size(), hipMemcpyDeviceToHost));
+    const int plane = bg.nbx * bg.nby;
+    for (int bz = 0; bz < bg.nbz; ++bz) {
+        int64_t listed = 0;
+        for (int k = 0; k < plane; ++k) listed += (f[(size_t)bz * plane + k] >> 4) == 0;
+        for (int l = bz * kBZ; l < std::min(layers, bz * kBZ + kBZ); ++l) out[(size_t)l] = listed;
+    }
+    return out;
+}
+
+std::vector<int> cuts_from_layer_work(const std::vector<int64_t>& listed, int64_t bricks_per_layer, int R, int nranks) {
+    const int L = R + 2;   // cell layers 1 .. L; cell layer c evaluates its lower sample layer c - 1
+    if (nranks < 1 || nranks > L) throw InputError("balance: more slabs than cell layers");
+    if ((int)listed.size() < L + 1) throw InputError("balance: per-layer counts do not cover the grid");
+    // a listed brick costs ~1.3 ns of eval + MC, a brick of the interval / fill passes ~27 ps
+    // (DESIGN.md section 6): the per-brick term weighs 0.02 of a listed brick
+    constexpr double kAllBrickWeight = 0.02;
+    std::vector<double> cum((size_t)L + 1, 0.0);
+    for (int c = 1; c <= L; ++c)
+        cum[(size_t)c] = cum[(size_t)c - 1] + (double)listed[(size_t)c - 1] / kBZ + kAllBrickWeight * bricks_per_layer / kBZ;
+    std::vector<int> cuts((size_t)nranks + 1);
+    cuts[0] = 1;
+    for (int r = 1; r < nranks; ++r) {
+        const double target = cum[(size_t)L] * r / nranks;
+        int c = cuts[(size_t)r - 1] + 1;   // at least one layer per slab
+        while (c < L && cum[(size_t)c - 1] + 0.5 * (cum[(size_t)c] - cum[(size_t)c - 1]) < target) ++c;
+        c = std::min(c, L + 1 - (nranks - r));   // leave one layer for every later slab
+        cuts[(size_t)r] = std::max(c, cuts[(size_t)r - 1] + 1);
+    }
+    cuts[(size_t)nranks] = L + 1;
+    return cuts;
+}
+
+std::vector<int> balance_cuts(const Program& prog, int R, const float box[6], int nranks, hipStream_t s) {
+    if (nranks == 1) return {1, R + 3};
+    Engine probe;
+    probe.set_object(prog);
+    probe.set_slab(R, box, SlabRange{1, R + 3, 0}, true);
+    probe.interval_pass(s);
+    const BrickGrid bg = brick_grid(probe.grid());
+    return cuts_from_layer_work(probe.listed_per_layer(s), (int64_t)bg.nbx * bg.nby, R, nranks);
+}
+
+void Engine::ensure_jit() {
+    // the object's tree module is requested once (TreeJit: compiled now, or on a background thread
+    // while the interpreter kernels run); every eval uses it as soon as it is loaded
+    if (!jit_requested_) {
+        jit_slot_ = TreeJit::instance().request(prog_host_);
+        jit_requested_ = true;
+    }
+    if (jit_slot_ && jit_slot_->ready.load(std::memory_order_acquire)) {
+        jit_fn_ = jit_slot_->k.bricks;
+        jit_iv_.coarse = jit_slot_->k.coarse;
+        jit_iv_.refine = jit_slot_->k.refine;
+    } else {
+        jit_fn_ = nullptr;
+        jit_iv_ = JitIntervalKernels{};
+    }
 }
 
 void Engine::count(hipStream_t s) {

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "host.hpp"
+#include "jit.hpp"
 #include "kernels.hpp"
 
 namespace impli {
@@ -32,14 +33,31 @@ struct SlabCounts {
 };
 
 
+// Balanced Z-slab cuts: nranks + 1 cell-layer boundaries (cuts[0] = 1, cuts[nranks] = R + 3) that
+// split the grid's estimated work evenly.  The work of a cell layer is its lower sample layer's
+// share of the bricks the pruned eval lists (field values + marching cubes scale with them) plus a
+// small per-brick term for the interval / fill passes over every brick.  Runs the interval pass of
+// the whole grid once on the current device (deterministic: every rank computes the same cuts).
+std::vector<int> balance_cuts(const Program& prog, int R, const float box[6], int nranks, hipStream_t stream);
+// the same from per-stored-layer listed-brick counts of the whole grid (host-only, tested on CPU)
+std::vector<int> cuts_from_layer_work(const std::vector<int64_t>& listed_per_layer, int64_t bricks_per_layer, int R,
+                                      int nranks);
+
 class Engine {
 public:
     Engine();
     ~Engine();
 
-    // object + grid.  rank/nranks select a Z-slab of cell layers (rank 0 of 1 = whole grid).
+    // object + grid.  rank/nranks select a Z-slab of cell layers (rank 0 of 1 = whole grid), or
+    // set_slab takes the slab's layer range itself (balanced cuts, balance_cuts below).
+    // probe_only: allocate only what the interval pass needs (interval_pass, listed_per_layer).
     void set_object(const Program& prog);
     void set_grid(int R, const float box[6], int rank, int nranks);
+    void set_slab(int R, const float box[6], const SlabRange& sr, bool probe_only = false);
+    // the pruned eval's interval and fill passes alone (no field values), then per stored sample
+    // layer of the slab: the number of bricks listed for evaluation (blocking)
+    void interval_pass(hipStream_t stream);
+    std::vector<int64_t> listed_per_layer(hipStream_t stream);
 
     // the MC pipeline, all asynchronous on `stream`
     void eval_field(hipStream_t stream);
@@ -100,15 +118,16 @@ private:
     int depth_ = 1;
     int n_csg_ = 0;
     Program prog_host_{};
-    bool jit_tried_ = false;
-    hipFunction_t jit_fn_ = nullptr;
+    TreeJit::Slot* jit_slot_ = nullptr;   // the object's module (null: JIT off); may still compile
+    bool jit_requested_ = false;
+    hipFunction_t jit_fn_ = nullptr;       // what the last eval used (null: interpreter)
     bool counters_fresh_ = false;   // eval_field zeroed the counters; the next count() need not
     uint32_t mark_id_ = 0;          // id of the last pruned eval's unit marks (umark_)
     bool marks_valid_ = false;      // the last eval was pruned: count only marked units
     JitIntervalKernels jit_iv_;
     void ensure_jit();
     float2 tab_range_{0.f, 0.f};
-    bool have_grid_ = false, have_object_ = false;
+    bool have_grid_ = false, have_object_ = false, probe_only_ = false;
     DevBuf prog_, rabbit_, cases_;
     DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, ulist_, upart_, umark_, counters_, lmodes_, vid3_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;

@@ -16,9 +16,14 @@
 #include <thread>
 #include <vector>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "generated/jit_headers.inc"
 
 namespace impli {
+
+#define IMPLI_HIP_THROW(x) do { if ((x) != hipSuccess) throw std::runtime_error(#x " failed"); } while (0)
 
 namespace {
 
@@ -99,11 +104,21 @@ const char* prim_call(int t) {
 //   - 1 * v == v exactly;
 //   - an identity row (only 1 * v, m3 == +0) is v itself: coordinates are never -0 (sample
 //     coordinates are a - b differences, every emitted row ends with + m3 != -0), so v + 0 == v.
-std::string xform_row(const float* m, int base, const std::string& x, const std::string& y, const std::string& z) {
+// a float as an exact literal of its bit pattern (value-baked kernels)
+std::string float_literal(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    char buf[48];
+    std::snprintf(buf, sizeof buf, "__builtin_bit_cast(float, 0x%08xu)", u);
+    return buf;
+}
+
+std::string xform_row(const float* m, int base, const std::string& x, const std::string& y, const std::string& z,
+                      bool bake) {
     const std::string v[3] = {x, y, z};
     auto is_bits = [](float f, uint32_t b) { uint32_t u; std::memcpy(&u, &f, 4); return u == b; };
     const float t = m[3];
-    auto at = [&](int k) { return "M[" + std::to_string(base + k) + "]"; };
+    auto at = [&](int k) { return bake ? float_literal(m[k]) : "M[" + std::to_string(base + k) + "]"; };
     if (is_bits(t, 0x80000000u) || !std::isfinite(t))   // -0 (or non-finite) translation: generic
         return "((" + at(0) + " * " + x + " + " + at(1) + " * " + y + ") + " + at(2) + " * " + z + ") + " + at(3);
     std::vector<std::string> terms;
@@ -123,10 +138,10 @@ std::string xform_row(const float* m, int base, const std::string& x, const std:
 // The interval row of xform_iv() (ifunc_interval.hpp), specialised like xform_row(): mulc(v, 1)
 // is v, a zero coefficient adds a [+-0, +-0] term (only zero endpoint signs can differ, which no
 // decision or class depends on), the final ivc(m3) and settle_point stay; an identity row is v.
-std::string xform_iv_row(const float* m, int base, const std::string& p) {
+std::string xform_iv_row(const float* m, int base, const std::string& p, bool bake) {
     const std::string v[3] = {p + ".x", p + ".y", p + ".z"};
     auto is_bits = [](float f, uint32_t b) { uint32_t u; std::memcpy(&u, &f, 4); return u == b; };
-    auto at = [&](int k) { return "M[" + std::to_string(base + k) + "]"; };
+    auto at = [&](int k) { return bake ? float_literal(m[k]) : "M[" + std::to_string(base + k) + "]"; };
     const std::string generic = "settle_point(add(add(add(mulc(" + v[0] + ", " + at(0) + "), mulc(" + v[1] + ", " +
                                 at(1) + ")), mulc(" + v[2] + ", " + at(2) + ")), ivc(" + at(3) + ")))";
     const float t = m[3];
@@ -148,6 +163,7 @@ std::string xform_iv_row(const float* m, int base, const std::string& p) {
 struct Emitter {
     const std::vector<Node>& nodes;
     const Program& prog;
+    bool bake;
     std::ostringstream out;
     int counter = 0;
 
@@ -159,9 +175,9 @@ struct Emitter {
         const std::string q = "q" + std::to_string(id), f = "f" + std::to_string(id);
         // matrix_vector_product (basic_functions.hpp:140-177), rows specialised by xform_row()
         const float* mm = prog.mats[n.mat];
-        out << pad << "const V3 " << q << " = V3{" << xform_row(mm, 12 * n.mat, x, y, z) << ",\n" << pad << "    "
-            << xform_row(mm + 4, 12 * n.mat + 4, x, y, z) << ",\n" << pad << "    "
-            << xform_row(mm + 8, 12 * n.mat + 8, x, y, z) << "};\n";
+        out << pad << "const V3 " << q << " = V3{" << xform_row(mm, 12 * n.mat, x, y, z, bake) << ",\n" << pad << "    "
+            << xform_row(mm + 4, 12 * n.mat + 4, x, y, z, bake) << ",\n" << pad << "    "
+            << xform_row(mm + 8, 12 * n.mat + 8, x, y, z, bake) << "};\n";
         if (n.leaf) {
             std::string call = n.type == NT_LID         ? "lid_f(" + q + ".z)"
                                : n.type == NT_EXTRUSION ? with_params("extr_f(P, ", n.prm) + q + ".x, " + q + ".y)"
@@ -218,6 +234,7 @@ const char* prim_iv_call(int t) {
 struct IvEmitter {
     const std::vector<Node>& nodes;
     const Program& prog;
+    bool bake;
     std::ostringstream out;
     int counter = 0;
 
@@ -227,9 +244,9 @@ struct IvEmitter {
         const std::string pad(ind, ' ');
         const std::string q = "q" + std::to_string(id), r = "r" + std::to_string(id);
         const float* mm = prog.mats[n.mat];
-        out << pad << "const Box " << q << " = Box{" << xform_iv_row(mm, 12 * n.mat, p) << ",\n" << pad << "    "
-            << xform_iv_row(mm + 4, 12 * n.mat + 4, p) << ",\n" << pad << "    "
-            << xform_iv_row(mm + 8, 12 * n.mat + 8, p) << "};\n";
+        out << pad << "const Box " << q << " = Box{" << xform_iv_row(mm, 12 * n.mat, p, bake) << ",\n" << pad << "    "
+            << xform_iv_row(mm + 4, 12 * n.mat + 4, p, bake) << ",\n" << pad << "    "
+            << xform_iv_row(mm + 8, 12 * n.mat + 8, p, bake) << "};\n";
         if (n.leaf) {
             out << pad << "const Iv " << r << " = settle(" << with_params(prim_iv_call(n.type), n.prm) << q << "));\n";
             return r;
@@ -263,23 +280,231 @@ void rtc_check(hiprtcResult r, const char* what) {
 }  // namespace
 
 TreeJit& TreeJit::instance() {
-    static TreeJit j;
-    return j;
+    static TreeJit* j = new TreeJit();   // never destroyed: workers are joined at exit (shutdown)
+    return *j;
 }
 
 TreeJit::TreeJit() {
-    const char* e = std::getenv("IMPLISOLID_JIT");
-    enabled_ = !(e && e[0] == '0');
+    if (const char* e = std::getenv("IMPLISOLID_JIT")) mode_.store(e[0] == '0' ? kOff : e[0] == '1' ? kSync : kAsync);
+    if (const char* e = std::getenv("IMPLISOLID_JIT_BAKE")) bake_.store(e[0] == '1');
+    const char* d = std::getenv("IMPLISOLID_JIT_CACHE");
+    if (d && (!std::strcmp(d, "off") || !std::strcmp(d, "0"))) {
+        disk_dir_.clear();
+    } else if (d && d[0]) {
+        disk_dir_ = d;
+    } else if (const char* x = std::getenv("XDG_CACHE_HOME")) {
+        disk_dir_ = std::string(x) + "/implisolid_amd";
+    } else if (const char* h = std::getenv("HOME")) {
+        disk_dir_ = std::string(h) + "/.cache/implisolid_amd";
+    }
 }
 
-std::string TreeJit::kernel_source(const Program& p) {
+double TreeJit::compile_seconds() const { return compile_us_.load() * 1e-6; }
+
+namespace {
+
+// FNV-1a over the source and the compile options: the disk cache key
+std::string source_hash(const std::string& src) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](const char* p, size_t n) {
+        for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)p[i]; h *= 1099511628211ull; }
+    };
+    mix(src.data(), src.size());
+    const char* tag = "gfx950 -O3 -ffp-contract=off -std=c++17 v2";
+    mix(tag, std::strlen(tag));
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
+    return buf;
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n > 0 && std::fread(out.data(), 1, out.size(), f) == out.size();
+    std::fclose(f);
+    return ok;
+}
+
+void write_file_atomic(const std::string& dir, const std::string& name, const std::vector<char>& data) {
+    std::string path;   // mkdir -p
+    for (size_t i = 1; i <= dir.size(); ++i)
+        if (i == dir.size() || dir[i] == '/') (void)::mkdir(dir.substr(0, i).c_str(), 0755);
+    const std::string tmp = dir + "/." + name + "." + std::to_string((long)::getpid()) + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const bool ok = std::fwrite(data.data(), 1, data.size(), f) == data.size();
+    std::fclose(f);
+    if (!ok || std::rename(tmp.c_str(), (dir + "/" + name).c_str()) != 0) std::remove(tmp.c_str());
+}
+
+}  // namespace
+
+void TreeJit::build(Slot* slot) {
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        std::vector<char> code;
+        const std::string name = source_hash(slot->src) + ".co";
+        // the disk copy is only trusted with its source beside it (a hash collision cannot alias)
+        std::vector<char> src_on_disk;
+        if (!disk_dir_.empty() && read_file(disk_dir_ + "/" + name, code) &&
+            read_file(disk_dir_ + "/" + name + ".src", src_on_disk) &&
+            std::string(src_on_disk.begin(), src_on_disk.end()) == slot->src) {
+            ++n_disk_;
+        } else {
+            code = compile(slot->src);
+            compile_us_ += (int64_t)(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
+            ++n_compiled_;
+            if (!disk_dir_.empty()) {
+                write_file_atomic(disk_dir_, name + ".src", std::vector<char>(slot->src.begin(), slot->src.end()));
+                write_file_atomic(disk_dir_, name, code);
+            }
+        }
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        if (prev != slot->device) IMPLI_HIP_THROW(hipSetDevice(slot->device));
+        Kernels k;
+        const bool ok = hipModuleLoadData(&slot->mod, code.data()) == hipSuccess &&
+                        hipModuleGetFunction(&k.bricks, slot->mod, "impli_eval_bricks") == hipSuccess &&
+                        hipModuleGetFunction(&k.coarse, slot->mod, "impli_coarse_modes") == hipSuccess &&
+                        hipModuleGetFunction(&k.refine, slot->mod, "impli_brick_refine") == hipSuccess;
+        if (prev != slot->device) (void)hipSetDevice(prev);
+        if (!ok) throw std::runtime_error("hipModuleLoadData / hipModuleGetFunction failed");
+        slot->k = k;
+        slot->ready.store(true, std::memory_order_release);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n", std::string(e.what()).substr(0, 400).c_str());
+        slot->failed.store(true, std::memory_order_release);
+    }
+}
+
+void TreeJit::worker() {
+    for (;;) {
+        Slot* slot = nullptr;
+        {
+            std::unique_lock<std::mutex> lock(mu_);
+            cv_.wait(lock, [this] { return stop_ || !queue_.empty(); });
+            if (queue_.empty()) return;   // stop_ and drained
+            slot = queue_.front();
+            queue_.pop_front();
+            ++busy_;
+        }
+        build(slot);
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            --busy_;
+        }
+        idle_cv_.notify_all();
+    }
+}
+
+void TreeJit::shutdown() {   // at exit: drop queued work, finish what is compiling, join
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        stop_ = true;
+        for (Slot* s : queue_) s->failed.store(true);
+        queue_.clear();
+    }
+    cv_.notify_all();
+    for (auto& t : workers_)
+        if (t.joinable()) t.join();
+    workers_.clear();
+}
+
+TreeJit::Slot* TreeJit::request(const Program& p) {
+    const int m = mode();
+    if (m == kOff) return nullptr;
+    std::string src;
+    try {
+        src = kernel_source(p, bake());
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "implisolid: tree JIT skipped (%s)\n", e.what());
+        return nullptr;
+    }
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    Slot* slot = nullptr;
+    bool fresh = false;
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        const std::string key = std::to_string(dev) + "\n" + src;
+        auto it = cache_.find(key);
+        if (it != cache_.end()) {
+            slot = it->second;
+        } else {
+            slot = new Slot();
+            slot->src = std::move(src);
+            slot->device = dev;
+            cache_.emplace(key, slot);
+            fresh = true;
+            if (m == kAsync && !stop_) {
+                queue_.push_back(slot);
+                if (workers_.empty()) {   // a small pool, started on first use
+                    const unsigned hw = std::thread::hardware_concurrency();
+                    const int n = (int)std::max(1u, std::min(4u, hw ? hw / 2 : 1u));
+                    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { worker(); });
+                    std::atexit([] { TreeJit::instance().shutdown(); });
+                }
+            }
+        }
+    }
+    if (fresh && m == kAsync) cv_.notify_one();
+    if (fresh && (m == kSync || stop_)) build(slot);
+    if (m == kSync) {   // a slot queued earlier in async mode: wait for it
+        std::unique_lock<std::mutex> lock(mu_);
+        idle_cv_.wait(lock, [slot] { return slot->ready.load() || slot->failed.load(); });
+    }
+    return slot;
+}
+
+void TreeJit::wait_idle() {
+    std::unique_lock<std::mutex> lock(mu_);
+    idle_cv_.wait(lock, [this] { return queue_.empty() && busy_ == 0; });
+}
+
+void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
+    if (mode() == kOff) return;
+    // register and queue every program's module (async), then drain the queue with extra threads
+    const int saved = mode();
+    mode_.store(kAsync);
+    for (const Program& p : progs) (void)request(p);
+    mode_.store(saved);
+    // let the pool drain the queue, with extra threads for a large batch
+    std::vector<std::thread> extra;
+    const int n_extra = std::max(0, std::min<int>(threads, (int)progs.size()) - 4);
+    for (int i = 0; i < n_extra; ++i) extra.emplace_back([this] {
+        for (;;) {
+            Slot* slot = nullptr;
+            {
+                std::lock_guard<std::mutex> lock(mu_);
+                if (queue_.empty()) return;
+                slot = queue_.front();
+                queue_.pop_front();
+                ++busy_;
+            }
+            build(slot);
+            {
+                std::lock_guard<std::mutex> lock(mu_);
+                --busy_;
+            }
+            idle_cv_.notify_all();
+        }
+    });
+    for (auto& t : extra) t.join();
+    wait_idle();
+}
+
+std::string TreeJit::kernel_source(const Program& p, bool bake) {
     std::vector<Node> nodes;
     int next = 0;
     const int root = parse(p, 0, nodes, next);
     if (next != p.n_instr) throw std::runtime_error("jit: trailing instructions");
-    Emitter em{nodes, p};
+    Emitter em{nodes, p, bake};
     const std::string f = em.emit(root, "x0", "y0", "z0", 4);
-    IvEmitter iv{nodes, p};
+    IvEmitter iv{nodes, p, bake};
     const std::string r = iv.emit(root, "p0", 4);
     std::ostringstream s;
     if (const char* e = std::getenv("IMPLISOLID_EVAL_PAIR")) s << "#define IMPLI_EVAL_PAIR " << (e[0] == '1' ? 1 : 0) << "\n";
@@ -350,90 +575,6 @@ std::vector<char> TreeJit::compile(const std::string& src) {
         if (FILE* f = std::fopen((base + ".co").c_str(), "wb")) { std::fwrite(code.data(), 1, code.size(), f); std::fclose(f); }
     }
     return code;
-}
-
-TreeJit::Kernels TreeJit::kernels(const Program& p) {
-    if (!enabled_) return Kernels{};
-    std::string src;
-    try {
-        src = kernel_source(p);
-    } catch (const std::exception& e) {
-        std::fprintf(stderr, "implisolid: tree JIT skipped (%s)\n", e.what());
-        return Kernels{};
-    }
-    std::lock_guard<std::mutex> lock(mu_);
-    auto it = cache_.find(src);
-    if (it != cache_.end()) return it->second.k;
-    Entry ent;
-    const auto t0 = std::chrono::steady_clock::now();
-    try {
-        const std::vector<char> code = compile(src);
-        if (hipModuleLoadData(&ent.mod, code.data()) != hipSuccess) throw std::runtime_error("hipModuleLoadData failed");
-        if (hipModuleGetFunction(&ent.k.bricks, ent.mod, "impli_eval_bricks") != hipSuccess ||
-            hipModuleGetFunction(&ent.k.coarse, ent.mod, "impli_coarse_modes") != hipSuccess ||
-            hipModuleGetFunction(&ent.k.refine, ent.mod, "impli_brick_refine") != hipSuccess)
-            throw std::runtime_error("hipModuleGetFunction failed");
-    } catch (const std::exception& e) {
-        std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n", e.what());
-        ent.k = Kernels{};
-    }
-    compile_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (ent.k.bricks) ++n_compiled_;
-    cache_.emplace(src, ent);
-    return ent.k;
-}
-
-void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
-    if (!enabled_) return;
-    std::vector<std::string> srcs;
-    {
-        std::set<std::string> seen;
-        std::lock_guard<std::mutex> lock(mu_);
-        for (const Program& p : progs) {
-            std::string src;
-            try {
-                src = kernel_source(p);
-            } catch (const std::exception&) {
-                continue;   // kernels() logs and falls back for this shape
-            }
-            if (!cache_.count(src) && seen.insert(src).second) srcs.push_back(std::move(src));
-        }
-    }
-    if (srcs.empty()) return;
-    std::vector<std::vector<char>> codes(srcs.size());
-    std::vector<std::string> errs(srcs.size());
-    std::atomic<size_t> next{0};
-    const auto t0 = std::chrono::steady_clock::now();
-    auto work = [&] {
-        for (size_t i; (i = next++) < srcs.size();) {
-            try {
-                codes[i] = compile(srcs[i]);
-            } catch (const std::exception& e) {
-                errs[i] = e.what();
-            }
-        }
-    };
-    const int nt = std::max(1, std::min<int>(threads, (int)srcs.size()));
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
-    work();
-    for (auto& t : pool) t.join();
-    std::lock_guard<std::mutex> lock(mu_);
-    for (size_t i = 0; i < srcs.size(); ++i) {
-        Entry ent;
-        if (!codes[i].empty() && hipModuleLoadData(&ent.mod, codes[i].data()) == hipSuccess &&
-            hipModuleGetFunction(&ent.k.bricks, ent.mod, "impli_eval_bricks") == hipSuccess &&
-            hipModuleGetFunction(&ent.k.coarse, ent.mod, "impli_coarse_modes") == hipSuccess &&
-            hipModuleGetFunction(&ent.k.refine, ent.mod, "impli_brick_refine") == hipSuccess) {
-            ++n_compiled_;
-        } else {
-            std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n",
-                         errs[i].empty() ? "module load failed" : errs[i].substr(0, 400).c_str());
-            ent.k = Kernels{};
-        }
-        cache_.emplace(srcs[i], ent);
-    }
-    compile_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,

@@ -9,7 +9,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -24,23 +28,44 @@ public:
     // process-wide instance; IMPLISOLID_JIT=0 disables compilation (interpreter only)
     static TreeJit& instance();
 
-    // C++ source of the brick kernel for this program's shape (no matrices in it)
-    static std::string kernel_source(const Program& p);
+    // C++ source of the tree kernels for this program's shape (no matrices in it), or with the
+    // object's transformation matrices baked in as exact literals (bake: one module per object,
+    // no matrix loads on the kernels' dependency chains)
+    static std::string kernel_source(const Program& p, bool bake = false);
 
     // hipRTC-compile the source to a gfx950 code object (no GPU needed); throws with the log
     static std::vector<char> compile(const std::string& src);
 
-    // compiled kernels for this shape, compiling on first use; nullptr if disabled or if
-    // compilation failed (the failure is logged once and the interpreter kernels are used)
     struct Kernels {
         hipFunction_t bricks = nullptr;   // brick-pruned field (eval_bricks_body)
         hipFunction_t coarse = nullptr;   // interval pass, coarse boxes (coarse_modes_body)
         hipFunction_t refine = nullptr;   // interval pass, bricks of mixed boxes (brick_refine_body)
     };
-    Kernels kernels(const Program& p);
-
-    // compile the kernels of many shapes on up to `threads` host threads (hipRTC runs outside the
-    // cache lock); shapes already cached are skipped.  kernels() then finds them cached.
+    // One compiled module (one source on one device).  Slots live as long as the process; `ready`
+    // is set (release) once `k` holds the loaded kernels, `failed` if compilation or loading failed.
+    struct Slot {
+        std::atomic<bool> ready{false}, failed{false};
+        Kernels k;
+        hipModule_t mod = nullptr;
+        std::string src;
+        int device = 0;
+    };
+    // Modes (IMPLISOLID_JIT=0|1|2, implisolid_set_jit):
+    //   0 off: the interpreter kernels only;
+    //   1 sync: request() compiles before it returns (the first call of a new shape waits for hipRTC);
+    //   2 async (default): request() returns at once; compilation runs on background threads and the
+    //     engine uses the interpreter kernels until the module is ready -- a never-seen shape costs
+    //     no compile latency.  Code objects persist in a disk cache (IMPLISOLID_JIT_CACHE=<dir>,
+    //     default $XDG_CACHE_HOME or ~/.cache /implisolid_amd; "off" disables it).
+    // Variants (IMPLISOLID_JIT_BAKE=0|1, implisolid_set_jit_bake): shape modules keep the matrices as
+    // data (one module per tree shape); baked modules hold the object's matrices as literals (one per
+    // object: no matrix loads on the dependency chains).
+    enum Mode { kOff = 0, kSync = 1, kAsync = 2 };
+    Slot* request(const Program& p);
+    // block until every scheduled compilation has finished (bench / batch setup)
+    void wait_idle();
+    // compile the modules of many programs (sync, up to `threads` host threads); request() then
+    // finds them ready
     void precompile(const std::vector<Program>& progs, int threads);
 
     // launch the compiled brick kernel (same contract as launch_eval_field_pruned's 2nd kernel)
@@ -51,22 +76,33 @@ public:
     // launch a compiled kernel with 256-thread blocks; args as for hipModuleLaunchKernel
     static void launch(hipFunction_t fn, unsigned blocks, void** args, hipStream_t s, const char* what);
 
-    bool enabled() const { return enabled_; }
-    void set_enabled(bool on) { enabled_ = on; }
-    int compiled() const { return n_compiled_; }
-    double compile_seconds() const { return compile_s_; }
+    int mode() const { return mode_.load(); }
+    void set_mode(int m) { mode_.store(m < 0 ? 0 : m > 2 ? 2 : m); }
+    bool bake() const { return bake_.load(); }
+    void set_bake(bool b) { bake_.store(b); }
+    bool enabled() const { return mode() != kOff; }
+    void set_enabled(bool on) { set_mode(on ? kAsync : kOff); }
+    int compiled() const { return n_compiled_.load(); }
+    int disk_hits() const { return n_disk_.load(); }
+    double compile_seconds() const;
 
 private:
     TreeJit();
-    struct Entry {
-        hipModule_t mod = nullptr;
-        Kernels k;
-    };
+    void build(Slot* slot);            // compile (or read from disk) + load; sets ready / failed
+    void worker();
+    void shutdown();
     std::mutex mu_;
-    std::unordered_map<std::string, Entry> cache_;
-    bool enabled_ = true;
-    int n_compiled_ = 0;
-    double compile_s_ = 0;
+    std::condition_variable cv_, idle_cv_;
+    std::unordered_map<std::string, Slot*> cache_;   // key: device + source
+    std::deque<Slot*> queue_;
+    std::vector<std::thread> workers_;
+    int busy_ = 0;
+    bool stop_ = false;
+    std::atomic<int> mode_{kAsync};
+    std::atomic<bool> bake_{false};
+    std::atomic<int> n_compiled_{0}, n_disk_{0};
+    std::atomic<int64_t> compile_us_{0};
+    std::string disk_dir_;
 };
 
 }  // namespace impli

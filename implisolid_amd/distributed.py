@@ -51,3 +51,55 @@ def global_offsets(local_counts, rank, world, group=None, out=None):
     """gather_counts + offsets_from_counts; returns (offsets int32[2], gathered int32[world, 4])."""
     g = gather_counts(local_counts, world, group)
     return offsets_from_counts(g, rank, out), g
+
+
+def balanced_cuts(shape, mc_settings, world):
+    """Balanced Z-slab cuts for `world` ranks (implisolid_slab_balance): every rank runs the same
+    interval pass of the whole grid on its own GPU and gets the same cuts, so the partition needs
+    no exchange.  Pass them to ``Slab(..., rank, world, cuts=cuts)``."""
+    import implisolid_amd as I
+    return I.slab_balance(shape, mc_settings, world)
+
+
+def gather_mesh(slab, gathered, rank, world, group=None, stream=0):
+    """Gather every rank's emitted mesh to rank 0 in rank order (the multi-GPU result of the C ABI's
+    build_geometry, mcc2.cpp:446-525).  `gathered` is the all-gathered counts tensor int32[world, 4]
+    (gather_counts); the faces must have been emitted with global vertex ids (Slab.emit_faces with
+    the gathered counts), so concatenation is the whole single-GPU mesh, byte for byte.
+
+    RCCL: point-to-point device buffers (rank r sends its slab to rank 0 over xGMI; rank 0 receives
+    all slabs concurrently into slices of one buffer).  gloo (CPU rehearsal): the same through host
+    copies.  Returns (verts float32 [V, 3], faces int32 [F, 3]) numpy arrays on rank 0, None elsewhere."""
+    import numpy as np
+    g = gathered.to("cpu").numpy().astype(np.int64)
+    nv = g[:, 0] - g[:, 3]
+    nf = g[:, 1]
+    gloo = dist.get_backend(group) == "gloo"
+    dev = gathered.device if not gloo else torch.device("cpu")
+    if gloo:
+        v_np, f_np = slab.download(int(nv[rank]), int(nf[rank]), stream)
+        v_loc, f_loc = torch.from_numpy(v_np.reshape(-1)), torch.from_numpy(f_np.reshape(-1))
+    else:
+        v_loc = torch.empty(int(nv[rank]) * 3, dtype=torch.float32, device=dev)
+        f_loc = torch.empty(int(nf[rank]) * 3, dtype=torch.int32, device=dev)
+        slab.copy_mesh(v_loc.data_ptr(), f_loc.data_ptr(), int(nv[rank]), int(nf[rank]), stream)
+        torch.cuda.current_stream(dev).synchronize()
+    if rank != 0:   # empty parts are skipped on both sides (both know the sizes)
+        works = [dist.isend(t, 0, group=group) for t in (v_loc, f_loc) if t.numel()]
+        for w in works:
+            w.wait()
+        return None
+    voff = np.concatenate([[0], np.cumsum(nv)])
+    foff = np.concatenate([[0], np.cumsum(nf)])
+    V = torch.empty(int(voff[-1]) * 3, dtype=torch.float32, device=dev)
+    F = torch.empty(int(foff[-1]) * 3, dtype=torch.int32, device=dev)
+    V[:int(nv[0]) * 3].copy_(v_loc)
+    F[:int(nf[0]) * 3].copy_(f_loc)
+    works = []
+    for r in range(1, world):
+        for t in (V[int(voff[r]) * 3:int(voff[r + 1]) * 3], F[int(foff[r]) * 3:int(foff[r + 1]) * 3]):
+            if t.numel():
+                works.append(dist.irecv(t, r, group=group))
+    for w in works:
+        w.wait()
+    return V.cpu().numpy().reshape(-1, 3), F.cpu().numpy().reshape(-1, 3)

@@ -103,6 +103,20 @@ int implisolid_parse_settings(const char* mc_json, float box[6], int32_t ints[7]
 /* Additive, host only: Z-slab decomposition used by the slab API -- rank owns cell layers
  * [out[0], out[1]) and recomputes out[2] (0/1) halo layers below. */
 int implisolid_slab_partition(int R, int rank, int nranks, int32_t out[3]);
+/* Additive: balanced Z-slab cuts (nranks + 1 cell-layer boundaries, cuts[0] = 1, cuts[nranks] =
+ * R + 3; rank r owns layers [cuts[r], cuts[r+1])).  Runs the interval pass of the whole grid once
+ * on the current HIP device and splits the estimated work (listed bricks per layer) evenly; every
+ * rank computing it gets the same cuts, so no exchange is needed (blocking). */
+int implisolid_slab_balance(const char* shape_json, const char* mc_json, int nranks, int32_t* cuts);
+/* host only: the same split from per-sample-layer listed-brick counts of the whole grid
+ * (n_layers = R + 3) and the bricks per layer */
+int implisolid_cuts_from_layer_work(const int64_t* listed, int n_layers, int64_t bricks_per_layer, int R, int nranks,
+                                    int32_t* cuts);
+/* Additive: the devices build_geometry uses for marching cubes (HIP ordinals; n <= 0 or NULL: the
+ * current device only).  With n > 1 the grid is split into n balanced Z-slabs, slab r on device
+ * ids[r] (a device may repeat), the slabs' meshes are concatenated in rank order on the host --
+ * byte-identical to one device -- and the OB02 steps run on ids[0]. */
+int implisolid_set_devices(const int32_t* ids, int n);
 /* evaluate n >= 0 points (no 50k limit) of the current set_object(); grad may be NULL */
 int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* grad_out);
 
@@ -119,6 +133,11 @@ int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int3
    hipStream_t (may be NULL); nothing blocks except implisolid_slab_counts. */
 typedef struct implisolid_slab implisolid_slab;
 implisolid_slab* implisolid_slab_create(const char* shape_json, const char* mc_json, int rank, int nranks);
+/* async device-to-device copy of the slab's emitted mesh (nv vertices, nf faces, as counted) into
+ * caller-owned device buffers on the slab's device (the multi-process output gather) */
+int implisolid_slab_copy_mesh(implisolid_slab* s, float* d_verts, int32_t* d_faces, int64_t nv, int64_t nf, void* stream);
+/* the slab of cell layers [z0, z1) (e.g. from implisolid_slab_balance); a halo layer below if z0 > 1 */
+implisolid_slab* implisolid_slab_create_range(const char* shape_json, const char* mc_json, int z0, int z1);
 void implisolid_slab_destroy(implisolid_slab* s);
 int implisolid_slab_eval(implisolid_slab* s, void* stream);            /* field (K1) */
 int implisolid_slab_count(implisolid_slab* s, void* stream);           /* counts + scan (K2) */
@@ -160,9 +179,19 @@ int implisolid_slab_set_timing(implisolid_slab* s, int on);
 int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]);
 /* 1 if the slab's last eval ran the JIT-compiled tree kernel, 0 if the interpreter */
 int implisolid_slab_used_jit(implisolid_slab* s);
-/* process-wide: compile tree kernels with hipRTC for objects set from now on (default on;
- * environment IMPLISOLID_JIT=0 starts with it off).  Results are bit-identical either way. */
-void implisolid_set_jit(int on);
+/* process-wide tree-kernel JIT mode for objects set from now on (environment IMPLISOLID_JIT):
+ *   0 off (interpreter kernels only), 1 sync (hipRTC compiles before the first eval of a new shape),
+ *   2 async (default: compilation runs on background threads, evals use the interpreter kernels
+ *   until the module is loaded -- a never-seen shape pays no compile latency).  Compiled code
+ *   objects are kept in a disk cache (IMPLISOLID_JIT_CACHE).  Results are bit-identical in every mode. */
+void implisolid_set_jit(int mode);
+/* 1: modules bake the object's matrices in as literals (one module per object); 0 (default): one
+ * module per tree shape, matrices read from memory (IMPLISOLID_JIT_BAKE) */
+void implisolid_set_jit_bake(int on);
+/* block until all scheduled tree-kernel compilations have finished */
+void implisolid_jit_wait(void);
+/* [mode, bake, modules compiled, modules read from the disk cache], total compile seconds */
+void implisolid_jit_stats(int32_t out[4], double* compile_seconds);
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]);
 /* blocking copy of the slab's sample signs (1: value < 0), n*n*layers bytes, x fastest; with
  * out == NULL returns the count.  At pruning level 2 sign-filled bricks keep no field values, so

@@ -389,6 +389,42 @@ def test_slab_32bit_cell_limit(impli):
         impli.slab_partition(2000, 0, 3000)   # more slabs than layers
 
 
+def _layer_work(listed, bpl, cuts):
+    w = np.asarray(listed, np.float64) / 2 + 0.02 * bpl / 2   # cell layer c costs sample layer c - 1
+    return [w[cuts[r] - 1:cuts[r + 1] - 1].sum() for r in range(len(cuts) - 1)]
+
+
+def test_balanced_cuts_from_layer_work(impli):
+    """Balanced Z-slab cuts (engine.hip cuts_from_layer_work): they cover the cell layers
+    1 .. R + 2 in order with at least one layer per slab, split a uniform load into equal slabs,
+    and keep a surface concentrated in the middle layers within 1.3x max / min."""
+    R, bpl = 512, 65 * 65
+    L = R + 2
+    for n in (1, 2, 3, 8):
+        cuts = impli.cuts_from_layer_work(np.full(R + 3, 100), bpl, R, n)
+        assert cuts[0] == 1 and cuts[-1] == R + 3 and all(b > a for a, b in zip(cuts, cuts[1:]))
+        sizes = np.diff(cuts)
+        assert sizes.max() - sizes.min() <= 1
+    z = np.arange(R + 3)
+    listed = (3000 * np.exp(-((z - 0.55 * R) / (0.18 * R)) ** 2)).astype(np.int64)   # surface mid-grid
+    for n in (2, 4, 8):
+        cuts = impli.cuts_from_layer_work(listed, bpl, R, n)
+        w = _layer_work(listed, bpl, cuts)
+        assert max(w) / min(w) < 1.3, (n, cuts, w)
+        eq = [impli.slab_partition(R, r, n)[0] for r in range(n)] + [L + 1]
+        weq = _layer_work(listed, bpl, eq)
+        assert max(w) < max(weq)                                  # better than equal layers
+    # degenerate inputs: all work in one layer; as many slabs as layers
+    one = np.zeros(R + 3, np.int64)
+    one[100] = 10 ** 6
+    cuts = impli.cuts_from_layer_work(one, bpl, R, 8)
+    assert all(b > a for a, b in zip(cuts, cuts[1:])) and cuts[-1] == R + 3
+    cuts = impli.cuts_from_layer_work(np.ones(18), 16, 15, 17)
+    assert cuts == list(range(1, 19))
+    with pytest.raises(impli.ImplisolidError):
+        impli.cuts_from_layer_work(np.ones(18), 16, 15, 18)
+
+
 # ---- multi-rank numbering exchange (gloo, CPU) -----------------------------------------------------
 def _slab_counts(codes, faces_cell_z, R, z0, z1, halo):
     """counts int32[4] a rank's Slab.count() produces: own vertices incl. halo, faces, -, halo."""

@@ -181,29 +181,62 @@ def test_empty_and_full(impli, oracle):
 @pytest.mark.parametrize("level", [1, 2])
 @pytest.mark.parametrize("name", sorted(TREES))
 def test_jit_field_matches_interpreter(impli, name, level):
-    """The hipRTC-compiled tree kernels (interval pass and field) and the interpreter produce the
-    same field, sign bitmap and brick classes bit for bit."""
+    """The hipRTC-compiled tree kernels (interval pass and field) -- per-shape modules (matrices
+    read from memory) and per-object modules with the matrices baked in as literals -- and the
+    interpreter produce the same field, sign bitmap and brick classes bit for bit."""
     from implisolid_amd import scenes
     mc = scenes.mc_settings(48, 1.0)
     out = []
     impli.set_pruning(level)
     try:
-        for jit in (False, True):
-            impli.set_jit(jit)
+        for mode, bake in ((0, False), (1, False), (1, True)):
+            impli.set_jit(mode)
+            impli.set_jit_bake(bake)
             s = impli.Slab(TREES[name], mc)
             try:
                 s.eval()
-                assert s.used_jit() == jit
+                assert s.used_jit() == bool(mode)
                 out.append((s.read_field(), s.read_signs(), s.brick_stats()))
             finally:
                 s.close()
     finally:
-        impli.set_jit(True)
+        impli.set_jit(2)
+        impli.set_jit_bake(False)
         impli.set_pruning(2)
-    (fa, sa, ba), (fb, sb, bb) = out
-    assert np.array_equal(fa.view(np.uint32), fb.view(np.uint32)), np.flatnonzero(fa != fb)[:10]
-    assert np.array_equal(sa, sb)
-    assert ba == bb
+    fa, sa, ba = out[0]
+    for fb, sb, bb in out[1:]:
+        assert np.array_equal(fa.view(np.uint32), fb.view(np.uint32)), np.flatnonzero(fa != fb)[:10]
+        assert np.array_equal(sa, sb)
+        assert ba == bb
+
+
+def test_jit_async_first_call_then_compiled(impli, oracle):
+    """Async JIT (the default): a never-seen shape is polygonised at once with the interpreter
+    kernels while its module compiles in the background; after jit_wait() the same slab's eval runs
+    the compiled kernels.  Both meshes are the oracle's."""
+    from implisolid_amd import scenes
+    shape = scenes.random_tree(424242, 7)      # a shape no other test compiles
+    mc = scenes.mc_settings(40, 1.0)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    impli.set_jit(2)
+    s = impli.Slab(shape, mc)
+    try:
+        s.eval()
+        first = s.used_jit()
+        s.count()
+        nv, nf, _ = s.counts()
+        s.emit()
+        v0, f0 = s.download(*s.counts()[:2])
+        impli.jit_wait()
+        s.eval()
+        assert s.used_jit() and not first
+        s.count()
+        s.emit()
+        v1, f1 = s.download(*s.counts()[:2])
+    finally:
+        s.close()
+    for v, f in ((v0, f0), (v1, f1)):
+        assert np.array_equal(f, fr) and np.array_equal(v.view(np.uint32), vr.view(np.uint32))
 
 
 @pytest.mark.parametrize("level", [0, 1, 2])
@@ -495,6 +528,9 @@ def _subdiv_compare(impli, oracle, shape, mc, seed):
     libc = ctypes.CDLL("libc.so.6")
     impli.srand(seed)
     v, f = impli.make_geometry(shape, mc)
+    # hipRTC (LLVM's Process::GetRandomNumber) calls the process-global srand()/rand(): let the
+    # background compile of this shape finish before the oracle draws from glibc's generator
+    impli.jit_wait()
     oracle.srand(seed)
     vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
     assert np.array_equal(f, fr)
@@ -599,3 +635,90 @@ def test_headline_against_oracle_summary(impli, name):
     assert np.abs(v[idx][ok].astype(np.float64) - vs[ok]).max(initial=0.0) < 1e-5
     tot = v[fin].astype(np.float64).sum(0)
     assert np.abs(tot - np.array(s["finite_sum"])).max() < 1e-5 * max(1, fin.sum())
+
+
+# ---- multi-GPU: balanced slabs, multi-device build_geometry, multi-process ranks -------------------
+def test_balanced_slabs_identical(impli, oracle):
+    """Balanced Z-slab cuts (one interval pass of the whole grid) split config 3's tree at R 96 into
+    4 unequal slabs whose concatenated meshes are the oracle's, byte for byte; the estimated work
+    is better balanced than with equal layers."""
+    from implisolid_amd import scenes
+    shape, mc = scenes.config3_tree(), scenes.mc_settings(96, 1.0)
+    cuts = impli.slab_balance(shape, mc, 4)
+    assert cuts[0] == 1 and cuts[-1] == 96 + 3 and all(b > a for a, b in zip(cuts, cuts[1:]))
+    assert cuts == impli.slab_balance(shape, mc, 4)          # deterministic: every rank agrees
+    ref_v, ref_f = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    slabs = [impli.Slab(shape, mc, r, 4, cuts=cuts) for r in range(4)]
+    counts = []
+    for s in slabs:
+        s.eval()
+        s.count()
+        counts.append(s.counts()[:2])
+    voff = np.concatenate([[0], np.cumsum([c[0] for c in counts])])
+    foff = np.concatenate([[0], np.cumsum([c[1] for c in counts])])
+    vs, fs = [], []
+    for r, s in enumerate(slabs):
+        assert (s.cz_emit, s.cz1) == (cuts[r], cuts[r + 1])
+        s.set_offsets(int(voff[r]), int(foff[r]))
+        s.emit()
+        nv, nf, of = s.counts()
+        assert not of
+        v, f = s.download(nv, nf)
+        vs.append(v)
+        fs.append(f)
+        s.close()
+    assert np.array_equal(np.concatenate(fs), ref_f)
+    assert np.array_equal(np.concatenate(vs).view(np.uint32), ref_v.view(np.uint32))
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0, 0]])
+def test_multi_device_build_geometry(impli, oracle, devices):
+    """build_geometry with implisolid_set_devices: marching cubes over balanced Z-slabs on several
+    devices (here the box's one GPU repeated), concatenated on the host == the oracle; the OB02
+    steps then run on the first device on the gathered mesh == the single-device result."""
+    from implisolid_amd import scenes
+    shape, mc = scenes.config3(56)
+    mc_only = scenes.mc_settings(56, 1.0)
+    v1, f1 = impli.make_geometry(shape, mc)
+    try:
+        impli.set_devices(devices)
+        v, f = impli.make_geometry(shape, mc_only)
+        vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc_only))
+        assert np.array_equal(f, fr) and np.array_equal(v.view(np.uint32), vr.view(np.uint32))
+        v2, f2 = impli.make_geometry(shape, mc)
+        assert np.array_equal(f2, f1)
+        assert np.array_equal(v2.view(np.uint32), v1.view(np.uint32))
+    finally:
+        impli.set_devices(None)
+
+
+@pytest.mark.parametrize("world,balanced", [(2, True), (3, False)])
+def test_multiprocess_slabs_gloo(impli, oracle, tmp_path, world, balanced):
+    """`world` fresh processes (torch.distributed.run, all on this box's GPU, gloo backend) run the
+    bench's multi-GPU step -- balanced or equal Z-slabs, eval, count, the count all-gather overlapped
+    with the vertex pass, the face pass with the gathered counts -- and gather the mesh to rank 0
+    (distributed.gather_mesh): byte-identical to the oracle."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from implisolid_amd import scenes
+    R = 72
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    out = str(tmp_path / "mesh.npz")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IMPLISOLID_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "tests", "dist_worker.py"),
+           out, str(R)] + (["balanced"] if balanced else [])
+    r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    g = np.load(out)
+    shape, mc = scenes.config3_tree(), scenes.mc_settings(R, 1.0)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    assert np.array_equal(g["faces"], fr)
+    assert np.array_equal(g["verts"].view(np.uint32), vr.view(np.uint32))
+    if balanced:
+        assert len(g["cuts"]) == world + 1

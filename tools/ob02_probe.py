@@ -24,7 +24,9 @@ def main():
     sub["debug"] = {"post_subdiv_noise": 0.01}
     cases.append(("config2 R128 MC+3xOB02+subdiv", scenes.union_sphere_cube(), sub))
     for name, shape, mc in cases:
-        I.make_geometry(shape, mc)   # warm (JIT, buffers)
+        I.make_geometry(shape, mc)   # warm (buffers; the tree module compiles in the background)
+        I.jit_wait()
+        I.make_geometry(shape, mc)
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
