@@ -55,7 +55,8 @@ def program_flops(shape):
         composite = {"screw": (c + x) + (x + OP_FLOPS[10]) + (x + OP_FLOPS[11]),
                      "inf_screw": x + OP_FLOPS[10],
                      "screw_diff_two_plane": 2 * (c + x) + (x + OP_FLOPS[10]) + 2 * (x + OP_FLOPS[12]),
-                     "top_bottom_lid": x + OP_FLOPS[11], "half_plane": x + OP_FLOPS[12]}
+                     "top_bottom_lid": x + OP_FLOPS[11], "half_plane": x + OP_FLOPS[12],
+                     "screw_gradient_wrong": x + OP_FLOPS[10] + OP_FLOPS[11] + c}
         if t in composite:
             return composite[t]
         code = {"iellipsoid": 3, "ellipsoid": 3, "cube": 4, "icube": 4, "icylinder": 5, "cylinder": 5, "icone": 6,

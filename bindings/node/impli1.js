@@ -9,6 +9,11 @@ const native = require(path.join(__dirname, 'build', 'implisolid.node'));
 
 const impli1 = {
   build_geometry: (mp5_str, params_str) => native.build_geometry(mp5_str, params_str),
+  // worker path (worker_api.js:315-345): call_specs = JSON of {progressCallback_id, call_id,
+  // shape_id}; progress(verts, faces, progressCallback_id, shape_id, call_id) is called at each
+  // send_mesh_back_to_client point, as wwapi.send_progress_update is (worker_api.js:399-416)
+  build_geometry_u: (mp5_str, params_str, call_specs, progress) =>
+    native.build_geometry_u(mp5_str, params_str, call_specs || '{}', progress),
   get_v_size: () => native.get_v_size(),
   get_f_size: () => native.get_f_size(),
   get_v: () => native.get_v(),              // Float32Array, 3 per vertex

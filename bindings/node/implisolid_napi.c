@@ -72,6 +72,54 @@ static napi_value js_build_geometry(napi_env env, napi_callback_info info) {   /
     return undefined(env);
 }
 
+/* build_geometry_u(shape, mc, call_specs[, progress]) (mcc2.cpp:90): `progress` is called
+   synchronously with (verts Float32Array, faces Uint32Array, progressCallback_id, shape_id,
+   call_id) at every send_mesh_back_to_client point -- the arguments the reference's worker gives
+   wwapi.send_progress_update (js/worker_api.js:399-416). */
+static napi_env g_progress_env = NULL;
+static napi_value g_progress_fn = NULL;
+
+static void progress_hook(const float* verts, int nv, const int32_t* faces, int nf, int pid, int sid, int cid, void* user) {
+    (void)user;
+    napi_env env = g_progress_env;
+    napi_value argv[5], global, result;
+    if (!env || !g_progress_fn) return;
+    argv[0] = typed_copy(env, verts, (size_t)nv * 3, napi_float32_array);
+    argv[1] = typed_copy(env, faces, (size_t)nf * 3, napi_uint32_array);
+    argv[2] = number(env, pid);
+    argv[3] = number(env, sid);
+    argv[4] = number(env, cid);
+    if (!argv[0] || !argv[1]) return;
+    napi_get_global(env, &global);
+    napi_call_function(env, global, g_progress_fn, 5, argv, &result);
+}
+
+static napi_value js_build_geometry_u(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    napi_valuetype t = napi_undefined;
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    char* shape = argc > 0 ? arg_string(env, argv[0]) : NULL;
+    char* mc = argc > 1 ? arg_string(env, argv[1]) : NULL;
+    char* specs = argc > 2 ? arg_string(env, argv[2]) : NULL;
+    if (argc > 3) napi_typeof(env, argv[3], &t);
+    if (t == napi_function) {
+        g_progress_env = env;
+        g_progress_fn = argv[3];
+        implisolid_set_progress_callback(progress_hook, NULL);
+    }
+    if (shape && mc) build_geometry_u(shape, mc, specs ? specs : "{}");
+    if (t == napi_function) {
+        implisolid_set_progress_callback(NULL, NULL);
+        g_progress_env = NULL;
+        g_progress_fn = NULL;
+    }
+    free(shape);
+    free(mc);
+    free(specs);
+    return undefined(env);
+}
+
 static napi_value js_get_v_size(napi_env env, napi_callback_info info) { (void)info; return number(env, get_v_size()); }
 static napi_value js_get_f_size(napi_env env, napi_callback_info info) { (void)info; return number(env, get_f_size()); }
 
@@ -205,6 +253,7 @@ static napi_value js_program_info(napi_env env, napi_callback_info info) {   /* 
 
 static napi_value init(napi_env env, napi_value exports) {
     EXPORT("build_geometry", js_build_geometry);
+    EXPORT("build_geometry_u", js_build_geometry_u);
     EXPORT("get_v_size", js_get_v_size);
     EXPORT("get_f_size", js_get_f_size);
     EXPORT("get_v", js_get_v);

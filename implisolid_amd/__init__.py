@@ -37,7 +37,13 @@ ABI_SYMBOLS = [
     "implisolid_batch_download", "implisolid_batch_destroy",
     "implisolid_slab_create_range", "implisolid_slab_balance", "implisolid_cuts_from_layer_work", "implisolid_set_devices",
     "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
+    "implisolid_set_progress_callback",
 ]
+
+# implisolid_progress_callback (include/implisolid.h): verts, n_verts, faces, n_faces,
+# progress_callback_id, shape_id, call_id, user
+PROGRESS_CALLBACK = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 
 _lib = None
 
@@ -125,6 +131,7 @@ def lib():
         "implisolid_set_jit_bake": ([c_int], None),
         "implisolid_jit_wait": ([], None),
         "implisolid_jit_stats": ([ip, ctypes.POINTER(ctypes.c_double)], None),
+        "implisolid_set_progress_callback": ([PROGRESS_CALLBACK, c_void_p], None),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -277,6 +284,38 @@ def make_geometry(shape, mc_settings):
         L.get_f(f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nf)
     L.finish_geometry()
     return v, f
+
+
+def make_geometry_progressive(shape, mc_settings, call_specs=None):
+    """build_geometry_u with a progress hook (the reference's worker path, worker_api.js:315-345 and
+    send_progress_update :399-416): returns (verts, faces, updates), updates = the intermediate
+    meshes the library reported -- after marching cubes, after each repeat's vertex resampling and
+    after each centroid projection -- as (verts, faces, progressCallback_id, shape_id, call_id)."""
+    L = lib()
+    updates = []
+
+    def hook(vp, nv, fp_, nf, pid, sid, cid, user):
+        v = np.ctypeslib.as_array(vp, shape=(nv * 3,)).copy().reshape(nv, 3) if nv else np.zeros((0, 3), np.float32)
+        f = np.ctypeslib.as_array(fp_, shape=(nf * 3,)).copy().reshape(nf, 3) if nf else np.zeros((0, 3), np.int32)
+        updates.append((v, f, int(pid), int(sid), int(cid)))
+
+    cb = PROGRESS_CALLBACK(hook)
+    L.finish_geometry()
+    L.implisolid_set_progress_callback(cb, None)
+    try:
+        L.build_geometry_u(_s(shape), _s(mc_settings), _s(call_specs if call_specs is not None else {}))
+    finally:
+        L.implisolid_set_progress_callback(PROGRESS_CALLBACK(), None)
+    _check()
+    nv, nf = L.get_v_size(), L.get_f_size()
+    v = np.empty((nv, 3), np.float32)
+    f = np.empty((nf, 3), np.int32)
+    if nv:
+        L.get_v(v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), nv)
+    if nf:
+        L.get_f(f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nf)
+    L.finish_geometry()
+    return v, f, updates
 
 
 def get_pointset(name):

@@ -36,6 +36,30 @@ struct GeometryState {               // state_t, mcc2.cpp:165-193
 };
 GeometryState g_state;
 
+// worker_call_sepcs_t (worker_call_specs.hpp:7-47): the ids a progress update carries back to the
+// caller; build_geometry uses the default (all -1), build_geometry_u the parsed call specs
+struct CallSpecs {
+    int progress_callback_id = -1, call_id = -1, shape_id = -1;
+};
+implisolid_progress_callback g_progress = nullptr;
+void* g_progress_user = nullptr;
+
+// polygonizer::send_mesh_back_to_client (polygonizer_algorithm_ob02.hpp:180-220): the reference
+// hands the current mesh to wwapi.send_progress_update through EM_ASM after marching cubes, after
+// each repeat's resampling and after each projection.  Here the registered callback gets it; as in
+// the reference, get_v_ptr / get_f_ptr / get_v_size / get_f_size read that intermediate mesh while
+// the callback runs.  Nothing is copied when no callback is registered.
+void send_mesh_back_to_client(Ob02* ob, const CallSpecs& cs) {
+    if (!g_progress) return;
+    if (ob) {
+        g_state.verts.resize((size_t)ob->n_verts() * 3);
+        g_state.faces.resize((size_t)ob->n_faces() * 3);
+        ob->fetch(g_state.verts.data(), g_state.faces.data());
+    }
+    g_progress(g_state.verts.data(), (int)(g_state.verts.size() / 3), g_state.faces.data(),
+               (int)(g_state.faces.size() / 3), cs.progress_callback_id, cs.shape_id, cs.call_id, g_progress_user);
+}
+
 std::map<std::string, std::vector<float>> g_pointsets;   // pointset_set.hpp:8
 
 struct EvalService {                 // ifunction_service, mcc2.cpp:699-705
@@ -143,7 +167,7 @@ void multi_device_mc(const Program& prog, const MCSettings& st, std::vector<floa
     }
 }
 
-void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.cpp:309-444
+void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpecs& cs) {   // mcc2.cpp:309-444
     if (g_state.active) {
         report("build_geometry() called in a bad state.", false);
         return;
@@ -161,6 +185,7 @@ void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.c
         nf = (int64_t)g_state.faces.size() / 3;
         const bool refine = st.overall_repeats > 0 && (st.vresampl_iters > 0 || st.projection || st.subdiv);
         if (!refine) {
+            send_mesh_back_to_client(nullptr, cs);   // mcc2.cpp:351
             g_state.active = true;
             return;
         }
@@ -181,9 +206,14 @@ void grand_algorithm(const char* shape_json, const MCSettings& st) {   // mcc2.c
         ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf);
     }
     Ob02& ob = *ob_ptr;
+    send_mesh_back_to_client(&ob, cs);   // after polygonize_step_0 (mcc2.cpp:351)
     for (int rep = 0; rep < st.overall_repeats; ++rep) {
         for (int i = 0; i < st.vresampl_iters; ++i) ob.vertex_resampling(st.vresampl_c);   // step 1
-        if (st.projection) ob.centroids_projection(st.qem);                             // step 2
+        send_mesh_back_to_client(&ob, cs);                                             // mcc2.cpp:372
+        if (st.projection) {
+            ob.centroids_projection(st.qem);                                            // step 2
+            send_mesh_back_to_client(&ob, cs);                                         // mcc2.cpp:390
+        }
         if (st.subdiv && (st.overall_repeats <= 1 || rep == st.overall_repeats - 1)) {
             // polygonize_step_3 (polygonizer_algorithm_ob02.hpp:119-157): the noise is applied only
             // on the last repeat, scaled by the constant 10
@@ -255,7 +285,12 @@ int implisolid_slab_partition(int R, int rank, int nranks, int32_t out[3]) {
     return 0;
 }
 
-void build_geometry(const char* shape_json, const char* mc_json) {
+void implisolid_set_progress_callback(implisolid_progress_callback cb, void* user) {
+    g_progress = cb;
+    g_progress_user = user;
+}
+
+static void build_geometry_specs(const char* shape_json, const char* mc_json, const CallSpecs& cs) {
     g_last_error.clear();
     MCSettings st;
     try {
@@ -265,7 +300,7 @@ void build_geometry(const char* shape_json, const char* mc_json) {
         return;
     }
     try {
-        grand_algorithm(shape_json, st);
+        grand_algorithm(shape_json, st, cs);
     } catch (const InputError& e) {
         report(e.what(), true);
     } catch (const std::exception& e) {
@@ -273,14 +308,22 @@ void build_geometry(const char* shape_json, const char* mc_json) {
     }
 }
 
+void build_geometry(const char* shape_json, const char* mc_json) {   // worker_call_sepcs_t() defaults
+    build_geometry_specs(shape_json, mc_json, CallSpecs{});
+}
+
 void build_geometry_u(const char* shape_json, const char* mc_json, const char* call_specs) {
-    try {
-        (void)Json::parse(call_specs ? call_specs : "{}");   // worker_call_specs.hpp:28-40
+    CallSpecs cs;
+    try {   // worker_call_sepcs_t(json), worker_call_specs.hpp:28-40: get<int>(key, -1)
+        const Json j = Json::parse(call_specs ? call_specs : "{}");
+        cs.progress_callback_id = j.get_int("progressCallback_id", -1);
+        cs.call_id = j.get_int("call_id", -1);
+        cs.shape_id = j.get_int("shape_id", -1);
     } catch (const JsonError& e) {
         report(std::string("call_specs: ") + e.what(), true);
         return;
     }
-    build_geometry(shape_json, mc_json);
+    build_geometry_specs(shape_json, mc_json, cs);
 }
 
 int get_v_size(void) { return (int)(g_state.verts.size() / 3); }

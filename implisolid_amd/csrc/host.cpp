@@ -383,6 +383,18 @@ struct Builder {
                 [&] { leaf(NT_HALF_PLANE, eye, bot, 6); });
             return;
         }
+        if (t == "screw_gradient_wrong") {
+            // :435-479: inf_top_bot_bound(T, screw(T)) -- the screw under the JSON matrix T (no
+            // ignore_root_matrix here) bounded by the lid at the same x' = T^-1 x.  The node's
+            // gradient applies T^-T twice (inf_top_bot_bound.hpp:142-166 over screw.hpp:476-486),
+            // so the primitive carries a copy of the inverse
+            float prm[24] = {};
+            screw_params(d, prm);
+            matrix12(d, m);
+            if (!invert_matrix12(m, prm + 12)) throw InputError("singular MP5 matrix");
+            leaf(NT_SCREW_TBB, m, prm, 24);
+            return;
+        }
         if (t == "top_bottom_lid") {   // :480-506: the matrix is read (get_child) and never applied
             matrix12(d, m);
             leaf(NT_LID, eye);
@@ -422,7 +434,7 @@ struct Builder {
             csg(NT_DIFFERENCE, m, [&] { leaf(NT_EXTRUSION, eye, prm, n); }, [&] { leaf(NT_LID, eye); });
             return;
         }
-        static const char* unsupported[] = {"sdf_3d", "screw_gradient_wrong", "rawjscode"};
+        static const char* unsupported[] = {"sdf_3d", "rawjscode"};
         for (auto* u : unsupported)
             if (t == u) throw InputError("MP5 type \"" + t + "\" is outside the implemented node families");
         throw InputError("Invalid object you asked for: \"" + t + "\"");

@@ -402,6 +402,21 @@ __device__ __forceinline__ float lid_f(float z) {
     return (a < b) ? b : a;
 }
 
+// ---- inf_top_bot_bound (inf_top_bot_bound.hpp:65-96) over the screw of the same matrix
+//      ("screw_gradient_wrong", object_factory.hpp:435-479), at x' = M^-1 x: Eigen's
+//      imp.min(tbb * -1) = std::min(screw, -lid); prm = {twist, r0, delta} | (next row) M^-1
+__device__ __forceinline__ float tbb_f(const float* __restrict__ prm, float x, float y, float z) {
+    return stdmin(screw_f(prm, x, y, z), lid_f(z) * -1.f);
+}
+// :142-166: the screw's gradient with its own M^-T (screw.hpp:476-486), replaced by (0, 0, -1)
+// where z' >= 0.5 and (0, 0, 1) where z' <= -0.5, whichever operand the min chose; the node's
+// M^-T is applied after this (the leaf's grad_xform), as the reference applies it again
+__device__ __forceinline__ V3 tbb_g(const float* __restrict__ prm, float x, float y, float z) {
+    if (z >= 0.5f) return V3{0.f, 0.f, -1.f};
+    if (z <= -0.5f) return V3{0.f, 0.f, 1.f};
+    return grad_xform(prm + 12, screw_g(prm, x, y, z));
+}
+
 // ---- half_plane.hpp:150-190: GEMV (x - plane_point) . plane_vector; prm = {unit pv, pp}
 __device__ __forceinline__ float hp_f(const float* __restrict__ prm, float x, float y, float z) {
     const float d0 = x - prm[3], d1 = y - prm[4], d2 = z - prm[5];
@@ -503,6 +518,7 @@ __device__ __forceinline__ float prim_f(int t, const float* __restrict__ tab, co
         case NT_TETRA: return tet_f(prm, x, y, z);
         case NT_METABALLS: return meta_f(prm, x, y, z);
         case NT_EXTRUSION: return extr_f(prm, x, y);
+        case NT_SCREW_TBB: return tbb_f(prm, x, y, z);
         default: return dm_f(x, y, z);
     }
 }
@@ -520,6 +536,7 @@ __device__ __forceinline__ V3 prim_g(int t, const float* __restrict__ prm, float
         case NT_TETRA: return tet_g(prm, x, y, z);
         case NT_METABALLS: return meta_g(prm, x, y, z);
         case NT_EXTRUSION: return extr_g(prm, x, y);
+        case NT_SCREW_TBB: return tbb_g(prm, x, y, z);
         default: return dm_g(x, y, z);
     }
 }

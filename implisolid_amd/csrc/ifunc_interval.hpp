@@ -226,6 +226,9 @@ __device__ __forceinline__ Iv lid_iv(Box p) {
     const Iv a = sub(p.z, ivc(0.5f)), b = mulc(add(p.z, ivc(0.5f)), -1.f);
     return Iv{fmax2(a.lo, b.lo), fmax2(a.hi, b.hi)};
 }
+__device__ __forceinline__ Iv tbb_iv(const float* __restrict__ prm, Box p) {   // tbb_f
+    return stdmin_iv(screw_iv(prm, p), mulc(lid_iv(p), -1.f));
+}
 __device__ __forceinline__ Iv hp_iv(const float* __restrict__ prm, Box p) {
     return add(add(add(ivc(0.f), mulc(sub(p.x, ivc(prm[3])), prm[0])), mulc(sub(p.y, ivc(prm[4])), prm[1])),
                mulc(sub(p.z, ivc(prm[5])), prm[2]));
@@ -277,6 +280,7 @@ __device__ __forceinline__ Iv prim_iv(int t, const float* __restrict__ tab, floa
         case NT_TETRA: r = tet_iv(prm, p); break;
         case NT_METABALLS: r = meta_iv(prm, p); break;
         case NT_EXTRUSION: r = extr_iv(prm, p); break;
+        case NT_SCREW_TBB: r = tbb_iv(prm, p); break;
         default: r = dm_iv(p); break;
     }
     return settle(r);

@@ -91,6 +91,7 @@ const char* prim_call(int t) {
         case NT_HALF_PLANE: return "hp_f(P, ";
         case NT_TETRA: return "tet_f(P, ";
         case NT_METABALLS: return "meta_f(P, ";
+        case NT_SCREW_TBB: return "tbb_f(P, ";
         default: throw std::runtime_error("jit: unknown primitive");
     }
 }
@@ -225,6 +226,7 @@ const char* prim_iv_call(int t) {
         case NT_TETRA: return "tet_iv(P, ";
         case NT_METABALLS: return "meta_iv(P, ";
         case NT_EXTRUSION: return "extr_iv(P, ";
+        case NT_SCREW_TBB: return "tbb_iv(P, ";
         default: throw std::runtime_error("jit: unknown primitive");
     }
 }

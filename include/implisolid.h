@@ -24,8 +24,19 @@ extern "C" {
    a message) while a previous result is active: call finish_geometry() first (:316-319). */
 void build_geometry(const char* shape_parameters_json, const char* mc_parameters_json);
 /* mcc2.cpp:90 (declared, body commented out at :296-302): build_geometry + worker call specs
-   ({"progressCallback_id", "call_id", "shape_id"}); progress callbacks are not emitted. */
+   ({"progressCallback_id", "call_id", "shape_id"}, worker_call_specs.hpp:28-40; each -1 when
+   absent).  Progress updates carry those ids (see implisolid_set_progress_callback). */
 void build_geometry_u(const char* shape_parameters_json, const char* mc_parameters_json, const char* call_specs);
+/* Additive: the progress hook of build_geometry / build_geometry_u -- the reference's
+   polygonizer::send_mesh_back_to_client (polygonizer_algorithm_ob02.hpp:180-220), which posts the
+   current mesh to wwapi.send_progress_update (js/worker_api.js:399-416) after marching cubes
+   (mcc2.cpp:351), after each repeat's vertex resampling (:372) and after each centroid projection
+   (:390).  The callback runs synchronously on the calling thread with the intermediate mesh
+   (library-owned, valid during the call; get_v_ptr / get_f_ptr / get_v_size / get_f_size read the
+   same mesh meanwhile) and the call specs' ids (-1 for plain build_geometry).  NULL unregisters. */
+typedef void (*implisolid_progress_callback)(const float* verts, int n_verts, const int32_t* faces, int n_faces,
+                                             int progress_callback_id, int shape_id, int call_id, void* user);
+void implisolid_set_progress_callback(implisolid_progress_callback cb, void* user);
 /* mcc2.cpp:91 / :470-473  vertex count */
 int get_v_size(void);
 /* mcc2.cpp:92 / :466-469  face count */

@@ -27,7 +27,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 
 (UNION, INTERSECTION, DIFFERENCE, ELLIPSOID, CUBE, CYLINDER, CONE, HEART, TORUS, DMUSHROOM, SCREW, LID, HALF_PLANE,
- TETRA, METABALLS, EXTRUSION) = range(16)
+ TETRA, METABALLS, EXTRUSION, SCREW_TBB) = range(17)
 
 # MP5 "type" strings accepted by object_factory.hpp:86-653 for the plain-arithmetic node families.
 PRIMITIVE_TYPES = {
@@ -40,7 +40,7 @@ PRIMITIVE_TYPES = {
     "itorus": TORUS,                         # :163-173
 }
 # types the reference knows but this build does not evaluate (Eigen-based or JS callbacks)
-KNOWN_UNSUPPORTED = {"sdf_3d", "screw_gradient_wrong", "rawjscode"}
+KNOWN_UNSUPPORTED = {"sdf_3d", "rawjscode"}
 
 
 class OrNode(ctypes.Structure):
@@ -307,6 +307,8 @@ def mp5_to_nodes(shape, ignore_root_matrix=False):
             first = add(DIFFERENCE, list(EYE12), s, top)
             bot = add(HALF_PLANE, list(EYE12), prm=_half_plane_params(["0", "0", "-1"], ["0", "0", "-0.25"]))
             return add(DIFFERENCE, m, first, bot)
+        if t == "screw_gradient_wrong":            # :435-479: inf_top_bot_bound(T, screw(T)), no
+            return add(SCREW_TBB, _matrix12(d), prm=_screw_params(d))   # ignore_root_matrix
         if t == "top_bottom_lid":                  # :480-506: the matrix is read, then unused
             _matrix12(d)
             return add(LID, list(EYE12))

@@ -484,6 +484,10 @@ static float eval1(const or_node* N, int i, const float p[3]) {
         case OR_TETRA: return tet_f(l, n->prm);
         case OR_METABALLS: return meta_f(l, n->prm);
         case OR_EXTRUSION: return extr_f(l, n->prm);
+        case OR_SCREW_TBB: {        /* inf_top_bot_bound.hpp:65-96: imp.min(tbb * -1), std::min */
+            const float s = screw_f(l, n->prm), t = lid_f(l) * -1.f;
+            return (t < s) ? t : s;
+        }
     }
     return NAN;
 }
@@ -518,6 +522,15 @@ static void grad1(const or_node* N, int i, const float p[3], float o[3]) {
         case OR_TETRA: tet_g(l, n->prm, g); break;
         case OR_METABALLS: meta_g(l, n->prm, g); break;
         case OR_EXTRUSION: extr_g(l, n->prm, g); break;
+        case OR_SCREW_TBB:          /* inf_top_bot_bound.hpp:142-166 over screw.hpp:450-486 */
+            if (l[2] >= 0.5) { g[0] = 0.f; g[1] = 0.f; g[2] = -1.f; }
+            else if (l[2] <= -0.5) { g[0] = 0.f; g[1] = 0.f; g[2] = 1.f; }
+            else {
+                float gs[3];
+                screw_g(l, n->prm, gs);
+                grad_xform(n->minv, gs, g);   /* the screw's own M^-T; the node's follows below */
+            }
+            break;
         default: g[0] = g[1] = g[2] = NAN;
     }
     grad_xform(n->minv, g, o);

@@ -41,6 +41,7 @@ enum {
     OR_TETRA,          /* tetrahedron               implicit_function/tetrahedron.hpp            */
     OR_METABALLS,      /* meta_ball_Rydgard         implicit_function/meta_balls_Rydgard.hpp     */
     OR_EXTRUSION,      /* extrusion (convex n-gon)  implicit_function/extrusion.hpp + 2d/GDT/convex_polygon.hpp */
+    OR_SCREW_TBB,      /* inf_top_bot_bound(screw)  implicit_function/inf_top_bot_bound.hpp ("screw_gradient_wrong") */
     OR_NTYPES
 };
 

@@ -218,7 +218,8 @@ def _screw_family():
                 {"type": "top_bottom_lid", "matrix": scenes.st(1, 0, 0, 0)}]},
             "config3_twist": scenes.config3_tree(),
             "tetrahedron": scenes.tetrahedron(), "meta_balls": scenes.meta_balls(), "extrusion": scenes.extrusion(6),
-            "extrusion_tri": scenes.extrusion(3, scale=0.5)}
+            "extrusion_tri": scenes.extrusion(3, scale=0.5),
+            "screw_gradient_wrong": dict(scenes.twist(1, 0, 0, 0.0625), type="screw_gradient_wrong")}
 
 
 @pytest.mark.parametrize("name", sorted(_screw_family()))
@@ -242,6 +243,30 @@ def test_screw_values_follow_the_reference_formula(oracle):
     x, y, z = p[:, 0].astype(np.float64), p[:, 1].astype(np.float64), p[:, 2].astype(np.float64)
     ref = 1 / 3 + (1 / 6) * np.sin(2 * np.pi * ((z + 0.5) / 0.5) - np.arctan2(y, x)) - np.hypot(x, y)
     assert np.abs(f - ref).max() < 2e-6
+
+
+def test_screw_gradient_wrong_semantics(oracle):
+    """inf_top_bot_bound over the screw (object_factory.hpp:435-479, inf_top_bot_bound.hpp:65-166):
+    the value is min(screw, -lid) at x' = T^-1 x, and the gradient ignores which operand won --
+    (0, 0, -/+1) outside |z'| < 0.5, the screw's gradient with T^-T applied twice inside."""
+    from implisolid_amd import scenes
+    sh = dict(scenes.twist(0.5, 0, 0, 0.125), type="screw_gradient_wrong")
+    tree = oracle.mp5_to_nodes(json.dumps(sh))
+    inf = oracle.mp5_to_nodes(json.dumps(dict(sh, type="inf_screw")))
+    rng = np.random.default_rng(8)
+    p = rng.uniform(-0.6, 0.6, (4000, 3)).astype(np.float32)
+    zl = (p[:, 2] - np.float32(0.125)) * np.float32(2)               # z' = T^-1 x (scale 1/2, exact)
+    lid = np.maximum(zl - np.float32(0.5), -(zl + np.float32(0.5)))
+    fs = oracle.eval_implicit(inf, p)
+    f = oracle.eval_implicit(tree, p)
+    assert np.array_equal(f, np.where(-lid < fs, -lid, fs).astype(np.float32))
+    g, gs = oracle.eval_gradient(tree, p), oracle.eval_gradient(inf, p)
+    up, dn = zl >= 0.5, zl <= -0.5
+    mid = ~(up | dn)
+    assert up.any() and dn.any() and mid.any()
+    assert np.array_equal(g[up], np.tile([0, 0, -2], (up.sum(), 1)).astype(np.float32))
+    assert np.array_equal(g[dn], np.tile([0, 0, 2], (dn.sum(), 1)).astype(np.float32))
+    assert np.array_equal(g[mid], gs[mid] * np.float32(2))           # T^-T = 2 I once more
 
 
 def test_screw_factory_errors(impli):
@@ -293,6 +318,7 @@ def test_ob02_properties(oracle):
 def _header_functions():
     txt = open(os.path.join(ROOT, "include", "implisolid.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"typedef[^;]*;", "", txt)   # function-pointer typedefs declare no symbol
     names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\([^;{]*\)\s*;", txt, flags=re.M)
     return sorted(set(names))
 
@@ -525,7 +551,7 @@ def test_node_addon_exports(impli):
     r = subprocess.run(["node", "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    need = {"build_geometry", "get_v_size", "get_f_size", "get_v", "get_f", "finish_geometry", "set_object",
+    need = {"build_geometry", "build_geometry_u", "get_v_size", "get_f_size", "get_v", "get_f", "finish_geometry", "set_object",
             "unset_object", "set_x", "unset_x", "calculate_implicit_values", "get_values",
             "calculate_implicit_gradients", "get_gradients", "get_pointset", "about"}
     assert need <= set(out["keys"])
