@@ -37,7 +37,8 @@ ABI_SYMBOLS = [
     "implisolid_batch_download", "implisolid_batch_destroy",
     "implisolid_slab_create_range", "implisolid_slab_balance", "implisolid_cuts_from_layer_work", "implisolid_set_devices",
     "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
-    "implisolid_set_progress_callback",
+    "implisolid_set_progress_callback", "implisolid_ob02_profile", "implisolid_last_build_stats",
+    "implisolid_jit_compile_points",
 ]
 
 # implisolid_progress_callback (include/implisolid.h): verts, n_verts, faces, n_faces,
@@ -132,6 +133,10 @@ def lib():
         "implisolid_jit_wait": ([], None),
         "implisolid_jit_stats": ([ip, ctypes.POINTER(ctypes.c_double)], None),
         "implisolid_set_progress_callback": ([PROGRESS_CALLBACK, c_void_p], None),
+        "implisolid_ob02_profile": ([c_int], None),
+        "implisolid_jit_compile_points": ([c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)],
+                                          ctypes.c_int64),
+        "implisolid_last_build_stats": ([ctypes.POINTER(ctypes.c_double)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -230,12 +235,14 @@ def jit_stats():
     return {"mode": out[0], "bake": bool(out[1]), "compiled": out[2], "disk_hits": out[3], "compile_s": secs.value}
 
 
-def jit_compile(shape):
-    """Host-only: (code-object bytes, compile seconds, generated source) of the shape's tree kernel."""
+def jit_compile(shape, points=False):
+    """Host-only: (code-object bytes, compile seconds, generated source) of the shape's tree kernel
+    module (points=True: its point module)."""
     L = lib()
     buf = ctypes.create_string_buffer(1 << 20)
     secs = ctypes.c_double(0)
-    n = L.implisolid_jit_compile(_s(shape), buf, len(buf), ctypes.byref(secs))
+    fn = L.implisolid_jit_compile_points if points else L.implisolid_jit_compile
+    n = fn(_s(shape), buf, len(buf), ctypes.byref(secs))
     if n < 0:
         raise ImplisolidError(last_error())
     return int(n), float(secs.value), buf.value.decode()
@@ -316,6 +323,27 @@ def make_geometry_progressive(shape, mc_settings, call_specs=None):
         L.get_f(f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nf)
     L.finish_geometry()
     return v, f, updates
+
+
+OB02_STAGES = ("topology", "resample", "edge_fold", "project", "qem", "subdiv", "fetch")
+
+
+def ob02_profile(on):
+    """Per-stage wall times and evaluation counts of the OB02 steps for following builds (drains
+    the stream at every stage boundary: for breakdowns, not for timing whole builds)."""
+    lib().implisolid_ob02_profile(1 if on else 0)
+
+
+def last_build_stats():
+    """Diagnostics of the last build_geometry: bisection cap hits, projection evaluations and stage
+    times (profiled builds), the last average edge length, faces and vertices."""
+    out = (ctypes.c_double * 13)()
+    if lib().implisolid_last_build_stats(out) != 0:
+        raise ImplisolidError(last_error())
+    d = {"bisection_cap_hits": int(out[0]), "projection_evals": int(out[1]), "avg_edge": float(out[2]),
+         "faces": int(out[10]), "verts": int(out[11]), "jit_launches": int(out[12])}
+    d["stage_ms"] = dict(zip(OB02_STAGES, [float(x) for x in out[3:10]]))
+    return d
 
 
 def get_pointset(name):

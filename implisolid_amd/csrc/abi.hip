@@ -61,6 +61,8 @@ void send_mesh_back_to_client(Ob02* ob, const CallSpecs& cs) {
 }
 
 std::map<std::string, std::vector<float>> g_pointsets;   // pointset_set.hpp:8
+std::unique_ptr<Ob02> g_ob02;   // the refinement state of the last build
+bool g_ob02_profile = false;
 
 struct EvalService {                 // ifunction_service, mcc2.cpp:699-705
     bool has_object = false;
@@ -177,7 +179,7 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
     hipStream_t s = abi_stream();
     E.set_object(prog);
     int64_t nv = 0, nf = 0;
-    static std::unique_ptr<Ob02> ob_ptr;   // one refinement state, its buffers reused by every build
+    std::unique_ptr<Ob02>& ob_ptr = g_ob02;   // one refinement state, its buffers reused by every build
     if (!g_devices.empty()) {
         // polygonize_step_0 over several devices: balanced Z-slabs, concatenated on the host
         multi_device_mc(prog, st, g_state.verts, g_state.faces);
@@ -196,6 +198,7 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         IMPLI_HIP(hipMemcpyAsync(dv.p, g_state.verts.data(), (size_t)nv * 12, hipMemcpyHostToDevice, s));
         IMPLI_HIP(hipMemcpyAsync(df.p, g_state.faces.data(), (size_t)nf * 12, hipMemcpyHostToDevice, s));
         if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+        ob_ptr->set_profile(g_ob02_profile);
         ob_ptr->load_mesh(dv.as<float>(), nv, df.as<int32_t>(), nf);
     } else {
         E.set_grid(st.resolution, st.box, 0, 1);
@@ -203,6 +206,7 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         nv = c.n_verts();
         nf = c.n_faces();
         if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+        ob_ptr->set_profile(g_ob02_profile);
         ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf);
     }
     Ob02& ob = *ob_ptr;
@@ -324,6 +328,28 @@ void build_geometry_u(const char* shape_json, const char* mc_json, const char* c
         return;
     }
     build_geometry_specs(shape_json, mc_json, cs);
+}
+
+void implisolid_ob02_profile(int on) { g_ob02_profile = on != 0; }
+
+int implisolid_last_build_stats(double out[13]) {
+    g_last_error.clear();
+    for (int k = 0; k < 13; ++k) out[k] = 0.0;
+    if (!g_ob02) return 0;
+    try {
+        g_ob02->read_counters();
+        out[0] = g_ob02->bisection_cap_hits();
+        out[1] = (double)g_ob02->projection_evals();
+        out[2] = g_ob02->last_average_edge();
+        for (int k = 0; k < Ob02::kStages; ++k) out[3 + k] = g_ob02->stage_ms()[k];
+        out[3 + Ob02::kStages] = (double)g_ob02->n_faces();
+        out[4 + Ob02::kStages] = (double)g_ob02->n_verts();
+        out[5 + Ob02::kStages] = (double)g_ob02->jit_launches();
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
 }
 
 int get_v_size(void) { return (int)(g_state.verts.size() / 3); }
@@ -503,11 +529,11 @@ void about(void) {
     std::fprintf(stderr, "CONFIG: ROOT_TOLERANCE=%g \n", (double)(float)(0.001 / 10.0));
 }
 
-int64_t implisolid_jit_compile(const char* shape_json, char* source_out, int64_t capacity, double* seconds) {
+static int64_t jit_compile_kind(const char* shape_json, int kind, char* source_out, int64_t capacity, double* seconds) {
     g_last_error.clear();
     try {
         const Program p = compile_mp5(shape_json, false);
-        const std::string src = TreeJit::kernel_source(p);
+        const std::string src = kind == TreeJit::kPoints ? TreeJit::point_source(p) : TreeJit::kernel_source(p);
         if (source_out && capacity > 0) {
             const size_t n = std::min<size_t>(src.size(), (size_t)capacity - 1);
             std::memcpy(source_out, src.data(), n);
@@ -521,6 +547,14 @@ int64_t implisolid_jit_compile(const char* shape_json, char* source_out, int64_t
         report(e.what(), false);
         return -1;
     }
+}
+
+int64_t implisolid_jit_compile(const char* shape_json, char* source_out, int64_t capacity, double* seconds) {
+    return jit_compile_kind(shape_json, TreeJit::kBricks, source_out, capacity, seconds);
+}
+
+int64_t implisolid_jit_compile_points(const char* shape_json, char* source_out, int64_t capacity, double* seconds) {
+    return jit_compile_kind(shape_json, TreeJit::kPoints, source_out, capacity, seconds);
 }
 
 int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int32_t info[4], float* mats_out) {

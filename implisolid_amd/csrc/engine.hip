@@ -30,6 +30,19 @@ void DevBuf::release() {
     bytes = 0;
 }
 
+void HostBuf::reserve(size_t n) {
+    if (n <= bytes && p) return;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    IMPLI_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+    bytes = want;
+}
+void HostBuf::release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
 static std::atomic<int> g_pruning{-1};
 
 void Engine::set_pruning(int level) { g_pruning.store(level < 0 ? 0 : level > 2 ? 2 : level); }
@@ -143,6 +156,8 @@ void Engine::set_object(const Program& prog) {
     prog_host_ = prog;
     jit_requested_ = false;
     jit_slot_ = nullptr;
+    pt_requested_ = false;
+    pt_slot_ = nullptr;
     jit_fn_ = nullptr;
     have_object_ = true;
 }
@@ -339,6 +354,18 @@ std::vector<int> balance_cuts(const Program& prog, int R, const float box[6], in
     return cuts_from_layer_work(probe.listed_per_layer(s), (int64_t)bg.nbx * bg.nby, R, nranks);
 }
 
+const float* Engine::d_mats() const {
+    return reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
+}
+
+const TreeJit::PointKernels* Engine::point_jit() {
+    if (!pt_requested_) {
+        pt_slot_ = TreeJit::instance().request(prog_host_, TreeJit::kPoints);
+        pt_requested_ = true;
+    }
+    return (pt_slot_ && pt_slot_->ready.load(std::memory_order_acquire)) ? &pt_slot_->pk : nullptr;
+}
+
 void Engine::ensure_jit() {
     // the object's tree module is requested once (TreeJit: compiled now, or on a background thread
     // while the interpreter kernels run); every eval uses it as soon as it is loaded
@@ -430,6 +457,15 @@ SlabCounts Engine::marching_cubes(hipStream_t s) {
 
 void Engine::eval_points(const float* d_xyz, int64_t n, float* d_f, float* d_grad, hipStream_t s) {
     if (!have_object_) throw InputError("engine: no object set");
+    if (const TreeJit::PointKernels* pk = point_jit()) {
+        if (n <= 0) return;
+        const float* m = d_mats();
+        const float* tab = rabbit_.as<float>();
+        void* args[] = {&m, &tab, &d_xyz, &n, &d_f, &d_grad};
+        TreeJit::launch(pk->points, (unsigned)((n + 255) / 256), args, s, "impli_pt_points");
+        IMPLI_HIP(hipGetLastError());
+        return;
+    }
     launch_eval_points(prog_.as<Program>(), depth_, rabbit_.as<float>(), d_xyz, n, d_f, d_grad, s);
     IMPLI_HIP(hipGetLastError());
 }

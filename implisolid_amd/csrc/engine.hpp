@@ -26,6 +26,15 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// pinned host memory (grow-only), for device-to-host copies at full PCIe rate
+struct HostBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void reserve(size_t n);
+    void release();
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
 struct SlabCounts {
     uint32_t own_total, tri_total, act_total, halo_own;
     uint32_t n_verts() const { return own_total - halo_own; }
@@ -92,6 +101,11 @@ public:
     // true if the last eval_field ran the JIT-compiled tree kernel
     bool used_jit() const { return jit_fn_ != nullptr; }
     const float* d_rabbit() const { return rabbit_.as<float>(); }
+    // the object's matrices as the JIT kernels read them (the Program's mats array)
+    const float* d_mats() const;
+    // the object's point module (OB02 passes, direct evaluation): requested on first use (compiled
+    // in the background in async mode); null until loaded -- the interpreter kernels run meanwhile
+    const TreeJit::PointKernels* point_jit();
 
     DevBuf& scratch(int k) { return scratch_[k]; }
 
@@ -120,6 +134,8 @@ private:
     Program prog_host_{};
     TreeJit::Slot* jit_slot_ = nullptr;   // the object's module (null: JIT off); may still compile
     bool jit_requested_ = false;
+    TreeJit::Slot* pt_slot_ = nullptr;     // the point module
+    bool pt_requested_ = false;
     hipFunction_t jit_fn_ = nullptr;       // what the last eval used (null: interpreter)
     bool counters_fresh_ = false;   // eval_field zeroed the counters; the next count() need not
     uint32_t mark_id_ = 0;          // id of the last pruned eval's unit marks (umark_)

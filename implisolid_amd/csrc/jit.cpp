@@ -275,6 +275,74 @@ struct IvEmitter {
     }
 };
 
+// Point version of the tree (eval_f / eval_fg of ifunc_device.hpp, straight-line): every node's
+// transform is the generic xform() -- points may be NaN (OB02 vertices of singular faces), and
+// dropping a zero coefficient would stop a NaN the interpreter propagates -- no pruning modes, and
+// with `grad` the gradient: the leaf's M^-T prim_g, the CSG's selected child (the difference's
+// second negated) under the node's M^-T (transformed_*.hpp:73-93).
+const char* prim_g_call(int t) {
+    switch (t) {
+        case NT_ELLIPSOID: return "egg_g(";
+        case NT_CUBE: return "cube_g(";
+        case NT_CYLINDER: return "cyl_g(";
+        case NT_CONE: return "cone_g(";
+        case NT_HEART: return "heart_g(";
+        case NT_TORUS: return "torus_g(";
+        case NT_DMUSHROOM: return "dm_g(";
+        case NT_SCREW: return "screw_g(P, ";
+        case NT_HALF_PLANE: return "hp_g(P, ";
+        case NT_TETRA: return "tet_g(P, ";
+        case NT_METABALLS: return "meta_g(P, ";
+        case NT_SCREW_TBB: return "tbb_g(P, ";
+        default: throw std::runtime_error("jit: unknown primitive");
+    }
+}
+
+struct PtEmitter {
+    const std::vector<Node>& nodes;
+    const Program& prog;
+    bool grad;
+    std::ostringstream out;
+    int counter = 0;
+
+    // returns the variable holding f; the gradient is "g" + the same id
+    std::string emit(int i, const std::string& x, const std::string& y, const std::string& z, int ind) {
+        const Node& n = nodes[i];
+        const int id = counter++;
+        const std::string pad(ind, ' ');
+        const std::string q = "q" + std::to_string(id), f = "f" + std::to_string(id), g = "g" + std::to_string(id);
+        const std::string M = "M + " + std::to_string(12 * n.mat);
+        out << pad << "const V3 " << q << " = xform(" << M << ", " << x << ", " << y << ", " << z << ");\n";
+        if (n.leaf) {
+            const std::string call = n.type == NT_LID         ? "lid_f(" + q + ".z)"
+                                     : n.type == NT_EXTRUSION ? with_params("extr_f(P, ", n.prm) + q + ".x, " + q + ".y)"
+                                                              : with_params(prim_call(n.type), n.prm) + q + ".x, " + q + ".y, " + q + ".z)";
+            out << pad << "const float " << f << " = " << call << ";\n";
+            if (grad) {
+                const std::string gc = n.type == NT_LID         ? std::string("V3{0.f, 0.f, 1.f}")
+                                       : n.type == NT_EXTRUSION ? with_params("extr_g(P, ", n.prm) + q + ".x, " + q + ".y)"
+                                                                : with_params(prim_g_call(n.type), n.prm) + q + ".x, " + q + ".y, " + q + ".z)";
+                out << pad << "const V3 " << g << " = grad_xform(" << M << ", " << gc << ");\n";
+            }
+            return f;
+        }
+        const std::string fa = emit(n.child[0], q + ".x", q + ".y", q + ".z", ind);
+        const std::string fb = emit(n.child[1], q + ".x", q + ".y", q + ".z", ind);
+        std::string sel;
+        if (n.type == NT_UNION) sel = "(" + fa + " > " + fb + ") ? " + fa + " : " + fb;
+        else if (n.type == NT_INTERSECTION) sel = "(" + fa + " > " + fb + ") ? " + fb + " : " + fa;
+        else sel = "(" + fa + " < -" + fb + ") ? " + fa + " : -" + fb;
+        out << pad << "const float " << f << " = " << sel << ";\n";
+        if (grad) {
+            const std::string ga = "g" + fa.substr(1), gb = "g" + fb.substr(1);
+            const std::string gbs = n.type == NT_DIFFERENCE ? "V3{-" + gb + ".x, -" + gb + ".y, -" + gb + ".z}" : gb;
+            out << pad << "const V3 " << g << " = grad_xform(" << M << ", csg_first(" << n.type << ", " << fa << ", " << fb
+                << ") ? " << ga << " : " << gbs << ");\n";
+        }
+        return f;
+    }
+};
+
 void rtc_check(hiprtcResult r, const char* what) {
     if (r != HIPRTC_SUCCESS) throw std::runtime_error(std::string(what) + ": " + hiprtcGetErrorString(r));
 }
@@ -369,13 +437,23 @@ void TreeJit::build(Slot* slot) {
         (void)hipGetDevice(&prev);
         if (prev != slot->device) IMPLI_HIP_THROW(hipSetDevice(slot->device));
         Kernels k;
-        const bool ok = hipModuleLoadData(&slot->mod, code.data()) == hipSuccess &&
-                        hipModuleGetFunction(&k.bricks, slot->mod, "impli_eval_bricks") == hipSuccess &&
-                        hipModuleGetFunction(&k.coarse, slot->mod, "impli_coarse_modes") == hipSuccess &&
-                        hipModuleGetFunction(&k.refine, slot->mod, "impli_brick_refine") == hipSuccess;
+        PointKernels pk;
+        bool ok = hipModuleLoadData(&slot->mod, code.data()) == hipSuccess;
+        if (ok && slot->kind == kBricks)
+            ok = hipModuleGetFunction(&k.bricks, slot->mod, "impli_eval_bricks") == hipSuccess &&
+                 hipModuleGetFunction(&k.coarse, slot->mod, "impli_coarse_modes") == hipSuccess &&
+                 hipModuleGetFunction(&k.refine, slot->mod, "impli_brick_refine") == hipSuccess;
+        if (ok && slot->kind == kPoints)
+            ok = hipModuleGetFunction(&pk.cnormals, slot->mod, "impli_pt_centroid_normals") == hipSuccess &&
+                 hipModuleGetFunction(&pk.prep, slot->mod, "impli_pt_project_prep") == hipSuccess &&
+                 hipModuleGetFunction(&pk.early, slot->mod, "impli_pt_project_early") == hipSuccess &&
+                 hipModuleGetFunction(&pk.late, slot->mod, "impli_pt_project_late") == hipSuccess &&
+                 hipModuleGetFunction(&pk.normals, slot->mod, "impli_pt_normals_at") == hipSuccess &&
+                 hipModuleGetFunction(&pk.points, slot->mod, "impli_pt_points") == hipSuccess;
         if (prev != slot->device) (void)hipSetDevice(prev);
         if (!ok) throw std::runtime_error("hipModuleLoadData / hipModuleGetFunction failed");
         slot->k = k;
+        slot->pk = pk;
         slot->ready.store(true, std::memory_order_release);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "implisolid: tree JIT failed, using the interpreter (%s)\n", std::string(e.what()).substr(0, 400).c_str());
@@ -416,12 +494,12 @@ void TreeJit::shutdown() {   // at exit: drop queued work, finish what is compil
     workers_.clear();
 }
 
-TreeJit::Slot* TreeJit::request(const Program& p) {
+TreeJit::Slot* TreeJit::request(const Program& p, int kind) {
     const int m = mode();
     if (m == kOff) return nullptr;
     std::string src;
     try {
-        src = kernel_source(p, bake());
+        src = kind == kPoints ? point_source(p) : kernel_source(p, bake());
     } catch (const std::exception& e) {
         std::fprintf(stderr, "implisolid: tree JIT skipped (%s)\n", e.what());
         return nullptr;
@@ -438,6 +516,7 @@ TreeJit::Slot* TreeJit::request(const Program& p) {
             slot = it->second;
         } else {
             slot = new Slot();
+            slot->kind = kind;
             slot->src = std::move(src);
             slot->device = dev;
             cache_.emplace(key, slot);
@@ -540,6 +619,47 @@ std::string TreeJit::kernel_source(const Program& p, bool bake) {
       << "    uint64_t* modes, uint8_t* cls) {\n"
       << "    impli::brick_refine_body(impli::JitIv{M, tab, tab_range}, g, bg, cg, cmodes, clist, ccount, modes, cls);\n}\n"
 ;
+    return s.str();
+}
+
+std::string TreeJit::point_source(const Program& p) {
+    std::vector<Node> nodes;
+    int next = 0;
+    const int root = parse(p, 0, nodes, next);
+    if (next != p.n_instr) throw std::runtime_error("jit: trailing instructions");
+    PtEmitter ef{nodes, p, false};
+    const std::string f = ef.emit(root, "x0", "y0", "z0", 4);
+    PtEmitter eg{nodes, p, true};
+    const std::string fg = eg.emit(root, "x0", "y0", "z0", 4);
+    std::ostringstream s;
+    s << kPrelude << "#include \"ob02_device.hpp\"\n"
+      << "namespace impli {\nusing namespace dev;\n"
+      << "__device__ __forceinline__ float tree_pf(const float* __restrict__ M, const float* __restrict__ tab,\n"
+      << "                                         float x0, float y0, float z0) {\n"
+      << ef.out.str() << "    return " << f << ";\n}\n"
+      << "__device__ __forceinline__ float tree_pfg(const float* __restrict__ M, const float* __restrict__ tab,\n"
+      << "                                          float x0, float y0, float z0, V3& g_out) {\n"
+      << eg.out.str() << "    g_out = g" << fg.substr(1) << ";\n    return " << fg << ";\n}\n"
+      << "struct JitPt {\n    const float* M;\n    const float* tab;\n"
+      << "    __device__ __forceinline__ float f(float x, float y, float z) const { return tree_pf(M, tab, x, y, z); }\n"
+      << "    __device__ __forceinline__ float fg(float x, float y, float z, V3& g) const { return tree_pfg(M, tab, x, y, z, g); }\n"
+      << "};\n}  // namespace impli\n"
+      << "using impli::JitPt;\nusing impli::ob::ProjArgs;\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_centroid_normals(const float* M, const float* tab,\n"
+      << "    const float* v, const int32_t* f, int64_t nf, float* C, float* N) {\n"
+      << "    impli::ob::centroid_normals_body(JitPt{M, tab}, v, f, nf, C, N);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_prep(const float* M, const float* tab, ProjArgs a) {\n"
+      << "    impli::ob::project_prep_body(JitPt{M, tab}, a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_early(const float* M, const float* tab, ProjArgs a) {\n"
+      << "    impli::ob::project_early_body(JitPt{M, tab}, a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
+      << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_normals_at(const float* M, const float* tab,\n"
+      << "    const float* P, int64_t n, float* G) {\n"
+      << "    impli::ob::normals_at_body(JitPt{M, tab}, P, n, G);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_points(const float* M, const float* tab,\n"
+      << "    const float* xyz, int64_t n, float* f, float* grad) {\n"
+      << "    impli::ob::points_body(JitPt{M, tab}, xyz, n, f, grad);\n}\n";
     return s.str();
 }
 

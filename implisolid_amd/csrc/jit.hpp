@@ -32,6 +32,9 @@ public:
     // object's transformation matrices baked in as exact literals (bake: one module per object,
     // no matrix loads on the kernels' dependency chains)
     static std::string kernel_source(const Program& p, bool bake = false);
+    // C++ source of the point kernels for this shape (OB02 passes and direct evaluation,
+    // ob02_device.hpp over straight-line f / (f, grad) code; NaN-exact: no transform specialisation)
+    static std::string point_source(const Program& p);
 
     // hipRTC-compile the source to a gfx950 code object (no GPU needed); throws with the log
     static std::vector<char> compile(const std::string& src);
@@ -41,11 +44,18 @@ public:
         hipFunction_t coarse = nullptr;   // interval pass, coarse boxes (coarse_modes_body)
         hipFunction_t refine = nullptr;   // interval pass, bricks of mixed boxes (brick_refine_body)
     };
+    struct PointKernels {                 // the point module (ob02_device.hpp bodies)
+        hipFunction_t cnormals = nullptr, prep = nullptr, early = nullptr, late = nullptr, normals = nullptr,
+                      points = nullptr;
+    };
+    enum Kind { kBricks = 0, kPoints = 1 };
     // One compiled module (one source on one device).  Slots live as long as the process; `ready`
     // is set (release) once `k` holds the loaded kernels, `failed` if compilation or loading failed.
     struct Slot {
         std::atomic<bool> ready{false}, failed{false};
         Kernels k;
+        PointKernels pk;
+        int kind = kBricks;
         hipModule_t mod = nullptr;
         std::string src;
         int device = 0;
@@ -61,7 +71,7 @@ public:
     // data (one module per tree shape); baked modules hold the object's matrices as literals (one per
     // object: no matrix loads on the dependency chains).
     enum Mode { kOff = 0, kSync = 1, kAsync = 2 };
-    Slot* request(const Program& p);
+    Slot* request(const Program& p, int kind = kBricks);
     // block until every scheduled compilation has finished (bench / batch setup)
     void wait_idle();
     // compile the modules of many programs (sync, up to `threads` host threads); request() then

@@ -69,6 +69,8 @@ void build_case_table(CaseInfo out[256]) {
             if (slot >= 0 && c.rank[slot] < 0) c.rank[slot] = (int8_t)r++;
         }
         c.nown = (uint8_t)r;
+        static const int owner_of_edge[12] = {5, 4, 4, 6, 2, 0, 0, 1, 3, 2, 0, 1};   // = c_edge_owner_idx
+        for (int k = 0; k < n; ++k) c.owners = (uint8_t)(c.owners | (1u << owner_of_edge[c.tri[k]]));
         // k_mc_count relies on two table properties (checked here for every case): the owned
         // edges a case's triangles use are exactly its crossing owned edges (Bourke edges 5 =
         // corners 5-6, 6 = 6-7, 10 = 2-6), and every non-trivial case has a triangle.
@@ -252,57 +254,69 @@ __global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells(const CaseInfo* _
     mc_cells_body(cases, g, b);
 }
 
-// owner offset (dx, dy, dz subtracted) and owned slot of each Bourke edge
-__constant__ int8_t c_edge_owner[12][4] = {
-    {0, 1, 1, 1}, {0, 0, 1, 0}, {0, 0, 1, 1}, {1, 0, 1, 0}, {0, 1, 0, 1}, {0, 0, 0, 0},
-    {0, 0, 0, 1}, {1, 0, 0, 0}, {1, 1, 0, 2}, {0, 1, 0, 2}, {0, 0, 0, 2}, {1, 0, 0, 2},
-};
-
 // The face grid: the XCD remap below is a permutation of the blocks only when it is a multiple of 8.
 constexpr unsigned kFacesBlocks = 2048;
 static_assert(kFacesBlocks % 8 == 0, "k_mc_faces' XCD remap needs a multiple of 8 blocks");
 
+// Bourke edge e of a cell is owned (edge 5, 6 or 10) by one of 7 cells: the cell itself, or its
+// neighbour at -x, -y, -x-y, -z, -y-z, -x-z; owner index and owned slot per edge
+__constant__ uint8_t c_edge_owner_idx[12] = {5, 4, 4, 6, 2, 0, 0, 1, 3, 2, 0, 1};
+__constant__ uint8_t c_edge_slot[12] = {1, 0, 1, 0, 1, 0, 1, 0, 2, 2, 2, 2};
+
+struct __attribute__((packed, aligned(4))) IdTriple { uint32_t a, b, c; };
+
+// K4: one lane per active cell, XCD-aware (the dispatcher puts block b on XCD b % 8, so XCD x takes
+// the x-th eighth of the records in cell order and the owner cells it gathers from stay in its L2).
+// A lane loads the owned-id triples of the owner cells its case uses -- one 12-byte load per owner,
+// at most 7, instead of one load per triangle corner (up to 15) -- spreads them to the 12 edges in
+// LDS, and writes each triangle as one 12-byte store.  (Vector-memory issue, not bytes, bounded the
+// corner-per-load version: 3 % VALU, 53 % of wave time ready but not issued.)
 __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     __shared__ CaseInfo s_case[256];
-    __shared__ int32_t s_off[12];
-    __shared__ int32_t s_slot[12];
+    __shared__ uint32_t s_w[12][256];   // per lane: the vertex id of each of its cell's 12 edges
     const int t = threadIdx.x;
     s_case[t] = cases[t];
-    if (t < 12) {
-        const int64_t m = g.m;
-        s_off[t] = (int32_t)(c_edge_owner[t][0] + c_edge_owner[t][1] * m + c_edge_owner[t][2] * m * m);
-        s_slot[t] = c_edge_owner[t][3];
-    }
     __syncthreads();
+    const int64_t m = g.m;
+    const uint32_t off[7] = {0u, 1u, (uint32_t)m, (uint32_t)(m + 1), (uint32_t)(m * m), (uint32_t)(m * m + m),
+                             (uint32_t)(m * m + 1)};
     const uint32_t n_rec = b.counters[4];
     const uint32_t lim = n_rec < (uint64_t)b.cap_rec ? n_rec : (uint32_t)b.cap_rec;
     uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
     if (b.gathered)
         for (int r = 0; r < b.rank; ++r) Voff += b.gathered[4 * r] - b.gathered[4 * r + 3];
     const uint32_t* __restrict__ vid3 = b.vid3;
-    // XCD-aware: the dispatcher puts block b on XCD b % 8, so XCD x takes the x-th eighth of the
-    // records (cell order): the owner cells a face gathers from stay in that XCD's L2
     const uint32_t nb = gridDim.x, lb = (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u;
     const uint32_t per = (lim + nb - 1u) / nb, i_end = min(lim, (lb + 1u) * per);
     for (uint32_t i = lb * per + t; i < i_end; i += 256) {
         const uint4 r = b.records[i];
         const uint32_t L = r.x, ci = r.y, fbase = r.z;
         const CaseInfo& C = s_case[ci];
-        const int n3 = 3 * C.ntri;
-        if (fbase + C.ntri > (uint64_t)b.cap_f) { *b.overflow = 1u; continue; }
-        // all corner ids gathered before any store: unconditional loads (corners past the case's
-        // triangles re-read corner 0), so the 15 round trips overlap instead of queueing behind
-        // the stores (faces and vid3 may alias for the compiler)
-        uint32_t v[15];
+        const int ntri = C.ntri;
+        if (fbase + ntri > (uint64_t)b.cap_f) { *b.overflow = 1u; continue; }
+        // every owner's triple loaded unconditionally (an owner the case does not use re-reads the
+        // cell's own triple), all before any use; the owners a case uses always exist
+        const uint32_t need = C.owners;
+        IdTriple w[7];
 #pragma unroll
-        for (int k = 0; k < 15; ++k) {
-            const int e = C.tri[k < n3 ? k : 0];
-            v[k] = vid3[(size_t)(L - (uint32_t)s_off[e]) * 3 + s_slot[e]];
+        for (int o = 0; o < 7; ++o) {
+            const uint32_t cell = ((need >> o) & 1u) ? L - off[o] : L;
+            w[o] = *reinterpret_cast<const IdTriple*>(vid3 + (size_t)cell * 3);
+        }
+#pragma unroll
+        for (int e = 0; e < 12; ++e) {
+            const IdTriple& q = w[c_edge_owner_idx[e]];
+            const int sl = c_edge_slot[e];
+            s_w[e][t] = sl == 0 ? q.a : sl == 1 ? q.b : q.c;
         }
         int32_t* out = b.faces + 3 * (size_t)fbase;
-#pragma unroll
-        for (int k = 0; k < 15; ++k)
-            if (k < n3) out[k] = (int32_t)(Voff + v[k]);
+        for (int k = 0; k < ntri; ++k) {
+            IdTriple f;
+            f.a = Voff + s_w[C.tri[3 * k]][t];
+            f.b = Voff + s_w[C.tri[3 * k + 1]][t];
+            f.c = Voff + s_w[C.tri[3 * k + 2]][t];
+            *reinterpret_cast<IdTriple*>(out + 3 * k) = f;
+        }
     }
 }
 

@@ -13,7 +13,8 @@ struct CaseInfo {
     int8_t rank[3];     // first-use rank of owned slot (edge 5, 6, 10) or -1
     uint8_t pad;
     uint8_t tri[15];    // Bourke edge ids, 3 per triangle
-    uint8_t pad2[11];
+    uint8_t owners;     // bit o: the case uses an edge owned by owner cell o (mc.hip k_mc_faces)
+    uint8_t pad2[10];
 };
 static_assert(sizeof(CaseInfo) == 32, "CaseInfo layout");
 // MC pipeline.  Cells are numbered L = row * m + (x - 1), row = (z - cz0) * m + (y - 1); a unit is

@@ -12,12 +12,19 @@
 //   step 2    compute_average_edge_length cp:70-82; set_centers_on_surface cp:421-1214;
 //             bisection bisection.hpp:117-459; vertex_apply_qem qem.hpp:321-599
 // (cp = centroids_projection.cpp)
+#include <chrono>
 #include <cmath>
 #include <cstring>
+#include <deque>
+#include <future>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "ifunc_device.hpp"
 #include "ob02.hpp"
+#include "ob02_device.hpp"
+#include "jit.hpp"
 
 namespace impli {
 
@@ -35,8 +42,6 @@ struct EdgeTab {
 
 namespace {
 
-constexpr float kRootTol = (float)(0.001 / 10.0);   // configs.hpp:33
-constexpr int kBisectCap = 200;                      // the reference has no cap (bisection.hpp:360-372)
 constexpr uint64_t kEmpty = ~0ull;
 
 #define DEPTH_LAUNCH(depth, KERNEL, GRID, BLOCK, STREAM, ...)                              \
@@ -49,7 +54,6 @@ constexpr uint64_t kEmpty = ~0ull;
 
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
-__device__ __forceinline__ float norm2f(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
 
 // ---- topology --------------------------------------------------------------------------------
 __global__ void k_degree(const int32_t* __restrict__ f, int64_t n3, uint32_t* __restrict__ deg) {
@@ -308,28 +312,38 @@ __global__ __launch_bounds__(256) void k_rand_noise(float* __restrict__ v, int64
     }
 }
 
-// ---- step 1 ----------------------------------------------------------------------------------
-__device__ __forceinline__ V3 centroid(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t j) {
-    const int32_t a = f[3 * j], b = f[3 * j + 1], c = f[3 * j + 2];
-    // compute_centroids implicit_vectorised_algorithms.hpp:161-171
-    return V3{(v[3 * a] + v[3 * b] + v[3 * c]) / (float)(3.0), (v[3 * a + 1] + v[3 * b + 1] + v[3 * c + 1]) / (float)(3.0),
-              (v[3 * a + 2] + v[3 * b + 2] + v[3 * c + 2]) / (float)(3.0)};
-}
+// ---- the tree-evaluating passes over the interpreter (ob02_device.hpp; the JIT point module has
+//      the same bodies over tree-specialised code) -------------------------------------------------
+using namespace ob;
 
 template <int D>
 __global__ __launch_bounds__(256) void k_centroid_normals(const Program* __restrict__ prog, const float* __restrict__ tab,
                                                           const float* __restrict__ v, const int32_t* __restrict__ f,
                                                           int64_t nf, float* __restrict__ C, float* __restrict__ N) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= nf) return;
-    const V3 c = centroid(v, f, j);
-    V3 g;
-    (void)eval_fg<D>(prog, tab, c.x, c.y, c.z, g);
-    const float nm = norm2f(g.x, g.y, g.z);   // normalize_1111 normalise_inplace.hpp:60-70
-    C[3 * j] = c.x; C[3 * j + 1] = c.y; C[3 * j + 2] = c.z;
-    N[3 * j] = g.x / nm; N[3 * j + 1] = g.y / nm; N[3 * j + 2] = g.z / nm;
+    centroid_normals_body(InterpPt<D>{prog, tab}, v, f, nf, C, N);
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_project_prep(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                      ProjArgs a) {
+    project_prep_body(InterpPt<D>{prog, tab}, a);
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_project_early(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                       ProjArgs a) {
+    project_early_body(InterpPt<D>{prog, tab}, a);
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_project_late(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                      ProjArgs a) {
+    project_late_body(InterpPt<D>{prog, tab}, a);
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_normals_at(const Program* __restrict__ prog, const float* __restrict__ tab,
+                                                    const float* __restrict__ P, int64_t n, float* __restrict__ G) {
+    normals_at_body(InterpPt<D>{prog, tab}, P, n, G);
 }
 
+// ---- step 1 ----------------------------------------------------------------------------------
 __device__ __forceinline__ float kij(int64_t i, int64_t j, const float* __restrict__ C, const float* __restrict__ N);
 
 // glibc 2.35 e_acosf.c (fdlibm), the libm std::acos(float) of vertex_resampling.hpp:75 resolves to
@@ -417,163 +431,6 @@ __global__ void k_edge_norms(const float* __restrict__ v, const int32_t* __restr
     o[3 * j] = norm2f(a[0] - b[0], a[1] - b[1], a[2] - b[2]);
     o[3 * j + 1] = norm2f(a[0] - c[0], a[1] - c[1], a[2] - c[2]);
     o[3 * j + 2] = norm2f(c[0] - b[0], c[1] - b[1], c[2] - b[2]);
-}
-
-__device__ __forceinline__ float get_sign(float v) { return (v > kRootTol) ? 1.f : (v < -kRootTol) ? -1.f : 0.f; }
-
-// normalise_inplace (normalise_inplace.hpp:26-54)
-__device__ __forceinline__ V3 normalise_min(V3 a, float min_norm) {
-    float nm = norm2f(a.x, a.y, a.z);
-    nm = (nm < min_norm) ? 1.0f : nm;
-    const float factor = (float)(1.0 / (double)nm);
-    return V3{a.x * factor, a.y * factor, a.z * factor};
-}
-
-__device__ __forceinline__ V3 cross3(V3 a, V3 b) {
-    return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
-}
-
-// produce_facet_normals (implicit_vectorised_algorithms.hpp:52-133)
-__device__ __forceinline__ V3 facet_normal(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t j) {
-    const float* p0 = v + 3 * f[3 * j];
-    const float* p1 = v + 3 * f[3 * j + 1];
-    const float* p2 = v + 3 * f[3 * j + 2];
-    const float x1 = p1[0] - p0[0], y1 = p1[1] - p0[1], z1 = p1[2] - p0[2];
-    const float x2 = p2[0] - p0[0], y2 = p2[1] - p0[1], z2 = p2[2] - p0[2];
-    float x = y1 * z2 - z1 * y2, y = z1 * x2 - x1 * z2, z = x1 * y2 - y1 * x2;
-    const float micro = (float)(1.0 / 1000.0), nano = (float)((double)micro / 1000.0);
-    const float min_area = (30 * nano) * (30 * nano);
-    const float n2 = x * x + y * y + z * z;
-    if (n2 < min_area * min_area) {
-        const float o = (float)(1.0 / (double)sqrtf(3.0f));
-        return V3{o, o, o};
-    }
-    const float n = sqrtf(n2);
-    return V3{x / n, y / n, z / n};
-}
-
-struct ProjArgs {
-    const float* v;
-    const int32_t* f;
-    int64_t nf;
-    const float* alphas;
-    int nal;
-    float max_dist;
-    const float* pert;      // type-2 perturbations (3 per centroid), only for the late pass
-    float* out;             // projected centroids
-    float* fn;              // facet normals (written by the early pass)
-    float* fc;              // f(centroid) (written by the early pass)
-    uint32_t* pend;         // early pass: unresolved centroid list; [0] is the count at pend_count
-    uint32_t* pend_count;
-    uint32_t* cap_hits;
-};
-
-// cp:904-1191 for one centroid: zero tests, swap (x1 outside), vectorised bisection restated per point
-template <int D>
-__device__ void finalize(const Program* prog, const float* tab, V3 x, float fcv, bool found, V3 best, float* out,
-                         uint32_t* cap_hits) {
-    const float f2 = eval_f<D>(prog, tab, best.x, best.y, best.z);
-    const bool z2 = fabsf(f2) <= kRootTol, z1 = fabsf(fcv) <= kRootTol;
-    if (z1) best = x;
-    V3 r;
-    if (found && !(z1 || z2)) {
-        V3 x1 = x, x2 = best;
-        if (f2 < -kRootTol) { const V3 t = x1; x1 = x2; x2 = t; }
-        V3 mid = x1;
-        int it = 0;
-        for (; it < kBisectCap; ++it) {
-            mid.x = (float)((double)(x1.x + x2.x) / 2.);
-            mid.y = (float)((double)(x1.y + x2.y) / 2.);
-            mid.z = (float)((double)(x1.z + x2.z) / 2.);
-            const float vm = eval_f<D>(prog, tab, mid.x, mid.y, mid.z);
-            if (fabsf(vm) <= kRootTol) break;
-            if (vm < -kRootTol) x1 = mid;
-            if (vm > +kRootTol) x2 = mid;
-        }
-        if (it == kBisectCap) atomicAdd(cap_hits, 1u);
-        r = mid;
-    } else if (z1 || z2) {
-        r = best;
-    } else {
-        r = x;
-    }
-    out[0] = r.x; out[1] = r.y; out[2] = r.z;
-}
-
-template <int D>
-__device__ __forceinline__ bool try_direction(const Program* prog, const float* tab, V3 x, V3 d, float sc,
-                                              const float* alphas, int na, float max_dist, V3& best) {
-    for (int ai = 0; ai < na; ++ai) {
-        const float cc = max_dist * alphas[ai];   // (length_factor * alpha) * 4.0 / 4.0 is exact
-        const V3 p{x.x + cc * d.x, x.y + cc * d.y, x.z + cc * d.z};
-        const float fa = eval_f<D>(prog, tab, p.x, p.y, p.z);
-        if (get_sign(fa) * sc <= 0) { best = p; return true; }
-    }
-    return false;
-}
-
-// set_centers_on_surface, direction types 0 (gradient) and 1 (mesh normal)
-template <int D>
-__global__ __launch_bounds__(256) void k_project_early(const Program* __restrict__ prog, const float* __restrict__ tab,
-                                                       ProjArgs a) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= a.nf) return;
-    const V3 x = centroid(a.v, a.f, j);
-    const V3 fnv = facet_normal(a.v, a.f, j);
-    a.fn[3 * j] = fnv.x; a.fn[3 * j + 1] = fnv.y; a.fn[3 * j + 2] = fnv.z;
-    V3 g;
-    const float fcv = eval_fg<D>(prog, tab, x.x, x.y, x.z, g);
-    a.fc[j] = fcv;
-    V3 gd = normalise_min(g, 0.000001f);
-    const float sc = get_sign(fcv);
-    if (sc < 0.0f) { gd.x = -gd.x; gd.y = -gd.y; gd.z = -gd.z; }
-    const V3 d0{-gd.x * sc, -gd.y * sc, -gd.z * sc};
-    V3 best = x;
-    bool found = try_direction<D>(prog, tab, x, d0, sc, a.alphas, a.nal, a.max_dist, best);
-    if (!found) found = try_direction<D>(prog, tab, x, fnv, sc, a.alphas, a.nal < 10 ? a.nal : 10, a.max_dist, best);
-    if (!found) {
-        a.pend[atomicAdd(a.pend_count, 1u)] = (uint32_t)j;
-        return;
-    }
-    finalize<D>(prog, tab, x, fcv, true, best, a.out + 3 * j, a.cap_hits);
-}
-
-// types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes)
-template <int D>
-__global__ __launch_bounds__(256) void k_project_late(const Program* __restrict__ prog, const float* __restrict__ tab,
-                                                      ProjArgs a) {
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= *a.pend_count) return;
-    const int64_t j = a.pend[k];
-    const V3 x = centroid(a.v, a.f, j);
-    const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
-    const float fcv = a.fc[j];
-    const float sc = get_sign(fcv);
-    const int n10 = a.nal < 10 ? a.nal : 10;
-    const V3 pv{a.pert[3 * j], a.pert[3 * j + 1], a.pert[3 * j + 2]};
-    V3 z = cross3(fnv, pv);               // cp:250-259, add_inplace is a no-op (F9)
-    const float nz = norm2f(z.x, z.y, z.z);
-    z = V3{z.x / nz, z.y / nz, z.z / nz};  // normalize_1111
-    V3 z2 = normalise_min(cross3(fnv, z), 0.000001f);   // cp:297-312
-    V3 best = x;
-    bool found = try_direction<D>(prog, tab, x, z, sc, a.alphas, n10, a.max_dist, best);
-    if (!found) found = try_direction<D>(prog, tab, x, z2, sc, a.alphas, n10, a.max_dist, best);
-    for (int ax = 0; ax < 3 && !found; ++ax) {
-        const V3 d{ax == 0 ? 1.f : 0.f, ax == 1 ? 1.f : 0.f, ax == 2 ? 1.f : 0.f};
-        found = try_direction<D>(prog, tab, x, d, sc, a.alphas, n10, a.max_dist, best);
-    }
-    finalize<D>(prog, tab, x, fcv, found, found ? best : x, a.out + 3 * j, a.cap_hits);
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void k_normals_at(const Program* __restrict__ prog, const float* __restrict__ tab,
-                                                    const float* __restrict__ P, int64_t n, float* __restrict__ G) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    V3 g;
-    (void)eval_fg<D>(prog, tab, P[3 * j], P[3 * j + 1], P[3 * j + 2], g);
-    const float nm = norm2f(g.x, g.y, g.z);
-    G[3 * j] = g.x / nm; G[3 * j + 1] = g.y / nm; G[3 * j + 2] = g.z / nm;
 }
 
 // ---- QEM: Eigen 3.3 JacobiSVD<Matrix3f> restated (Eigen/src/SVD/JacobiSVD.h, Jacobi/Jacobi.h) ----
@@ -748,34 +605,62 @@ std::vector<float> make_alpha_list(float initial_step, float min_step, float max
 }
 
 // boost::random::mt11213b (seed 12) + uniform_01<float>: make_random_pm1(n, 3, 1e-6)
+// (make_random_pm1.hpp:15-29): the twist in three runs (no index wrap inside), tempering of a
+// whole block at once, then uniform_01's rejection of draws that round to 1.0f
 std::vector<float> make_random_pm1(int64_t n, float amplitude) {
-    std::vector<uint32_t> x(351);
+    constexpr int N = 351, M = 175;
+    constexpr uint32_t UM = 0xffffffffu << 19, LM = ~UM, A = 0xccab8ee7u;
+    uint32_t x[N], t[N];
     x[0] = 12u;
-    for (int i = 1; i < 351; ++i) x[i] = 1812433253u * (x[i - 1] ^ (x[i - 1] >> 30)) + (uint32_t)i;
-    int idx = 351;
-    auto next = [&]() -> uint32_t {
-        if (idx >= 351) {
-            for (int k = 0; k < 351; ++k) {
-                const uint32_t y = (x[k] & (0xffffffffu << 19)) | (x[(k + 1) % 351] & ~(0xffffffffu << 19));
-                x[k] = x[(k + 175) % 351] ^ (y >> 1) ^ ((y & 1u) ? 0xccab8ee7u : 0u);
-            }
-            idx = 0;
-        }
-        uint32_t z = x[idx++];
-        z ^= (z >> 11);
-        z ^= (z << 7) & 0x31b6ab00u;
-        z ^= (z << 15) & 0xffe50000u;
-        z ^= (z >> 17);
-        return z;
-    };
+    for (int i = 1; i < N; ++i) x[i] = 1812433253u * (x[i - 1] ^ (x[i - 1] >> 30)) + (uint32_t)i;
     const float factor = 1.0f / ((float)4294967295u + 1.0f);
+    const double amp = (double)amplitude;
     std::vector<float> out((size_t)(3 * n));
-    for (auto& o : out) {
-        float r;
-        do { r = (float)next() * factor; } while (!(r < 1.0f));
-        o = (float)(((double)r * 2.0 - 1.0) * (double)amplitude);
+    size_t o = 0;
+    while (o < out.size()) {
+        int k = 0;
+        for (; k < N - M; ++k) {
+            const uint32_t y = (x[k] & UM) | (x[k + 1] & LM);
+            x[k] = x[k + M] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        }
+        for (; k < N - 1; ++k) {
+            const uint32_t y = (x[k] & UM) | (x[k + 1] & LM);
+            x[k] = x[k + M - N] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        }
+        const uint32_t y = (x[N - 1] & UM) | (x[0] & LM);
+        x[N - 1] = x[M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        for (int i = 0; i < N; ++i) {
+            uint32_t z = x[i];
+            z ^= (z >> 11);
+            z ^= (z << 7) & 0x31b6ab00u;
+            z ^= (z << 15) & 0xffe50000u;
+            z ^= (z >> 17);
+            t[i] = z;
+        }
+        for (int i = 0; i < N && o < out.size(); ++i) {
+            const float r = (float)t[i] * factor;
+            if (!(r < 1.0f)) continue;
+            out[o++] = (float)(((double)r * 2.0 - 1.0) * amp);
+        }
     }
     return out;
+}
+
+// the perturbations depend on the face count alone (seeded afresh on every call): the last few
+// face counts' tables are kept, so rebuilding a mesh of the same size does not redraw them
+std::shared_ptr<const std::vector<float>> random_pm1_cached(int64_t n) {
+    static std::mutex mu;
+    static std::deque<std::pair<int64_t, std::shared_ptr<const std::vector<float>>>> cache;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        for (auto& e : cache)
+            if (e.first == n) return e.second;
+    }
+    auto v = std::make_shared<const std::vector<float>>(make_random_pm1(n, 0.000001f));
+    std::lock_guard<std::mutex> lock(mu);
+    cache.emplace_front(n, v);
+    if (cache.size() > 4) cache.pop_back();
+    return v;
 }
 
 }  // namespace
@@ -791,12 +676,18 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     snaps_.clear();
     pointsets_.clear();
     cap_hits_ = 0;
+    evals_ = 0;
+    jit_launches_ = 0;
     avg_edge_ = 0.f;
+    for (double& t : stage_ms_) t = 0.0;
+    Stage st(this, kStageTopology);
+    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 64, s));   // pending count, cap hits, evaluations
     verts_.reserve((size_t)(nv + 1) * 12);
     vnew_.reserve((size_t)(nv + 1) * 12);
     faces_.reserve((size_t)(nf + 1) * 12);
     if (nv) IMPLI_HIP(hipMemcpyAsync(verts_.p, d_verts, (size_t)nv * 12, hipMemcpyDeviceToDevice, s));
     if (nf) IMPLI_HIP(hipMemcpyAsync(faces_.p, d_faces, (size_t)nf * 12, hipMemcpyDeviceToDevice, s));
+    start_perturbations();   // host thread, overlaps the topology and resampling kernels
     build_topology();
 }
 
@@ -881,6 +772,11 @@ const std::map<std::string, std::vector<float>>& Ob02::pointsets() {
 }
 
 Ob02::~Ob02() {
+    if (pert_job_.valid()) pert_job_.wait();
+    if (norms_ready_) (void)hipEventDestroy(norms_ready_);
+    host_norms_.release();
+    dir_.release();
+    evals_buf_.release();
     for (DevBuf* b : {&verts_, &faces_, &vnew_, &cen_, &nrm_, &w_, &fof_, &uoff_, &ulst_, &etab_, &deg_, &proj_, &grad_,
                       &fn_, &norms_, &alphas_, &pert_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_})
         b->release();
@@ -890,9 +786,19 @@ Ob02::~Ob02() {
 void Ob02::vertex_resampling(float c) {
     if (!nf) return;
     if (!topo_valid_) build_topology();
+    Stage st(this, kStageResample);
     store_pointset("pre_resampling_vertices", verts_.as<float>(), nv, true);   // vertex_resampling.hpp:176-180
-    DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), verts_.as<float>(),
-                 faces_.as<int32_t>(), nf, cen_.as<float>(), nrm_.as<float>());
+    if (const TreeJit::PointKernels* pk = E.point_jit()) {
+        const float *m = E.d_mats(), *tab = E.d_rabbit(), *v = verts_.as<float>();
+        const int32_t* f = faces_.as<int32_t>();
+        float *C = cen_.as<float>(), *N = nrm_.as<float>();
+        void* args[] = {&m, &tab, &v, &f, &nf, &C, &N};
+        TreeJit::launch(pk->cnormals, blocks_for(nf), args, s, "impli_pt_centroid_normals");
+        ++jit_launches_;
+    } else {
+        DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), verts_.as<float>(),
+                     faces_.as<int32_t>(), nf, cen_.as<float>(), nrm_.as<float>());
+    }
     k_face_weights<<<blocks_for(nf), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(), nf, c, w_.as<float>());
     k_resample<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), w_.as<float>(), cen_.as<float>(),
                                               nv, vnew_.as<float>());
@@ -901,76 +807,158 @@ void Ob02::vertex_resampling(float c) {
     store_pointset("post_resampling_vertices", verts_.as<float>(), nv, true);   // :207-211
 }
 
-float Ob02::average_edge_length() {
+// compute_average_edge_length (cp:70-82) is one serial float chain in face order: the terms are
+// computed on the device and copied to pinned host memory; the chain runs on the host (one GPU lane
+// adds a dependent term every ~4 cycles at 2.4 GHz, slower than a host core) while the GPU runs the
+// projection's prep pass, which does not need the average.
+void Ob02::start_edge_fold() {
     norms_.reserve((size_t)(nf + 1) * 12);
     k_edge_norms<<<blocks_for(nf), 256, 0, s>>>(verts_.as<float>(), faces_.as<int32_t>(), nf, norms_.as<float>());
-    std::vector<float> h((size_t)nf * 3);
-    IMPLI_HIP(hipMemcpyAsync(h.data(), norms_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
-    IMPLI_HIP(hipStreamSynchronize(s));
+    host_norms_.reserve((size_t)nf * 12);
+    IMPLI_HIP(hipMemcpyAsync(host_norms_.p, norms_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
+    if (!norms_ready_) IMPLI_HIP(hipEventCreateWithFlags(&norms_ready_, hipEventDisableTiming));
+    IMPLI_HIP(hipEventRecord(norms_ready_, s));
+}
+
+float Ob02::finish_edge_fold() {
+    IMPLI_HIP(hipEventSynchronize(norms_ready_));
+    const float* h = host_norms_.as<float>();
     float el = 0.f;   // the reference starts from an uninitialised float (F8a); defined as 0
-    for (float x : h) el += x;
+    for (int64_t k = 0; k < 3 * nf; ++k) el += h[k];
     return (float)((double)el / (3. * (double)nf));
+}
+
+// make_random_pm1(nf, 3, 1e-6) (centroids_projection.cpp:239-262) is seeded afresh (seed 12) on
+// every call, so it depends on nf alone: it is generated once per face count on a host thread,
+// started when the mesh is loaded, and uploaded once -- the projection never waits for it unless
+// a centroid needs the type-2 directions before the thread is done
+void Ob02::start_perturbations() {
+    if (pert_nf_ == nf || nf == 0) return;
+    if (pert_job_.valid()) pert_job_.wait();
+    const int64_t n = nf;
+    pert_job_ = std::async(std::launch::async, [n] { return random_pm1_cached(n); });
+    pert_nf_ = nf;
+    pert_uploaded_ = false;
+}
+
+const float* Ob02::perturbations() {
+    if (pert_nf_ != nf) start_perturbations();
+    if (!pert_uploaded_) {
+        pert_host_ = pert_job_.get();
+        pert_.reserve(pert_host_->size() * 4 + 16);
+        IMPLI_HIP(hipMemcpyAsync(pert_.p, pert_host_->data(), pert_host_->size() * 4, hipMemcpyHostToDevice, s));
+        pert_uploaded_ = true;
+    }
+    return pert_.as<float>();
 }
 
 void Ob02::centroids_projection(bool enable_qem) {
     if (!nf) return;
     if (!topo_valid_) build_topology();
-    const float avg = average_edge_length();
-    avg_edge_ = avg;
-    const std::vector<float> alphas = make_alpha_list((float)(avg * 1.0), (float)(0.001 * 1.0), avg, 20);
-    alphas_.reserve((alphas.size() + 1) * 4);
-    if (!alphas.empty())
-        IMPLI_HIP(hipMemcpyAsync(alphas_.p, alphas.data(), alphas.size() * 4, hipMemcpyHostToDevice, s));
+    Stage st(this, kStageEdgeFold);
+    start_edge_fold();
     proj_.reserve((size_t)(nf + 1) * 12);
     fn_.reserve((size_t)(nf + 1) * 12);
+    dir_.reserve((size_t)(nf + 1) * 12);
     pend_.reserve((size_t)(nf + 2) * 4);
+    if (profile_) evals_buf_.reserve((size_t)(nf + 1) * 4);
     DevBuf& fcbuf = w_;   // f(centroid) per face; the resampling weights are dead here
-    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 64, s));
+    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 4, s));   // pending count (the cap hits accumulate)
     ProjArgs a{};
     a.v = verts_.as<float>();
     a.f = faces_.as<int32_t>();
     a.nf = nf;
-    a.alphas = alphas_.as<float>();
-    a.nal = (int)alphas.size();
-    a.max_dist = avg;
     a.out = proj_.as<float>();
     a.fn = fn_.as<float>();
     a.fc = fcbuf.as<float>();
     a.pend = pend_.as<uint32_t>();
     a.pend_count = misc_.as<uint32_t>();
     a.cap_hits = misc_.as<uint32_t>() + 1;
-    // pre_p_centroids (cp:1236-1238): the centroids themselves
-    if (capture_pointsets) {
-        DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), a.v, a.f, nf,
-                     cen_.as<float>(), nrm_.as<float>());
-        store_pointset("pre_p_centroids", cen_.as<float>(), nf, false);
+    a.cen = cen_.as<float>();
+    a.dir = dir_.as<float>();
+    a.evals = profile_ ? evals_buf_.as<uint32_t>() : nullptr;
+    const TreeJit::PointKernels* pk = E.point_jit();   // one choice for the whole projection
+    const float *jm = E.d_mats(), *jtab = E.d_rabbit();
+    void* jargs[] = {&jm, &jtab, &a};
+    if (pk) {
+        TreeJit::launch(pk->prep, blocks_for(nf), jargs, s, "impli_pt_project_prep");
+        ++jit_launches_;
+    } else {
+        DEPTH_LAUNCH(E.depth(), k_project_prep, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), a);
     }
-    DEPTH_LAUNCH(E.depth(), k_project_early, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), a);
-    uint32_t hm[2];
-    IMPLI_HIP(hipMemcpyAsync(hm, misc_.p, 8, hipMemcpyDeviceToHost, s));
-    IMPLI_HIP(hipStreamSynchronize(s));
-    if (hm[0] > 0) {   // some centroids need the randomised directions (types 2-6)
-        const std::vector<float> pert = make_random_pm1(nf, 0.000001f);
-        pert_.reserve(pert.size() * 4);
-        IMPLI_HIP(hipMemcpyAsync(pert_.p, pert.data(), pert.size() * 4, hipMemcpyHostToDevice, s));
-        a.pert = pert_.as<float>();
-        DEPTH_LAUNCH(E.depth(), k_project_late, blocks_for(hm[0]), 256, s, E.d_program(), E.d_rabbit(), a);
-        IMPLI_HIP(hipMemcpyAsync(hm, misc_.p, 8, hipMemcpyDeviceToHost, s));
-        IMPLI_HIP(hipStreamSynchronize(s));
-    }
-    cap_hits_ += hm[1];
+    store_pointset("pre_p_centroids", cen_.as<float>(), nf, false);   // cp:1236-1238: the centroids
+    const float avg = finish_edge_fold();
+    avg_edge_ = avg;
+    alphas_host_ = make_alpha_list((float)(avg * 1.0), (float)(0.001 * 1.0), avg, 20);
+    alphas_.reserve((alphas_host_.size() + 1) * 4);
+    if (!alphas_host_.empty())
+        IMPLI_HIP(hipMemcpyAsync(alphas_.p, alphas_host_.data(), alphas_host_.size() * 4, hipMemcpyHostToDevice, s));
+    a.alphas = alphas_.as<float>();
+    a.nal = (int)alphas_host_.size();
+    a.max_dist = avg;
+    st.next(kStageProject);
+    const unsigned grid = blocks_for(nf * kProjGroup);
+    if (pk) TreeJit::launch(pk->early, grid, jargs, s, "impli_pt_project_early");
+    else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
+    // centroids left unresolved need the randomised directions (types 2-6): the late pass covers
+    // every face and reads the pending count on the device (no host round trip)
+    a.pert = perturbations();
+    if (pk) TreeJit::launch(pk->late, grid, jargs, s, "impli_pt_project_late");
+    else DEPTH_LAUNCH(E.depth(), k_project_late, grid, 256, s, E.d_program(), E.d_rabbit(), a);
     IMPLI_HIP(hipGetLastError());
+    if (profile_) {   // the evaluations of this projection, summed on the host
+        std::vector<uint32_t> h((size_t)nf);
+        IMPLI_HIP(hipMemcpyAsync(h.data(), evals_buf_.p, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+        for (uint32_t e : h) evals_ += e;
+    }
     store_pointset("post_p_centroids", proj_.as<float>(), nf, false);
     store_pointset("pre_qem_verts", verts_.as<float>(), nv, false);
     if (enable_qem) {
+        st.next(kStageQem);
         grad_.reserve((size_t)(nf + 1) * 12);
-        DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>(), nf,
-                     grad_.as<float>());
+        if (pk) {
+            const float* P = proj_.as<float>();
+            float* G = grad_.as<float>();
+            void* nargs[] = {&jm, &jtab, &P, &nf, &G};
+            TreeJit::launch(pk->normals, blocks_for(nf), nargs, s, "impli_pt_normals_at");
+        } else {
+            DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>(), nf,
+                         grad_.as<float>());
+        }
         if (nv) k_qem<<<blocks_for(nv), 256, 0, s>>>(verts_.as<float>(), nv, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
                                                      proj_.as<float>(), grad_.as<float>(), avg);
         IMPLI_HIP(hipGetLastError());
         store_pointset("post_qem_verts", verts_.as<float>(), nv, false);
     }
+}
+
+void Ob02::read_counters() {   // cap hits and (profiling) evaluations since load_mesh (blocking)
+    uint32_t h[2] = {0, 0};
+    IMPLI_HIP(hipMemcpyAsync(h, misc_.p, sizeof h, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    cap_hits_ = h[1];
+}
+
+// profiling (set_profile): per-stage wall time with the stream drained at every stage boundary
+Ob02::Stage::Stage(Ob02* o, int k) : ob(o), stage(k) {
+    if (ob->profile_) {
+        IMPLI_HIP(hipStreamSynchronize(ob->s));
+        t0 = std::chrono::steady_clock::now();
+    }
+}
+void Ob02::Stage::next(int k) {
+    if (!ob->profile_) return;
+    IMPLI_HIP(hipStreamSynchronize(ob->s));
+    const auto t1 = std::chrono::steady_clock::now();
+    ob->stage_ms_[stage] += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    t0 = t1;
+    stage = k;
+}
+Ob02::Stage::~Stage() {
+    if (!ob->profile_) return;
+    (void)hipStreamSynchronize(ob->s);
+    ob->stage_ms_[stage] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // z^(kL) mod P for k = 0..63 and z^(64 L h) mod P for h = 0..H-1 (constant tables, grown on demand)
@@ -1024,6 +1012,7 @@ void Ob02::add_rand_noise(float amplitude) {
 
 void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cpp:1314-1367)
     if (!topo_valid_) build_topology();
+    Stage st(this, kStageSubdiv);
     int64_t added = 0;
     if (nf) {
         const EdgeTab t = edge_table();
@@ -1055,6 +1044,7 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
 }
 
 void Ob02::fetch(float* verts, int32_t* faces) {
+    Stage st(this, kStageFetch);
     if (nv) IMPLI_HIP(hipMemcpyAsync(verts, verts_.p, (size_t)nv * 12, hipMemcpyDeviceToHost, s));
     if (nf) IMPLI_HIP(hipMemcpyAsync(faces, faces_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
     IMPLI_HIP(hipStreamSynchronize(s));

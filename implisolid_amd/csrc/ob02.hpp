@@ -1,6 +1,9 @@
 // ob02.hpp -- the Ohtake-Belyaev refinement loop on the GPU (polygonizer steps 1-3).
 #pragma once
+#include <chrono>
+#include <future>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -33,7 +36,18 @@ public:
     // host copies of the point sets stored since load_mesh (blocking)
     const std::map<std::string, std::vector<float>>& pointsets();
     float last_average_edge() const { return avg_edge_; }
+    // after read_counters(): bisections that hit the cap, implicit evaluations of the projection
+    // (counted only while profiling)
+    void read_counters();
     uint32_t bisection_cap_hits() const { return cap_hits_; }
+    uint64_t projection_evals() const { return evals_; }
+    int64_t jit_launches() const { return jit_launches_; }
+    // profiling: the stream is drained at every stage boundary and the wall time of each stage is
+    // summed since load_mesh (topology, resampling, edge-length fold, projection, QEM, subdivision,
+    // fetch); evaluations are counted.  Off by default (the stages then overlap freely).
+    enum { kStageTopology, kStageResample, kStageEdgeFold, kStageProject, kStageQem, kStageSubdiv, kStageFetch, kStages };
+    void set_profile(bool on) { profile_ = on; }
+    const double* stage_ms() const { return stage_ms_; }
     bool capture_pointsets = true;
 
 private:
@@ -43,7 +57,18 @@ private:
     EdgeTab edge_table();
     void rand_tables(int64_t lanes);
     void add_rand_noise(float amplitude);
-    float average_edge_length();
+    void start_edge_fold();
+    float finish_edge_fold();
+    void start_perturbations();
+    const float* perturbations();
+    struct Stage {   // profiling scope: stage k from construction to next() / destruction
+        Ob02* ob;
+        int stage;
+        std::chrono::steady_clock::time_point t0;
+        Stage(Ob02* o, int k);
+        void next(int k);
+        ~Stage();
+    };
 
     Engine& E;
     hipStream_t s;
@@ -54,6 +79,18 @@ private:
     int64_t rand_hi_rows_ = 0;
     float avg_edge_ = 0.f;
     uint32_t cap_hits_ = 0;
+    uint64_t evals_ = 0;
+    int64_t jit_launches_ = 0;   // OB02 passes that ran the JIT point module (since load_mesh)
+    bool profile_ = false;
+    double stage_ms_[kStages] = {};
+    HostBuf host_norms_;                     // pinned: the edge-length terms' D2H
+    hipEvent_t norms_ready_ = nullptr;
+    DevBuf dir_, evals_buf_;
+    std::vector<float> alphas_host_;         // kept until the next projection (async H2D source)
+    std::future<std::shared_ptr<const std::vector<float>>> pert_job_;
+    std::shared_ptr<const std::vector<float>> pert_host_;
+    int64_t pert_nf_ = -1;
+    bool pert_uploaded_ = false;
     struct Snapshot {
         DevBuf buf;
         int64_t n = 0;

@@ -1,0 +1,329 @@
+// ob02_device.hpp -- device side of the OB02 steps that evaluate the implicit tree, written over an
+// evaluator `ev` (ev.f(x, y, z) -> f, ev.fg(x, y, z, g) -> f with the gradient), so the same code is
+// compiled twice: over the node-program interpreter (ob02.hip, any tree at once) and over the
+// tree-specialised point code of the JIT point module (jit.cpp; generated per tree shape).
+//   centroid_normals_body  vertex_resampling.hpp:185-188 (step 1's normals)
+//   project_*_body         set_centers_on_surface cp:421-1214 + bisection bisection.hpp:117-459
+//   normals_at_body        the QEM normals at the projected centroids (qem.hpp:256-316)
+//   points_body            direct evaluation (mcc2.cpp:815-911)
+#pragma once
+#include "ifunc_device.hpp"
+
+namespace impli {
+namespace ob {
+
+using dev::V3;
+
+constexpr float kRootTol = (float)(0.001 / 10.0);   // configs.hpp:33
+constexpr int kBisectCap = 200;                      // the reference has no cap (bisection.hpp:360-372)
+
+__device__ __forceinline__ float norm2f(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
+
+// the node-program interpreter (ifunc_device.hpp, stack capacity D) as an evaluator
+template <int D>
+struct InterpPt {
+    const Program* prog;
+    const float* tab;
+    __device__ __forceinline__ float f(float x, float y, float z) const { return dev::eval_f<D>(prog, tab, x, y, z); }
+    __device__ __forceinline__ float fg(float x, float y, float z, V3& g) const {
+        return dev::eval_fg<D>(prog, tab, x, y, z, g);
+    }
+};
+
+__device__ __forceinline__ V3 centroid(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t j) {
+    const int32_t a = f[3 * j], b = f[3 * j + 1], c = f[3 * j + 2];
+    // compute_centroids implicit_vectorised_algorithms.hpp:161-171
+    return V3{(v[3 * a] + v[3 * b] + v[3 * c]) / (float)(3.0), (v[3 * a + 1] + v[3 * b + 1] + v[3 * c + 1]) / (float)(3.0),
+              (v[3 * a + 2] + v[3 * b + 2] + v[3 * c + 2]) / (float)(3.0)};
+}
+
+// vertex_resampling.hpp:185-188: f and normalize_1111(grad) at the face centroids
+template <class Ev>
+__device__ __forceinline__ void centroid_normals_body(const Ev& ev, const float* __restrict__ v,
+                                                      const int32_t* __restrict__ f, int64_t nf, float* __restrict__ C,
+                                                      float* __restrict__ N) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nf) return;
+    const V3 c = centroid(v, f, j);
+    V3 g;
+    (void)ev.fg(c.x, c.y, c.z, g);
+    const float nm = norm2f(g.x, g.y, g.z);   // normalize_1111 normalise_inplace.hpp:60-70
+    C[3 * j] = c.x; C[3 * j + 1] = c.y; C[3 * j + 2] = c.z;
+    N[3 * j] = g.x / nm; N[3 * j + 1] = g.y / nm; N[3 * j + 2] = g.z / nm;
+}
+
+__device__ __forceinline__ float get_sign(float v) { return (v > kRootTol) ? 1.f : (v < -kRootTol) ? -1.f : 0.f; }
+
+// normalise_inplace (normalise_inplace.hpp:26-54)
+__device__ __forceinline__ V3 normalise_min(V3 a, float min_norm) {
+    float nm = norm2f(a.x, a.y, a.z);
+    nm = (nm < min_norm) ? 1.0f : nm;
+    const float factor = (float)(1.0 / (double)nm);
+    return V3{a.x * factor, a.y * factor, a.z * factor};
+}
+
+__device__ __forceinline__ V3 cross3(V3 a, V3 b) {
+    return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+// produce_facet_normals (implicit_vectorised_algorithms.hpp:52-133)
+__device__ __forceinline__ V3 facet_normal(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t j) {
+    const float* p0 = v + 3 * f[3 * j];
+    const float* p1 = v + 3 * f[3 * j + 1];
+    const float* p2 = v + 3 * f[3 * j + 2];
+    const float x1 = p1[0] - p0[0], y1 = p1[1] - p0[1], z1 = p1[2] - p0[2];
+    const float x2 = p2[0] - p0[0], y2 = p2[1] - p0[1], z2 = p2[2] - p0[2];
+    float x = y1 * z2 - z1 * y2, y = z1 * x2 - x1 * z2, z = x1 * y2 - y1 * x2;
+    const float micro = (float)(1.0 / 1000.0), nano = (float)((double)micro / 1000.0);
+    const float min_area = (30 * nano) * (30 * nano);
+    const float n2 = x * x + y * y + z * z;
+    if (n2 < min_area * min_area) {
+        const float o = (float)(1.0 / (double)sqrtf(3.0f));
+        return V3{o, o, o};
+    }
+    const float n = sqrtf(n2);
+    return V3{x / n, y / n, z / n};
+}
+
+struct ProjArgs {
+    const float* v;
+    const int32_t* f;
+    int64_t nf;
+    const float* alphas;
+    int nal;
+    float max_dist;
+    const float* pert;      // type-2 perturbations (3 per centroid), only for the late pass
+    float* out;             // projected centroids
+    float* fn;              // facet normals (written by the early pass)
+    float* fc;              // f(centroid) (written by the early pass)
+    uint32_t* pend;         // early pass: unresolved centroid list; its length at pend_count
+    uint32_t* pend_count;
+    uint32_t* cap_hits;     // bisections that reached kBisectCap (accumulated over the build)
+    float* cen;             // centroids (written by the prep pass)
+    float* dir;             // the type-0 direction per face (prep pass)
+    uint32_t* evals;        // profiling: implicit evaluations per face (null: not counted)
+};
+
+// Lanes per centroid.  The reference's searches are sequential per centroid (first alpha of the list
+// whose sign differs, then bisection); one lane per centroid left ~2 waves per SIMD, each waiting on
+// its slowest centroid's chain of evaluations.  A group of kProjGroup lanes evaluates kProjGroup
+// alphas at once (the first hit in list order wins) and kBisLevels bisection levels at once (the
+// decision tree of the next levels, then the serial path through it), so the chains are shorter and
+// the wave is filled: the result is the serial one exactly.
+constexpr int kProjGroup = 8;
+constexpr int kBisLevels = 3;
+static_assert((1 << kBisLevels) - 1 <= kProjGroup && 64 % kProjGroup == 0, "bisection tree fits the group");
+
+struct Grp {   // a centroid's lanes inside the wave (control flow is uniform per group)
+    int sub, base;
+    __device__ Grp() {
+        const int lane = (int)(threadIdx.x & 63);
+        sub = lane & (kProjGroup - 1);
+        base = lane - sub;
+    }
+    __device__ uint32_t bits(bool p) const {
+        return (uint32_t)((__ballot(p) >> base) & ((1ull << kProjGroup) - 1ull));
+    }
+    __device__ float from(float v, int k) const { return __shfl(v, base + k, 64); }
+    __device__ V3 from(V3 v, int k) const { return V3{from(v.x, k), from(v.y, k), from(v.z, k)}; }
+};
+
+// cp:904-1191 for one centroid: zero tests, swap (x1 outside), vectorised bisection restated per point
+__device__ __forceinline__ V3 bis_mid(V3 a, V3 b) {   // bisection.hpp:225-231: (x1 + x2) / 2. in double
+    return V3{(float)((double)(a.x + b.x) / 2.), (float)((double)(a.y + b.y) / 2.), (float)((double)(a.z + b.z) / 2.)};
+}
+
+// bisection.hpp:190-378 per point: mid, stop at |f(mid)| <= tol, x1 <- mid where f < -tol, x2 <- mid
+// where f > tol (a NaN moves neither: the serial loop repeats that mid until the cap).  Lane k < 2^L - 1
+// evaluates node k of the next L levels' decision tree (heap order: child 2k+1 after f < -tol, 2k+2
+// after f > tol); the group then walks the path the serial loop takes through those levels.
+template <class Ev>
+__device__ V3 bisect_g(const Grp& g, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_hits,
+                       uint32_t& evals) {
+    int it = 0;
+    const int node = g.sub < (1 << kBisLevels) - 1 ? g.sub : 0;
+    int depth = 0, bits = 0;   // node's path from the root, first decision in the lowest bit (1: x1 <- mid)
+    for (int n = node; n > 0; n = (n - 1) >> 1) bits = (bits << 1) | ((n & 1) ? 1 : 0), ++depth;
+    for (;;) {
+        V3 a = x1, b = x2;
+        for (int k = 0; k < depth; ++k) {
+            const V3 m = bis_mid(a, b);
+            if ((bits >> k) & 1) a = m;
+            else b = m;
+        }
+        const V3 mid = bis_mid(a, b);
+        const float vm = ev.f(mid.x, mid.y, mid.z);
+        evals += (1 << kBisLevels) - 1;
+        int cur = 0;
+        for (int lvl = 0; lvl < kBisLevels; ++lvl) {
+            const float v = g.from(vm, cur);
+            ++it;
+            if (fabsf(v) <= kRootTol) return g.from(mid, cur);
+            const bool lo = v < -kRootTol, hi = v > kRootTol;
+            if (!(lo || hi) || it == kBisectCap) {
+                if (g.sub == 0) atomicAdd(cap_hits, 1u);
+                return g.from(mid, cur);
+            }
+            if (lvl + 1 < kBisLevels) {
+                cur = lo ? 2 * cur + 1 : 2 * cur + 2;
+            } else {   // the state after this level: node cur's interval with its outcome applied
+                const V3 na = g.from(a, cur), nb = g.from(b, cur), nm = g.from(mid, cur);
+                x1 = lo ? nm : na;
+                x2 = lo ? nb : nm;
+            }
+        }
+    }
+}
+
+// f2 = f(best) (cp:904-951) is known: the search evaluated f at the point it returned, and
+// best == x when nothing was found (f(x) = fcv: eval_fg's value is eval_f's)
+template <class Ev>
+__device__ void finalize_g(const Grp& g, const Ev& ev, V3 x, float fcv, bool found, V3 best,
+                           float f2, float* out, const ProjArgs& a, uint32_t& evals) {
+    const bool z2 = fabsf(f2) <= kRootTol, z1 = fabsf(fcv) <= kRootTol;
+    if (z1) best = x;
+    V3 r;
+    if (found && !(z1 || z2)) {
+        V3 x1 = x, x2 = best;
+        if (f2 < -kRootTol) { const V3 t = x1; x1 = x2; x2 = t; }
+        r = bisect_g(g, ev, x1, x2, a.cap_hits, evals);
+    } else if (z1 || z2) {
+        r = best;
+    } else {
+        r = x;
+    }
+    if (g.sub == 0) { out[0] = r.x; out[1] = r.y; out[2] = r.z; }
+}
+
+// make_alpha_list's alphas along d, kProjGroup at a time; the first in list order whose sign
+// differs from the centroid's (cp:595-903)
+template <class Ev>
+__device__ __forceinline__ bool try_direction(const Grp& g, const Ev& ev, V3 x, V3 d, float sc,
+                                              const float* alphas, int na, float max_dist, V3& best,
+                                              float& best_f, uint32_t& evals) {
+    for (int a0 = 0; a0 < na; a0 += kProjGroup) {
+        const int ai = a0 + g.sub;
+        V3 p = x;
+        float fa = 0.f;
+        bool hit = false;
+        if (ai < na) {
+            const float cc = max_dist * alphas[ai];   // (length_factor * alpha) * 4.0 / 4.0 is exact
+            p = V3{x.x + cc * d.x, x.y + cc * d.y, x.z + cc * d.z};
+            fa = ev.f(p.x, p.y, p.z);
+            hit = get_sign(fa) * sc <= 0;
+        }
+        evals += na - a0 < kProjGroup ? na - a0 : kProjGroup;
+        const uint32_t m = g.bits(hit);
+        if (m) {
+            best = g.from(p, __ffs(m) - 1);
+            best_f = g.from(fa, __ffs(m) - 1);
+            return true;
+        }
+    }
+    return false;
+}
+
+// set_centers_on_surface (cp:421-594), the part before the searches: centroid, facet normal,
+// f(centroid) and the type-0 direction -normalise(grad) s_c; one lane per face.  Nothing here needs
+// the average edge length, so it runs while the host folds the edge lengths.
+template <class Ev>
+__device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& a) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= a.nf) return;
+    const V3 x = centroid(a.v, a.f, j);
+    const V3 fnv = facet_normal(a.v, a.f, j);
+    V3 gr;
+    const float fcv = ev.fg(x.x, x.y, x.z, gr);
+    V3 gd = normalise_min(gr, 0.000001f);
+    const float sc = get_sign(fcv);
+    if (sc < 0.0f) { gd.x = -gd.x; gd.y = -gd.y; gd.z = -gd.z; }
+    a.cen[3 * j] = x.x; a.cen[3 * j + 1] = x.y; a.cen[3 * j + 2] = x.z;
+    a.fn[3 * j] = fnv.x; a.fn[3 * j + 1] = fnv.y; a.fn[3 * j + 2] = fnv.z;
+    a.fc[j] = fcv;
+    a.dir[3 * j] = -gd.x * sc; a.dir[3 * j + 1] = -gd.y * sc; a.dir[3 * j + 2] = -gd.z * sc;
+    if (a.evals) a.evals[j] = 1;
+}
+
+// direction types 0 (gradient) and 1 (mesh normal); kProjGroup lanes per face
+template <class Ev>
+__device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs& a) {
+    const Grp g;
+    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kProjGroup;
+    if (j >= a.nf) return;   // uniform per group
+    const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
+    const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
+    const V3 d0{a.dir[3 * j], a.dir[3 * j + 1], a.dir[3 * j + 2]};
+    const float fcv = a.fc[j];
+    const float sc = get_sign(fcv);
+    uint32_t evals = 0;
+    V3 best = x;
+    float bf = fcv;
+    bool found = try_direction(g, ev, x, d0, sc, a.alphas, a.nal, a.max_dist, best, bf, evals);
+    if (!found) found = try_direction(g, ev, x, fnv, sc, a.alphas, a.nal < 10 ? a.nal : 10, a.max_dist, best, bf, evals);
+    if (found) finalize_g(g, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
+    else if (g.sub == 0) a.pend[atomicAdd(a.pend_count, 1u)] = (uint32_t)j;
+    if (a.evals && g.sub == 0) a.evals[j] += evals;
+}
+
+// types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes); the grid
+// covers every face, groups past the pending count (read on the device) exit at once
+template <class Ev>
+__device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& a) {
+    const Grp g;
+    const uint64_t k = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kProjGroup;
+    if (k >= *a.pend_count) return;
+    const int64_t j = a.pend[k];
+    const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
+    const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
+    const float fcv = a.fc[j];
+    const float sc = get_sign(fcv);
+    const int n10 = a.nal < 10 ? a.nal : 10;
+    const V3 pv{a.pert[3 * j], a.pert[3 * j + 1], a.pert[3 * j + 2]};
+    V3 z = cross3(fnv, pv);               // cp:250-259, add_inplace is a no-op (F9)
+    const float nz = norm2f(z.x, z.y, z.z);
+    z = V3{z.x / nz, z.y / nz, z.z / nz};  // normalize_1111
+    V3 z2 = normalise_min(cross3(fnv, z), 0.000001f);   // cp:297-312
+    uint32_t evals = 0;
+    V3 best = x;
+    float bf = fcv;
+    bool found = try_direction(g, ev, x, z, sc, a.alphas, n10, a.max_dist, best, bf, evals);
+    if (!found) found = try_direction(g, ev, x, z2, sc, a.alphas, n10, a.max_dist, best, bf, evals);
+    for (int ax = 0; ax < 3 && !found; ++ax) {
+        const V3 d{ax == 0 ? 1.f : 0.f, ax == 1 ? 1.f : 0.f, ax == 2 ? 1.f : 0.f};
+        found = try_direction(g, ev, x, d, sc, a.alphas, n10, a.max_dist, best, bf, evals);
+    }
+    finalize_g(g, ev, x, fcv, found, found ? best : x, found ? bf : fcv, a.out + 3 * j, a, evals);
+    if (a.evals && g.sub == 0) a.evals[j] += evals;
+}
+
+// normalize_1111(grad) at arbitrary points (the QEM normals at the projected centroids, qem.hpp:256-316)
+template <class Ev>
+__device__ __forceinline__ void normals_at_body(const Ev& ev, const float* __restrict__ P, int64_t n, float* __restrict__ G) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    V3 g;
+    (void)ev.fg(P[3 * j], P[3 * j + 1], P[3 * j + 2], g);
+    const float nm = norm2f(g.x, g.y, g.z);
+    G[3 * j] = g.x / nm; G[3 * j + 1] = g.y / nm; G[3 * j + 2] = g.z / nm;
+}
+
+
+// direct evaluation of n points (mcc2.cpp:815-911): f, and the gradient when grad != null
+template <class Ev>
+__device__ __forceinline__ void points_body(const Ev& ev, const float* __restrict__ xyz, int64_t n, float* __restrict__ f,
+                                            float* __restrict__ grad) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    if (grad) {
+        V3 g;
+        const float v = ev.fg(x, y, z, g);
+        if (f) f[i] = v;
+        grad[3 * i] = g.x; grad[3 * i + 1] = g.y; grad[3 * i + 2] = g.z;
+    } else {
+        f[i] = ev.f(x, y, z);
+    }
+}
+
+}  // namespace ob
+}  // namespace impli

@@ -128,6 +128,16 @@ int implisolid_cuts_from_layer_work(const int64_t* listed, int n_layers, int64_t
  * ids[r] (a device may repeat), the slabs' meshes are concatenated in rank order on the host --
  * byte-identical to one device -- and the OB02 steps run on ids[0]. */
 int implisolid_set_devices(const int32_t* ids, int n);
+/* Additive diagnostics of the OB02 steps (polygonizer_algorithm_ob02.hpp:74-157 keeps per-step
+ * timers, timer.hpp:33-75).  With profiling on, build_geometry drains its stream at every stage
+ * boundary and sums each stage's wall time, and counts the projection's implicit evaluations (off
+ * by default: the stages then overlap and nothing is counted).  last_build_stats (blocking) returns
+ * [bisections that hit the 200-round cap (F8e), projection evaluations (profiled builds),
+ *  last average edge length, ms of: topology, vertex resampling, edge-length fold, projection, QEM,
+ *  subdivision, result fetch (profiled builds), faces, vertices, OB02 passes that ran the JIT point
+ *  module] of the last build. */
+void implisolid_ob02_profile(int on);
+int implisolid_last_build_stats(double out[13]);
 /* evaluate n >= 0 points (no 50k limit) of the current set_object(); grad may be NULL */
 int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* grad_out);
 
@@ -137,6 +147,9 @@ int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* gra
  * Returns the code-object size (> 0), or -1 with implisolid_last_error(); optionally copies the
  * generated source (NUL-terminated, truncated to capacity) and the compile time in seconds. */
 int64_t implisolid_jit_compile(const char* shape_json, char* source_out, int64_t capacity, double* seconds);
+/* the same for the shape's point module (the OB02 passes and direct evaluation over straight-line
+ * tree code; used by build_geometry's OB02 steps and implisolid_eval_points once loaded) */
+int64_t implisolid_jit_compile_points(const char* shape_json, char* source_out, int64_t capacity, double* seconds);
 int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int32_t info[4], float* mats_out);
 
 /* Device-resident slab pipeline (benchmarks / multi-GPU Z-slab runs).  A slab engine owns the

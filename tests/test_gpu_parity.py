@@ -393,6 +393,57 @@ def test_ob02_config3_nonfinite_rows(impli, oracle):
     assert (~np.isfinite(vr).all(1)).sum() > 0
 
 
+@pytest.fixture
+def sync_jit(impli):
+    """JIT in sync mode: every new shape's modules are compiled before its first use, so the JIT
+    kernels (not the interpreter) run from the first call."""
+    impli.set_jit(1)
+    yield
+    impli.set_jit(2)
+
+
+@pytest.mark.parametrize("name", ["config2_48", "config3_64", "twist_tbb", "meta_balls"])
+def test_ob02_point_jit_matches_oracle(impli, oracle, sync_jit, name):
+    """The OB02 passes over the JIT point module (ob02_device.hpp bodies over straight-line tree
+    code) give the oracle's mesh -- config 3 at 64 includes the non-finite rows (NaN centroids
+    through the unspecialised transforms)."""
+    from implisolid_amd import scenes
+    if name == "config2_48":
+        shape, mc = scenes.config2(48)
+    elif name == "config3_64":
+        shape, mc = scenes.config3(64)
+    else:
+        shape = SCREW_TREES[name]
+        mc = scenes.mc_settings(40, 0.7, vresampl_iters=1, vresampl_c=0.4, projection=1, qem=1, overall_repeats=2)
+    _ob02_compare(impli, oracle, shape, mc)
+    assert impli.last_build_stats()["jit_launches"] > 0
+
+
+@pytest.mark.parametrize("name", ["config3_tree", "union_sphere_cube", "twist_tbb", "extrusion_tri", "leaf_cube"])
+def test_eval_points_jit_bit_exact(impli, oracle, sync_jit, name):
+    """Direct evaluation through the JIT point module, including non-finite coordinates (the
+    interpreter's transforms propagate NaN through zero coefficients, and so must the JIT's)."""
+    shape = TREES[name]
+    rng = np.random.default_rng(77)
+    pts = rng.uniform(-1.1, 1.1, size=(20000, 3)).astype(np.float32)
+    pts[:50, 1] = np.nan
+    pts[50:100, 0] = np.inf
+    pts[100:150, 2] = -np.inf
+    tree = oracle.mp5_to_nodes(json.dumps(shape))
+    f_ref, g_ref = oracle.eval_implicit(tree, pts), oracle.eval_gradient(tree, pts)
+    with impli.ImplicitService(shape) as svc:
+        f, g = svc.eval(pts, gradient=True)
+    assert np.array_equal(f.view(np.uint32), f_ref.view(np.uint32)) or np.array_equal(
+        np.isnan(f), np.isnan(f_ref)) and np.array_equal(f[~np.isnan(f)], f_ref[~np.isnan(f_ref)])
+    ok = np.isfinite(g_ref).all(1)
+    assert np.array_equal(np.isfinite(g).all(1), ok)
+    if _has_twist(shape):
+        scale = np.maximum(np.abs(g_ref[ok]), 1.0)
+        assert (np.abs(g[ok] - g_ref[ok]) <= GRAD_TOL * scale).all()
+    else:
+        assert np.array_equal(g[ok], g_ref[ok])
+
+
 def _field(impli, shape, mc, level, signs=False):
     impli.set_pruning(level)
     try:

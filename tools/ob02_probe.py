@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """End-to-end build_geometry timings (host-resident result, PCIe included) for the OB02 configs:
 config 2 (union sphere+rabbit, 128^3, MC + 3 x [resample, project, QEM]) and config 3 (twist tree,
-256^3, same loop), plus MC-only and subdivision variants.  usage: python tools/ob02_probe.py [reps]"""
+256^3, same loop), plus MC-only and subdivision variants; then one profiled build of each (stream
+drained per stage) for the per-stage breakdown and the projection's evaluation count.
+usage: python tools/ob02_probe.py [reps]"""
+import json
 import os
 import sys
 import time
@@ -32,8 +35,17 @@ def main():
             t0 = time.perf_counter()
             v, f = I.make_geometry(shape, mc)
             ts.append(time.perf_counter() - t0)
-        print("%-32s V %8d F %8d  build_geometry %.2f ms (min of %d)" % (name, len(v), len(f), min(ts) * 1e3, reps),
-              flush=True)
+        st = I.last_build_stats()
+        print("%-32s V %8d F %8d  build_geometry %.2f ms (min of %d)  cap hits %d" % (
+            name, len(v), len(f), min(ts) * 1e3, reps, st["bisection_cap_hits"]), flush=True)
+    I.ob02_profile(True)
+    for name, shape, mc in cases:
+        if "OB02" not in name:
+            continue
+        I.make_geometry(shape, mc)
+        st = I.last_build_stats()
+        print("profile %-24s %s" % (name, json.dumps(st)), flush=True)
+    I.ob02_profile(False)
 
 
 if __name__ == "__main__":
