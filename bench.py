@@ -538,12 +538,14 @@ def main():
     vname, vj = newest("valu_r*.json")
     traffic = tj.get("pipeline_bytes") if tj else None
     phase_traffic = tj.get("phase_bytes", {}) if tj else {}
-    valu_phase = {}
+    valu_phase, valu_insts = {}, {}
     if vj:
         for k, v in vj.get("kernels", {}).items():
             ph = KERNEL_PHASE.get(k)
             if ph:   # the phase's busiest kernel
                 valu_phase[ph] = max(valu_phase.get(ph, 0.0), v["valu_busy"])
+                if "valu_insts_per_wave" in v and "waves_per_dispatch" in v:
+                    valu_insts[ph] = valu_insts.get(ph, 0.0) + v["valu_insts_per_wave"] * v["waves_per_dispatch"]
     # Per-kernel roofline table (per launch, this slab): time from the engine's HIP events, HBM
     # bytes from the PMC summary, achieved GB/s and fraction of the 8 TB/s peak, VALU busy.  The
     # field kernel's algorithmic bytes (per evaluated sample: one 4 B store) use the
@@ -563,6 +565,11 @@ def main():
             row["alg_frac"] = round(row["alg_gbs"] / HBM_PEAK_GBS, 4)
         if k in valu_phase:
             row["valu_busy"] = valu_phase[k]
+        if k in valu_insts:
+            # VALU issue roofline: wave instructions x 2 cycles each (a wave64 VALU op on a SIMD-32,
+            # MI355X_MICROARCH.md) over the 1024 SIMDs x 2.4 GHz for the kernel's time -- a lower bound
+            # of the VALU pipe's occupancy (f64 and transcendental ops take longer)
+            row["valu_issue_frac"] = round(valu_insts[k] * 2.0 / (1024 * 2.4e9 * ms_k * 1e-3), 4)
         per_kernel[k] = row
     # The pass: the counter-measured HBM bytes over the kernel sequence's time (what the hardware
     # moved), next to SURVEY.md 8d's dense-equivalent bytes B = 8 (R+1)^3 + 12 V + 12 F (what a

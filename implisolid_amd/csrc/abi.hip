@@ -801,7 +801,16 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
         if (out) {
             if (capacity < n) throw InputError("implisolid_slab_read_field: buffer too small");
             IMPLI_HIP(hipDeviceSynchronize());
-            IMPLI_HIP(hipMemcpy(out, s->engine.d_field(), (size_t)n * sizeof(float), hipMemcpyDeviceToHost));
+            // the field is stored brick-major (grid.hpp field_index): copy it whole, then lay the
+            // stored samples out x fastest, then y, then layer
+            std::vector<float> raw((size_t)field_samples(g));
+            if (!raw.empty())
+                IMPLI_HIP(hipMemcpy(raw.data(), s->engine.d_field(), raw.size() * sizeof(float), hipMemcpyDeviceToHost));
+            const int layers = g.fz1 - g.fz0;
+            for (int l = 0; l < layers; ++l)
+                for (int y = 0; y < g.n; ++y)
+                    for (int x = 0; x < g.n; ++x)
+                        out[((int64_t)l * g.n + y) * g.n + x] = raw[(size_t)field_index(g, x, y, l)];
         }
         return n;
     } catch (const std::exception& e) {

@@ -189,7 +189,7 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
         have_grid_ = true;
         return;
     }
-    const size_t field_bytes = (size_t)grid_.n * grid_.n * (size_t)(grid_.fz1 - grid_.fz0) * sizeof(float);
+    const size_t field_bytes = (size_t)field_samples(grid_) * sizeof(float);   // brick-major (grid.hpp)
     field_.reserve(field_bytes);
     // the pruned eval writes only the listed bricks: the rest of the field reads as 0, not as
     // whatever the allocation held (deterministic read_field; nothing on the path reads it)

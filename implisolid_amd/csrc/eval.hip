@@ -30,19 +30,23 @@ namespace impli {
 
 using namespace dev;
 
+// one wave per brick layer (64 stored samples, lane = (y % 8) * 8 + x % 8), in storage order: the
+// wave writes its 256 contiguous bytes (this unpruned path also calibrates the PMC write counter,
+// tools/pmc_traffic.py)
 template <int D>
 __global__ __launch_bounds__(256) void k_eval_field(const Program* __restrict__ prog, const float* __restrict__ tab,
-                                                    GridDesc g, float* __restrict__ field) {
-    const uint32_t n = (uint32_t)g.n;
-    const uint32_t plane = n * n;
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= plane) return;
-    const uint32_t sy = i / n, sx = i - sy * n;
-    const int layer = (int)blockIdx.y;
+                                                    GridDesc g, BrickGrid bg, float* __restrict__ field) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // brick layer: brick w / kBZ, layer w % kBZ
+    const int lane = threadIdx.x & 63;
+    if (w >= (int64_t)bg.n_bricks * kBZ) return;
+    int bx, by, bz;
+    brick_of((int)(w / kBZ), bg, bx, by, bz);
+    const int sx = bx * kBX + lane % kBX, sy = by * kBY + lane / kBX, layer = bz * kBZ + (int)(w % kBZ);
     float f = kSealed;
-    if (!(sealed_xy(g, (int)sx) || sealed_xy(g, (int)sy) || sealed_z(g, layer)))
-        f = 0.f + eval_f<D>(prog, tab, sample_xy(g, 0, (int)sx), sample_xy(g, 1, (int)sy), sample_z(g, layer));
-    field[(size_t)layer * plane + i] = f;   // eval_shape: field (zero) += value
+    if (sx < g.n && sy < g.n && layer < g.fz1 - g.fz0 &&
+        !(sealed_xy(g, sx) || sealed_xy(g, sy) || sealed_z(g, layer)))
+        f = 0.f + eval_f<D>(prog, tab, sample_xy(g, 0, sx), sample_xy(g, 1, sy), sample_z(g, layer));
+    field[w * (kBX * kBY) + lane] = f;   // eval_shape: field (zero) += value
 }
 
 template <int D>
@@ -195,19 +199,25 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
     }
 }
 
-// sign bitmap of a fully evaluated field (unpruned path): one thread per 64-bit word
-__global__ __launch_bounds__(256) void k_signs_from_field(GridDesc g, const float* __restrict__ field,
-                                                          uint64_t* __restrict__ signs) {
-    // one wave per 64-bit word: lane k reads sample 64 w + k of the row (coalesced 4 B per lane)
-    const int rw = sign_row_words(g);
-    const int64_t rows = (int64_t)g.n * (g.fz1 - g.fz0);
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= rows * rw) return;
-    const int64_t row = i / rw;
-    const int x = 64 * (int)(i - row * rw) + (threadIdx.x & 63);
-    const bool neg = x < g.n && field[row * g.n + x] < 0.f;
+// sign bitmap of a fully evaluated field (unpruned path), in storage order: one wave per brick
+// layer reads its 256 contiguous bytes (the PMC fetch calibration, tools/pmc_traffic.py) and writes
+// the layer's kBY sign pieces, as the pruned eval does
+__global__ __launch_bounds__(256) void k_signs_from_field(GridDesc g, BrickGrid bg, const float* __restrict__ field,
+                                                          sign_piece_t* __restrict__ signs) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= (int64_t)bg.n_bricks * kBZ) return;
+    int bx, by, bz;
+    brick_of((int)(w / kBZ), bg, bx, by, bz);
+    const int layer = bz * kBZ + (int)(w % kBZ);
+    const int sx = bx * kBX + lane % kBX;
+    const bool neg = sx < g.n && field[w * (kBX * kBY) + lane] < 0.f;
     const uint64_t bits = __ballot(neg);
-    if ((threadIdx.x & 63) == 0) signs[i] = bits;
+    const int row_pieces = (64 / kBX) * sign_row_words(g);
+    if (lane < kBY && layer < g.fz1 - g.fz0) {
+        const int yy = by * kBY + lane;
+        if (yy < g.n) signs[((size_t)layer * g.n + yy) * row_pieces + bx] = (sign_piece_t)(bits >> (kBX * lane));
+    }
 }
 
 template <int D>
@@ -241,15 +251,14 @@ static int eval_depth(int depth) {
 
 void launch_eval_field(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g, float* d_field,
                        hipStream_t s) {
-    const uint32_t plane = (uint32_t)g.n * (uint32_t)g.n;
-    const int layers = g.fz1 - g.fz0;
-    if (layers <= 0) return;
-    dim3 grid((plane + 255) / 256, layers);
+    const BrickGrid bg = brick_grid(g);
+    if (bg.n_bricks <= 0) return;
+    const unsigned grid = (unsigned)(((int64_t)bg.n_bricks * kBZ + 3) / 4);   // 4 brick layers per block
     depth = eval_depth(depth);
-    if (depth <= 4) k_eval_field<4><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
-    else if (depth <= 8) k_eval_field<8><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
-    else if (depth <= 12) k_eval_field<12><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
-    else k_eval_field<16><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, d_field);
+    if (depth <= 4) k_eval_field<4><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_field);
+    else if (depth <= 8) k_eval_field<8><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_field);
+    else if (depth <= 12) k_eval_field<12><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_field);
+    else k_eval_field<16><<<grid, 256, 0, s>>>(d_prog, d_rabbit, g, bg, d_field);
 }
 
 BrickGrid brick_grid(const GridDesc& g) {
@@ -303,9 +312,10 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
 }
 
 void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s) {
-    const int64_t words = (int64_t)g.n * (g.fz1 - g.fz0) * sign_row_words(g);
-    if (words <= 0) return;
-    k_signs_from_field<<<(unsigned)((words + 3) / 4), 256, 0, s>>>(g, d_field, d_signs);
+    const BrickGrid bg = brick_grid(g);
+    if (bg.n_bricks <= 0) return;
+    k_signs_from_field<<<(unsigned)(((int64_t)bg.n_bricks * kBZ + 3) / 4), 256, 0, s>>>(
+        g, bg, d_field, reinterpret_cast<sign_piece_t*>(d_signs));
 }
 
 void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t* d_cmodes, const uint8_t* d_cls,

@@ -56,7 +56,6 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
     const int lane = threadIdx.x & 63;
     const int n = g.n;
     const int layers = g.fz1 - g.fz0;
-    const size_t plane = (size_t)n * n;
     const int row_pieces = (64 / kBX) * sign_row_words(g);
     const uint32_t wpb = blockDim.x >> 6;   // waves per block
     const uint32_t stride = gridDim.x * wpb;
@@ -76,7 +75,9 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
         const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
         const bool ok = sx < n && sy < n;
         const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
-        float* out = field + (size_t)(ok ? sy : 0) * n + (ok ? sx : 0);
+        // brick-major field (grid.hpp field_index): the brick's layer k is 64 consecutive floats, one
+        // per lane -- the wave stores two whole lines (lanes past the grid edge fill the padding)
+        float* out = field + (size_t)b * kBrickSamples + lane;
         const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
                            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
         const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
@@ -92,7 +93,7 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
             const int layer = l0 + k;
             if (layer >= layers) break;
             const float v = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + (k ? f1 : f0);
-            if (ok) out[(size_t)layer * plane] = v;
+            out[k * kBX * kBY] = v;
             const uint64_t neg = __ballot(v < 0.f);
             if (lane < kBY) {
                 const int yy = by * kBY + lane;
@@ -106,7 +107,7 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
             if (layer >= layers) break;
             const float f = ev(m, x, y, sample_z(g, layer));
             const float v = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
-            if (ok) out[(size_t)layer * plane] = v;
+            out[k * kBX * kBY] = v;
             const uint64_t neg = __ballot(v < 0.f);
             if (lane < kBY) {
                 const int yy = by * kBY + lane;

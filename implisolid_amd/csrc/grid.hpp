@@ -49,6 +49,34 @@ enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBric
 // then no cell corner in it needs its exact value and MC may take the sign from fill -- else 0.
 struct BrickGrid { int nbx, nby, nbz, n_bricks; };
 
+// Field storage, brick-major: brick (bx, by, bz) of the slab's brick grid holds its kBX x kBY x kBZ
+// stored samples contiguously (x fastest, then y, then layer), so one brick layer is kBX kBY floats
+// (256 B: two whole 128 B lines).  The eval kernel's wave stores whole lines and a cell's corners
+// mostly share lines.  Brick b's samples start at b * kBrickSamples (b as numbered by brick_of).
+constexpr int kBrickSamples = kBX * kBY * kBZ;
+__host__ __device__ inline int64_t field_index(const GridDesc& g, int sx, int sy, int layer) {
+    const int nbx = (g.n + kBX - 1) / kBX, nby = (g.n + kBY - 1) / kBY;
+    const int64_t b = (int64_t)(sx / kBX) + (int64_t)nbx * ((sy / kBY) + (int64_t)nby * (layer / kBZ));
+    return b * kBrickSamples + ((layer % kBZ) * kBY + (sy % kBY)) * kBX + (sx % kBX);
+}
+// field_index = field_layer_term + field_y_term + field_x_term (the x and y terms stay below 2^31:
+// one brick layer of the slab)
+__host__ __device__ inline uint32_t field_x_term(int sx) {
+    return (uint32_t)(sx / kBX) * kBrickSamples + (uint32_t)(sx % kBX);
+}
+__host__ __device__ inline uint32_t field_y_term(const GridDesc& g, int sy) {
+    return (uint32_t)(sy / kBY) * (uint32_t)((g.n + kBX - 1) / kBX) * kBrickSamples + (uint32_t)(sy % kBY) * kBX;
+}
+__host__ __device__ inline int64_t field_layer_term(const GridDesc& g, int layer) {
+    const int64_t nbx = (g.n + kBX - 1) / kBX, nby = (g.n + kBY - 1) / kBY;
+    return (int64_t)(layer / kBZ) * nbx * nby * kBrickSamples + (int64_t)(layer % kBZ) * (kBX * kBY);
+}
+__host__ __device__ inline int64_t field_samples(const GridDesc& g) {   // allocation, padded bricks included
+    const int64_t nbx = (g.n + kBX - 1) / kBX, nby = (g.n + kBY - 1) / kBY;
+    const int64_t nbz = (g.fz1 - g.fz0 + kBZ - 1) / kBZ;
+    return nbx * nby * (nbz > 0 ? nbz : 0) * kBrickSamples;
+}
+
 // Sign bitmap of the stored samples (bit set <=> sample < 0, MC's cube-index test): per stored
 // sample row (layer, y) `sign_row_words(g)` 64-bit words, sample x at bit x % 64 of word x / 64.
 // The eval kernels write it as kBX-bit pieces (one per brick row).

@@ -195,12 +195,25 @@ __device__ __forceinline__ V3 torus_g(float x, float y, float z) {
 
 // ---- double mushroom via linearly_transformed, object_factory.hpp:86-100,
 //      double_mushroom.hpp:90-160 with (0.9, 0.4/2, 0.4/2, 1/0.2) -------------------------------
+// a / D for the double square a of a float and a constant D, by one correction step from
+// R = RN(1/D): q0 = a R, q = q0 + (a - q0 D) R with both steps fused (q0 when not finite).  Equal to
+// the IEEE quotient for all 2^32 floats at the constant dm_f uses (tools/divconst_check.c, run by
+// test_divconst_identity_exhaustive); three f64 ops instead of the division's scale / reciprocal /
+// refinement / fixup sequence.
+__device__ __forceinline__ double div_sq_const(double a, double D, double R) {
+    const double q0 = a * R;
+    return __builtin_isfinite(q0) ? __fma_rn(__fma_rn(-q0, D, a), R, q0) : q0;
+}
 __device__ __forceinline__ float dm_f(float x, float y, float z) {
     const float r = 0.9f / 2, a = (float)(0.4 / 2), c = 1.f / (float)(1 / 0.2);
     const float a2 = a * a, b2 = a * a, c2 = c * c;
     if (z > r) return r - z;
     if (z < -r) return r + z;
-    const double v = sq_exact(x - 0.f) / (double)a2 + sq_exact(y - 0.f) / (double)b2 - sq_exact(z - 0.f) / (double)c2 - 1;
+    // a2 == b2 == c2 (object_factory.hpp:86-100): one constant, one reciprocal
+    const double D = (double)a2, R = 1.0 / (double)a2;
+    static_assert(0.2f * 0.2f == (float)(0.4 / 2) * (float)(0.4 / 2), "the checked constant");
+    const double v = div_sq_const(sq_exact(x - 0.f), D, R) + div_sq_const(sq_exact(y - 0.f), (double)b2, R) -
+                     div_sq_const(sq_exact(z - 0.f), (double)c2, R) - 1;
     return (float)(-v);
 }
 __device__ __forceinline__ V3 dm_g(float x, float y, float z) {

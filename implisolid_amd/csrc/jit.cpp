@@ -380,7 +380,8 @@ std::string source_hash(const std::string& src) {
         for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)p[i]; h *= 1099511628211ull; }
     };
     mix(src.data(), src.size());
-    const char* tag = "gfx950 -O3 -ffp-contract=off -std=c++17 v2";
+    for (int k = 0; k < kJitNumHeaders; ++k) mix(kJitHeaderSources[k], std::strlen(kJitHeaderSources[k]));   // the headers it includes
+    const char* tag = "gfx950 -O3 -ffp-contract=off -std=c++17 v3";
     mix(tag, std::strlen(tag));
     char buf[32];
     std::snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);

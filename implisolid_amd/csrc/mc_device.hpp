@@ -207,11 +207,17 @@ __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases
                 if (mine) {
                     const int y = (int)erow % g.m + 1;
                     const int sx = x - 1, sy = y - 1, sl = z - g.fz0;
-                    const int n_ = g.n;
-                    const int64_t base = has ? (int64_t)sx + (int64_t)sy * n_ + (int64_t)sl * n_ * n_ : 0;
-                    const int64_t dx = has ? 1 : 0, dy = has ? n_ : 0, dz = has ? (int64_t)n_ * n_ : 0;
-                    const float r7 = b.field[base + dx + dy + dz], r5 = b.field[base + dx + dz];
-                    const float r6 = b.field[base + dy + dz], r3 = b.field[base + dx + dy];
+                    // corners 7 (1,1,1), 5 (1,0,1), 6 (0,1,1), 3 (1,1,0) of the brick-major field
+                    // (grid.hpp field_index, split into per-axis terms); lanes without a cell read
+                    // sample 0
+                    const int cx = has ? sx : 0, cy = has ? sy : 0, cl = has ? sl : 0, d = has ? 1 : 0;
+                    const uint32_t fx0 = field_x_term(cx), fx1 = field_x_term(cx + d);
+                    const uint32_t fy0 = field_y_term(g, cy), fy1 = field_y_term(g, cy + d);
+                    const int64_t fl0 = field_layer_term(g, cl), fl1 = field_layer_term(g, cl + d);
+                    const float r7 = b.field[fl1 + (fy1 + fx1)];
+                    const float r5 = b.field[fl1 + (fy0 + fx1)];
+                    const float r6 = b.field[fl1 + (fy1 + fx0)];
+                    const float r3 = b.field[fl0 + (fy1 + fx1)];
                     const bool sx1 = sealed_xy(g, sx + 1), sy1 = sealed_xy(g, sy + 1), sz1 = sealed_z(g, sl + 1);
                     const bool sx0 = sealed_xy(g, sx), sy0 = sealed_xy(g, sy), sz0 = sealed_z(g, sl);
                     const float f7 = (sx1 || sy1 || sz1) ? kSealed : r7;

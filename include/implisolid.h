@@ -190,8 +190,9 @@ int implisolid_slab_download(implisolid_slab* s, float* verts, int32_t* faces, v
 float* implisolid_slab_verts(implisolid_slab* s);     /* device pointers */
 int32_t* implisolid_slab_faces(implisolid_slab* s);
 float* implisolid_slab_field(implisolid_slab* s);
-/* blocking copy of the slab's stored field samples (n*n*layers floats, x fastest); with out ==
- * NULL returns the sample count only */
+/* blocking copy of the slab's stored field samples (n*n*layers floats, x fastest, converted from
+ * the device's brick-major storage); with out == NULL returns the sample count only.
+ * implisolid_slab_field's device pointer is brick-major (8x8x2-sample bricks, x fastest inside). */
 int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capacity);
 /* per-kernel HIP-event timing (stream-ordered, no synchronisation) of the following eval /
  * count / emit calls; kernel_times blocks and returns milliseconds of the last timed calls for

@@ -578,3 +578,14 @@ def test_headline_summary_oracle_regression(oracle):
     assert (len(v), len(f)) == (s["n_verts"], s["n_faces"])
     assert hashlib.sha256(np.ascontiguousarray(f).tobytes()).hexdigest() == s["sha256_faces"]
     assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"]
+
+
+def test_divconst_identity_exhaustive(tmp_path):
+    """The double mushroom's divisions by its constant use q0 = a R, q = fma(fma(-q0, D, a), R, q0)
+    (ifunc_device.hpp div_sq_const); it must equal the IEEE quotient for the square of every float
+    (all 2^32 bit patterns, tools/divconst_check.c)."""
+    exe = str(tmp_path / "divconst_check")
+    subprocess.run(["gcc", "-O2", "-mfma", "-ffp-contract=off", "-pthread", os.path.join(ROOT, "tools", "divconst_check.c"),
+                    "-o", exe, "-lm"], check=True)
+    r = subprocess.run([exe, str(min(8, os.cpu_count() or 1))], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
