@@ -355,11 +355,11 @@ def main():
     # Headline: the interpreter kernels (no per-object compilation, so nothing is left out of the
     # rate); beside it the JIT tier, whose hipRTC time for the 64 shapes is reported and folded
     # into an objects/s over one pass that includes it.
-    def run_batch(objs, jit_mode):
+    def run_batch(objs, jit_mode, n_streams):
         I.set_jit(jit_mode)
         try:
             t0 = time.perf_counter()
-            batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=args.config5_streams)
+            batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=n_streams)
             setup_s = time.perf_counter() - t0
         finally:
             I.set_jit(2)
@@ -379,7 +379,8 @@ def main():
             tv, tf = tv + a, tf + b_
         ms5 = el / args.steps * 1e3
         res = {"objects_per_s": round(batch.n / (ms5 * 1e-3), 1), "value": round(batch.n * 128 ** 3 / (ms5 * 1e-3) / 1e6, 2),
-               "unit": "Mvoxels/s", "ms_per_stream": round(ms5, 4), "graphs": batch.graphs, "verts": tv, "faces": tf,
+               "unit": "Mvoxels/s", "ms_per_stream": round(ms5, 4), "graphs": batch.graphs, "merged": batch.merged,
+               "verts": tv, "faces": tf,
                "setup_s": round(setup_s, 2), "jit_compile_s": round(batch.jit_seconds, 2),
                "objects_per_s_incl_setup": round(batch.n / (ms5 * 1e-3 + setup_s), 1)}
         n_streams = batch.n_streams
@@ -389,10 +390,13 @@ def main():
     c5 = None
     if world == 1 and not args.skip_config5:
         objs = scenes.config5_objects(64, 128)
-        c5, ns5 = run_batch(objs, 0)
+        c5, _ = run_batch(objs, 0, 0)
         c5["workload"] = ("config5: 64 seeded random MP5 objects (scenes.config5_objects, 1-12 leaves) at 128^3, eval+MC, "
-                          "interpreter kernels (no per-object compilation), hipGraph per object, %d streams" % ns5)
-        c5["jit"], _ = run_batch(objs, 1)
+                          "interpreter kernels (no per-object compilation), merged launches: each stage once for all "
+                          "64 objects")
+        c5["graphs_interpreter"], _ = run_batch(objs, 0, args.config5_streams)
+        c5["jit"], ns5 = run_batch(objs, 1, args.config5_streams)
+        c5["jit"]["workload"] = "JIT tree kernels, hipGraph per object over %d streams" % ns5
 
     # First-call latency of a never-seen shape (async JIT: the interpreter kernels run at once, the
     # module compiles in the background): build_geometry (eval + MC, host-resident result) of fresh

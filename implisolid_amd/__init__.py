@@ -586,9 +586,10 @@ class Slab:
 
 
 class Batch:
-    """A stream of objects polygonised with one mc-settings dict (BASELINE config 5): every
-    object's eval + count + emit is captured in a hipGraph on creation; run() replays them all
-    (asynchronously, on `stream`), counts()/download() block."""
+    """A stream of objects polygonised with one mc-settings dict (BASELINE config 5).  n_streams=0:
+    merged launches (every stage once for all objects, interpreter kernels); n_streams >= 1: one
+    hipGraph per object (JIT tree kernels) replayed over that many streams.  run() is async on
+    `stream`; counts()/download() block."""
 
     def __init__(self, shapes, mc_settings, n_streams=4):
         L = lib()
@@ -601,6 +602,7 @@ class Batch:
         secs = ctypes.c_double(0)
         L.implisolid_batch_info(self.h, info, ctypes.byref(secs))
         self.n, self.n_streams, self.graphs, self.jit_seconds = int(info[0]), int(info[1]), bool(info[2]), secs.value
+        self.merged = bool(info[3])
 
     def run(self, stream=None):
         if lib().implisolid_batch_run(self.h, stream) != 0:

@@ -13,6 +13,7 @@
 #include "jit.hpp"
 
 #include <chrono>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include "host.hpp"
 #include "ob02.hpp"
 
@@ -202,7 +203,9 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         ob_ptr->load_mesh(dv.as<float>(), nv, df.as<int32_t>(), nf);
     } else {
         E.set_grid(st.resolution, st.box, 0, 1);
+        roctxRangePush("marching cubes");
         SlabCounts c = E.marching_cubes(s);   // polygonize_step_0
+        roctxRangePop();
         nv = c.n_verts();
         nf = c.n_faces();
         if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
@@ -304,6 +307,8 @@ static void build_geometry_specs(const char* shape_json, const char* mc_json, co
         return;
     }
     try {
+        roctxRangePush("build_geometry");
+        struct Pop { ~Pop() { roctxRangePop(); } } pop;
         grand_algorithm(shape_json, st, cs);
     } catch (const InputError& e) {
         report(e.what(), true);
@@ -823,6 +828,9 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
 //      once in a hipGraph and replayed; objects spread over a few streams ----------------------------
 struct implisolid_batch {
     std::vector<std::unique_ptr<Engine>> engines;
+    bool merged = false;                 // one launch per stage for all objects (ObjArgs rows)
+    DevBuf objs;                         // merged: ObjArgs[n] on the device
+    int depth = 0;
     std::vector<hipGraphExec_t> execs;   // empty when capture is unavailable (direct launches)
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> events;      // fork (0) and one join event per stream
@@ -837,10 +845,13 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         const MCSettings st = parse_mc_settings(mc_json);
         std::vector<Program> progs;
         for (int i = 0; i < n; ++i) progs.push_back(compile_mp5(shapes[i], st.ignore_root_matrix));
+        // n_streams <= 0: merged launches (the interpreter kernels, every stage once for all
+        // objects); otherwise one hipGraph per object (JIT tree kernels when enabled) over streams
+        b->merged = n_streams <= 0 && Engine::pruning() > 0;
         const auto t0 = std::chrono::steady_clock::now();
-        if (Engine::pruning() > 0) TreeJit::instance().precompile(progs, 16);
+        if (Engine::pruning() > 0 && !b->merged) TreeJit::instance().precompile(progs, 16);
         b->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        const int ns = std::max(1, std::min(n_streams, 8));
+        const int ns = b->merged ? 1 : std::max(1, std::min(n_streams, 8));
         for (int k = 0; k < ns; ++k) {
             hipStream_t q;
             IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
@@ -858,6 +869,17 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             E.set_object(progs[(size_t)i]);
             E.set_grid(st.resolution, st.box, 0, 1);
             E.marching_cubes(s0);
+        }
+        if (b->merged) {   // the objects' device state, one row each; every object has the same grid
+            std::vector<ObjArgs> rows;
+            for (auto& e : b->engines) {
+                rows.push_back(e->obj_args());
+                b->depth = std::max(b->depth, e->depth());
+            }
+            b->objs.reserve(rows.size() * sizeof(ObjArgs));
+            IMPLI_HIP(hipMemcpy(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice));
+            IMPLI_HIP(hipStreamSynchronize(s0));
+            return b;
         }
         bool graphs = !std::getenv("IMPLISOLID_NO_GRAPH");
         for (int i = 0; i < n && graphs; ++i) {
@@ -899,6 +921,15 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
 int implisolid_batch_run(implisolid_batch* b, void* stream) {
     try {
         hipStream_t s = (hipStream_t)stream;
+        if (b->merged) {
+            Engine& E0 = *b->engines[0];
+            const int n = (int)b->engines.size();
+            launch_batch_eval(b->objs.as<ObjArgs>(), n, b->depth, E0.d_rabbit(), E0.tab_range(), E0.grid(),
+                              Engine::pruning() >= 2 ? 1 : 0, s);
+            launch_batch_mc(b->objs.as<ObjArgs>(), n, E0.d_cases(), E0.grid(), s);
+            IMPLI_HIP(hipGetLastError());
+            return 0;
+        }
         const int ns = (int)b->streams.size();
         IMPLI_HIP(hipEventRecord(b->events[0], s));
         for (int k = 0; k < ns; ++k) IMPLI_HIP(hipStreamWaitEvent(b->streams[(size_t)k], b->events[0], 0));
@@ -927,7 +958,7 @@ int implisolid_batch_info(implisolid_batch* b, int32_t out[4], double* jit_secon
     out[0] = (int32_t)b->engines.size();
     out[1] = (int32_t)b->streams.size();
     out[2] = b->execs.empty() ? 0 : 1;
-    out[3] = 0;
+    out[3] = b->merged ? 1 : 0;
     if (jit_seconds) *jit_seconds = b->jit_seconds;
     return 0;
 }
@@ -936,6 +967,7 @@ int implisolid_batch_counts(implisolid_batch* b, int i, uint32_t out[3]) {
     try {
         if (i < 0 || i >= (int)b->engines.size()) throw InputError("implisolid_batch_counts: bad index");
         for (auto q : b->streams) IMPLI_HIP(hipStreamSynchronize(q));
+        if (b->merged) IMPLI_HIP(hipDeviceSynchronize());   // run() went to the caller's stream
         bool of = false;
         const SlabCounts c = b->engines[(size_t)i]->read_counts(b->streams[0], &of);
         out[0] = c.n_verts();
@@ -952,6 +984,7 @@ int implisolid_batch_download(implisolid_batch* b, int i, float* verts, int32_t*
     try {
         if (i < 0 || i >= (int)b->engines.size()) throw InputError("implisolid_batch_download: bad index");
         for (auto q : b->streams) IMPLI_HIP(hipStreamSynchronize(q));
+        if (b->merged) IMPLI_HIP(hipDeviceSynchronize());
         bool of = false;
         Engine& E = *b->engines[(size_t)i];
         const SlabCounts c = E.read_counts(b->streams[0], &of);
@@ -970,6 +1003,7 @@ void implisolid_batch_destroy(implisolid_batch* b) {
     for (auto x : b->execs) (void)hipGraphExecDestroy(x);
     for (auto e : b->events) (void)hipEventDestroy(e);
     for (auto q : b->streams) (void)hipStreamDestroy(q);
+    b->objs.release();
     delete b;
 }
 

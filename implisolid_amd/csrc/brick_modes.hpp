@@ -102,7 +102,25 @@ __device__ __forceinline__ void coarse_modes_body(const IvEval& ev, const GridDe
     block_append<256>(b < cg.n_bricks && c == kBrickMixed, (uint32_t)b, clist, ccount, (uint32_t)cg.n_bricks);
 }
 
-// Bricks of the listed mixed coarse boxes: one thread per (listed box, brick in it).
+// Bricks of the listed mixed coarse boxes: one thread per (listed box, brick in it); item i is brick
+// i % kCZ of listed box i / kCZ.
+template <class IvEval>
+__device__ __forceinline__ void brick_refine_item(const IvEval& ev, const GridDesc& g, const BrickGrid& bg,
+                                                  const BrickGrid& cg, const uint64_t* __restrict__ cmodes,
+                                                  const uint32_t* __restrict__ clist, uint64_t* __restrict__ modes,
+                                                  uint8_t* __restrict__ cls, uint32_t i) {
+    const uint32_t cb = clist[i / kCZ];
+    int cx, cy, cz;
+    brick_of((int)cb, cg, cx, cy, cz);
+    const int bz = cz * kCZ + (int)(i % kCZ);
+    if (bz >= bg.nbz) return;
+    const int b = cx + cy * bg.nbx + bz * bg.nbx * bg.nby;
+    const BrickBox q = brick_box(g, cx, cy, bz, kBZ);
+    uint64_t m = cmodes[cb];
+    const uint8_t c = sign_class(ev(sample_box(g, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1), m, m));
+    modes[b] = m;
+    cls[b] = sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
+}
 template <class IvEval>
 __device__ __forceinline__ void brick_refine_body(const IvEval& ev, const GridDesc& g, const BrickGrid& bg,
                                                   const BrickGrid& cg, const uint64_t* __restrict__ cmodes,
@@ -110,19 +128,8 @@ __device__ __forceinline__ void brick_refine_body(const IvEval& ev, const GridDe
                                                   const uint32_t* __restrict__ ccount, uint64_t* __restrict__ modes,
                                                   uint8_t* __restrict__ cls) {
     const uint32_t total = min(*ccount, (uint32_t)cg.n_bricks) * kCZ;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-        const uint32_t cb = clist[i / kCZ];
-        int cx, cy, cz;
-        brick_of((int)cb, cg, cx, cy, cz);
-        const int bz = cz * kCZ + (int)(i % kCZ);
-        if (bz >= bg.nbz) continue;
-        const int b = cx + cy * bg.nbx + bz * bg.nbx * bg.nby;
-        const BrickBox q = brick_box(g, cx, cy, bz, kBZ);
-        uint64_t m = cmodes[cb];
-        const uint8_t c = sign_class(ev(sample_box(g, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1), m, m));
-        modes[b] = m;
-        cls[b] = sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
-    }
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256)
+        brick_refine_item(ev, g, bg, cg, cmodes, clist, modes, cls, i);
 }
 
 }  // namespace impli

@@ -455,6 +455,28 @@ SlabCounts Engine::marching_cubes(hipStream_t s) {
     return c;
 }
 
+ObjArgs Engine::obj_args() const {
+    if (!marks_valid_) throw InputError("engine: obj_args needs one pruned eval_field first");
+    ObjArgs o{};
+    o.prog = prog_.as<Program>();
+    o.cmodes = cmodes_.as<uint64_t>();
+    o.ccls = ccls_.as<uint8_t>();
+    o.clist = clist_.as<uint32_t>();
+    o.modes = modes_.as<uint64_t>();
+    o.cls = cls_.as<uint8_t>();
+    o.fill = fill_.as<uint8_t>();
+    o.blist = blist_.as<uint32_t>();
+    o.lmodes = lmodes_.as<uint64_t>();
+    o.umark = umark_.as<uint32_t>();
+    o.mark_id = mark_id_;
+    o.field = field_.as<float>();
+    o.signs = signs_.p;
+    o.counters = counters_.as<uint32_t>();
+    o.mc = buffers();
+    o.mc.offsets = offsets_.as<uint32_t>();
+    return o;
+}
+
 void Engine::eval_points(const float* d_xyz, int64_t n, float* d_f, float* d_grad, hipStream_t s) {
     if (!have_object_) throw InputError("engine: no object set");
     if (const TreeJit::PointKernels* pk = point_jit()) {

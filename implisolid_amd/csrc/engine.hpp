@@ -87,6 +87,12 @@ public:
     // whole single-GPU marching cubes: eval + count + emit (+ retry on overflow); returns counts
     SlabCounts marching_cubes(hipStream_t stream);
 
+    // this object's state for the merged launches of an object stream (kernels.hpp ObjArgs); the
+    // pruned path after one eval_field (its unit marks), valid until the buffers grow
+    ObjArgs obj_args() const;
+    float2 tab_range() const { return tab_range_; }
+    const CaseInfo* d_cases() const { return cases_.as<CaseInfo>(); }
+
     // direct evaluation at device points
     void eval_points(const float* d_xyz, int64_t n, float* d_f, float* d_grad, hipStream_t stream);
 

@@ -16,6 +16,7 @@
 //                (test_sign_fill_field_equivalent + every MC parity test).
 // k_eval_points: arbitrary points (direct-eval ABI, mcc2.cpp:815-911) with optional gradient.
 #include <algorithm>
+#include <stdexcept>
 #include <cstddef>
 #include <cstdlib>
 
@@ -25,6 +26,7 @@
 #include "brick_modes.hpp"
 #include "kernels.hpp"
 #include "jit.hpp"
+#include "batch_device.hpp"
 
 namespace impli {
 
@@ -102,16 +104,13 @@ __global__ __launch_bounds__(kEvalBlock) void k_eval_field_pruned(const Program*
 // kernel reads them in list order).  List appends are aggregated per block: one atomic per
 // block (same-address atomics serialise: a wave-level append measured +30 us).
 constexpr int kFillBlock = 512;   // one list atomic per 512 bricks (256: +3 us, 1024: +1.5 us at 512^3)
-__global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid bg, BrickGrid cg,
-                                                           const uint8_t* __restrict__ ccls,
-                                                           const uint64_t* __restrict__ cmodes,
-                                                           const uint8_t* __restrict__ cls,
-                                                           const uint64_t* __restrict__ modes, int sign_fill,
-                                                           uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
-                                                           uint64_t* __restrict__ lmodes, uint32_t* __restrict__ count,
-                                                           sign_piece_t* __restrict__ signs,
-                                                           uint32_t* __restrict__ ccount_reset,
-                                                           uint32_t* __restrict__ umark, uint32_t mark_id) {
+__device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGrid& bg, const BrickGrid& cg,
+                                                const uint8_t* __restrict__ ccls, const uint64_t* __restrict__ cmodes,
+                                                const uint8_t* __restrict__ cls, const uint64_t* __restrict__ modes,
+                                                int sign_fill, uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
+                                                uint64_t* __restrict__ lmodes, uint32_t* __restrict__ count,
+                                                sign_piece_t* __restrict__ signs, uint32_t* __restrict__ ccount_reset,
+                                                uint32_t* __restrict__ umark, uint32_t mark_id) {
     __shared__ uint32_t wcnt[kFillBlock / 64], wbase[kFillBlock / 64];
     __shared__ uint8_t s_cls[kFillBlock];   // the block's bricks' classes (its x / y neighbours mostly)
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // the refine pass has read it; kept in [14] for stats
@@ -196,6 +195,60 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid
         const int y1 = min(by * kBY + kBY, g.n), z1 = min(bz * kBZ + kBZ, layers);
         for (int z = bz * kBZ; z < z1; ++z)
             for (int y = by * kBY; y < y1; ++y) signs[((size_t)z * g.n + y) * row_pieces + bx] = piece;
+    }
+}
+__global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid bg, BrickGrid cg,
+                                                           const uint8_t* __restrict__ ccls,
+                                                           const uint64_t* __restrict__ cmodes,
+                                                           const uint8_t* __restrict__ cls,
+                                                           const uint64_t* __restrict__ modes, int sign_fill,
+                                                           uint8_t* __restrict__ fill, uint32_t* __restrict__ list,
+                                                           uint64_t* __restrict__ lmodes, uint32_t* __restrict__ count,
+                                                           sign_piece_t* __restrict__ signs,
+                                                           uint32_t* __restrict__ ccount_reset,
+                                                           uint32_t* __restrict__ umark, uint32_t mark_id) {
+    brick_fill_body(g, bg, cg, ccls, cmodes, cls, modes, sign_fill, fill, list, lmodes, count, signs, ccount_reset,
+                    umark, mark_id);
+}
+
+// ---- merged launches of an object stream (ObjArgs, kernels.hpp): block row y = object y ----------
+template <int D>
+__global__ __launch_bounds__(256) void k_coarse_modes_b(const ObjArgs* __restrict__ objs, const float* __restrict__ tab,
+                                                        float2 tab_range, GridDesc g, BrickGrid cg) {
+    const ObjArgs& o = objs[blockIdx.y];
+    coarse_modes_body(InterpIv<D>{o.prog, tab, tab_range}, g, cg, o.cmodes, o.ccls, o.clist, o.counters);
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_brick_refine_b(const ObjArgs* __restrict__ objs, int n, const float* __restrict__ tab,
+                                                        float2 tab_range, GridDesc g, BrickGrid bg, BrickGrid cg) {
+    __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
+    const uint32_t total = batch_prefix(objs, n, kCoarseListWord, (uint32_t)kCZ, (uint32_t)cg.n_bricks, s_pre);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const int k = batch_object_of(s_pre, n, i);
+        const ObjArgs& o = objs[k];
+        brick_refine_item(InterpIv<D>{o.prog, tab, tab_range}, g, bg, cg, o.cmodes, o.clist, o.modes, o.cls, i - s_pre[k]);
+    }
+}
+__global__ __launch_bounds__(kFillBlock) void k_brick_fill_b(const ObjArgs* __restrict__ objs, GridDesc g, BrickGrid bg,
+                                                             BrickGrid cg, int sign_fill) {
+    const ObjArgs& o = objs[blockIdx.y];
+    brick_fill_body(g, bg, cg, o.ccls, o.cmodes, o.cls, o.modes, sign_fill, o.fill, o.blist, o.lmodes,
+                    o.counters + kBrickListWord, static_cast<sign_piece_t*>(o.signs), o.counters + kCoarseListWord,
+                    o.umark, o.mark_id);
+}
+template <int D>
+__global__ __launch_bounds__(256) void k_eval_field_pruned_b(const ObjArgs* __restrict__ objs, int n,
+                                                             const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
+    __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
+    const uint32_t total = batch_prefix(objs, n, kBrickListWord, 1u, (uint32_t)bg.n_bricks, s_pre);
+    const uint32_t stride = gridDim.x * 4;
+    for (uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); i < total; i += stride) {
+        const int k = __builtin_amdgcn_readfirstlane(batch_object_of(s_pre, n, i));
+        const ObjArgs& o = objs[k];
+        const uint32_t li = i - s_pre[k];
+        // one layer at a time: the interpreter's node stacks are VGPR arrays, a layer pair doubles them
+        eval_one_brick<InterpEval<D>, false>(InterpEval<D>{o.prog, tab}, g, bg, (int)o.blist[li], o.lmodes[li], o.field,
+                                             static_cast<sign_piece_t*>(o.signs));
     }
 }
 
@@ -346,6 +399,31 @@ void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_
     else if (depth <= 8) k_eval_field_pruned<8><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
     else if (depth <= 12) k_eval_field_pruned<12><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
     else k_eval_field_pruned<16><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+}
+
+// flat merged kernels (refine, eval): a fixed grid over all objects' items
+constexpr unsigned kBatchRefineBlocks = 2048, kBatchEvalBlocks = 4096;
+
+void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
+                       int sign_fill, hipStream_t s) {
+    const BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
+    if (bg.n_bricks <= 0 || n <= 0) return;
+    if (n > kMaxBatchObjects) throw std::runtime_error("merged object stream: more than 1024 objects per launch");
+    depth = eval_depth(depth);
+    const dim3 gc((unsigned)((cg.n_bricks + 255) / 256), (unsigned)n);
+    const dim3 gf((unsigned)((bg.n_bricks + kFillBlock - 1) / kFillBlock), (unsigned)n);
+#define IMPLI_BATCH_EVAL(DD)                                                                               \
+    do {                                                                                                   \
+        k_coarse_modes_b<DD><<<gc, 256, 0, s>>>(d_objs, d_rabbit, tab_range, g, cg);                       \
+        k_brick_refine_b<DD><<<kBatchRefineBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, tab_range, g, bg, cg); \
+        k_brick_fill_b<<<gf, kFillBlock, 0, s>>>(d_objs, g, bg, cg, sign_fill);                            \
+        k_eval_field_pruned_b<DD><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);            \
+    } while (0)
+    if (depth <= 4) IMPLI_BATCH_EVAL(4);
+    else if (depth <= 8) IMPLI_BATCH_EVAL(8);
+    else if (depth <= 12) IMPLI_BATCH_EVAL(12);
+    else IMPLI_BATCH_EVAL(16);
+#undef IMPLI_BATCH_EVAL
 }
 
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,

@@ -4,7 +4,8 @@
 #include "grid.hpp"
 
 // evaluate a brick's two layers as one straight-line block (measured 57 -> 45 us at 512^3 on the
-// config-4 tree); IMPLISOLID_EVAL_PAIR=0 in the environment compiles the JIT kernels without it
+// config-4 tree); IMPLISOLID_EVAL_PAIR=0 in the environment compiles the JIT kernels without it.
+// eval_bricks_body's Pair parameter chooses per kernel (the merged interpreter launch: off)
 #ifndef IMPLI_EVAL_PAIR
 #define IMPLI_EVAL_PAIR 1
 #endif
@@ -46,45 +47,29 @@ __device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, in
 // `ev(modes, x, y, z)`, stored, and its sign bit set (wave ballot: 64 bits = kBY rows x kBX
 // samples).  Sign-filled bricks never reach this kernel -- k_brick_fill wrote their constant sign
 // bits.
-template <class Eval>
-__device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
-                                                 const uint64_t* __restrict__ modes,
-                                                 const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
-                                                 float* __restrict__ field, void* __restrict__ signs_raw) {
-    sign_piece_t* signs = static_cast<sign_piece_t*>(signs_raw);
-    const uint32_t nb = *count;
+// one listed brick (b, its modes m) by the calling wave
+template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
+__device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g, const BrickGrid& bg, int b, uint64_t m64,
+                                               float* __restrict__ field, sign_piece_t* __restrict__ signs) {
     const int lane = threadIdx.x & 63;
     const int n = g.n;
     const int layers = g.fz1 - g.fz0;
     const int row_pieces = (64 / kBX) * sign_row_words(g);
-    const uint32_t wpb = blockDim.x >> 6;   // waves per block
-    const uint32_t stride = gridDim.x * wpb;
-    uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-    // the next brick's list entry and modes are loaded while this brick is evaluated
-    uint32_t b_next = i < nb ? list[i] : 0u;
-    uint64_t m_next = i < nb ? modes[i] : 0ull;
-    for (; i < nb; i += stride) {
-        const int b = __builtin_amdgcn_readfirstlane((int)b_next);
-        const uint64_t m64 = m_next;
-        if (i + stride < nb) {
-            b_next = list[i + stride];
-            m_next = modes[i + stride];
-        }
-        int bx, by, bz;
-        brick_of(b, bg, bx, by, bz);
-        const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
-        const bool ok = sx < n && sy < n;
-        const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
-        // brick-major field (grid.hpp field_index): the brick's layer k is 64 consecutive floats, one
-        // per lane -- the wave stores two whole lines (lanes past the grid edge fill the padding)
-        float* out = field + (size_t)b * kBrickSamples + lane;
-        const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
-                           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
-        const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
-#if IMPLI_EVAL_PAIR
+    int bx, by, bz;
+    brick_of(b, bg, bx, by, bz);
+    const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
+    const bool ok = sx < n && sy < n;
+    const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
+    // brick-major field (grid.hpp field_index): the brick's layer k is 64 consecutive floats, one
+    // per lane -- the wave stores two whole lines (lanes past the grid edge fill the padding)
+    float* out = field + (size_t)b * kBrickSamples + lane;
+    const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
+                       (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
+    const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
+    if constexpr (Pair) {
         // both layers' tree evaluations in one straight-line block: two independent dependency
         // chains per lane (a layer past the slab is evaluated at a clamped z and not stored)
-        static_assert(kBZ == 2, "IMPLI_EVAL_PAIR needs two layers per brick");
+        static_assert(!Pair || kBZ == 2, "the layer pair needs two layers per brick");
         const int l0 = bz * kBZ, l1 = l0 + 1;
         const float f0 = ev(m, x, y, sample_z(g, l0));
         const float f1 = ev(m, x, y, sample_z(g, l1 < layers ? l1 : l0));
@@ -100,7 +85,7 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
                 if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg >> (kBX * lane));
             }
         }
-#else
+    } else {
 #pragma unroll 1
         for (int k = 0; k < kBZ; ++k) {
             const int layer = bz * kBZ + k;
@@ -114,7 +99,30 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
                 if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg >> (kBX * lane));
             }
         }
-#endif
+    }
+}
+
+template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
+__device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
+                                                 const uint64_t* __restrict__ modes,
+                                                 const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                 float* __restrict__ field, void* __restrict__ signs_raw) {
+    sign_piece_t* signs = static_cast<sign_piece_t*>(signs_raw);
+    const uint32_t nb = *count;
+    const uint32_t wpb = blockDim.x >> 6;   // waves per block
+    const uint32_t stride = gridDim.x * wpb;
+    uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+    // the next brick's list entry and modes are loaded while this brick is evaluated
+    uint32_t b_next = i < nb ? list[i] : 0u;
+    uint64_t m_next = i < nb ? modes[i] : 0ull;
+    for (; i < nb; i += stride) {
+        const int b = __builtin_amdgcn_readfirstlane((int)b_next);
+        const uint64_t m64 = m_next;
+        if (i + stride < nb) {
+            b_next = list[i + stride];
+            m_next = modes[i + stride];
+        }
+        eval_one_brick<Eval, Pair>(ev, g, bg, b, m64, field, signs);
     }
 }
 

@@ -52,4 +52,31 @@ void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 void launch_mc_faces(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);
 
+// One object's device state for the merged launches of an object stream (BASELINE config 5): every
+// stage of eval + MC runs once for all objects, block row y = object y (same grid for all objects,
+// each with its own node program, buffers and counters; the interpreter kernels, since every
+// object has its own tree).
+struct ObjArgs {
+    const Program* prog;
+    uint64_t* cmodes;
+    uint8_t* ccls;
+    uint32_t* clist;
+    uint64_t* modes;
+    uint8_t* cls;
+    uint8_t* fill;
+    uint32_t* blist;
+    uint64_t* lmodes;
+    uint32_t* umark;
+    uint32_t mark_id;
+    float* field;
+    void* signs;
+    uint32_t* counters;
+    MCBuffers mc;
+};
+// eval (interval passes, fill, listed bricks) and MC (count, scan, vertices, faces) of n objects;
+// blocks per object are capped for the grid-stride kernels (small grids: most blocks would idle)
+void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
+                       int sign_fill, hipStream_t s);
+void launch_batch_mc(const ObjArgs* d_objs, int n, const CaseInfo* d_cases, const GridDesc& g, hipStream_t s);
+
 }  // namespace impli

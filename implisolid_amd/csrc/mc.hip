@@ -30,6 +30,7 @@
 #include "ifunc_device.hpp"
 #include "kernels.hpp"
 #include "mc_device.hpp"
+#include "batch_device.hpp"
 
 namespace impli {
 
@@ -105,12 +106,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 //   -> unit_cnt[64 group + k] = k-th non-empty unit of the group {unit in group, own / tri / act
 //      exclusive bases in the group}; scan_blk[c][group] = the group's sums (own, tri, act, halo
 //      own, non-empty units), read by k_unit_scan.
-__global__ __launch_bounds__(512) void k_mc_count(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+__device__ __forceinline__ void mc_count_body(const GridDesc& g, const MCBuffers& b) {
     __shared__ uint32_t s_u[kGroupUnits][4];
     __shared__ uint8_t s_fu[kGroupUnits];   // the group's candidate units, in order
     __shared__ uint32_t s_nf;
-    const int t = threadIdx.x, nt_ = blockDim.x;
-    (void)cases;   // triangle counts come from chunk_triangles (checked against the table)
+    const int t = threadIdx.x, nt_ = blockDim.x;   // triangle counts: chunk_triangles (checked against the table)
     for (int k = t; k < 4 * kGroupUnits; k += nt_) (&s_u[0][0])[k] = 0u;
     const int64_t G = blockIdx.x;
     const int nch = (g.m + 63) / 64;
@@ -193,6 +193,7 @@ __global__ __launch_bounds__(512) void k_mc_count(const CaseInfo* __restrict__ c
         }
     }
 }
+__global__ __launch_bounds__(512) void k_mc_count(GridDesc g, MCBuffers b) { mc_count_body(g, b); }
 
 // K2b: one block per group.  Its global bases are the sums of the groups before it, read straight
 // from L2 (kScanParts x G words, all loads in flight together; nothing waits on another block), then
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(512) void k_mc_count(const CaseInfo* __restrict__ c
 // cross the XCDs' L2s at memory latency, one round trip per 64 groups walked.)
 constexpr int kScanBlock = 256;
 constexpr int kScanRows = kScanParts + 1;   // + the non-empty unit counts (summed for statistics)
-__global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) {
+__device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffers& b) {
     __shared__ uint32_t s_part[kScanBlock / 64][kScanRows];
     __shared__ uint32_t s_base[kScanRows];
     const int64_t G = blockIdx.x, ng = n_groups(g);
@@ -249,6 +250,7 @@ __global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers 
         b.counters[6] = s_base[5] + nne;                          // non-empty units (statistics)
     }
 }
+__global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) { unit_scan_body(g, b); }
 
 __global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     mc_cells_body(cases, g, b);
@@ -271,7 +273,42 @@ struct __attribute__((packed, aligned(4))) IdTriple { uint32_t a, b, c; };
 // at most 7, instead of one load per triangle corner (up to 15) -- spreads them to the 12 edges in
 // LDS, and writes each triangle as one 12-byte store.  (Vector-memory issue, not bytes, bounded the
 // corner-per-load version: 3 % VALU, 53 % of wave time ready but not issued.)
-__global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+// one active-cell record i of a slab: its triangles with the vertex ids of their corners
+__device__ __forceinline__ void face_record(const CaseInfo* s_case, uint32_t (*s_w)[256], const uint32_t off[7],
+                                            const MCBuffers& b, uint32_t Voff, uint32_t i) {
+    const int t = threadIdx.x;
+    const uint32_t* __restrict__ vid3 = b.vid3;
+    const uint4 r = b.records[i];
+    const uint32_t L = r.x, ci = r.y, fbase = r.z;
+    const CaseInfo& C = s_case[ci];
+    const int ntri = C.ntri;
+    if (fbase + ntri > (uint64_t)b.cap_f) { *b.overflow = 1u; return; }
+    // every owner's triple loaded unconditionally (an owner the case does not use re-reads the
+    // cell's own triple), all before any use; the owners a case uses always exist
+    const uint32_t need = C.owners;
+    IdTriple w[7];
+#pragma unroll
+    for (int o = 0; o < 7; ++o) {
+        const uint32_t cell = ((need >> o) & 1u) ? L - off[o] : L;
+        w[o] = *reinterpret_cast<const IdTriple*>(vid3 + (size_t)cell * 3);
+    }
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+        const IdTriple& q = w[c_edge_owner_idx[e]];
+        const int sl = c_edge_slot[e];
+        s_w[e][t] = sl == 0 ? q.a : sl == 1 ? q.b : q.c;
+    }
+    int32_t* out = b.faces + 3 * (size_t)fbase;
+    for (int k = 0; k < ntri; ++k) {
+        IdTriple f;
+        f.a = Voff + s_w[C.tri[3 * k]][t];
+        f.b = Voff + s_w[C.tri[3 * k + 1]][t];
+        f.c = Voff + s_w[C.tri[3 * k + 2]][t];
+        *reinterpret_cast<IdTriple*>(out + 3 * k) = f;
+    }
+}
+
+__device__ __forceinline__ void mc_faces_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
     __shared__ CaseInfo s_case[256];
     __shared__ uint32_t s_w[12][256];   // per lane: the vertex id of each of its cell's 12 edges
     const int t = threadIdx.x;
@@ -285,38 +322,55 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
     uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
     if (b.gathered)
         for (int r = 0; r < b.rank; ++r) Voff += b.gathered[4 * r] - b.gathered[4 * r + 3];
-    const uint32_t* __restrict__ vid3 = b.vid3;
     const uint32_t nb = gridDim.x, lb = (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u;
     const uint32_t per = (lim + nb - 1u) / nb, i_end = min(lim, (lb + 1u) * per);
-    for (uint32_t i = lb * per + t; i < i_end; i += 256) {
-        const uint4 r = b.records[i];
-        const uint32_t L = r.x, ci = r.y, fbase = r.z;
-        const CaseInfo& C = s_case[ci];
-        const int ntri = C.ntri;
-        if (fbase + ntri > (uint64_t)b.cap_f) { *b.overflow = 1u; continue; }
-        // every owner's triple loaded unconditionally (an owner the case does not use re-reads the
-        // cell's own triple), all before any use; the owners a case uses always exist
-        const uint32_t need = C.owners;
-        IdTriple w[7];
-#pragma unroll
-        for (int o = 0; o < 7; ++o) {
-            const uint32_t cell = ((need >> o) & 1u) ? L - off[o] : L;
-            w[o] = *reinterpret_cast<const IdTriple*>(vid3 + (size_t)cell * 3);
-        }
-#pragma unroll
-        for (int e = 0; e < 12; ++e) {
-            const IdTriple& q = w[c_edge_owner_idx[e]];
-            const int sl = c_edge_slot[e];
-            s_w[e][t] = sl == 0 ? q.a : sl == 1 ? q.b : q.c;
-        }
-        int32_t* out = b.faces + 3 * (size_t)fbase;
-        for (int k = 0; k < ntri; ++k) {
-            IdTriple f;
-            f.a = Voff + s_w[C.tri[3 * k]][t];
-            f.b = Voff + s_w[C.tri[3 * k + 1]][t];
-            f.c = Voff + s_w[C.tri[3 * k + 2]][t];
-            *reinterpret_cast<IdTriple*>(out + 3 * k) = f;
-        }
+    for (uint32_t i = lb * per + t; i < i_end; i += 256) face_record(s_case, s_w, off, b, Voff, i);
+}
+
+__global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+    mc_faces_body(cases, g, b);
+}
+
+// ---- merged launches of an object stream (ObjArgs, kernels.hpp): block row y = object y ----------
+__global__ __launch_bounds__(512) void k_mc_count_b(const ObjArgs* __restrict__ objs, GridDesc g) {
+    mc_count_body(g, objs[blockIdx.y].mc);
+}
+__global__ __launch_bounds__(kScanBlock) void k_unit_scan_b(const ObjArgs* __restrict__ objs, GridDesc g) {
+    unit_scan_body(g, objs[blockIdx.y].mc);
+}
+// vertex pass: one flat index over every object's unit parts (batch_device.hpp), a wave per part
+__global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells_b(const CaseInfo* __restrict__ cases,
+                                                                const ObjArgs* __restrict__ objs, int n, GridDesc g) {
+    __shared__ CaseInfo s_case[256];
+    __shared__ uint64_t s_bits[kVertsWaves][9][64];
+    __shared__ uint32_t s_excl[kVertsWaves][64];
+    __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
+    const int t = threadIdx.x, wid = t >> 6;
+    for (int k = t; k < 256; k += blockDim.x) s_case[k] = cases[k];
+    const uint32_t total = batch_prefix(objs, n, 0, 1u, 0xffffffffu, s_pre);   // counters[0]: unit parts
+    for (uint32_t e = blockIdx.x * kVertsWaves + wid; e < total; e += gridDim.x * kVertsWaves) {
+        const int k = __builtin_amdgcn_readfirstlane(batch_object_of(s_pre, n, e));
+        mc_cells_part(s_case, g, objs[k].mc, e - s_pre[k], s_bits[wid], s_excl[wid]);
+    }
+}
+// face pass: one flat index over every object's records, a lane per record
+__global__ __launch_bounds__(256) void k_mc_faces_b(const CaseInfo* __restrict__ cases, const ObjArgs* __restrict__ objs,
+                                                    int n, GridDesc g) {
+    __shared__ CaseInfo s_case[256];
+    __shared__ uint32_t s_w[12][256];
+    __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
+    const int t = threadIdx.x;
+    s_case[t] = cases[t];
+    const uint32_t total = batch_prefix(objs, n, 4, 1u, 0xffffffffu, s_pre);   // counters[4]: active cells
+    const int64_t m = g.m;
+    const uint32_t off[7] = {0u, 1u, (uint32_t)m, (uint32_t)(m + 1), (uint32_t)(m * m), (uint32_t)(m * m + m),
+                             (uint32_t)(m * m + 1)};
+    for (uint32_t gi = blockIdx.x * 256 + t; gi < total; gi += gridDim.x * 256) {
+        const int k = batch_object_of(s_pre, n, gi);
+        const MCBuffers& b = objs[k].mc;
+        const uint32_t i = gi - s_pre[k];
+        if (i >= (uint64_t)b.cap_rec) { *b.overflow = 1u; continue; }
+        face_record(s_case, s_w, off, b, b.offsets ? b.offsets[0] : 0u, i);
     }
 }
 
@@ -329,7 +383,8 @@ void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
     // most 512: twice the resident groups of 1024-lane blocks
     const int items = kGroupUnits * kUnitRows * ((g.m + 63) / 64);
     const unsigned threads = (unsigned)std::min(512, (items + 63) / 64 * 64);
-    k_mc_count<<<(unsigned)ng, threads, 0, s>>>(d_cases, g, b);
+    (void)d_cases;
+    k_mc_count<<<(unsigned)ng, threads, 0, s>>>(g, b);
 }
 
 void launch_mc_scan(const GridDesc& g, const MCBuffers& b, hipStream_t s) {
@@ -347,6 +402,25 @@ void launch_mc_verts(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers
         k_mc_cells<<<(unsigned)std::min<int64_t>((nu + kVertsWaves - 1) / kVertsWaves, kVertsMaxBlocks),
                      64 * kVertsWaves, 0, s>>>(d_cases, g, b);
     }
+}
+
+}  // namespace impli
+
+namespace impli {
+
+// grids of the flat merged vertex / face kernels
+constexpr unsigned kBatchCellBlocks = 4096, kBatchFaceBlocks = 2048;
+
+void launch_batch_mc(const ObjArgs* d_objs, int n, const CaseInfo* d_cases, const GridDesc& g, hipStream_t s) {
+    const int64_t ng = n_groups(g), nu = n_units(g);
+    if (ng == 0 || n <= 0) return;
+    const int items = kGroupUnits * kUnitRows * ((g.m + 63) / 64);
+    const unsigned threads = (unsigned)std::min(512, (items + 63) / 64 * 64);
+    k_mc_count_b<<<dim3((unsigned)ng, (unsigned)n), threads, 0, s>>>(d_objs, g);
+    k_unit_scan_b<<<dim3((unsigned)ng, (unsigned)n), kScanBlock, 0, s>>>(d_objs, g);
+    (void)nu;
+    k_mc_cells_b<<<kBatchCellBlocks, 64 * kVertsWaves, 0, s>>>(d_cases, d_objs, n, g);
+    k_mc_faces_b<<<kBatchFaceBlocks, 256, 0, s>>>(d_cases, d_objs, n, g);
 }
 
 }  // namespace impli

@@ -135,23 +135,16 @@ __device__ __forceinline__ int select_bit(uint64_t x, uint32_t r) {
 // unit's items (row, 64-cell chunk) go to LDS with their exclusive cell counts; each lane then
 // finds its own cell -- the item by binary search, the cell by selecting the bit -- so cells are
 // listed in cell order 64 at a time, with no lane looping over a dense chunk's bits.
-__device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
-    __shared__ CaseInfo s_case[256];
-    __shared__ uint64_t s_bits[kVertsWaves][9][64];   // per wave and item: the 8 corner words + nt
-    __shared__ uint32_t s_excl[kVertsWaves][64];      // per wave and item: cells in the items before it
-    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t n_ne = b.counters[0];              // non-empty units
-    const uint32_t w0 = blockIdx.x * kVertsWaves;
-    if (w0 >= n_ne) return;                           // uniform over the block
-    for (int k = t; k < 256; k += blockDim.x) s_case[k] = cases[k];
-    __syncthreads();
+// one part e of the flat unit list, by the calling wave (s_case: the case table in LDS; bits /
+// excl: the wave's LDS scratch)
+__device__ __forceinline__ void mc_cells_part(const CaseInfo* s_case, const GridDesc& g, const MCBuffers& b, uint32_t e,
+                                              uint64_t (*bits)[64], uint32_t* excl) {
+    const int lane = threadIdx.x & 63;
     const uint32_t H = b.counters[1];
     const int nch = (g.m + 63) / 64;
     const int64_t rows = n_rows(g);
-    uint64_t(*bits)[64] = s_bits[wid];
-    uint32_t* excl = s_excl[wid];
     const int items = kUnitRows * nch;
-    for (uint32_t e = w0 + wid; e < n_ne; e += gridDim.x * kVertsWaves) {
+    {
         const uint4 ent = b.ulist[e];   // {unit, vbase, fbase, abase}
         const uint32_t up = b.upart[e];   // part | parts << 8: this wave emits windows w % parts == part
         const uint32_t part = up & 255u, parts = up >> 8;
@@ -256,6 +249,19 @@ __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases
             }
         }
     }
+}
+
+__device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
+    __shared__ CaseInfo s_case[256];
+    __shared__ uint64_t s_bits[kVertsWaves][9][64];   // per wave and item: the 8 corner words + nt
+    __shared__ uint32_t s_excl[kVertsWaves][64];      // per wave and item: cells in the items before it
+    const int t = threadIdx.x, wid = t >> 6;
+    const uint32_t n_ne = b.counters[0];              // non-empty units
+    const uint32_t w0 = blockIdx.x * kVertsWaves;
+    if (w0 >= n_ne) return;                           // uniform over the block
+    for (int k = t; k < 256; k += blockDim.x) s_case[k] = cases[k];
+    __syncthreads();
+    for (uint32_t e = w0 + wid; e < n_ne; e += gridDim.x * kVertsWaves) mc_cells_part(s_case, g, b, e, s_bits[wid], s_excl[wid]);
 }
 
 }  // namespace impli

@@ -26,6 +26,8 @@
 #include "ob02_device.hpp"
 #include "jit.hpp"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace impli {
 
 using namespace dev;
@@ -940,15 +942,25 @@ void Ob02::read_counters() {   // cap hits and (profiling) evaluations since loa
     cap_hits_ = h[1];
 }
 
-// profiling (set_profile): per-stage wall time with the stream drained at every stage boundary
+// Every stage is a roctx range (SURVEY.md section 5 tracing; rocprofv3 --marker-trace shows them
+// beside the kernels).  Profiling (set_profile) adds per-stage wall times, the stream drained at
+// every stage boundary.
+static const char* const kStageNames[Ob02::kStages] = {"ob02 topology", "ob02 vertex resampling", "ob02 edge-length fold",
+                                                       "ob02 projection", "ob02 qem", "ob02 subdivision", "ob02 fetch"};
 Ob02::Stage::Stage(Ob02* o, int k) : ob(o), stage(k) {
+    roctxRangePush(kStageNames[k]);
     if (ob->profile_) {
         IMPLI_HIP(hipStreamSynchronize(ob->s));
         t0 = std::chrono::steady_clock::now();
     }
 }
 void Ob02::Stage::next(int k) {
-    if (!ob->profile_) return;
+    roctxRangePop();
+    roctxRangePush(kStageNames[k]);
+    if (!ob->profile_) {
+        stage = k;
+        return;
+    }
     IMPLI_HIP(hipStreamSynchronize(ob->s));
     const auto t1 = std::chrono::steady_clock::now();
     ob->stage_ms_[stage] += std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -956,6 +968,7 @@ void Ob02::Stage::next(int k) {
     stage = k;
 }
 Ob02::Stage::~Stage() {
+    roctxRangePop();
     if (!ob->profile_) return;
     (void)hipStreamSynchronize(ob->s);
     ob->stage_ms_[stage] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -225,12 +225,16 @@ int64_t implisolid_slab_read_signs(implisolid_slab* s, uint8_t* out, int64_t cap
 /* bricks of the last slab eval: out = [bricks, mixed-sign bricks, sign-filled bricks] (blocking) */
 int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]);
 
-/* Object stream (BASELINE config 5): n objects polygonised with the same mc settings, each by
- * its own engine.  create compiles every tree kernel (parallel hipRTC), runs each object once to
- * size its outputs, then captures each object's eval + count + emit in a hipGraph (direct
- * launches when capture is unavailable, or with IMPLISOLID_NO_GRAPH=1).  run replays all objects,
- * round-robin over n_streams internal streams joined back into `stream` (async).  counts and
- * download block.  info = {objects, streams, graphs (1/0), 0} and the JIT compile seconds. */
+/* Object stream (BASELINE config 5): n objects polygonised with the same mc settings, each with
+ * its own buffers.  create runs each object once to size its outputs, then:
+ *   n_streams <= 0 (merged): run() launches every stage of eval + MC once for all objects (block row
+ *     y = object y; the interpreter kernels, no per-object compilation);
+ *   n_streams >= 1: compiles every tree kernel (parallel hipRTC), captures each object's eval +
+ *     count + emit in a hipGraph (direct launches when capture is unavailable, or with
+ *     IMPLISOLID_NO_GRAPH=1), and run() replays them round-robin over n_streams streams joined back
+ *     into `stream`.
+ * run is async on `stream`; counts and download block.  info = {objects, streams, graphs (1/0),
+ * merged (1/0)} and the JIT compile seconds. */
 typedef struct implisolid_batch implisolid_batch;
 implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, const char* mc_json, int n_streams);
 int implisolid_batch_run(implisolid_batch* b, void* stream);

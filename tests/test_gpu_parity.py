@@ -693,12 +693,15 @@ def test_golden_subdivision_gpu(impli):
 
 
 # ---- object stream (config 5): hipGraph-captured per-object pipelines --------------------------
-def test_batch_stream_matches_oracle(impli, oracle):
+@pytest.mark.parametrize("n_streams", [0, 3])
+def test_batch_stream_matches_oracle(impli, oracle, n_streams):
+    """The object stream, merged launches (n_streams 0: one launch per stage for all objects, block
+    row = object) and per-object graphs over streams: every object's mesh is the oracle's."""
     from implisolid_amd import scenes
     objs = scenes.config5_objects(10, 56) + [(scenes.config3_tree(), scenes.mc_settings(56, 1.0))]
     shapes, mc = [o[0] for o in objs], objs[0][1]
-    with impli.Batch(shapes, mc, n_streams=3) as b:
-        assert b.n == len(shapes)
+    with impli.Batch(shapes, mc, n_streams=n_streams) as b:
+        assert b.n == len(shapes) and b.merged == (n_streams == 0)
         for rep in range(2):                   # replays give the same meshes
             b.run()
             for i, sh in enumerate(shapes):

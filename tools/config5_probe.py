@@ -18,6 +18,20 @@ def main():
     objs = scenes.config5_objects(n, R)
     shapes, mc = [o[0] for o in objs], objs[0][1]
     sp = torch.cuda.current_stream().cuda_stream
+    I.set_jit(0)   # merged launches: the interpreter kernels
+    b = I.Batch(shapes, mc, n_streams=0)
+    for _ in range(3):
+        b.run(sp)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        b.run(sp)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / 20 * 1e3
+    print("merged launches (interpreter)  %.3f ms / %d objects  (%.1f us/object, %.0f Mvox/s)" %
+          (ms, n, ms * 1e3 / n, n * R ** 3 / ms / 1e3), flush=True)
+    b.close()
+    I.set_jit(2)
     for graphs in (True, False):
         if graphs:
             os.environ.pop("IMPLISOLID_NO_GRAPH", None)
