@@ -39,9 +39,9 @@ enum NodeType : int32_t {
     NT_HALF_PLANE = 12,   // half_plane.hpp, params {unit plane_vector, plane_point}
     NT_TETRA = 13,        // tetrahedron.hpp, params {a, b, c, d} x 4 oriented planes
     NT_METABALLS = 14,    // meta_balls_Rydgard.hpp, params {x, y, z, strength, subtract} x 4 balls
-    NT_EXTRUSION = 15,
+    NT_EXTRUSION = 15,    // extrusion.hpp + convex_polygon.hpp, params {n, (nx, ny, n0) x n}
     NT_SCREW_TBB = 16,    // inf_top_bot_bound.hpp over the screw ("screw_gradient_wrong"), params
-                          // {twist, r0, delta} then (next row) the node's inverse matrix    // extrusion.hpp + convex_polygon.hpp, params {n, (nx, ny, n0) x n}
+                          // {twist, r0, delta} then (next row) the node's inverse matrix
 };
 
 enum OpCode : int32_t {
