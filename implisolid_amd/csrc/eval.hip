@@ -101,9 +101,40 @@ __global__ __launch_bounds__(kEvalBlock) void k_eval_field_pruned(const Program*
 // Per brick: its class (inherited from a sign-definite coarse box, or refined), the neighbour rule
 // (brick_modes.hpp), fill[b] = class | fill class << 4, and either the constant sign pieces of a
 // sign-filled brick or an entry in the list of bricks to evaluate (with its modes, so the eval
-// kernel reads them in list order).  List appends are aggregated per block: one atomic per
-// block (same-address atomics serialise: a wave-level append measured +30 us).
-constexpr int kFillBlock = 512;   // one list atomic per 512 bricks (256: +3 us, 1024: +1.5 us at 512^3)
+// kernel reads them in list order).
+//
+// One thread per sign word of a brick row: the kFillP bricks (bx = kFillP c ...) whose pieces make
+// up word c of the row's sample rows.  The class bytes of the bricks and of their neighbour rows
+// (y +- 1, z +- 1) are kFillP consecutive bytes each (one unaligned 8-byte load per row), and the
+// word is the same for every sample row of the brick row: kBY kBZ whole-word stores, consecutive
+// lanes on consecutive words.  Listed bricks get a zero placeholder piece that the eval kernel
+// overwrites (stream order); bytes past a row's last brick are bitmap padding (never read as a cell
+// corner).  List appends are aggregated per block: one atomic per block (same-address atomics
+// serialise: a wave-level append measured +30 us); the units a listed brick marks depend on its
+// row only, so a thread marks them once.
+constexpr int kFillBlock = 256;
+constexpr int kFillP = 64 / kBX;   // bricks (sign pieces) per sign word
+static_assert(kFillP <= 8, "one 8-byte class load per row");
+
+struct RowSeal { bool has, only; };   // sealed_class's row terms (y, z) of a brick row
+__device__ __forceinline__ RowSeal row_seal(const GridDesc& g, int by, int bz) {
+    const BrickBox q = brick_box(g, 0, by, bz, kBZ);
+    return RowSeal{q.y0 == 0 || q.y1 == g.n - 1 || g.fz0 + q.z0 <= 1 || g.fz0 + q.z1 >= g.res - 2,
+                   q.y0 == g.n - 1 || (q.z0 == q.z1 && (g.fz0 + q.z0 <= 1 || g.fz0 + q.z0 >= g.res - 2))};
+}
+// brick_class_of (brick_modes.hpp) from the row's terms and the brick's x terms
+__device__ __forceinline__ uint32_t class_adj(uint8_t c, uint8_t r, bool has, bool only) {
+    if (c == kBrickMixed) return r;
+    uint32_t v = only ? (uint32_t)kBrickNeg : (uint32_t)c;
+    if (has && v == kBrickPos) v |= kBrickNoFill;
+    return v;
+}
+__device__ __forceinline__ uint64_t load_row_bytes(const uint8_t* p) {   // kFillP bytes, any alignment
+    uint64_t v = 0;
+    __builtin_memcpy(&v, p, kFillP);
+    return v;
+}
+
 __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGrid& bg, const BrickGrid& cg,
                                                 const uint8_t* __restrict__ ccls, const uint64_t* __restrict__ cmodes,
                                                 const uint8_t* __restrict__ cls, const uint64_t* __restrict__ modes,
@@ -111,91 +142,137 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
                                                 uint64_t* __restrict__ lmodes, uint32_t* __restrict__ count,
                                                 sign_piece_t* __restrict__ signs, uint32_t* __restrict__ ccount_reset,
                                                 uint32_t* __restrict__ umark, uint32_t mark_id) {
-    __shared__ uint32_t wcnt[kFillBlock / 64], wbase[kFillBlock / 64];
-    __shared__ uint8_t s_cls[kFillBlock];   // the block's bricks' classes (its x / y neighbours mostly)
+    __shared__ uint32_t wsum[kFillBlock / 64], wbase[kFillBlock / 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // the refine pass has read it; kept in [14] for stats
         ccount_reset[1] = ccount_reset[0];
         ccount_reset[0] = 0u;
     }
-    const int b0 = blockIdx.x * kFillBlock, b = b0 + threadIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t fc = kBrickMixed;
-    int bx = 0, by = 0, bz = 0, cb = 0;
-    const bool valid = b < bg.n_bricks;
-    // the neighbour rule (brick_modes.hpp): the brick and its six face neighbours share a definite
-    // class.  Its own and its z neighbours' class bytes (other brick layers) are loaded together;
-    // x / y neighbours come from LDS when they belong to this block.  Neighbours outside the grid
-    // are the brick itself.
-    uint32_t own = kBrickMixed;
-    int zl = 0, zh = 0;
-    uint8_t czl = 0, rzl = 0, czh = 0, rzh = 0;
+    const int rw = sign_row_words(g), layers = g.fz1 - g.fz0;
     const int plane = bg.nbx * bg.nby, cplane = cg.nbx * cg.nby;
+    const int64_t item = (int64_t)blockIdx.x * kFillBlock + threadIdx.x;
+    const bool valid = item < (int64_t)bg.nby * bg.nbz * rw;
+    int c = 0, by = 0, bz = 0, nv = 0, bx0 = 0, b0 = 0;
+    uint32_t own[kFillP], fc[kFillP];
+    uint64_t oc = 0;   // the row's coarse class bytes
     if (valid) {
-        brick_of(b, bg, bx, by, bz);
-        cb = bx + by * cg.nbx + (bz / kCZ) * cplane;
-        zl = bz > 0 ? bz - 1 : bz;
-        zh = bz + 1 < bg.nbz ? bz + 1 : bz;
-        const uint8_t c0 = ccls[cb], r0 = cls[b];
-        czl = ccls[bx + by * cg.nbx + (zl / kCZ) * cplane];
-        rzl = cls[b + (zl - bz) * plane];
-        czh = ccls[bx + by * cg.nbx + (zh / kCZ) * cplane];
-        rzh = cls[b + (zh - bz) * plane];
-        own = brick_class_of(g, c0, r0, bx, by, bz);
+        c = (int)(item % rw);
+        const int rr = (int)(item / rw);
+        by = rr % bg.nby;
+        bz = rr / bg.nby;
+        bx0 = kFillP * c;
+        nv = min(kFillP, bg.nbx - bx0);   // >= 1: rw words cover nbx bricks
+        b0 = bx0 + by * bg.nbx + bz * plane;
+        const int cb0 = bx0 + by * cg.nbx + (bz / kCZ) * cplane;
+        const int yl = by > 0 ? by - 1 : by, yh = by + 1 < bg.nby ? by + 1 : by;
+        const int zl = bz > 0 ? bz - 1 : bz, zh = bz + 1 < bg.nbz ? bz + 1 : bz;
+        // rows: own, y - 1, y + 1, z - 1, z + 1 (a neighbour outside the grid is the row itself)
+        const int rb[5] = {b0, b0 + (yl - by) * bg.nbx, b0 + (yh - by) * bg.nbx, b0 + (zl - bz) * plane,
+                           b0 + (zh - bz) * plane};
+        const int rc[5] = {cb0, cb0 + (yl - by) * cg.nbx, cb0 + (yh - by) * cg.nbx,
+                           bx0 + by * cg.nbx + (zl / kCZ) * cplane, bx0 + by * cg.nbx + (zh / kCZ) * cplane};
+        const int ry[5] = {by, yl, yh, by, by}, rz[5] = {bz, bz, bz, zl, zh};
+        uint64_t rcls[5], rccl[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            rcls[k] = load_row_bytes(cls + rb[k]);
+            rccl[k] = load_row_bytes(ccls + rc[k]);
+        }
+        // x neighbours of the word's first and last brick (the brick itself at the grid's edge)
+        const int xl = bx0 > 0 ? bx0 - 1 : bx0, xh = bx0 + nv < bg.nbx ? bx0 + nv : bx0 + nv - 1;
+        const uint8_t lcls = cls[b0 + xl - bx0], lccl = ccls[cb0 + xl - bx0];
+        const uint8_t hcls = cls[b0 + xh - bx0], hccl = ccls[cb0 + xh - bx0];
+        oc = rccl[0];
+        RowSeal rs[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) rs[k] = row_seal(g, ry[k], rz[k]);
+        auto xs_has = [&](int x) { return x * kBX == 0 || min(x * kBX + kBX - 1, g.n - 1) == g.n - 1; };
+        auto xs_only = [&](int x) { return x * kBX == g.n - 1; };
+        uint32_t nb[5][kFillP];
+#pragma unroll
+        for (int j = 0; j < kFillP; ++j) {
+            const int x = bx0 + j;
+            const bool hx = xs_has(x), ox = xs_only(x);
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                nb[k][j] = class_adj((uint8_t)(rccl[k] >> (8 * j)), (uint8_t)(rcls[k] >> (8 * j)), hx || rs[k].has,
+                                     ox || rs[k].only);
+        }
+        const uint32_t left = class_adj(lccl, lcls, xs_has(xl) || rs[0].has, xs_only(xl) || rs[0].only);
+        const uint32_t right = class_adj(hccl, hcls, xs_has(xh) || rs[0].has, xs_only(xh) || rs[0].only);
+#pragma unroll
+        for (int j = 0; j < kFillP; ++j) {
+            own[j] = nb[0][j];
+            const uint32_t xm = j == 0 ? left : nb[0][j - 1];
+            const uint32_t xp = j + 1 < nv ? nb[0][j + 1] : right;
+            uint32_t f = kBrickMixed;
+            const uint32_t o = own[j] & 3u;
+            if (sign_fill && o != kBrickMixed && !(own[j] & kBrickNoFill) && (xm & 3u) == o && (xp & 3u) == o &&
+                (nb[1][j] & 3u) == o && (nb[2][j] & 3u) == o && (nb[3][j] & 3u) == o && (nb[4][j] & 3u) == o)
+                f = o;
+            fc[j] = f;
+        }
     }
-    s_cls[threadIdx.x] = (uint8_t)own;
-    __syncthreads();
+    uint32_t emask = 0;   // listed bricks of this word
     if (valid) {
-        const int nx[4] = {bx > 0 ? bx - 1 : bx, bx + 1 < bg.nbx ? bx + 1 : bx, bx, bx};
-        const int ny[4] = {by, by, by > 0 ? by - 1 : by, by + 1 < bg.nby ? by + 1 : by};
-        uint32_t n[6];
+        uint64_t fv = 0, wv = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int bn = b + (nx[k] - bx) + (ny[k] - by) * bg.nbx, tn = bn - b0;
-            n[k] = (tn >= 0 && tn < kFillBlock)
-                       ? (uint32_t)s_cls[tn]
-                       : brick_class_of(g, ccls[nx[k] + ny[k] * cg.nbx + (bz / kCZ) * cplane], cls[bn], nx[k], ny[k], bz);
+        for (int j = 0; j < kFillP; ++j) {
+            fv |= (uint64_t)(uint8_t)(own[j] | (fc[j] << 4)) << (8 * j);
+            if (j < nv && fc[j] == kBrickNeg) wv |= (uint64_t)(sign_piece_t)~(sign_piece_t)0 << (kBX * j);
+            if (j < nv && fc[j] == kBrickMixed) emask |= 1u << j;
         }
-        n[4] = brick_class_of(g, czl, rzl, bx, by, zl);
-        n[5] = brick_class_of(g, czh, rzh, bx, by, zh);
-        fc = kBrickMixed;
-        if ((own & 3u) != kBrickMixed && !(own & kBrickNoFill)) {
-            bool same = true;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) same &= (n[k] & 3u) == (own & 3u);
-            if (same) fc = own & 3u;
+        if (nv == kFillP) {
+            __builtin_memcpy(fill + b0, &fv, kFillP);
+        } else {
+            for (int j = 0; j < nv; ++j) fill[b0 + j] = (uint8_t)(fv >> (8 * j));
         }
-        if (!sign_fill) fc = kBrickMixed;
-        fill[b] = (uint8_t)(own | (fc << 4));
+        if (sign_fill) {
+            uint64_t* words = reinterpret_cast<uint64_t*>(signs);
+            const int y1 = min(by * kBY + kBY, g.n), z1 = min(bz * kBZ + kBZ, layers);
+            for (int zz = bz * kBZ; zz < z1; ++zz)
+                for (int yy = by * kBY; yy < y1; ++yy) words[((size_t)zz * g.n + yy) * rw + c] = wv;
+        }
     }
-    const bool eval = valid && fc == kBrickMixed;
-    const uint64_t mask = __ballot(eval);
-    if (lane == 0) wcnt[w] = (uint32_t)__popcll(mask);
+    // block-aggregated list append: wave prefix sums of the per-thread counts, one atomic
+    const uint32_t cnt = (uint32_t)__popc(emask);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t t = 0;
-        for (int k = 0; k < kFillBlock / 64; ++k) { wbase[k] = t; t += wcnt[k]; }
+        for (int k = 0; k < kFillBlock / 64; ++k) { wbase[k] = t; t += wsum[k]; }
         const uint32_t base = t ? atomicAdd(count, t) : 0u;
         for (int k = 0; k < kFillBlock / 64; ++k) wbase[k] += base;
     }
     __syncthreads();
-    if (eval) {
-        const uint32_t i = wbase[w] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-        list[i] = (uint32_t)b;
-        const uint64_t mb = modes[b], mc = cmodes[cb];   // both loaded: no branch around a load
-        lmodes[i] = (ccls[cb] == kBrickMixed) ? mb : mc;
-        // MC units (kUnitRows cell rows) whose cells have a corner in this brick: cell rows
+    if (emask) {
+        uint32_t i = wbase[w] + incl - cnt;
+        for (uint32_t m = emask; m; m &= m - 1u) {
+            const int j = __ffs(m) - 1;
+            const int b = b0 + j, cb = bx0 + j + by * cg.nbx + (bz / kCZ) * cplane;
+            list[i] = (uint32_t)b;
+            const uint64_t mb = modes[b], mc = cmodes[cb];   // both loaded: no branch around a load
+            lmodes[i] = ((uint8_t)(oc >> (8 * j)) == kBrickMixed) ? mb : mc;
+            ++i;
+        }
+        // MC units (kUnitRows cell rows) whose cells have a corner in this brick row: cell rows
         // sy in [by kBY - 1, by kBY + kBY - 1], cell layers lz in [bz kBZ - 1, bz kBZ + kBZ - 1]
         const int m = g.m, cl = g.cz1 - g.cz0;
         const int sy0 = max(by * kBY - 1, 0), sy1 = min(by * kBY + kBY - 1, m - 1);
         for (int lz = max(bz * kBZ - 1, 0); lz <= min(bz * kBZ + kBZ - 1, cl - 1); ++lz)
             for (int u = (lz * m + sy0) / kUnitRows; u <= (lz * m + sy1) / kUnitRows; ++u) umark[u] = mark_id;
-    } else if (valid) {   // sign-filled: constant pieces (all samples of the brick share the sign)
-        const sign_piece_t piece = fc == kBrickNeg ? (sign_piece_t)~(sign_piece_t)0 : (sign_piece_t)0;
-        const int layers = g.fz1 - g.fz0, row_pieces = (64 / kBX) * sign_row_words(g);
-        const int y1 = min(by * kBY + kBY, g.n), z1 = min(bz * kBZ + kBZ, layers);
-        for (int z = bz * kBZ; z < z1; ++z)
-            for (int y = by * kBY; y < y1; ++y) signs[((size_t)z * g.n + y) * row_pieces + bx] = piece;
     }
+}
+// one thread per sign word of every brick row
+static unsigned fill_grid(const GridDesc& g) {
+    const BrickGrid bg = brick_grid(g);
+    return (unsigned)(((int64_t)bg.nby * bg.nbz * sign_row_words(g) + kFillBlock - 1) / kFillBlock);
 }
 __global__ __launch_bounds__(kFillBlock) void k_brick_fill(GridDesc g, BrickGrid bg, BrickGrid cg,
                                                            const uint8_t* __restrict__ ccls,
@@ -376,9 +453,9 @@ void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t*
                        uint32_t* d_count, void* d_signs, uint32_t* d_umark, uint32_t mark_id, hipStream_t s) {
     const BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0) return;
-    k_brick_fill<<<(unsigned)((bg.n_bricks + kFillBlock - 1) / kFillBlock), kFillBlock, 0, s>>>(
-        g, bg, cg, d_ccls, d_cmodes, d_cls, d_modes, sign_fill, d_fill, d_list, d_lmodes, d_count,
-        static_cast<sign_piece_t*>(d_signs), d_count - kBrickListWord + kCoarseListWord, d_umark, mark_id);
+    k_brick_fill<<<fill_grid(g), kFillBlock, 0, s>>>(g, bg, cg, d_ccls, d_cmodes, d_cls, d_modes, sign_fill, d_fill, d_list,
+                                                   d_lmodes, d_count, static_cast<sign_piece_t*>(d_signs),
+                                                   d_count - kBrickListWord + kCoarseListWord, d_umark, mark_id);
 }
 
 unsigned eval_bricks_grid(const GridDesc& g) {   // blocks of kEvalBlock lanes, one brick per wave
@@ -411,7 +488,7 @@ void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_r
     if (n > kMaxBatchObjects) throw std::runtime_error("merged object stream: more than 1024 objects per launch");
     depth = eval_depth(depth);
     const dim3 gc((unsigned)((cg.n_bricks + 255) / 256), (unsigned)n);
-    const dim3 gf((unsigned)((bg.n_bricks + kFillBlock - 1) / kFillBlock), (unsigned)n);
+    const dim3 gf(fill_grid(g), (unsigned)n);
 #define IMPLI_BATCH_EVAL(DD)                                                                               \
     do {                                                                                                   \
         k_coarse_modes_b<DD><<<gc, 256, 0, s>>>(d_objs, d_rabbit, tab_range, g, cg);                       \

@@ -211,16 +211,41 @@ __device__ __forceinline__ Iv dm_iv(Box p) {
     return res;
 }
 
-// screw: f = (-r + r0) + delta * sinf(.) with |sinf| <= 1 and r = |(x, y, d2)|, where d2 = z - p2 is
-// the rounding residual of p2 = (z + 0.5) - 0.5: |d2| <= 2^-23 (|z| + 1) (bounded by twice that)
+// screw: f = (-r + r0) + delta * sinf(arg) with r = |(x, y, d2)|, where d2 = z - p2 is the rounding
+// residual of p2 = (z + 0.5) - 0.5: |d2| <= 2^-23 (|z| + 1) (bounded by twice that), and
+// arg = 2 pi (t / tw - theta / 2 pi), t = z + 0.5, theta = atan2(y, x) (screw_f).
 __device__ __forceinline__ float absmin_iv(Iv a) { return a.lo > 0.f ? a.lo : (a.hi < 0.f ? -a.hi : 0.f); }
 __device__ __forceinline__ float absmax_iv(Iv a) { return fmax2(fabsf(a.lo), fabsf(a.hi)); }
+// Range of sinf(arg) over the box, from the box's centre: the xy rectangle lies in the disc of
+// radius R (half diagonal) around (xc, yc), at distance d from the axis, so theta is within
+// asin(R / d) <= 1.0472 R / d (R / d <= 1/2) of atan2(yc, xc) -- modulo 2 pi, which the sine does
+// not see (theta's jump at atan2's cut and y = -0 reading as +0 change arg by 2 pi).  With
+// arg = 2 pi u - theta, u = t / tw, |arg - ac| <= h and sin is 1-Lipschitz.  A margin of
+// 2^-12 (1 + |ac| + h) on arg and 2^-16 on the sine covers the device atan2f / sinf errors (a
+// few ulps) and the rounding of the reference's float expression (t / tw - theta / pi2) * 2 * pi
+// (|ac| < 2^12 is required, else [-1, 1]).  One atan2f and one sinf per box.
+__device__ __forceinline__ Iv screw_sin_iv(float tw, Box p) {
+    const Iv full{-1.f, 1.f};
+    const float xc = 0.5f * (p.x.lo + p.x.hi), yc = 0.5f * (p.y.lo + p.y.hi);
+    const float hx = 0.5f * (p.x.hi - p.x.lo), hy = 0.5f * (p.y.hi - p.y.lo);
+    const float R = sqrtf(hx * hx + hy * hy), d = sqrtf(xc * xc + yc * yc);
+    const float u0 = (p.z.lo + 0.5f) / tw, u1 = (p.z.hi + 0.5f) / tw;
+    const float kPi = 3.14159265358979323846f;
+    const float ac = kPi * (u0 + u1) - atan2f(yc, xc);
+    const float h0 = kPi * fabsf(u1 - u0) + 1.0472f * (R / d);
+    const float h = h0 + (1.f + fabsf(ac) + h0) * 0x1p-12f;
+    // NaN / infinite inputs fail the comparisons
+    if (!(R < 0.5f * d) || !(fabsf(ac) < 4096.f) || !(h < 2.f)) return full;
+    const float s = sinf(ac);
+    return Iv{fmax2(s - h - 0x1p-16f, -1.f), fmin2(s + h + 0x1p-16f, 1.f)};
+}
 __device__ __forceinline__ Iv screw_iv(const float* __restrict__ prm, Box p) {
-    const float r0 = prm[1], ad = fabsf(prm[2]);
+    const float r0 = prm[1];
     const float ax = absmax_iv(p.x), ay = absmax_iv(p.y), bx = absmin_iv(p.x), by = absmin_iv(p.y);
     const float dz = (absmax_iv(p.z) + 1.f) * 0x1p-22f;
     const float rhi = sqrtf(ax * ax + (ay * ay + dz * dz)), rlo = sqrtf(bx * bx + (by * by + 0.f));
-    return Iv{(-rhi + r0) - ad, (-rlo + r0) + ad};
+    const Iv ds = mulc(screw_sin_iv(prm[0], p), prm[2]);
+    return Iv{(-rhi + r0) + ds.lo, (-rlo + r0) + ds.hi};
 }
 __device__ __forceinline__ Iv lid_iv(Box p) {
     const Iv a = sub(p.z, ivc(0.5f)), b = mulc(add(p.z, ivc(0.5f)), -1.f);

@@ -504,6 +504,28 @@ def test_pruned_field_random_trees(impli, seed):
     assert np.array_equal(c[need].view(np.uint32), b[need].view(np.uint32))
 
 
+@pytest.mark.parametrize("pitch,delta_ratio,off", [(0.5, 1.5, (0, 0, 0)), (-0.3, 1.5, (0.2, -0.1, 0.05)),
+                                                   (0.0625, 3.0, (0, 0.3, 0)), (2.0, 1.2, (-0.25, 0, 0.1)),
+                                                   (-4.0, 2.0, (0.1, 0.1, -0.2))])
+def test_pruned_field_twist_phase_bounds(impli, pitch, delta_ratio, off):
+    """The screw's interval bound follows the sine's phase over the brick (screw_sin_iv): unions
+    and differences of twists with other leaves must keep every needed field bit."""
+    from implisolid_amd import scenes
+    tw = scenes.twist(0.8, *off, pitch=pitch, delta_ratio=delta_ratio)
+    for shape in (tw,
+                  {"type": "Union", "matrix": scenes.EYE, "children": [tw, scenes.twist(0.5, 0.3, 0.2, 0.1, pitch=-pitch)]},
+                  {"type": "Difference", "matrix": scenes.EYE,
+                   "children": [tw, dict(scenes.twist(0.4, -0.1, 0, 0, pitch=pitch * 0.7), type="screw_gradient_wrong")]}):
+        mc = scenes.mc_settings(56, 1.0)
+        a = _field(impli, shape, mc, 1)
+        b = _field(impli, shape, mc, 0)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), np.flatnonzero(a != b)[:10]
+        c, cs = _field(impli, shape, mc, 2, signs=True)
+        assert np.array_equal(cs.astype(bool), b < 0)
+        need = _needed_samples(b)
+        assert np.array_equal(c[need].view(np.uint32), b[need].view(np.uint32))
+
+
 # ---- against the committed golden fixtures (tests/golden/make_golden.py) ---------------------------
 def _golden(name):
     import os
