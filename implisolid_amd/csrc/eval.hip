@@ -213,14 +213,43 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
             fc[j] = f;
         }
     }
-    uint32_t emask = 0;   // listed bricks of this word
+    // listed bricks of this word; their modes are loaded now and land while the list slot is fetched
+    uint32_t emask = 0;
+    uint64_t lm[kFillP];
+#pragma unroll
+    for (int j = 0; j < kFillP; ++j) {
+        lm[j] = 0;
+        if (valid && j < nv && fc[j] == kBrickMixed) {
+            emask |= 1u << j;
+            const int b = b0 + j, cb = bx0 + j + by * cg.nbx + (bz / kCZ) * cplane;
+            lm[j] = ((uint8_t)(oc >> (8 * j)) == kBrickMixed) ? modes[b] : cmodes[cb];
+        }
+    }
+    // block-aggregated list append: the wave's exclusive prefix of the per-thread counts (<= 8)
+    // from the bit planes of the counts, one atomic per block
+    const uint32_t cnt = (uint32_t)__popc(emask);
+    uint32_t excl = 0, wtot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t bits = __ballot((cnt >> k) & 1u);
+        excl += (uint32_t)__popcll(bits & ((1ull << lane) - 1ull)) << k;
+        wtot += (uint32_t)__popcll(bits) << k;
+    }
+    if (lane == 0) wsum[w] = wtot;
+    __syncthreads();
+    uint32_t base = 0;
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < kFillBlock / 64; ++k) t += wsum[k];
+        if (t) base = atomicAdd(count, t);
+    }
+    // the stores drain while the atomic is in flight
     if (valid) {
         uint64_t fv = 0, wv = 0;
 #pragma unroll
         for (int j = 0; j < kFillP; ++j) {
             fv |= (uint64_t)(uint8_t)(own[j] | (fc[j] << 4)) << (8 * j);
             if (j < nv && fc[j] == kBrickNeg) wv |= (uint64_t)(sign_piece_t)~(sign_piece_t)0 << (kBX * j);
-            if (j < nv && fc[j] == kBrickMixed) emask |= 1u << j;
         }
         if (nv == kFillP) {
             __builtin_memcpy(fill + b0, &fv, kFillP);
@@ -234,31 +263,20 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
                 for (int yy = by * kBY; yy < y1; ++yy) words[((size_t)zz * g.n + yy) * rw + c] = wv;
         }
     }
-    // block-aggregated list append: wave prefix sums of the per-thread counts, one atomic
-    const uint32_t cnt = (uint32_t)__popc(emask);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t v = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += v;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int k = 0; k < kFillBlock / 64; ++k) { wbase[k] = t; t += wsum[k]; }
-        const uint32_t base = t ? atomicAdd(count, t) : 0u;
-        for (int k = 0; k < kFillBlock / 64; ++k) wbase[k] += base;
+        for (int k = 0; k < kFillBlock / 64; ++k) {
+            wbase[k] = base;
+            base += wsum[k];
+        }
     }
     __syncthreads();
     if (emask) {
-        uint32_t i = wbase[w] + incl - cnt;
-        for (uint32_t m = emask; m; m &= m - 1u) {
-            const int j = __ffs(m) - 1;
-            const int b = b0 + j, cb = bx0 + j + by * cg.nbx + (bz / kCZ) * cplane;
-            list[i] = (uint32_t)b;
-            const uint64_t mb = modes[b], mc = cmodes[cb];   // both loaded: no branch around a load
-            lmodes[i] = ((uint8_t)(oc >> (8 * j)) == kBrickMixed) ? mb : mc;
+        uint32_t i = wbase[w] + excl;
+#pragma unroll
+        for (int j = 0; j < kFillP; ++j) {
+            if (!((emask >> j) & 1u)) continue;
+            list[i] = (uint32_t)(b0 + j);
+            lmodes[i] = lm[j];
             ++i;
         }
         // MC units (kUnitRows cell rows) whose cells have a corner in this brick row: cell rows
