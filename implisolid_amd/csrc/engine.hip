@@ -65,7 +65,7 @@ void Engine::brick_stats(int64_t out[3], hipStream_t s) {
     int64_t mixed = 0, filled = 0;
     for (int b = 0; b < bg.n_bricks; ++b) {
         mixed += (f[b] & 3) == kBrickMixed;
-        filled += (f[b] >> 4) != 0;
+        filled += ((f[b] >> 4) & 3) != 0;
     }
     out[0] = bg.n_bricks;
     out[1] = pruning() > 0 ? mixed : bg.n_bricks;
@@ -269,14 +269,17 @@ void Engine::eval_field(hipStream_t s) {
                           signs_.p, umark_.as<uint32_t>(), ++mark_id_, s);
         marks_valid_ = true;
         mark(1, s);
+        const BrickGrid bg = brick_grid(grid_);
+        const ClaimCtx cc{level >= 2 ? fill_.as<uint8_t>() : nullptr, ccls_.as<uint8_t>(), modes_.as<uint64_t>(),
+                          cmodes_.as<uint64_t>(), bg.nbx, bg.nbx * bg.nby};
         if (jit_fn_) {
             const float* d_mats = reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
-            TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, brick_grid(grid_), lmodes_.as<uint64_t>(),
-                                   blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, eval_bricks_grid(grid_),
+            TreeJit::launch_bricks(jit_fn_, d_mats, rabbit_.as<float>(), grid_, bg, lmodes_.as<uint64_t>(),
+                                   blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, cc, eval_bricks_grid(grid_),
                                    s);
         } else {
             launch_eval_bricks_interp(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, lmodes_.as<uint64_t>(),
-                                      blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, s);
+                                      blist_.as<uint32_t>(), d_count, field_.as<float>(), signs_.p, cc, s);
         }
     } else {
         marks_valid_ = false;   // dense field: MC counts every unit
@@ -315,7 +318,7 @@ std::vector<int64_t> Engine::listed_per_layer(hipStream_t s) {
     const int plane = bg.nbx * bg.nby;
     for (int bz = 0; bz < bg.nbz; ++bz) {
         int64_t listed = 0;
-        for (int k = 0; k < plane; ++k) listed += (f[(size_t)bz * plane + k] >> 4) == 0;
+        for (int k = 0; k < plane; ++k) listed += ((f[(size_t)bz * plane + k] >> 4) & 3) == 0;
         for (int l = bz * kBZ; l < std::min(layers, bz * kBZ + kBZ); ++l) out[(size_t)l] = listed;
     }
     return out;

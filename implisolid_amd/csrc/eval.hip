@@ -94,8 +94,9 @@ __global__ __launch_bounds__(kEvalBlock) void k_eval_field_pruned(const Program*
                                                            const uint64_t* __restrict__ modes,
                                                            const uint32_t* __restrict__ list,
                                                            const uint32_t* __restrict__ count,
-                                                           float* __restrict__ field, void* __restrict__ signs) {
-    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, modes, list, count, field, signs);
+                                                           float* __restrict__ field, void* __restrict__ signs,
+                                                           ClaimCtx cc) {
+    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, cc, modes, list, count, field, signs);
 }
 
 // Per brick: its class (inherited from a sign-definite coarse box, or refined), the neighbour rule
@@ -205,12 +206,21 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
             own[j] = nb[0][j];
             const uint32_t xm = j == 0 ? left : nb[0][j - 1];
             const uint32_t xp = j + 1 < nv ? nb[0][j + 1] : right;
-            uint32_t f = kBrickMixed;
+            // sign-filled: all six neighbours of its class; candidate: the others all of mixed class
+            uint32_t f = kBrickMixed, cand = 0;
             const uint32_t o = own[j] & 3u;
-            if (sign_fill && o != kBrickMixed && !(own[j] & kBrickNoFill) && (xm & 3u) == o && (xp & 3u) == o &&
-                (nb[1][j] & 3u) == o && (nb[2][j] & 3u) == o && (nb[3][j] & 3u) == o && (nb[4][j] & 3u) == o)
-                f = o;
-            fc[j] = f;
+            if (sign_fill && o != kBrickMixed && !(own[j] & kBrickNoFill)) {
+                const uint32_t nn[6] = {xm & 3u, xp & 3u, nb[1][j] & 3u, nb[2][j] & 3u, nb[3][j] & 3u, nb[4][j] & 3u};
+                bool same = true, other_def = false;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    same &= nn[k] == o;
+                    other_def |= nn[k] != o && nn[k] != kBrickMixed;
+                }
+                if (same || !other_def) f = o;
+                if (!same && !other_def) cand = kBrickCandidate;
+            }
+            fc[j] = f | (cand << 8);
         }
     }
     // listed bricks of this word; their modes are loaded now and land while the list slot is fetched
@@ -219,7 +229,7 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
 #pragma unroll
     for (int j = 0; j < kFillP; ++j) {
         lm[j] = 0;
-        if (valid && j < nv && fc[j] == kBrickMixed) {
+        if (valid && j < nv && (fc[j] & 3u) == kBrickMixed) {
             emask |= 1u << j;
             const int b = b0 + j, cb = bx0 + j + by * cg.nbx + (bz / kCZ) * cplane;
             lm[j] = ((uint8_t)(oc >> (8 * j)) == kBrickMixed) ? modes[b] : cmodes[cb];
@@ -248,8 +258,8 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
         uint64_t fv = 0, wv = 0;
 #pragma unroll
         for (int j = 0; j < kFillP; ++j) {
-            fv |= (uint64_t)(uint8_t)(own[j] | (fc[j] << 4)) << (8 * j);
-            if (j < nv && fc[j] == kBrickNeg) wv |= (uint64_t)(sign_piece_t)~(sign_piece_t)0 << (kBX * j);
+            fv |= (uint64_t)(uint8_t)(own[j] | ((fc[j] & 3u) << 4) | (fc[j] >> 8)) << (8 * j);
+            if (j < nv && (fc[j] & 3u) == kBrickNeg) wv |= (uint64_t)(sign_piece_t)~(sign_piece_t)0 << (kBX * j);
         }
         if (nv == kFillP) {
             __builtin_memcpy(fill + b0, &fv, kFillP);
@@ -275,7 +285,8 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
 #pragma unroll
         for (int j = 0; j < kFillP; ++j) {
             if (!((emask >> j) & 1u)) continue;
-            list[i] = (uint32_t)(b0 + j);
+            // mixed-class bricks claim their candidate neighbours after their own evaluation
+            list[i] = (uint32_t)(b0 + j) | ((own[j] & 3u) == kBrickMixed && sign_fill ? kListCheck : 0u);
             lmodes[i] = lm[j];
             ++i;
         }
@@ -342,8 +353,9 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned_b(const ObjArgs* __re
         const ObjArgs& o = objs[k];
         const uint32_t li = i - s_pre[k];
         // one layer at a time: the interpreter's node stacks are VGPR arrays, a layer pair doubles them
-        eval_one_brick<InterpEval<D>, false>(InterpEval<D>{o.prog, tab}, g, bg, (int)o.blist[li], o.lmodes[li], o.field,
-                                             static_cast<sign_piece_t*>(o.signs));
+        const ClaimCtx cc{o.fill, o.ccls, o.modes, o.cmodes, bg.nbx, bg.nbx * bg.nby};
+        eval_listed<InterpEval<D>, false>(InterpEval<D>{o.prog, tab}, g, bg, cc, o.blist[li], o.lmodes[li], o.field,
+                                          static_cast<sign_piece_t*>(o.signs));
     }
 }
 
@@ -485,15 +497,15 @@ unsigned eval_bricks_grid(const GridDesc& g) {   // blocks of kEvalBlock lanes, 
 
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint32_t* d_list, const uint32_t* d_count,
-                               float* d_field, void* d_signs, hipStream_t s) {
+                               float* d_field, void* d_signs, const ClaimCtx& cc, hipStream_t s) {
     const BrickGrid bg = brick_grid(g);
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
     const unsigned eb = eval_bricks_grid(g);
-    if (depth <= 4) k_eval_field_pruned<4><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
-    else if (depth <= 8) k_eval_field_pruned<8><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
-    else if (depth <= 12) k_eval_field_pruned<12><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
-    else k_eval_field_pruned<16><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs);
+    if (depth <= 4) k_eval_field_pruned<4><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
+    else if (depth <= 8) k_eval_field_pruned<8><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
+    else if (depth <= 12) k_eval_field_pruned<12><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
+    else k_eval_field_pruned<16><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
 }
 
 // flat merged kernels (refine, eval): a fixed grid over all objects' items

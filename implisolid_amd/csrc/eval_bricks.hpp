@@ -46,11 +46,14 @@ __device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, in
 // k_brick_fill, modes[i] the listed brick's pruning modes): every sample is evaluated with
 // `ev(modes, x, y, z)`, stored, and its sign bit set (wave ballot: 64 bits = kBY rows x kBX
 // samples).  Sign-filled bricks never reach this kernel -- k_brick_fill wrote their constant sign
-// bits.
-// one listed brick (b, its modes m) by the calling wave
+// bits -- except claimed candidates (grid.hpp ClaimCtx), evaluated by the wave of the mixed brick
+// that claimed them, values only (their sign pieces are constant and already written).
+// one brick (b, its modes m) by the calling wave; neg[k]: layer k's sign bits, valid: the lanes
+// inside the grid
 template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
 __device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g, const BrickGrid& bg, int b, uint64_t m64,
-                                               float* __restrict__ field, sign_piece_t* __restrict__ signs) {
+                                               float* __restrict__ field, sign_piece_t* __restrict__ signs,
+                                               bool write_signs, uint64_t neg[kBZ], uint64_t& valid) {
     const int lane = threadIdx.x & 63;
     const int n = g.n;
     const int layers = g.fz1 - g.fz0;
@@ -59,6 +62,7 @@ __device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g
     brick_of(b, bg, bx, by, bz);
     const int sx = bx * kBX + (lane % kBX), sy = by * kBY + (lane / kBX);
     const bool ok = sx < n && sy < n;
+    valid = __ballot(ok);
     const bool sealed_col = sealed_xy(g, sx) || sealed_xy(g, sy);
     // brick-major field (grid.hpp field_index): the brick's layer k is 64 consecutive floats, one
     // per lane -- the wave stores two whole lines (lanes past the grid edge fill the padding)
@@ -66,6 +70,8 @@ __device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g
     const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m64 >> 32)) << 32) |
                        (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m64);
     const float x = sample_xy(g, 0, ok ? sx : 0), y = sample_xy(g, 1, ok ? sy : 0);
+#pragma unroll
+    for (int k = 0; k < kBZ; ++k) neg[k] = 0;
     if constexpr (Pair) {
         // both layers' tree evaluations in one straight-line block: two independent dependency
         // chains per lane (a layer past the slab is evaluated at a clamped z and not stored)
@@ -79,10 +85,10 @@ __device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g
             if (layer >= layers) break;
             const float v = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + (k ? f1 : f0);
             out[k * kBX * kBY] = v;
-            const uint64_t neg = __ballot(v < 0.f);
-            if (lane < kBY) {
+            neg[k] = __ballot(v < 0.f);
+            if (write_signs && lane < kBY) {
                 const int yy = by * kBY + lane;
-                if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg >> (kBX * lane));
+                if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg[k] >> (kBX * lane));
             }
         }
     } else {
@@ -93,18 +99,92 @@ __device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g
             const float f = ev(m, x, y, sample_z(g, layer));
             const float v = (sealed_col || sealed_z(g, layer)) ? kSealed : 0.f + f;
             out[k * kBX * kBY] = v;
-            const uint64_t neg = __ballot(v < 0.f);
-            if (lane < kBY) {
+            const uint64_t nk = __ballot(v < 0.f);
+            neg[k] = nk;
+            if (write_signs && lane < kBY) {
                 const int yy = by * kBY + lane;
-                if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(neg >> (kBX * lane));
+                if (yy < n) signs[((size_t)layer * n + yy) * row_pieces + bx] = (sign_piece_t)(nk >> (kBX * lane));
             }
         }
     }
 }
 
+// The face neighbours of a just evaluated mixed brick that it claims (bit d: direction d = -x, +x,
+// -y, +y, -z, +z): candidates (grid.hpp) of sign s such that some sample of this brick on the
+// shared face has the other sign -- a cell edge across the face changes sign there, so marching
+// cubes reads the candidate's value -- and that no other wave claimed first (atomic on the fill
+// byte).  Face samples are the lanes of the face column / row in both layers, or a whole layer.
+__device__ __forceinline__ uint32_t claim_neighbours(const GridDesc& g, const BrickGrid& bg, const ClaimCtx& cc, int b,
+                                                     const uint64_t neg[kBZ], uint64_t valid) {
+    static_assert(kBZ == 2, "face masks of two-layer bricks");
+    int bx, by, bz;
+    brick_of(b, bg, bx, by, bz);
+    const int layers = g.fz1 - g.fz0;
+    const bool has1 = bz * kBZ + 1 < layers;
+    uint64_t col0 = 0, row0 = (1ull << kBX) - 1ull;
+#pragma unroll
+    for (int r = 0; r < kBY; ++r) col0 |= 1ull << (r * kBX);
+    const uint64_t colL = col0 << (kBX - 1), rowL = row0 << (kBX * (kBY - 1));
+    uint32_t claimed = 0;
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const int ax = d >> 1, up = d & 1;
+        const int c = ax == 0 ? bx : ax == 1 ? by : bz;
+        const int lim = ax == 0 ? bg.nbx : ax == 1 ? bg.nby : bg.nbz;
+        if (up ? c + 1 >= lim : c == 0) continue;
+        const int step = ax == 0 ? 1 : ax == 1 ? bg.nbx : bg.nbx * bg.nby;
+        const int a = up ? b + step : b - step;
+        const uint32_t fa = cc.fill[a];
+        if (!(fa & kBrickCandidate)) continue;
+        uint64_t f0, f1;
+        if (ax == 0) f0 = f1 = up ? colL : col0;
+        else if (ax == 1) f0 = f1 = up ? rowL : row0;
+        else { f0 = up ? 0ull : ~0ull; f1 = up ? ~0ull : 0ull; }
+        f0 &= valid;
+        f1 = has1 ? (f1 & valid) : 0ull;
+        const bool aneg = (fa & 3u) == kBrickNeg;
+        const uint64_t differ = aneg ? ((~neg[0] & f0) | (~neg[1] & f1)) : ((neg[0] & f0) | (neg[1] & f1));
+        if (!differ) continue;
+        uint32_t old = 0;
+        const int sh = 8 * (a & 3);
+        if ((threadIdx.x & 63) == 0) old = atomicOr(reinterpret_cast<uint32_t*>(cc.fill + (a & ~3)), (uint32_t)kBrickClaimed << sh);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (!((old >> sh) & kBrickClaimed)) claimed |= 1u << d;
+    }
+    return claimed;
+}
+
+// a listed entry: the brick, then (mixed bricks) the candidates it claimed, with their own modes --
+// one loop around a single copy of the tree code
+template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
+__device__ __forceinline__ void eval_listed(const Eval& ev, const GridDesc& g, const BrickGrid& bg, const ClaimCtx& cc,
+                                            uint32_t entry, uint64_t m64, float* __restrict__ field,
+                                            sign_piece_t* __restrict__ signs) {
+    const int b = (int)(entry & ~kListCheck);
+    const bool check = (entry & kListCheck) && cc.fill;
+    int cur = b;
+    uint64_t mcur = m64;
+    uint32_t claimed = 0;
+    for (bool first = true;; first = false) {
+        uint64_t neg[kBZ], valid;
+        eval_one_brick<Eval, Pair>(ev, g, bg, cur, mcur, field, signs, first, neg, valid);
+        if (first && check) claimed = claim_neighbours(g, bg, cc, b, neg, valid);
+        if (!claimed) break;
+        const int d = __builtin_ctz(claimed);
+        claimed &= claimed - 1u;
+        const int ax = d >> 1, up = d & 1;
+        const int step = ax == 0 ? 1 : ax == 1 ? bg.nbx : bg.nbx * bg.nby;
+        cur = up ? b + step : b - step;
+        int cx, cy, cz;
+        brick_of(cur, bg, cx, cy, cz);
+        const int cb = cx + cy * cc.cnbx + (cz / kCZ) * cc.cplane;
+        mcur = cc.ccls[cb] == kBrickMixed ? cc.bmodes[cur] : cc.cmodes[cb];
+    }
+}
+
 template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
 __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
-                                                 const uint64_t* __restrict__ modes,
+                                                 const ClaimCtx& cc, const uint64_t* __restrict__ modes,
                                                  const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                                  float* __restrict__ field, void* __restrict__ signs_raw) {
     sign_piece_t* signs = static_cast<sign_piece_t*>(signs_raw);
@@ -116,13 +196,13 @@ __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc&
     uint32_t b_next = i < nb ? list[i] : 0u;
     uint64_t m_next = i < nb ? modes[i] : 0ull;
     for (; i < nb; i += stride) {
-        const int b = __builtin_amdgcn_readfirstlane((int)b_next);
+        const uint32_t e = __builtin_amdgcn_readfirstlane(b_next);
         const uint64_t m64 = m_next;
         if (i + stride < nb) {
             b_next = list[i + stride];
             m_next = modes[i + stride];
         }
-        eval_one_brick<Eval, Pair>(ev, g, bg, b, m64, field, signs);
+        eval_listed<Eval, Pair>(ev, g, bg, cc, e, m64, field, signs);
     }
 }
 

@@ -608,8 +608,8 @@ std::string TreeJit::kernel_source(const Program& p, bool bake) {
       << "}  // namespace impli\n"
       << "extern \"C\" __global__ __launch_bounds__(" << kEvalBlock << ") void impli_eval_bricks(\n"
       << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
-      << "    const uint32_t* list, const uint32_t* count, float* field, void* signs) {\n"
-      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, modes, list, count, field, signs);\n}\n"
+      << "    const uint32_t* list, const uint32_t* count, float* field, void* signs, impli::ClaimCtx cc) {\n"
+      << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, cc, modes, list, count, field, signs);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_coarse_modes(\n"
       << "    const float* M, const float* tab, float2 tab_range, impli::GridDesc g, impli::BrickGrid cg,\n"
       << "    uint64_t* cmodes, uint8_t* ccls, uint32_t* clist, uint32_t* counters) {\n"
@@ -702,12 +702,14 @@ std::vector<char> TreeJit::compile(const std::string& src) {
 
 void TreeJit::launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
                             const BrickGrid& bg, const uint64_t* d_modes, const uint32_t* d_list,
-                            const uint32_t* d_count, float* d_field, void* d_signs, unsigned blocks, hipStream_t s) {
+                            const uint32_t* d_count, float* d_field, void* d_signs, const ClaimCtx& cc, unsigned blocks,
+                            hipStream_t s) {
     if (bg.n_bricks <= 0) return;
     GridDesc gg = g;
     BrickGrid bb = bg;
+    ClaimCtx c = cc;
     void* args[] = {(void*)&d_mats, (void*)&d_rabbit, (void*)&gg, (void*)&bb, (void*)&d_modes,
-                    (void*)&d_list, (void*)&d_count, (void*)&d_field, (void*)&d_signs};
+                    (void*)&d_list, (void*)&d_count, (void*)&d_field, (void*)&d_signs, (void*)&c};
     if (hipModuleLaunchKernel(fn, blocks, 1, 1, kEvalBlock, 1, 1, 0, s, args, nullptr) != hipSuccess)
         throw std::runtime_error("hipModuleLaunchKernel(impli_eval_bricks) failed");
 }

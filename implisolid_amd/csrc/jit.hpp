@@ -81,7 +81,8 @@ public:
     // launch the compiled brick kernel (same contract as launch_eval_field_pruned's 2nd kernel)
     static void launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
                               const BrickGrid& bg, const uint64_t* d_modes, const uint32_t* d_list,
-                              const uint32_t* d_count, float* d_field, void* d_signs, unsigned blocks, hipStream_t s);
+                              const uint32_t* d_count, float* d_field, void* d_signs, const ClaimCtx& cc,
+                              unsigned blocks, hipStream_t s);
 
     // launch a compiled kernel with 256-thread blocks; args as for hipModuleLaunchKernel
     static void launch(hipFunction_t fn, unsigned blocks, void** args, hipStream_t s, const char* what);

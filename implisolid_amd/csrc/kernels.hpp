@@ -39,7 +39,7 @@ static_assert(kEvalBlock % 64 == 0 && kEvalBlock <= 256, "kEvalBlock: whole wave
 unsigned eval_bricks_grid(const GridDesc& g);
 void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_rabbit, const GridDesc& g,
                                const uint64_t* d_modes, const uint32_t* d_list, const uint32_t* d_count,
-                               float* d_field, void* d_signs, hipStream_t s);
+                               float* d_field, void* d_signs, const ClaimCtx& cc, hipStream_t s);
 // sign bitmap of a fully written field (unpruned path)
 void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s);
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
