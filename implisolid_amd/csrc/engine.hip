@@ -65,7 +65,7 @@ void Engine::brick_stats(int64_t out[3], hipStream_t s) {
     int64_t mixed = 0, filled = 0;
     for (int b = 0; b < bg.n_bricks; ++b) {
         mixed += (f[b] & 3) == kBrickMixed;
-        filled += ((f[b] >> 4) & 3) != 0;
+        filled += ((f[b] >> 4) & 3) != 0 && !(f[b] & kBrickClaimed);   // claimed candidates were evaluated
     }
     out[0] = bg.n_bricks;
     out[1] = pruning() > 0 ? mixed : bg.n_bricks;
@@ -178,8 +178,10 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     blist_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     lmodes_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint64_t));
-    umark_.reserve((size_t)(n_units(grid_) + 1) * sizeof(uint32_t));
-    IMPLI_HIP(hipMemset(umark_.p, 0, (size_t)(n_units(grid_) + 1) * sizeof(uint32_t)));   // ids start at 1
+    if (n_chunks(grid_) > kMaxChunks) throw InputError("grid: more than 8189 cells per row");
+    const size_t mark_bytes = (size_t)(n_units(grid_) * n_chunks(grid_) + 1) * sizeof(uint32_t);
+    umark_.reserve(mark_bytes);
+    IMPLI_HIP(hipMemset(umark_.p, 0, mark_bytes));   // ids start at 1
     marks_valid_ = false;
     const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
     signs_.reserve(sign_bytes + 64);

@@ -290,12 +290,18 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
             lmodes[i] = lm[j];
             ++i;
         }
-        // MC units (kUnitRows cell rows) whose cells have a corner in this brick row: cell rows
-        // sy in [by kBY - 1, by kBY + kBY - 1], cell layers lz in [bz kBZ - 1, bz kBZ + kBZ - 1]
-        const int m = g.m, cl = g.cz1 - g.cz0;
+        // MC (unit, chunk) pairs whose cells have a corner in a listed brick of this word: cell
+        // rows sy in [by kBY - 1, by kBY + kBY - 1], cell layers lz in [bz kBZ - 1, bz kBZ + kBZ - 1],
+        // chunk c (cells 64 c ... 64 c + 63 by their low corner) and, when the word's first brick is
+        // listed, chunk c - 1 (its last cell reaches sample 64 c)
+        const int m = g.m, cl = g.cz1 - g.cz0, nch = n_chunks(g);
         const int sy0 = max(by * kBY - 1, 0), sy1 = min(by * kBY + kBY - 1, m - 1);
+        const bool own_chunk = c < nch, prev_chunk = c > 0 && (emask & 1u) && c - 1 < nch;
         for (int lz = max(bz * kBZ - 1, 0); lz <= min(bz * kBZ + kBZ - 1, cl - 1); ++lz)
-            for (int u = (lz * m + sy0) / kUnitRows; u <= (lz * m + sy1) / kUnitRows; ++u) umark[u] = mark_id;
+            for (int u = (lz * m + sy0) / kUnitRows; u <= (lz * m + sy1) / kUnitRows; ++u) {
+                if (own_chunk) umark[(size_t)u * nch + c] = mark_id;
+                if (prev_chunk) umark[(size_t)u * nch + c - 1] = mark_id;
+            }
     }
 }
 // one thread per sign word of every brick row

@@ -100,7 +100,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 
 // K2: one block per group of kGroupUnits units; lanes take the group's items (row, 64-cell chunk)
 // round robin, so every lane has work (a wave per unit would leave 64 - 4 nch lanes idle).  Only
-// units whose cells touch an evaluated brick are visited (b.umark): all others are trivial.  Owned
+// the 64-cell chunks of a unit whose cells touch an evaluated brick are visited (b.umark, marked per
+// (unit, chunk) by k_brick_fill): all others are trivial.  Owned
 // vertices and triangles of a chunk are popcounts of corner-mask expressions (chunk_triangles).
 // Per-unit sums through LDS atomics.
 //   -> unit_cnt[64 group + k] = k-th non-empty unit of the group {unit in group, own / tri / act
@@ -108,62 +109,57 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 //      own, non-empty units), read by k_unit_scan.
 __device__ __forceinline__ void mc_count_body(const GridDesc& g, const MCBuffers& b) {
     __shared__ uint32_t s_u[kGroupUnits][4];
-    __shared__ uint8_t s_fu[kGroupUnits];   // the group's candidate units, in order
+    __shared__ uint16_t s_fp[kGroupUnits * kMaxChunks];   // the group's candidate (unit, chunk) pairs
     __shared__ uint32_t s_nf;
     const int t = threadIdx.x, nt_ = blockDim.x;   // triangle counts: chunk_triangles (checked against the table)
     for (int k = t; k < 4 * kGroupUnits; k += nt_) (&s_u[0][0])[k] = 0u;
+    if (t == 0) s_nf = 0u;
     const int64_t G = blockIdx.x;
-    const int nch = (g.m + 63) / 64;
+    const int nch = n_chunks(g);
     const int64_t rows = n_rows(g), nu = n_units(g);
     const int64_t row0 = G * kGroupUnits * kUnitRows;
-    if (t < 64) {   // candidates: units whose cells touch an evaluated brick (others are all trivial)
-        const int64_t u = G * kGroupUnits + t;
-        const bool cand = u < nu && (!b.umark || b.umark[u] == b.mark_id);
+    __syncthreads();
+    // candidates: the (unit, chunk) pairs whose cells touch an evaluated brick (the others hold no
+    // non-trivial cell), appended in any order (the counts are sums); a wave's appends take one
+    // LDS atomic
+    for (int p0 = 0; p0 < kGroupUnits * nch; p0 += nt_) {
+        const int p = p0 + t, ui = p / nch, c = p - ui * nch;
+        const int64_t u = G * kGroupUnits + ui;
+        const bool cand = p < kGroupUnits * nch && u < nu && (!b.umark || b.umark[u * nch + c] == b.mark_id);
         const uint64_t m = __ballot(cand);
-        if (cand) s_fu[__popcll((unsigned long long)(m & ((1ull << t) - 1ull)))] = (uint8_t)t;
-        if (t == 0) s_nf = (uint32_t)__popcll((unsigned long long)m);
+        uint32_t base = 0;
+        if ((t & 63) == 0 && m) base = atomicAdd(&s_nf, (uint32_t)__popcll((unsigned long long)m));
+        base = __shfl(base, 0, 64);
+        if (cand) s_fp[base + __popcll((unsigned long long)(m & ((1ull << (t & 63)) - 1ull)))] = (uint16_t)(ui * kMaxChunks + c);
     }
     __syncthreads();
-    // a lane's items are loaded kCountBatch at a time, then counted (1 with 512-lane blocks: 14.8 us
-    // at 512^3; 3 items with 1024 lanes: 24.5 us; 1 with 1024: 16.4; 1 with 256: 15.7)
-    constexpr int kCountBatch = 1;
-    const int per_unit = kUnitRows * nch;
-    const int n_items = (int)s_nf * per_unit;
-    for (int i0 = t; i0 < n_items; i0 += kCountBatch * nt_) {
-        ChunkBits kb[kCountBatch];
-        int rb[kCountBatch];
-#pragma unroll
-        for (int q = 0; q < kCountBatch; ++q) {
-            // out-of-range items read a valid chunk (clamped) and drop it: no branch around loads
-            const int i = i0 + q * nt_;
-            const int ic = i < n_items ? i : 0;
-            const int fu = s_fu[ic / per_unit], w = ic - (ic / per_unit) * per_unit;
-            rb[q] = fu * kUnitRows + w / nch;
-            const bool ok = i < n_items && row0 + rb[q] < rows;
-            load_chunk(g, b.signs, ok ? row0 + rb[q] : 0, ok ? w - (w / nch) * nch : 0, kb[q]);
-            if (!ok) kb[q].nt = 0;
+    const int n_items = (int)s_nf * kUnitRows;
+    for (int i = t; i < n_items; i += nt_) {
+        ChunkBits k;
+        const uint32_t pr = s_fp[i / kUnitRows];
+        const int ui = (int)(pr / kMaxChunks), c = (int)(pr % kMaxChunks);
+        const int rb = ui * kUnitRows + i % kUnitRows;
+        const bool ok = row0 + rb < rows;
+        // out-of-range rows read a valid chunk (row 0) and drop it: no branch around loads
+        load_chunk(g, b.signs, ok ? row0 + rb : 0, c, k);
+        if (!ok) k.nt = 0;
+        if (!k.nt) continue;
+        // owned vertices = crossing owned edges (build_case_table checks the identity):
+        // edge 5 = corners 5-6 (t01, t11), 6 = 6-7 (t11, s11), 10 = 2-6 (t10, t11)
+        const unsigned own = (unsigned)(__popcll((unsigned long long)((k.t01 ^ k.t11) & k.nt)) +
+                                        __popcll((unsigned long long)((k.s11 ^ k.t11) & k.nt)) +
+                                        __popcll((unsigned long long)((k.t10 ^ k.t11) & k.nt)));
+        unsigned tri = 0, act = 0, hal = 0;
+        if (k.z >= g.cz_emit) {
+            act = (unsigned)__popcll((unsigned long long)k.nt);   // every non-trivial case has a triangle
+            tri = chunk_triangles(k);
+        } else {
+            hal = own;
         }
-#pragma unroll
-        for (int q = 0; q < kCountBatch; ++q) {
-            const ChunkBits& k = kb[q];
-            if (!k.nt) continue;
-            // owned vertices = crossing owned edges (build_case_table checks the identity):
-            // edge 5 = corners 5-6 (t01, t11), 6 = 6-7 (t11, s11), 10 = 2-6 (t10, t11)
-            const unsigned own = (unsigned)(__popcll((unsigned long long)((k.t01 ^ k.t11) & k.nt)) +
-                                            __popcll((unsigned long long)((k.s11 ^ k.t11) & k.nt)) +
-                                            __popcll((unsigned long long)((k.t10 ^ k.t11) & k.nt)));
-            unsigned tri = 0, act = 0, hal = 0;
-            if (k.z >= g.cz_emit) {
-                act = (unsigned)__popcll((unsigned long long)k.nt);   // every non-trivial case has a triangle
-                tri = chunk_triangles(k);
-            } else {
-                hal = own;
-            }
-            uint32_t* d = s_u[rb[q] / kUnitRows];
-            if (own) atomicAdd(&d[0], own);
-            if (tri) { atomicAdd(&d[1], tri); atomicAdd(&d[2], act); }
-            if (hal) atomicAdd(&d[3], hal);
-        }
+        uint32_t* d = s_u[ui];
+        if (own) atomicAdd(&d[0], own);
+        if (tri) { atomicAdd(&d[1], tri); atomicAdd(&d[2], act); }
+        if (hal) atomicAdd(&d[3], hal);
     }
     __syncthreads();
     if (t < 64) {   // wave 0, one lane per unit of the group (kGroupUnits == 64; blockDim >= 64)

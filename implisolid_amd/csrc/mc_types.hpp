@@ -37,8 +37,8 @@ struct MCBuffers {
                              // then the group's non-empty unit count (not scanned)
     uint4* ulist;            // all parts of the non-empty units in order: {unit, vbase, fbase, abase}
     uint32_t* upart;         // ... part index | part count << 8 (k_unit_scan)
-    const uint32_t* umark;   // units whose cells touch an evaluated brick hold mark_id (k_brick_fill);
-    uint32_t mark_id;        // null: every unit is counted (dense eval)
+    const uint32_t* umark;   // [unit][chunk]: the 64-cell chunks of a unit whose cells touch an evaluated
+    uint32_t mark_id;        // brick hold mark_id (k_brick_fill); null: every chunk is counted (dense eval)
     uint32_t* counters;      // [0] unit parts, [1] halo own (read by the vertex pass), [2..5] totals
                              // own/tri/act/halo (copied as one block; [5] == [1]), [6] non-empty units
     uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
@@ -54,5 +54,8 @@ struct MCBuffers {
 __host__ __device__ inline int64_t n_rows(const GridDesc& g) { return (int64_t)g.m * (g.cz1 - g.cz0); }
 __host__ __device__ inline int64_t n_units(const GridDesc& g) { return (n_rows(g) + kUnitRows - 1) / kUnitRows; }
 __host__ __device__ inline int64_t n_groups(const GridDesc& g) { return (n_units(g) + kGroupUnits - 1) / kGroupUnits; }
+// 64-cell chunks per cell row (chunk c: the cells whose low corner is stored sample 64 c + j)
+__host__ __device__ inline int n_chunks(const GridDesc& g) { return (g.m + 63) / 64; }
+constexpr int kMaxChunks = 128;   // per row (R <= 8189): the count kernel's candidate list in LDS
 
 }  // namespace impli
