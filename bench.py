@@ -172,7 +172,8 @@ def main():
     ap.add_argument("--skip-config5", action="store_true", help="do not time the 64-object stream (config 5)")
     ap.add_argument("--config5-streams", type=int, default=8)
     ap.add_argument("--skip-ob02", action="store_true", help="do not time build_geometry with the OB02 loop")
-    ap.add_argument("--bake", type=int, default=None, help="1: tree modules with the matrices baked in (per object)")
+    ap.add_argument("--bake", type=int, default=None,
+                    help="tree modules with the matrices baked in: 0 never, 1 every object, 2 hot objects (library default)")
     ap.add_argument("--graph", action="store_true",
                     help="N = 1: replay the step as a hipGraph (measured no faster than direct launches: "
                          "0.176 vs 0.172 ms at 512^3)")
@@ -187,7 +188,7 @@ def main():
     if args.prune is not None:
         I.set_pruning(args.prune)
     if args.bake is not None:
-        I.set_jit_bake(bool(args.bake))
+        I.set_jit_bake(args.bake)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -247,6 +248,10 @@ def main():
         I.jit_wait()
         for _ in range(max(1, warmup)):
             step()
+        # a hot object's baked module (bake mode 2) is requested after a few evals: wait for it too
+        I.jit_wait()
+        for _ in range(max(1, warmup)):
+            step()
         nv, nf, grew = slab.counts(sp)
         if grew:
             step()
@@ -276,15 +281,15 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
+        # the timed steps carry no event records (each record is a queue marker: ~4 us per step
+        # at 512^3 with four of them); the phase split is timed on extra steps afterwards
         t0 = time.perf_counter()
         if graph is not None:
             for k in range(steps):
-                ev[k][0].record(stream)
                 graph.replay()
-                ev[k][3].record(stream)
         else:
             for k in range(steps):
-                step(ev[k])
+                step()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -298,6 +303,16 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot)
         el = float(t.item())
+        n_phase = min(steps, 10)   # phase split (eval / count + scan / emit): extra steps with events
+        for k in range(n_phase):
+            if graph is not None:
+                ev[k][0].record(stream)
+                graph.replay()
+                ev[k][3].record(stream)
+            else:
+                step(ev[k])
+        torch.cuda.synchronize(dev)
+        ev = ev[:n_phase]
         if graph is not None:   # one interval per replay: eval + count + scan + emit
             kms = {"step_graph": float(np.mean([e[0].elapsed_time(e[3]) for e in ev]))}
         else:
@@ -316,7 +331,7 @@ def main():
         info = dict(R=R, nv=int(tot[0]), nf=int(tot[1]), elapsed=el, kernels_ms=kms, kernel_ms=kernel_ms,
                     shape=shape, slab_layers=slab.cz1 - slab.cz_emit, depth=slab.depth, bricks=slab.brick_stats(),
                     graph=graph is not None, cuts=cuts, cut_s=t_cut,
-                    fz=(slab.fz0, slab.fz1), jit=slab.used_jit(), stats=slab.stats())
+                    fz=(slab.fz0, slab.fz1), jit=slab.used_jit(), jit_module=slab.jit_module(), stats=slab.stats())
         if world > 1:
             # every rank's own step time (the max over ranks is the headline's): the balance
             rt = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -605,7 +620,8 @@ def main():
         },
         "kernels_ms": {k: round(v, 4) for k, v in kms.items()},
         "kernel_ms": {k: round(v, 4) for k, v in kern.items()},
-        "eval_kernel": "jit" if main_run["jit"] else "interpreter",
+        "eval_kernel": {"shape": "jit", "baked": "jit (object's module, matrices as literals)"}.get(
+            main_run["jit_module"], "interpreter"),
         "launch": "hipGraph replay of the step" if main_run["graph"] else "direct launches",
         "bricks": {"total": bricks_total, "mixed": bricks_mixed, "sign_filled": bricks_filled,
                    "evaluated_sample_frac": round(1.0 - bricks_filled / max(1, bricks_total), 4),

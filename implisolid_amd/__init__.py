@@ -218,9 +218,11 @@ def set_jit(mode):
     lib().implisolid_set_jit(int(mode))
 
 
-def set_jit_bake(on):
-    """Bake each object's matrices into its tree module (one module per object) or not (per shape)."""
-    lib().implisolid_set_jit_bake(1 if on else 0)
+def set_jit_bake(mode):
+    """Tree modules with the object's matrices baked in as literals: 0 never (one module per shape),
+    1 every object, 2 (default) hot objects -- an object evaluated 4 times by the same engine gets its
+    baked module (compiled in the background in async mode).  True / False mean 1 / 0."""
+    lib().implisolid_set_jit_bake(int(mode))
 
 
 def jit_wait():
@@ -232,7 +234,7 @@ def jit_stats():
     out = (ctypes.c_int32 * 4)()
     secs = ctypes.c_double(0)
     lib().implisolid_jit_stats(out, ctypes.byref(secs))
-    return {"mode": out[0], "bake": bool(out[1]), "compiled": out[2], "disk_hits": out[3], "compile_s": secs.value}
+    return {"mode": out[0], "bake": int(out[1]), "compiled": out[2], "disk_hits": out[3], "compile_s": secs.value}
 
 
 def jit_compile(shape, points=False):
@@ -544,6 +546,11 @@ class Slab:
 
     def used_jit(self):
         return bool(lib().implisolid_slab_used_jit(self.h))
+
+    def jit_module(self):
+        """The tree kernels of the last eval: "interpreter", "shape" (JIT module per tree shape) or
+        "baked" (the object's module with its matrices as literals)."""
+        return ("interpreter", "shape", "baked")[lib().implisolid_slab_used_jit(self.h)]
 
     def brick_stats(self):
         """[bricks, mixed-sign bricks, sign-filled bricks] of the last eval."""

@@ -753,14 +753,14 @@ int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]) {
     return 0;
 }
 
-int implisolid_slab_used_jit(implisolid_slab* s) { return s->engine.used_jit() ? 1 : 0; }
+int implisolid_slab_used_jit(implisolid_slab* s) { return s->engine.used_baked() ? 2 : s->engine.used_jit() ? 1 : 0; }
 void implisolid_set_jit(int mode) { TreeJit::instance().set_mode(mode); }
-void implisolid_set_jit_bake(int on) { TreeJit::instance().set_bake(on != 0); }
+void implisolid_set_jit_bake(int mode) { TreeJit::instance().set_bake(mode); }
 void implisolid_jit_wait(void) { TreeJit::instance().wait_idle(); }
 void implisolid_jit_stats(int32_t out[4], double* compile_seconds) {
     TreeJit& j = TreeJit::instance();
     out[0] = j.mode();
-    out[1] = j.bake() ? 1 : 0;
+    out[1] = j.bake();
     out[2] = j.compiled();
     out[3] = j.disk_hits();
     if (compile_seconds) *compile_seconds = j.compile_seconds();
@@ -866,6 +866,7 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         for (int i = 0; i < n; ++i) {   // warm run: JIT lookup, output capacities from the real counts
             b->engines.emplace_back(new Engine());
             Engine& E = *b->engines.back();
+            E.set_hot_bake(false);   // graphs capture the modules found now
             E.set_object(progs[(size_t)i]);
             E.set_grid(st.resolution, st.box, 0, 1);
             E.marching_cubes(s0);

@@ -114,6 +114,7 @@ Engine::Engine() {
 
 void Engine::set_offsets(uint32_t voff, uint32_t foff) {
     const uint32_t h[2] = {voff, foff};
+    IMPLI_HIP(hipDeviceSynchronize());   // no kernel of an earlier emit may still read them
     IMPLI_HIP(hipMemcpy(offsets_.p, h, sizeof h, hipMemcpyHostToDevice));
 }
 
@@ -150,12 +151,20 @@ Engine::~Engine() {
 }
 
 void Engine::set_object(const Program& prog) {
+    // the same object again (repeated builds): keep its modules and its eval count
+    if (have_object_ && std::memcmp(&prog, &prog_host_, sizeof(Program)) == 0) return;
+    // the engine's kernels run on caller streams (often non-blocking): nothing in flight may still
+    // read the program being replaced
+    IMPLI_HIP(hipDeviceSynchronize());
     IMPLI_HIP(hipMemcpy(prog_.p, &prog, sizeof(Program), hipMemcpyHostToDevice));
     depth_ = prog.max_depth;
     n_csg_ = prog.n_csg;
     prog_host_ = prog;
     jit_requested_ = false;
     jit_slot_ = nullptr;
+    bake_requested_ = false;
+    bake_slot_ = nullptr;
+    evals_ = 0;
     pt_requested_ = false;
     pt_slot_ = nullptr;
     jit_fn_ = nullptr;
@@ -168,6 +177,9 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
 
 void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool probe_only) {
     const SlabRange sr = slab_range(R, sr_in.z0, sr_in.z1);   // validated, 32-bit limits checked
+    // the buffers below are reset on the null stream, which a non-blocking caller stream does not
+    // order against: no earlier kernel may still run, and the resets finish before the next launch
+    IMPLI_HIP(hipDeviceSynchronize());
     grid_ = make_grid(R, box, sr.z0 - sr.halo, sr.z1, sr.z0);
     probe_only_ = probe_only;
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
@@ -188,6 +200,7 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     // the pieces past the last brick of a row are never written by the pruned path: keep them 0
     IMPLI_HIP(hipMemset(signs_.p, 0, sign_bytes + 64));
     if (probe_only) {   // interval_pass / listed_per_layer only
+        IMPLI_HIP(hipDeviceSynchronize());
         have_grid_ = true;
         return;
     }
@@ -205,6 +218,7 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     const int64_t m2 = (int64_t)grid_.m * grid_.m;
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
                                (uint32_t)std::min<int64_t>(6 * m2, 1u << 31), 0});
+    IMPLI_HIP(hipDeviceSynchronize());
     have_grid_ = true;
 }
 
@@ -374,14 +388,24 @@ const TreeJit::PointKernels* Engine::point_jit() {
 void Engine::ensure_jit() {
     // the object's tree module is requested once (TreeJit: compiled now, or on a background thread
     // while the interpreter kernels run); every eval uses it as soon as it is loaded
+    TreeJit& J = TreeJit::instance();
     if (!jit_requested_) {
-        jit_slot_ = TreeJit::instance().request(prog_host_);
+        jit_slot_ = J.request(prog_host_, TreeJit::kBricks, J.bake() == TreeJit::kBakeAlways);
         jit_requested_ = true;
     }
-    if (jit_slot_ && jit_slot_->ready.load(std::memory_order_acquire)) {
-        jit_fn_ = jit_slot_->k.bricks;
-        jit_iv_.coarse = jit_slot_->k.coarse;
-        jit_iv_.refine = jit_slot_->k.refine;
+    // a hot object (evaluated kBakeAfter times since set_object) gets its baked module
+    if (++evals_ >= TreeJit::kBakeAfter && !bake_requested_ && allow_hot_bake_ && J.bake() == TreeJit::kBakeHot &&
+        jit_slot_) {
+        bake_slot_ = J.request(prog_host_, TreeJit::kBricks, true);
+        bake_requested_ = true;
+    }
+    const TreeJit::Slot* use = bake_slot_ && bake_slot_->ready.load(std::memory_order_acquire) ? bake_slot_
+                               : jit_slot_ && jit_slot_->ready.load(std::memory_order_acquire) ? jit_slot_
+                                                                                                : nullptr;
+    if (use) {
+        jit_fn_ = use->k.bricks;
+        jit_iv_.coarse = use->k.coarse;
+        jit_iv_.refine = use->k.refine;
     } else {
         jit_fn_ = nullptr;
         jit_iv_ = JitIntervalKernels{};

@@ -106,6 +106,8 @@ public:
     const Program* d_program() const { return prog_.as<Program>(); }
     // true if the last eval_field ran the JIT-compiled tree kernel
     bool used_jit() const { return jit_fn_ != nullptr; }
+    // ... and whether that was the object's baked module (TreeJit bake modes)
+    bool used_baked() const { return jit_fn_ != nullptr && bake_slot_ && jit_fn_ == bake_slot_->k.bricks; }
     const float* d_rabbit() const { return rabbit_.as<float>(); }
     // the object's matrices as the JIT kernels read them (the Program's mats array)
     const float* d_mats() const;
@@ -114,6 +116,8 @@ public:
     const TreeJit::PointKernels* point_jit();
 
     DevBuf& scratch(int k) { return scratch_[k]; }
+    // engines whose kernels are captured once (object streams): no switch to a baked module later
+    void set_hot_bake(bool on) { allow_hot_bake_ = on; }
 
     // per-brick interval pruning of the field evaluation (process-wide level, default 2;
     // IMPLISOLID_PRUNE=<level> or implisolid_set_pruning(level)):
@@ -140,6 +144,10 @@ private:
     Program prog_host_{};
     TreeJit::Slot* jit_slot_ = nullptr;   // the object's module (null: JIT off); may still compile
     bool jit_requested_ = false;
+    TreeJit::Slot* bake_slot_ = nullptr;  // its baked module (TreeJit bake modes), preferred once loaded
+    bool bake_requested_ = false;
+    int evals_ = 0;                        // evals of this object (hot objects get a baked module)
+    bool allow_hot_bake_ = true;
     TreeJit::Slot* pt_slot_ = nullptr;     // the point module
     bool pt_requested_ = false;
     hipFunction_t jit_fn_ = nullptr;       // what the last eval used (null: interpreter)

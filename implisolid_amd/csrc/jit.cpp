@@ -356,7 +356,7 @@ TreeJit& TreeJit::instance() {
 
 TreeJit::TreeJit() {
     if (const char* e = std::getenv("IMPLISOLID_JIT")) mode_.store(e[0] == '0' ? kOff : e[0] == '1' ? kSync : kAsync);
-    if (const char* e = std::getenv("IMPLISOLID_JIT_BAKE")) bake_.store(e[0] == '1');
+    if (const char* e = std::getenv("IMPLISOLID_JIT_BAKE")) set_bake(e[0] - '0');
     const char* d = std::getenv("IMPLISOLID_JIT_CACHE");
     if (d && (!std::strcmp(d, "off") || !std::strcmp(d, "0"))) {
         disk_dir_.clear();
@@ -495,12 +495,12 @@ void TreeJit::shutdown() {   // at exit: drop queued work, finish what is compil
     workers_.clear();
 }
 
-TreeJit::Slot* TreeJit::request(const Program& p, int kind) {
+TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
     const int m = mode();
     if (m == kOff) return nullptr;
     std::string src;
     try {
-        src = kind == kPoints ? point_source(p) : kernel_source(p, bake());
+        src = kind == kPoints ? point_source(p) : kernel_source(p, bake);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "implisolid: tree JIT skipped (%s)\n", e.what());
         return nullptr;
@@ -552,7 +552,7 @@ void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
     // register and queue every program's module (async), then drain the queue with extra threads
     const int saved = mode();
     mode_.store(kAsync);
-    for (const Program& p : progs) (void)request(p);
+    for (const Program& p : progs) (void)request(p, kBricks, bake() == kBakeAlways);
     mode_.store(saved);
     // let the pool drain the queue, with extra threads for a large batch
     std::vector<std::thread> extra;

@@ -67,11 +67,16 @@ public:
     //     engine uses the interpreter kernels until the module is ready -- a never-seen shape costs
     //     no compile latency.  Code objects persist in a disk cache (IMPLISOLID_JIT_CACHE=<dir>,
     //     default $XDG_CACHE_HOME or ~/.cache /implisolid_amd; "off" disables it).
-    // Variants (IMPLISOLID_JIT_BAKE=0|1, implisolid_set_jit_bake): shape modules keep the matrices as
-    // data (one module per tree shape); baked modules hold the object's matrices as literals (one per
-    // object: no matrix loads on the dependency chains).
+    // Variants: shape modules keep the matrices as data (one module per tree shape); baked modules
+    // hold the object's matrices as literals (one per object: no matrix loads on the dependency
+    // chains, 5 % faster at 512^3).  Bake modes (IMPLISOLID_JIT_BAKE, implisolid_set_jit_bake):
+    //   0 never; 1 every object; 2 (default) hot objects -- an engine evaluating the same object
+    //   kBakeAfter times requests its baked module (in the background in async mode) and switches
+    //   to it once loaded, so objects that change every call never compile one.
     enum Mode { kOff = 0, kSync = 1, kAsync = 2 };
-    Slot* request(const Program& p, int kind = kBricks);
+    enum BakeMode { kBakeNever = 0, kBakeAlways = 1, kBakeHot = 2 };
+    static constexpr int kBakeAfter = 4;
+    Slot* request(const Program& p, int kind = kBricks, bool bake = false);
     // block until every scheduled compilation has finished (bench / batch setup)
     void wait_idle();
     // compile the modules of many programs (sync, up to `threads` host threads); request() then
@@ -89,8 +94,8 @@ public:
 
     int mode() const { return mode_.load(); }
     void set_mode(int m) { mode_.store(m < 0 ? 0 : m > 2 ? 2 : m); }
-    bool bake() const { return bake_.load(); }
-    void set_bake(bool b) { bake_.store(b); }
+    int bake() const { return bake_.load(); }
+    void set_bake(int b) { bake_.store(b < 0 ? 0 : b > 2 ? 2 : b); }
     bool enabled() const { return mode() != kOff; }
     void set_enabled(bool on) { set_mode(on ? kAsync : kOff); }
     int compiled() const { return n_compiled_.load(); }
@@ -110,7 +115,7 @@ private:
     int busy_ = 0;
     bool stop_ = false;
     std::atomic<int> mode_{kAsync};
-    std::atomic<bool> bake_{false};
+    std::atomic<int> bake_{kBakeHot};
     std::atomic<int> n_compiled_{0}, n_disk_{0};
     std::atomic<int64_t> compile_us_{0};
     std::string disk_dir_;

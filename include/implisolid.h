@@ -202,7 +202,8 @@ int implisolid_slab_set_timing(implisolid_slab* s, int on);
  * halo-owned vertices, cells, mixed coarse boxes of the last eval, halo-owned vertices as the
  * vertex pass reads them (counter word 1, must equal [5]), unit parts] (blocking) */
 int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]);
-/* 1 if the slab's last eval ran the JIT-compiled tree kernel, 0 if the interpreter */
+/* the tree kernels the slab's last eval ran: 0 the interpreter, 1 the shape's JIT module, 2 the
+ * object's baked JIT module */
 int implisolid_slab_used_jit(implisolid_slab* s);
 /* process-wide tree-kernel JIT mode for objects set from now on (environment IMPLISOLID_JIT):
  *   0 off (interpreter kernels only), 1 sync (hipRTC compiles before the first eval of a new shape),
@@ -210,9 +211,11 @@ int implisolid_slab_used_jit(implisolid_slab* s);
  *   until the module is loaded -- a never-seen shape pays no compile latency).  Compiled code
  *   objects are kept in a disk cache (IMPLISOLID_JIT_CACHE).  Results are bit-identical in every mode. */
 void implisolid_set_jit(int mode);
-/* 1: modules bake the object's matrices in as literals (one module per object); 0 (default): one
- * module per tree shape, matrices read from memory (IMPLISOLID_JIT_BAKE) */
-void implisolid_set_jit_bake(int on);
+/* tree modules with the object's matrices baked in as literals (IMPLISOLID_JIT_BAKE): 0 never (one
+ * module per tree shape, matrices read from memory), 1 every object (one module per object), 2
+ * (default) hot objects: an engine that evaluates the same object 4 times requests its baked module
+ * (in the background in async mode) and switches to it once loaded.  Bit-identical in every mode. */
+void implisolid_set_jit_bake(int mode);
 /* block until all scheduled tree-kernel compilations have finished */
 void implisolid_jit_wait(void);
 /* [mode, bake, modules compiled, modules read from the disk cache], total compile seconds */

@@ -204,7 +204,7 @@ def test_jit_field_matches_interpreter(impli, name, level):
                 s.close()
     finally:
         impli.set_jit(2)
-        impli.set_jit_bake(False)
+        impli.set_jit_bake(2)
         impli.set_pruning(2)
     fa, sa, ba = out[0]
     for fb, sb, bb in out[1:]:
@@ -766,6 +766,23 @@ def test_headline_against_oracle_summary(impli, name):
     assert np.abs(v[idx][ok].astype(np.float64) - vs[ok]).max(initial=0.0) < 1e-5
     tot = v[fin].astype(np.float64).sum(0)
     assert np.abs(tot - np.array(s["finite_sum"])).max() < 1e-5 * max(1, fin.sum())
+
+
+def test_rebuild_sequence_consistent(impli):
+    """Repeated builds of one object at growing and shrinking resolutions through the C ABI (one
+    engine, its buffers reset between grids on the null stream while its kernels run on a
+    non-blocking stream): every build of a resolution gives the same mesh.  Regression: a 256^3
+    build right after a 512^3 one once raced its buffer resets and came back empty."""
+    import hashlib
+    from implisolid_amd import scenes
+    shape = scenes.config3_tree()
+    seen = {}
+    for R in [64, 64, 64, 64, 64, 384, 192, 128, 192, 384, 192]:
+        v, f = impli.make_geometry(shape, scenes.mc_settings(R, 1.0))
+        key = (len(v), len(f), hashlib.sha256(np.ascontiguousarray(f).tobytes()).hexdigest())
+        assert len(f) > 0, R
+        assert seen.setdefault(R, key) == key, R
+        impli.jit_wait()
 
 
 # ---- multi-GPU: balanced slabs, multi-device build_geometry, multi-process ranks -------------------
