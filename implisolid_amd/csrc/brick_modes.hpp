@@ -102,22 +102,50 @@ __device__ __forceinline__ void coarse_modes_body(const IvEval& ev, const GridDe
     block_append<256>(b < cg.n_bricks && c == kBrickMixed, (uint32_t)b, clist, ccount, (uint32_t)cg.n_bricks);
 }
 
-// Bricks of the listed mixed coarse boxes: one thread per (listed box, brick in it); item i is brick
-// i % kCZ of listed box i / kCZ.
+// Bricks of the listed mixed coarse boxes, kRefineSplit = kBZ lanes per brick: item i is sample
+// layer i % kBZ of brick (i / kBZ) % kCZ of listed box i / (kBZ kCZ).  A layer's box is flat in z,
+// so z-piecewise primitives pick their pieces exactly (the double mushroom's caps r - z: over the
+// whole brick the cap piece's bound spans the layer below the cap and reaches above 0, a false
+// mixed class for every brick along the cap plane).  Interval arithmetic is inclusion-monotone, so
+// each layer's bound is at least as tight as the brick's: the brick is of a definite class iff its
+// layers are of that class, and a CSG operand pruned over all layers is pruned over the brick
+// (modes agreeing over the layers are kept, the others reset to both operands -- never less
+// pruning than the brick's own interval).
+constexpr int kRefineSplit = kBZ;
 template <class IvEval>
 __device__ __forceinline__ void brick_refine_item(const IvEval& ev, const GridDesc& g, const BrickGrid& bg,
                                                   const BrickGrid& cg, const uint64_t* __restrict__ cmodes,
                                                   const uint32_t* __restrict__ clist, uint64_t* __restrict__ modes,
-                                                  uint8_t* __restrict__ cls, uint32_t i) {
-    const uint32_t cb = clist[i / kCZ];
+                                                  uint8_t* __restrict__ cls, uint32_t i, bool live) {
+    static_assert((kRefineSplit & (kRefineSplit - 1)) == 0 && 64 % kRefineSplit == 0, "lane groups in a wave");
+    const uint32_t bi = i / kRefineSplit, qd = i % kRefineSplit;
+    const uint32_t cb = live ? clist[bi / kCZ] : 0u;
     int cx, cy, cz;
     brick_of((int)cb, cg, cx, cy, cz);
-    const int bz = cz * kCZ + (int)(i % kCZ);
-    if (bz >= bg.nbz) return;
-    const int b = cx + cy * bg.nbx + bz * bg.nbx * bg.nby;
-    const BrickBox q = brick_box(g, cx, cy, bz, kBZ);
+    const int bz = cz * kCZ + (int)(bi % kCZ);
+    const bool ok = live && bz < bg.nbz;
+    const BrickBox q = brick_box(g, cx, cy, ok ? bz : 0, kBZ);
+    // the lane's layer (a brick past the slab's last layer repeats its last one)
+    const int lz = min(q.z0 + (int)qd, q.z1);
     uint64_t m = cmodes[cb];
-    const uint8_t c = sign_class(ev(sample_box(g, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1), m, m));
+    uint8_t c = sign_class(ev(sample_box(g, q.x0, q.x1, q.y0, q.y1, lz, lz), m, m));
+    // combine the brick's lanes (consecutive lanes of one wave)
+    uint64_t m_and = m, m_or = m;
+    uint32_t c_and = c, c_or = c;
+#pragma unroll
+    for (int o = 1; o < kRefineSplit; o <<= 1) {
+        const uint64_t a = __shfl_xor(m_and, o, 64), b = __shfl_xor(m_or, o, 64);
+        m_and &= a;
+        m_or |= b;
+        c_and &= (uint32_t)__shfl_xor((int)c_and, o, 64);
+        c_or |= (uint32_t)__shfl_xor((int)c_or, o, 64);
+    }
+    const uint64_t d = m_and ^ m_or;
+    const uint64_t differ = ((d | (d >> 1)) & 0x5555555555555555ull) * 3ull;
+    m = m_and & ~differ;
+    c = c_and == c_or ? (uint8_t)c_and : (uint8_t)kBrickMixed;
+    if (!ok || qd != 0) return;
+    const int b = cx + cy * bg.nbx + bz * bg.nbx * bg.nby;
     modes[b] = m;
     cls[b] = sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
 }
@@ -127,9 +155,12 @@ __device__ __forceinline__ void brick_refine_body(const IvEval& ev, const GridDe
                                                   const uint32_t* __restrict__ clist,
                                                   const uint32_t* __restrict__ ccount, uint64_t* __restrict__ modes,
                                                   uint8_t* __restrict__ cls) {
-    const uint32_t total = min(*ccount, (uint32_t)cg.n_bricks) * kCZ;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256)
-        brick_refine_item(ev, g, bg, cg, cmodes, clist, modes, cls, i);
+    const uint32_t total = min(*ccount, (uint32_t)cg.n_bricks) * kCZ * kRefineSplit;
+    // the loop runs while any lane of the wave has an item: a brick's layer lanes shuffle together
+    for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < total; i0 += gridDim.x * 256) {
+        const uint32_t i = i0 + (threadIdx.x & 63u);
+        brick_refine_item(ev, g, bg, cg, cmodes, clist, modes, cls, i, i < total);
+    }
 }
 
 }  // namespace impli

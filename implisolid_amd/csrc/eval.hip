@@ -334,11 +334,17 @@ template <int D>
 __global__ __launch_bounds__(256) void k_brick_refine_b(const ObjArgs* __restrict__ objs, int n, const float* __restrict__ tab,
                                                         float2 tab_range, GridDesc g, BrickGrid bg, BrickGrid cg) {
     __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
-    const uint32_t total = batch_prefix(objs, n, kCoarseListWord, (uint32_t)kCZ, (uint32_t)cg.n_bricks, s_pre);
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-        const int k = batch_object_of(s_pre, n, i);
+    const uint32_t total =
+        batch_prefix(objs, n, kCoarseListWord, (uint32_t)(kCZ * kRefineSplit), (uint32_t)cg.n_bricks, s_pre);
+    // whole waves iterate (a brick's layer lanes shuffle together); object ranges start at
+    // multiples of kRefineSplit, so a brick's lanes share their object
+    for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < total; i0 += gridDim.x * 256) {
+        const uint32_t i = i0 + (threadIdx.x & 63u);
+        const bool live = i < total;
+        const int k = batch_object_of(s_pre, n, live ? i : 0u);
         const ObjArgs& o = objs[k];
-        brick_refine_item(InterpIv<D>{o.prog, tab, tab_range}, g, bg, cg, o.cmodes, o.clist, o.modes, o.cls, i - s_pre[k]);
+        brick_refine_item(InterpIv<D>{o.prog, tab, tab_range}, g, bg, cg, o.cmodes, o.clist, o.modes, o.cls,
+                          live ? i - s_pre[k] : 0u, live);
     }
 }
 __global__ __launch_bounds__(kFillBlock) void k_brick_fill_b(const ObjArgs* __restrict__ objs, GridDesc g, BrickGrid bg,
@@ -453,7 +459,7 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
     uint32_t* d_ccount = d_counters + kCoarseListWord;
     depth = eval_depth(depth);
     const unsigned tc = (unsigned)((cg.n_bricks + 255) / 256);
-    const unsigned tr = (unsigned)std::min<int64_t>(((int64_t)cg.n_bricks * kCZ + 255) / 256, 2048);
+    const unsigned tr = (unsigned)std::min<int64_t>(((int64_t)cg.n_bricks * kCZ * kRefineSplit + 255) / 256, 4096);
     if (jit && jit->coarse && jit->refine) {
         GridDesc gg = g;
         const float* d_mats = reinterpret_cast<const float*>(reinterpret_cast<const char*>(d_prog) + offsetof(Program, mats));

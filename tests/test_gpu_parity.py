@@ -181,6 +181,44 @@ def test_empty_and_full(impli, oracle):
     _mc_compare(impli, oracle, big, scenes.mc_settings(16, 1.0))
 
 
+def test_hot_object_switches_to_baked_module(impli):
+    """Bake mode 2 (default): a slab evaluating the same object runs the shape module first, then
+    (after a few evals, compiled in the background) the object's baked module -- with the same
+    field, signs and mesh bit for bit; bake mode 0 never switches."""
+    import hashlib
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(64, 1.0)
+    shape = TREES["config3_64"] if "config3_64" in TREES else scenes.config3_tree()
+    try:
+        for bake in (2, 0):
+            impli.set_jit_bake(bake)
+            s = impli.Slab(shape, mc)
+            try:
+                kinds, outs = [], []
+                for _ in range(8):
+                    s.eval()
+                    kinds.append(s.jit_module())
+                    outs.append((s.read_field(), s.read_signs()))
+                    impli.jit_wait()
+                nv, nf = s.run()
+                v, f = s.download(nv, nf)
+            finally:
+                s.close()
+            assert ("baked" in kinds) == (bake == 2), kinds
+            assert kinds[-1] == ("baked" if bake == 2 else "shape"), kinds
+            fa, sa = outs[0]
+            for fb, sb in outs[1:]:
+                assert np.array_equal(fa.view(np.uint32), fb.view(np.uint32))
+                assert np.array_equal(sa, sb)
+            key = hashlib.sha256(np.ascontiguousarray(f).tobytes() + np.ascontiguousarray(v).tobytes()).hexdigest()
+            if bake == 2:
+                ref = key
+            else:
+                assert key == ref
+    finally:
+        impli.set_jit_bake(2)
+
+
 @pytest.mark.parametrize("level", [1, 2])
 @pytest.mark.parametrize("name", sorted(TREES))
 def test_jit_field_matches_interpreter(impli, name, level):
