@@ -12,11 +12,13 @@
 //   step 2    compute_average_edge_length cp:70-82; set_centers_on_surface cp:421-1214;
 //             bisection bisection.hpp:117-459; vertex_apply_qem qem.hpp:321-599
 // (cp = centroids_projection.cpp)
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <deque>
 #include <future>
+#include <limits>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -683,7 +685,7 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     avg_edge_ = 0.f;
     for (double& t : stage_ms_) t = 0.0;
     Stage st(this, kStageTopology);
-    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 64, s));   // pending count, cap hits, evaluations
+    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 64, s));   // (unused), cap hits, evaluations
     verts_.reserve((size_t)(nv + 1) * 12);
     vnew_.reserve((size_t)(nv + 1) * 12);
     faces_.reserve((size_t)(nf + 1) * 12);
@@ -825,8 +827,18 @@ void Ob02::start_edge_fold() {
 float Ob02::finish_edge_fold() {
     IMPLI_HIP(hipEventSynchronize(norms_ready_));
     const float* h = host_norms_.as<float>();
+    // a NaN length makes the chain NaN from there on whatever the order (lengths are >= 0, so no
+    // inf - inf either): a vectorised scan answers that case without the serial chain (meshes with
+    // the reference's non-finite rows)
+    const int64_t n = 3 * nf;
+    for (int64_t k0 = 0; k0 < n; k0 += 4096) {
+        const int64_t k1 = std::min<int64_t>(n, k0 + 4096);
+        int nan = 0;
+        for (int64_t k = k0; k < k1; ++k) nan |= h[k] != h[k];
+        if (nan) return std::numeric_limits<float>::quiet_NaN();
+    }
     float el = 0.f;   // the reference starts from an uninitialised float (F8a); defined as 0
-    for (int64_t k = 0; k < 3 * nf; ++k) el += h[k];
+    for (int64_t k = 0; k < n; ++k) el += h[k];
     return (float)((double)el / (3. * (double)nf));
 }
 
@@ -865,7 +877,6 @@ void Ob02::centroids_projection(bool enable_qem) {
     pend_.reserve((size_t)(nf + 2) * 4);
     if (profile_) evals_buf_.reserve((size_t)(nf + 1) * 4);
     DevBuf& fcbuf = w_;   // f(centroid) per face; the resampling weights are dead here
-    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 4, s));   // pending count (the cap hits accumulate)
     ProjArgs a{};
     a.v = verts_.as<float>();
     a.f = faces_.as<int32_t>();
@@ -903,7 +914,7 @@ void Ob02::centroids_projection(bool enable_qem) {
     if (pk) TreeJit::launch(pk->early, grid, jargs, s, "impli_pt_project_early");
     else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
     // centroids left unresolved need the randomised directions (types 2-6): the late pass covers
-    // every face and reads the pending count on the device (no host round trip)
+    // every face and reads the early pass's per-face flags on the device (no host round trip)
     a.pert = perturbations();
     if (pk) TreeJit::launch(pk->late, grid, jargs, s, "impli_pt_project_late");
     else DEPTH_LAUNCH(E.depth(), k_project_late, grid, 256, s, E.d_program(), E.d_rabbit(), a);

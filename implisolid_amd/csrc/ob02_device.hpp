@@ -96,8 +96,8 @@ struct ProjArgs {
     float* out;             // projected centroids
     float* fn;              // facet normals (written by the early pass)
     float* fc;              // f(centroid) (written by the early pass)
-    uint32_t* pend;         // early pass: unresolved centroid list; its length at pend_count
-    uint32_t* pend_count;
+    uint32_t* pend;         // early pass: per face, 1 if its centroid is unresolved (the late pass's)
+    uint32_t* pend_count;   // (unused)
     uint32_t* cap_hits;     // bisections that reached kBisectCap (accumulated over the build)
     float* cen;             // centroids (written by the prep pass)
     float* dir;             // the type-0 direction per face (prep pass)
@@ -261,18 +261,19 @@ __device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs&
     bool found = try_direction(g, ev, x, d0, sc, a.alphas, a.nal, a.max_dist, best, bf, evals);
     if (!found) found = try_direction(g, ev, x, fnv, sc, a.alphas, a.nal < 10 ? a.nal : 10, a.max_dist, best, bf, evals);
     if (found) finalize_g(g, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
-    else if (g.sub == 0) a.pend[atomicAdd(a.pend_count, 1u)] = (uint32_t)j;
+    // unresolved faces are flagged for the late pass (a compacted list cost one same-address atomic
+    // per wave: 258 us per pass when every face pends, as with a non-finite average edge length)
+    if (g.sub == 0) a.pend[j] = found ? 0u : 1u;
     if (a.evals && g.sub == 0) a.evals[j] += evals;
 }
 
 // types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes); the grid
-// covers every face, groups past the pending count (read on the device) exit at once
+// covers every face, groups of faces the early pass resolved exit at once
 template <class Ev>
 __device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& a) {
     const Grp g;
-    const uint64_t k = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / kProjGroup;
-    if (k >= *a.pend_count) return;
-    const int64_t j = a.pend[k];
+    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kProjGroup;
+    if (j >= a.nf || !a.pend[j]) return;   // uniform per group
     const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const float fcv = a.fc[j];
