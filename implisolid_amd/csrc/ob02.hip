@@ -40,6 +40,7 @@ struct EdgeTab {
     uint32_t* last;
     uint32_t* cnt;
     uint32_t* slot_of;   // 3 * nf
+    uint32_t* f2;        // 2 * cap: the faces of an edge's first two insertions (cnt says which hold one)
     uint64_t mask;
 };
 
@@ -184,9 +185,15 @@ __global__ void k_edge_insert(const int32_t* __restrict__ f, int64_t nf, int64_t
         if (prev == kEmpty || prev == key) break;
         s = (s + 1) & t.mask;
     }
-    atomicMin(&t.first[s], (uint32_t)fi);
-    atomicMax(&t.last[s], (uint32_t)fi);
-    atomicAdd(&t.cnt[s], 1u);
+    // two atomics per half-edge: the arrival index keeps the first two faces (an edge of a closed
+    // manifold mesh has exactly two); min / max over further ones only for non-manifold edges
+    const uint32_t k = atomicAdd(&t.cnt[s], 1u);
+    if (k < 2) {
+        t.f2[2 * s + k] = (uint32_t)fi;
+    } else {
+        atomicMin(&t.first[s], (uint32_t)fi);
+        atomicMax(&t.last[s], (uint32_t)fi);
+    }
     t.slot_of[i] = (uint32_t)s;
 }
 
@@ -197,8 +204,13 @@ __global__ void k_fof(int64_t nf, EdgeTab t, int32_t* __restrict__ fof) {
     if (i >= 3 * nf) return;
     const uint32_t s = t.slot_of[i];
     const uint32_t fi = (uint32_t)(i / 3);
-    const uint32_t first = t.first[s];
-    fof[i] = (int32_t)((first != fi) ? first : (t.cnt[s] >= 2 ? t.last[s] : 0u));
+    const uint32_t c = t.cnt[s], a = t.f2[2 * s], b = c >= 2 ? t.f2[2 * s + 1] : a;
+    // first / last face of the edge (the min / max words hold only non-manifold extras); every
+    // half-edge of the slot stores the same values for the subdivision pass
+    const uint32_t first = min(min(a, b), t.first[s]), last = max(max(a, b), t.last[s]);
+    t.first[s] = first;
+    t.last[s] = last;
+    fof[i] = (int32_t)((first != fi) ? first : (c >= 2 ? last : 0u));
 }
 
 // ---- step 3: my_subdiv_ (centroids_projection.cpp:1314-1367) -----------------------------------
@@ -698,13 +710,14 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
 EdgeTab Ob02::edge_table() {
     uint64_t cap = 1024;
     while (cap < (uint64_t)(4 * nf + 16)) cap <<= 1;
-    etab_.reserve((size_t)cap * (8 + 12) + (size_t)(3 * nf + 1) * 4);
+    etab_.reserve((size_t)cap * (8 + 12 + 8) + (size_t)(3 * nf + 1) * 4);
     EdgeTab t;
     t.key = etab_.as<unsigned long long>();
     t.first = reinterpret_cast<uint32_t*>(t.key + cap);
     t.last = t.first + cap;
     t.cnt = t.last + cap;
     t.slot_of = t.cnt + cap;
+    t.f2 = t.slot_of + (3 * nf + 1);
     t.mask = cap - 1;
     return t;
 }
