@@ -45,7 +45,7 @@ def main():
     pad[:L, :n, :n] = need
     del need
     # brick classes from the exact signs (0 positive, 1 negative, 2 mixed) and the neighbour rule
-    sp = np.zeros((Lp, npad, npad), bool)
+    sp = np.ones((Lp, npad, npad), bool)   # padding: negative like the sealed ring
     sp[:L, :n, :n] = s_exact
     sb = sp.reshape(Lp // 2, 2, npad // 8, 8, npad // 8, 8)
     allneg, anyneg = sb.all(axis=(1, 3, 5)), sb.any(axis=(1, 3, 5))
@@ -82,6 +82,8 @@ def main():
         "exact_mixed_bricks": int((~definite).sum()),
         "exact_listed_bricks": int(listed_exact.sum()),
         "exact_listed_half_bricks_z_only": int(half.sum()),
+        "definite_bricks_with_needed": int((any_b & definite).sum()),
+        "mixed_bricks_with_needed": int((any_b & ~definite).sum()),
     }
     print(json.dumps(out, indent=1))
 
