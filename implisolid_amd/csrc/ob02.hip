@@ -25,6 +25,7 @@
 
 #include "ifunc_device.hpp"
 #include "ob02.hpp"
+#include "fold.hpp"
 #include "ob02_device.hpp"
 #include "jit.hpp"
 
@@ -449,6 +450,82 @@ __global__ void k_edge_norms(const float* __restrict__ v, const int32_t* __restr
     o[3 * j + 2] = norm2f(c[0] - b[0], c[1] - b[1], c[2] - b[2]);
 }
 
+// the fold's chunk table (fold.hpp), three small passes: each chunk's terms summed in double (one
+// wave per chunk); the exclusive prefix of those sums (one block) -> each chunk's binade window;
+// the table cells of the window (one wave per chunk, 4 terms per lane, wave sums of the lanes'
+// saturating partial sums, flags OR-ed)
+__global__ __launch_bounds__(256) void k_fold_chunk_sums(const float* __restrict__ e, int64_t n, double* __restrict__ cs) {
+    const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (c >= fold_chunks(n)) return;   // uniform per wave
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t k = c * kFoldChunk + q * 64 + lane;
+        if (k < n) v += (double)e[k];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) cs[c] = v;
+}
+__global__ __launch_bounds__(1024) void k_fold_bases(const double* __restrict__ cs, int64_t nc, int32_t* __restrict__ base) {
+    __shared__ double s_w[16];
+    __shared__ double s_carry;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) s_carry = 0.0;
+    __syncthreads();
+    for (int64_t i0 = 0; i0 < nc; i0 += 1024) {
+        const int64_t i = i0 + t;
+        const double v = i < nc ? cs[i] : 0.0;
+        double inc = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double y = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        double off = s_carry;
+        for (int k = 0; k < w; ++k) off += s_w[k];
+        if (i < nc) base[i] = fold_base(off + inc - v);   // the estimate of the sum before chunk i
+        __syncthreads();
+        if (t == 1023) s_carry = off + inc;
+        __syncthreads();
+    }
+}
+__global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e, int64_t n, const int32_t* __restrict__ base,
+                                                    uint32_t* __restrict__ sum, uint8_t* __restrict__ flags) {
+    const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (c >= fold_chunks(n)) return;   // uniform per wave
+    uint32_t bits[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t k = c * kFoldChunk + q * 64 + lane;
+        bits[q] = k < n ? __float_as_uint(e[k]) : 0u;   // +0 past the end contributes nothing
+    }
+    const int E0 = base[c];
+#pragma unroll
+    for (int b = 0; b < kFoldBinades; ++b) {
+        uint32_t s = 0, f = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint8_t fq;
+            s = fold_add(s, fold_term(bits[q], E0 + b, fq));
+            f |= fq;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s = fold_add(s, (uint32_t)__shfl_xor((int)s, o, 64));
+            f |= (uint32_t)__shfl_xor((int)f, o, 64);
+        }
+        if (lane == 0) {
+            sum[c * kFoldBinades + b] = s;
+            flags[c * kFoldBinades + b] = (uint8_t)f;
+        }
+    }
+}
+
 // ---- QEM: Eigen 3.3 JacobiSVD<Matrix3f> restated (Eigen/src/SVD/JacobiSVD.h, Jacobi/Jacobi.h) ----
 struct JRot { float c, s; };
 __device__ __forceinline__ void rot_rows(float W[3][3], int p, int q, JRot j) {
@@ -791,6 +868,8 @@ const std::map<std::string, std::vector<float>>& Ob02::pointsets() {
 Ob02::~Ob02() {
     if (pert_job_.valid()) pert_job_.wait();
     if (norms_ready_) (void)hipEventDestroy(norms_ready_);
+    if (table_done_) (void)hipEventDestroy(table_done_);
+    if (copy_s_) (void)hipStreamDestroy(copy_s_);
     host_norms_.release();
     dir_.release();
     evals_buf_.release();
@@ -831,27 +910,47 @@ void Ob02::vertex_resampling(float c) {
 void Ob02::start_edge_fold() {
     norms_.reserve((size_t)(nf + 1) * 12);
     k_edge_norms<<<blocks_for(nf), 256, 0, s>>>(verts_.as<float>(), faces_.as<int32_t>(), nf, norms_.as<float>());
+    // the chunk table of the serial fold (fold.hpp) and the terms themselves go to pinned memory
+    const int64_t chunks = fold_chunks(3 * nf), cells = chunks * kFoldBinades;
+    // device layout: [sum (cells u32) | bases (chunks i32) | chunk sums (chunks f64)], flags apart
+    fold_sum_.reserve((size_t)(cells + chunks + 2) * 4 + (size_t)(chunks + 1) * 8);
+    fold_flags_.reserve((size_t)cells + 16);
+    host_fold_sum_.reserve((size_t)(cells + chunks + 2) * 4);
+    host_fold_flags_.reserve((size_t)cells + 16);
+    uint32_t* d_sum = fold_sum_.as<uint32_t>();
+    int32_t* d_base = reinterpret_cast<int32_t*>(d_sum + cells);
+    double* d_cs = reinterpret_cast<double*>(fold_sum_.as<char>() + (((size_t)(cells + chunks) * 4 + 7) & ~(size_t)7));
+    if (cells) {
+        k_fold_chunk_sums<<<blocks_for(chunks * 64), 256, 0, s>>>(norms_.as<float>(), 3 * nf, d_cs);
+        k_fold_bases<<<1, 1024, 0, s>>>(d_cs, chunks, d_base);
+        k_fold_table<<<blocks_for(chunks * 64), 256, 0, s>>>(norms_.as<float>(), 3 * nf, d_base, d_sum,
+                                                             fold_flags_.as<uint8_t>());
+    }
     host_norms_.reserve((size_t)nf * 12);
-    IMPLI_HIP(hipMemcpyAsync(host_norms_.p, norms_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
+    // the copies run on their own stream, so the projection's prep pass (next on s) overlaps them
+    if (!copy_s_) IMPLI_HIP(hipStreamCreateWithFlags(&copy_s_, hipStreamNonBlocking));
+    if (!table_done_) IMPLI_HIP(hipEventCreateWithFlags(&table_done_, hipEventDisableTiming));
     if (!norms_ready_) IMPLI_HIP(hipEventCreateWithFlags(&norms_ready_, hipEventDisableTiming));
-    IMPLI_HIP(hipEventRecord(norms_ready_, s));
+    IMPLI_HIP(hipEventRecord(table_done_, s));
+    IMPLI_HIP(hipStreamWaitEvent(copy_s_, table_done_, 0));
+    if (cells) {
+        IMPLI_HIP(hipMemcpyAsync(host_fold_sum_.p, fold_sum_.p, (size_t)(cells + chunks) * 4, hipMemcpyDeviceToHost,
+                                 copy_s_));
+        IMPLI_HIP(hipMemcpyAsync(host_fold_flags_.p, fold_flags_.p, (size_t)cells, hipMemcpyDeviceToHost, copy_s_));
+    }
+    IMPLI_HIP(hipMemcpyAsync(host_norms_.p, norms_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, copy_s_));
+    IMPLI_HIP(hipEventRecord(norms_ready_, copy_s_));
 }
 
 float Ob02::finish_edge_fold() {
     IMPLI_HIP(hipEventSynchronize(norms_ready_));
-    const float* h = host_norms_.as<float>();
-    // a NaN length makes the chain NaN from there on whatever the order (lengths are >= 0, so no
-    // inf - inf either): a vectorised scan answers that case without the serial chain (meshes with
-    // the reference's non-finite rows)
-    const int64_t n = 3 * nf;
-    for (int64_t k0 = 0; k0 < n; k0 += 4096) {
-        const int64_t k1 = std::min<int64_t>(n, k0 + 4096);
-        int nan = 0;
-        for (int64_t k = k0; k < k1; ++k) nan |= h[k] != h[k];
-        if (nan) return std::numeric_limits<float>::quiet_NaN();
-    }
-    float el = 0.f;   // the reference starts from an uninitialised float (F8a); defined as 0
-    for (int64_t k = 0; k < n; ++k) el += h[k];
+    // the serial chain (the reference starts from an uninitialised float, F8a; defined as 0), from
+    // the device's chunk table: bit-identical (fold.hpp, tools/fold_check.cpp), a few chunks term
+    // by term
+    const int64_t cells = fold_chunks(3 * nf) * kFoldBinades;
+    const float el = fold_walk(host_norms_.as<float>(), 3 * nf,
+                               reinterpret_cast<const int32_t*>(host_fold_sum_.as<uint32_t>() + cells),
+                               host_fold_sum_.as<uint32_t>(), host_fold_flags_.as<uint8_t>());
     return (float)((double)el / (3. * (double)nf));
 }
 

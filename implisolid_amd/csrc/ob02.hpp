@@ -84,7 +84,11 @@ private:
     bool profile_ = false;
     double stage_ms_[kStages] = {};
     HostBuf host_norms_;                     // pinned: the edge-length terms' D2H
+    DevBuf fold_sum_, fold_flags_;           // the fold's chunk table (fold.hpp), built on the device
+    HostBuf host_fold_sum_, host_fold_flags_;
     hipEvent_t norms_ready_ = nullptr;
+    hipStream_t copy_s_ = nullptr;           // the fold's D2H copies, beside the projection's prep pass
+    hipEvent_t table_done_ = nullptr;
     DevBuf dir_, evals_buf_;
     std::vector<float> alphas_host_;         // kept until the next projection (async H2D source)
     std::future<std::shared_ptr<const std::vector<float>>> pert_job_;

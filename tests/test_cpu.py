@@ -580,6 +580,20 @@ def test_headline_summary_oracle_regression(oracle):
     assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"]
 
 
+def test_fold_table_exact(tmp_path):
+    """The OB02 edge-length fold from the device's chunk table (implisolid_amd/csrc/fold.hpp) equals
+    the serial float chain bit for bit on 600+ seeded arrays: edge-length-like terms, wide spreads,
+    engineered ties near binade tops, zeros, subnormals, inf, NaN payloads, saturation past 2^24
+    (tools/fold_check.cpp; most chunks taken from the table, the rest term by term)."""
+    exe = str(tmp_path / "fold_check")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17", os.path.join(ROOT, "tools", "fold_check.cpp"),
+                    "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+    table = int(r.stdout.split("from the table")[1].split()[0])
+    assert table > 50000, r.stdout
+
+
 def test_divconst_identity_exhaustive(tmp_path):
     """The double mushroom's divisions by its constant use q0 = a R, q = fma(fma(-q0, D, a), R, q0)
     (ifunc_device.hpp div_sq_const); it must equal the IEEE quotient for the square of every float
