@@ -874,7 +874,7 @@ Ob02::~Ob02() {
     dir_.release();
     evals_buf_.release();
     for (DevBuf* b : {&verts_, &faces_, &vnew_, &cen_, &nrm_, &w_, &fof_, &uoff_, &ulst_, &etab_, &deg_, &proj_, &grad_,
-                      &fn_, &norms_, &alphas_, &pert_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_})
+                      &fn_, &norms_, &alphas_, &pert_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_, &fold_sum_})
         b->release();
     for (auto& kv : snaps_) kv.second.buf.release();
 }
@@ -912,32 +912,29 @@ void Ob02::start_edge_fold() {
     k_edge_norms<<<blocks_for(nf), 256, 0, s>>>(verts_.as<float>(), faces_.as<int32_t>(), nf, norms_.as<float>());
     // the chunk table of the serial fold (fold.hpp) and the terms themselves go to pinned memory
     const int64_t chunks = fold_chunks(3 * nf), cells = chunks * kFoldBinades;
-    // device layout: [sum (cells u32) | bases (chunks i32) | chunk sums (chunks f64)], flags apart
-    fold_sum_.reserve((size_t)(cells + chunks + 2) * 4 + (size_t)(chunks + 1) * 8);
-    fold_flags_.reserve((size_t)cells + 16);
-    host_fold_sum_.reserve((size_t)(cells + chunks + 2) * 4);
-    host_fold_flags_.reserve((size_t)cells + 16);
+    // the table, device and host alike: [sums (cells u32) | bases (chunks i32) | flags (cells u8)],
+    // then on the device the chunks' double sums; the host's pinned buffer holds the terms first
+    const size_t tab_bytes = (size_t)(cells + chunks) * 4 + (size_t)cells, cs_off = (tab_bytes + 15) & ~(size_t)15;
+    fold_sum_.reserve(cs_off + (size_t)(chunks + 1) * 8);
+    const size_t terms_bytes = ((size_t)nf * 12 + 15) & ~(size_t)15;
+    host_norms_.reserve(terms_bytes + tab_bytes + 16);
     uint32_t* d_sum = fold_sum_.as<uint32_t>();
     int32_t* d_base = reinterpret_cast<int32_t*>(d_sum + cells);
-    double* d_cs = reinterpret_cast<double*>(fold_sum_.as<char>() + (((size_t)(cells + chunks) * 4 + 7) & ~(size_t)7));
+    uint8_t* d_flags = reinterpret_cast<uint8_t*>(d_base + chunks);
+    double* d_cs = reinterpret_cast<double*>(fold_sum_.as<char>() + cs_off);
     if (cells) {
         k_fold_chunk_sums<<<blocks_for(chunks * 64), 256, 0, s>>>(norms_.as<float>(), 3 * nf, d_cs);
         k_fold_bases<<<1, 1024, 0, s>>>(d_cs, chunks, d_base);
-        k_fold_table<<<blocks_for(chunks * 64), 256, 0, s>>>(norms_.as<float>(), 3 * nf, d_base, d_sum,
-                                                             fold_flags_.as<uint8_t>());
+        k_fold_table<<<blocks_for(chunks * 64), 256, 0, s>>>(norms_.as<float>(), 3 * nf, d_base, d_sum, d_flags);
     }
-    host_norms_.reserve((size_t)nf * 12);
     // the copies run on their own stream, so the projection's prep pass (next on s) overlaps them
     if (!copy_s_) IMPLI_HIP(hipStreamCreateWithFlags(&copy_s_, hipStreamNonBlocking));
     if (!table_done_) IMPLI_HIP(hipEventCreateWithFlags(&table_done_, hipEventDisableTiming));
     if (!norms_ready_) IMPLI_HIP(hipEventCreateWithFlags(&norms_ready_, hipEventDisableTiming));
     IMPLI_HIP(hipEventRecord(table_done_, s));
     IMPLI_HIP(hipStreamWaitEvent(copy_s_, table_done_, 0));
-    if (cells) {
-        IMPLI_HIP(hipMemcpyAsync(host_fold_sum_.p, fold_sum_.p, (size_t)(cells + chunks) * 4, hipMemcpyDeviceToHost,
-                                 copy_s_));
-        IMPLI_HIP(hipMemcpyAsync(host_fold_flags_.p, fold_flags_.p, (size_t)cells, hipMemcpyDeviceToHost, copy_s_));
-    }
+    if (cells)
+        IMPLI_HIP(hipMemcpyAsync(host_norms_.as<char>() + terms_bytes, fold_sum_.p, tab_bytes, hipMemcpyDeviceToHost, copy_s_));
     IMPLI_HIP(hipMemcpyAsync(host_norms_.p, norms_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, copy_s_));
     IMPLI_HIP(hipEventRecord(norms_ready_, copy_s_));
 }
@@ -947,10 +944,10 @@ float Ob02::finish_edge_fold() {
     // the serial chain (the reference starts from an uninitialised float, F8a; defined as 0), from
     // the device's chunk table: bit-identical (fold.hpp, tools/fold_check.cpp), a few chunks term
     // by term
-    const int64_t cells = fold_chunks(3 * nf) * kFoldBinades;
-    const float el = fold_walk(host_norms_.as<float>(), 3 * nf,
-                               reinterpret_cast<const int32_t*>(host_fold_sum_.as<uint32_t>() + cells),
-                               host_fold_sum_.as<uint32_t>(), host_fold_flags_.as<uint8_t>());
+    const int64_t chunks = fold_chunks(3 * nf), cells = chunks * kFoldBinades;
+    const uint32_t* sums = reinterpret_cast<const uint32_t*>(host_norms_.as<char>() + (((size_t)nf * 12 + 15) & ~(size_t)15));
+    const int32_t* bases = reinterpret_cast<const int32_t*>(sums + cells);
+    const float el = fold_walk(host_norms_.as<float>(), 3 * nf, bases, sums, reinterpret_cast<const uint8_t*>(bases + chunks));
     return (float)((double)el / (3. * (double)nf));
 }
 

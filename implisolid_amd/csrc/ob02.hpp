@@ -83,9 +83,8 @@ private:
     int64_t jit_launches_ = 0;   // OB02 passes that ran the JIT point module (since load_mesh)
     bool profile_ = false;
     double stage_ms_[kStages] = {};
-    HostBuf host_norms_;                     // pinned: the edge-length terms' D2H
-    DevBuf fold_sum_, fold_flags_;           // the fold's chunk table (fold.hpp), built on the device
-    HostBuf host_fold_sum_, host_fold_flags_;
+    HostBuf host_norms_;                     // pinned: the edge-length terms and the fold's table (D2H)
+    DevBuf fold_sum_;                        // the fold's chunk table (fold.hpp), built on the device
     hipEvent_t norms_ready_ = nullptr;
     hipStream_t copy_s_ = nullptr;           // the fold's D2H copies, beside the projection's prep pass
     hipEvent_t table_done_ = nullptr;
