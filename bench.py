@@ -160,7 +160,7 @@ def copy_attainable(dev, nbytes=1 << 30, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--resolution", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
