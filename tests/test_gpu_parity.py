@@ -291,6 +291,26 @@ def test_mc_identical_at_every_pruning_level(impli, oracle, level):
         impli.set_pruning(2)
 
 
+@pytest.mark.parametrize("seed", list(range(300, 312)))
+def test_pruning_levels_agree_random_twist_trees(impli, seed):
+    """Random trees with twists at odd and even resolutions (partial bricks and coarse boxes at the
+    grid's ends, one-layer top bricks): the default pipeline -- per-layer refinement, neighbour
+    candidates claimed by their mixed neighbours, chunk marks -- gives the unpruned mesh bit for bit."""
+    from implisolid_amd import scenes
+    shape = scenes.random_tree(seed, 4 + seed % 9, twist_leaves=True)
+    R = [23, 31, 45, 66, 37, 52][seed % 6]
+    mc = scenes.mc_settings(R, 1.0)
+    out = []
+    try:
+        for level in (0, 2):
+            impli.set_pruning(level)
+            out.append(impli.make_geometry(shape, mc))
+    finally:
+        impli.set_pruning(2)
+    (v0, f0), (v2, f2) = out
+    assert np.array_equal(f0, f2) and np.array_equal(v0.view(np.uint32), v2.view(np.uint32))
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 5])
 def test_zslab_split_identical(impli, oracle, nranks):
     """Z-slab decomposition (one-layer recomputed halo, global offsets) == single GPU."""
