@@ -248,7 +248,7 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
 }
 __global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) { unit_scan_body(g, b); }
 
-__global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
+__global__ __launch_bounds__(64 * kVertsWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_mc_cells(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     mc_cells_body(cases, g, b);
 }
 
@@ -337,16 +337,16 @@ __global__ __launch_bounds__(kScanBlock) void k_unit_scan_b(const ObjArgs* __res
 // vertex pass: one flat index over every object's unit parts (batch_device.hpp), a wave per part
 __global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells_b(const CaseInfo* __restrict__ cases,
                                                                 const ObjArgs* __restrict__ objs, int n, GridDesc g) {
-    __shared__ CaseInfo s_case[256];
+    __shared__ uint32_t s_cw[256];
     __shared__ uint64_t s_bits[kVertsWaves][9][64];
     __shared__ uint32_t s_excl[kVertsWaves][64];
     __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
     const int t = threadIdx.x, wid = t >> 6;
-    for (int k = t; k < 256; k += blockDim.x) s_case[k] = cases[k];
+    for (int k = t; k < 256; k += blockDim.x) s_cw[k] = case_word(cases[k]);
     const uint32_t total = batch_prefix(objs, n, 0, 1u, 0xffffffffu, s_pre);   // counters[0]: unit parts
     for (uint32_t e = blockIdx.x * kVertsWaves + wid; e < total; e += gridDim.x * kVertsWaves) {
         const int k = __builtin_amdgcn_readfirstlane(batch_object_of(s_pre, n, e));
-        mc_cells_part(s_case, g, objs[k].mc, e - s_pre[k], s_bits[wid], s_excl[wid]);
+        mc_cells_part(s_cw, g, objs[k].mc, e - s_pre[k], s_bits[wid], s_excl[wid]);
     }
 }
 // face pass: one flat index over every object's records, a lane per record

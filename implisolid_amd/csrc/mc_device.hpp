@@ -137,7 +137,16 @@ __device__ __forceinline__ int select_bit(uint64_t x, uint32_t r) {
 // listed in cell order 64 at a time, with no lane looping over a dense chunk's bits.
 // one part e of the flat unit list, by the calling wave (s_case: the case table in LDS; bits /
 // excl: the wave's LDS scratch)
-__device__ __forceinline__ void mc_cells_part(const CaseInfo* s_case, const GridDesc& g, const MCBuffers& b, uint32_t e,
+// the case facts the vertex pass needs, one word per case: nown (bits 0-1), ntri (2-4), and the
+// rank of owned edge slot s + 1 (0: unused) in bits 5 + 3 s (an 8 KB CaseInfo table in LDS held
+// the cells kernel to five waves per SIMD)
+__device__ __forceinline__ uint32_t case_word(const CaseInfo& c) {
+    uint32_t w = (uint32_t)c.nown | ((uint32_t)c.ntri << 2);
+    for (int s = 0; s < 3; ++s) w |= (uint32_t)(c.rank[s] + 1) << (5 + 3 * s);
+    return w;
+}
+
+__device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDesc& g, const MCBuffers& b, uint32_t e,
                                               uint64_t (*bits)[64], uint32_t* excl) {
     const int lane = threadIdx.x & 63;
     const uint32_t H = b.counters[1];
@@ -190,9 +199,10 @@ __device__ __forceinline__ void mc_cells_part(const CaseInfo* s_case, const Grid
                 const int x = 64 * (it % nch) + 1 + j;
                 const int z = (int)erow / g.m + g.cz0;
                 const uint32_t L = (uint32_t)(erow * g.m + (x - 1));
-                const CaseInfo& C = s_case[ci];
+                const uint32_t cw = s_cw[ci];
+                const unsigned c_nown = cw & 3u, c_ntri = (cw >> 2) & 7u;
                 const bool emit = has && z >= g.cz_emit;
-                const unsigned own = has ? C.nown : 0u, tri = emit ? C.ntri : 0u, act = (emit && C.ntri) ? 1u : 0u;
+                const unsigned own = has ? c_nown : 0u, tri = emit ? c_ntri : 0u, act = (emit && c_ntri) ? 1u : 0u;
                 const unsigned long long p = pack4(own, tri, act, 0u);
                 const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
                 const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
@@ -224,7 +234,7 @@ __device__ __forceinline__ void mc_cells_part(const CaseInfo* s_case, const Grid
                         const float fx2 = fx + g.w[0], fy2 = fy + g.w[1], fz2 = fz + g.w[2];
 #pragma unroll
                         for (int slot = 0; slot < 3; ++slot) {
-                            const int r = C.rank[slot];
+                            const int r = (int)((cw >> (5 + 3 * slot)) & 7u) - 1;
                             if (r < 0) continue;
                             const uint32_t out = vrun + (uint32_t)r - H;
                             b.vid3[(size_t)L * 3 + slot] = out;
@@ -252,16 +262,16 @@ __device__ __forceinline__ void mc_cells_part(const CaseInfo* s_case, const Grid
 }
 
 __device__ __forceinline__ void mc_cells_body(const CaseInfo* __restrict__ cases, const GridDesc& g, const MCBuffers& b) {
-    __shared__ CaseInfo s_case[256];
+    __shared__ uint32_t s_cw[256];
     __shared__ uint64_t s_bits[kVertsWaves][9][64];   // per wave and item: the 8 corner words + nt
     __shared__ uint32_t s_excl[kVertsWaves][64];      // per wave and item: cells in the items before it
     const int t = threadIdx.x, wid = t >> 6;
     const uint32_t n_ne = b.counters[0];              // non-empty units
     const uint32_t w0 = blockIdx.x * kVertsWaves;
     if (w0 >= n_ne) return;                           // uniform over the block
-    for (int k = t; k < 256; k += blockDim.x) s_case[k] = cases[k];
+    for (int k = t; k < 256; k += blockDim.x) s_cw[k] = case_word(cases[k]);
     __syncthreads();
-    for (uint32_t e = w0 + wid; e < n_ne; e += gridDim.x * kVertsWaves) mc_cells_part(s_case, g, b, e, s_bits[wid], s_excl[wid]);
+    for (uint32_t e = w0 + wid; e < n_ne; e += gridDim.x * kVertsWaves) mc_cells_part(s_cw, g, b, e, s_bits[wid], s_excl[wid]);
 }
 
 }  // namespace impli
