@@ -38,7 +38,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_create_range", "implisolid_slab_balance", "implisolid_cuts_from_layer_work", "implisolid_set_devices",
     "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
     "implisolid_set_progress_callback", "implisolid_ob02_profile", "implisolid_last_build_stats",
-    "implisolid_jit_compile_points",
+    "implisolid_jit_compile_points", "implisolid_debug_libm",
 ]
 
 # implisolid_progress_callback (include/implisolid.h): verts, n_verts, faces, n_faces,
@@ -85,6 +85,7 @@ def lib():
         "get_pointset_size": ([c_char_p], c_int), "about": ([], None),
         "implisolid_last_error": ([], c_char_p), "implisolid_set_error_mode": ([c_int], None),
         "implisolid_eval_points": ([fp, ctypes.c_int64, fp, fp], c_int),
+        "implisolid_debug_libm": ([c_int, fp, fp, ctypes.c_int64, fp], c_int),
         "implisolid_program_info": ([c_char_p, c_int, ip, fp], c_int),
         "implisolid_slab_create": ([c_char_p, c_char_p, c_int, c_int], c_void_p),
         "implisolid_slab_destroy": ([c_void_p], None),
@@ -418,6 +419,21 @@ class ImplicitService:
             return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy().reshape(-1, 3)
         finally:
             L.unset_x()
+
+
+def debug_libm(which, a, b=None):
+    """Diagnostics: the device restatements of glibc sinf (0) / atanf (1) / atan2f (2: atan2f(a, b))."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    bb = np.ascontiguousarray(b, dtype=np.float32) if b is not None else None
+    if bb is not None and bb.shape != a.shape:
+        raise ValueError("debug_libm: a and b differ in shape")
+    out = np.empty_like(a)
+    fp = ctypes.POINTER(ctypes.c_float)
+    rc = lib().implisolid_debug_libm(int(which), a.ctypes.data_as(fp), bb.ctypes.data_as(fp) if bb is not None else None,
+                                     a.size, out.ctypes.data_as(fp))
+    if rc != 0:
+        raise ImplisolidError(last_error())
+    return out
 
 
 def program_info(shape, ignore_root_matrix=False):

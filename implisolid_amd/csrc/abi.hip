@@ -469,6 +469,34 @@ int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* gra
     return 0;
 }
 
+int implisolid_debug_libm(int which, const float* a, const float* b, int64_t n, float* out) {
+    if (which < 0 || which > 2 || n < 0 || (n && (!a || !out || (which == 2 && !b)))) {
+        report("implisolid_debug_libm: bad arguments", false);
+        return -1;
+    }
+    if (n == 0) return 0;
+    try {
+        Engine& E = engine();
+        hipStream_t s = abi_stream();
+        DevBuf& da = E.scratch(0);
+        DevBuf& db = E.scratch(1);
+        DevBuf& dout = E.scratch(2);
+        da.reserve((size_t)n * 4);
+        if (which == 2) db.reserve((size_t)n * 4);
+        dout.reserve((size_t)n * 4);
+        IMPLI_HIP(hipMemcpyAsync(da.p, a, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        if (which == 2) IMPLI_HIP(hipMemcpyAsync(db.p, b, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        launch_libm_probe(which, da.as<float>(), which == 2 ? db.as<float>() : nullptr, n, dout.as<float>(), s);
+        IMPLI_HIP(hipGetLastError());
+        IMPLI_HIP(hipMemcpyAsync(out, dout.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
 void calculate_implicit_values(void) {
     if (!g_eval.has_x || !g_eval.has_object) {
         report("Error: You need to set_x() and set_object() first.", false);

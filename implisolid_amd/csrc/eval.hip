@@ -556,4 +556,18 @@ void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit,
     else k_eval_points<16><<<blocks, 256, 0, s>>>(d_prog, d_rabbit, d_xyz, n, d_f, d_grad);
 }
 
+// diagnostics: the screw family's restated glibc float functions on n operands (which: 0 sinf(a),
+// 1 atanf(a), 2 atan2f(a, b)) -- the GPU test compares them with the oracle's, pattern by pattern
+__global__ __launch_bounds__(256) void k_libm_probe(int which, const float* __restrict__ a, const float* __restrict__ b,
+                                                     int64_t n, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = which == 0 ? dev::glibc_sinf(a[i]) : which == 1 ? dev::glibc_atanf(a[i]) : dev::glibc_atan2f(a[i], b[i]);
+}
+
+void launch_libm_probe(int which, const float* d_a, const float* d_b, int64_t n, float* d_out, hipStream_t s) {
+    if (n <= 0) return;
+    k_libm_probe<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(which, d_a, d_b, n, d_out);
+}
+
 }  // namespace impli

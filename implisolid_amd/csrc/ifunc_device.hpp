@@ -239,39 +239,37 @@ __device__ __forceinline__ uint32_t inv_pio4(int i) {   // __inv_pio4: 32-bit wi
     return T[i];
 }
 
-// sinf_poly; __sincosf_table[1] (n & 2) is table 0 with the cosine coefficients negated
+// sinf_poly; __sincosf_table[1] (n & 2) is table 0 with the cosine coefficients negated.  The sine
+// (n even) and cosine (n odd) polynomials as one chain of the same operations on selected operands:
+//   sine   x3 = x x2, x7 = x3 x2:  fma(x7, fma(x2, S3, S2), fma(x3, S1, x))
+//   cosine x4 = x2 x2, x6 = x4 x2: fma(x6, fma(x2, C3, C2), fma(x4, C1, fma(x2, C0, 1)))
+// (k = -1 negates every cosine coefficient, an exact sign flip) -- lanes of one wave whose n differ
+// in parity no longer run both polynomials one after the other
 __device__ __forceinline__ float sinf_poly(double x, double x2, int n, bool neg) {
-    if ((n & 1) == 0) {
-        const double x3 = x * x2;
-        const double s1 = __fma_rn(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
-        const double x7 = x3 * x2;
-        const double s = __fma_rn(x3, -0x1.555545995a603p-3, x);
-        return (float)__fma_rn(x7, s1, s);
-    }
+    const bool sn = (n & 1) == 0;
     const double k = neg ? -1.0 : 1.0;
-    const double x4 = x2 * x2;
-    const double c2 = __fma_rn(x2, k * 0x1.99343027bf8c3p-16, k * -0x1.6c087e89a359dp-10);
+    const double u = sn ? x : x2;
+    const double v = u * x2, w = v * x2;                  // x3, x7 | x4, x6
     const double c1 = __fma_rn(x2, k * -0x1.ffffffd0c621cp-2, k * 0x1p0);
-    const double x6 = x4 * x2;
-    const double c = __fma_rn(x4, k * 0x1.55553e1068f19p-5, c1);
-    return (float)__fma_rn(x6, c2, c);
+    const double base = sn ? x : c1;
+    const double mid = __fma_rn(v, sn ? -0x1.555545995a603p-3 : k * 0x1.55553e1068f19p-5, base);
+    const double t = __fma_rn(x2, sn ? -0x1.994eb3774cf24p-13 : k * 0x1.99343027bf8c3p-16,
+                              sn ? 0x1.1107605230bc4p-7 : k * -0x1.6c087e89a359dp-10);
+    return (float)__fma_rn(w, t, mid);
 }
 
 __device__ __forceinline__ float glibc_sinf(float y) {
-    double x = y;
-    int n;
     const uint32_t top = abstop12(y);
-    if (top < 0x3f4u) {                                   // |y| < pi/4
-        if (top < 0x398u) return y;                       // |y| < 2^-12
-        return sinf_poly(x, x * x, 0, false);
-    }
-    double s;
     if (top < 0x42fu) {                                   // |y| < 120: reduce_fast
+        // (|y| < pi/4 is glibc's unreduced branch: here n = 0, the fma returns x and the sign 1,
+        // the same polynomial call; |y| < 2^-12 returns y)
+        double x = y;
         const double r = x * 0x1.45f306dc9c883p+23;
-        n = ((int32_t)r + 0x800000) >> 24;
+        const int n = ((int32_t)r + 0x800000) >> 24;
         x = __fma_rn(-(double)n, 0x1.921fb54442d18p+0, x);
-        s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
-        return sinf_poly(x * s, x * x, n, (n & 2) != 0);
+        const double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+        const float p = sinf_poly(x * s, x * x, n, (n & 2) != 0);
+        return top < 0x398u ? y : p;
     }
     if (top < 0x7f8u) {                                   // reduce_large
         uint32_t xi = __float_as_uint(y);
@@ -287,74 +285,69 @@ __device__ __forceinline__ float glibc_sinf(float y) {
         res0 += res1;
         const uint64_t nn = (res0 + (1ull << 61)) >> 62;
         res0 -= nn << 62;
-        n = (int)nn;
-        x = (double)(int64_t)res0 * 0x1.921fb54442d18p-62;
+        const int n = (int)nn;
+        const double x = (double)(int64_t)res0 * 0x1.921fb54442d18p-62;
         const int q = (n + sign) & 3;
-        s = (q == 1 || q == 2) ? -1.0 : 1.0;
+        const double s = (q == 1 || q == 2) ? -1.0 : 1.0;
         return sinf_poly(x * s, x * x, n, (q & 2) != 0);
     }
     return (y - y) / (y - y);
 }
 
+// fdlibm's four argument reductions select their operands into one division: each lane divides
+// exactly the numerator and denominator of its own branch (a wave whose lanes span several ranges
+// ran up to four IEEE division sequences)
 __device__ __forceinline__ float glibc_atanf(float x) {
-    const float hi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
-    const float lo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const float hi0 = 4.6364760399e-01f, hi1 = 7.8539812565e-01f, hi2 = 9.8279368877e-01f, hi3 = 1.5707962513e+00f;
+    const float lo0 = 5.0121582440e-09f, lo1 = 3.7748947079e-08f, lo2 = 3.4473217170e-08f, lo3 = 7.5497894159e-08f;
     const int32_t hx = (int32_t)__float_as_uint(x), ix = hx & 0x7fffffff;
-    int id;
-    if (ix >= 0x4c000000) {
-        if (ix > 0x7f800000) return x + x;
-        return hx > 0 ? hi[3] + lo[3] : -hi[3] - lo[3];
-    }
-    if (ix < 0x3ee00000) {
-        if (ix < 0x31000000) return x;
-        id = -1;
-    } else {
-        x = fabsf(x);
-        if (ix < 0x3f980000) {
-            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
-            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
-        } else {
-            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
-            else { id = 3; x = -1.0f / x; }
-        }
-    }
-    const float z = x * x, w = z * z;
+    const float a = fabsf(x);
+    const bool small = ix < 0x3ee00000;                   // id = -1: no reduction
+    const int id = ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
+    const float num = id == 0 ? 2.0f * a - 1.0f : id == 1 ? a - 1.0f : id == 2 ? a - 1.5f : -1.0f;
+    const float den = id == 0 ? 2.0f + a : id == 1 ? a + 1.0f : id == 2 ? 1.0f + 1.5f * a : a;
+    const float q = num / den;
+    const float t = small ? x : q;
+    const float z = t * t, w = z * z;
     const float s1 = z * (3.3333334327e-01f + w * (1.4285714924e-01f + w * (9.0908870101e-02f +
                      w * (6.6610731184e-02f + w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
     const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
                      w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
-    if (id < 0) return x - x * (s1 + s2);
-    const float h = id == 0 ? hi[0] : id == 1 ? hi[1] : id == 2 ? hi[2] : hi[3];
-    const float l = id == 0 ? lo[0] : id == 1 ? lo[1] : id == 2 ? lo[2] : lo[3];
-    const float r = h - ((x * (s1 + s2) - l) - x);
-    return hx < 0 ? -r : r;
+    const float h = id == 0 ? hi0 : id == 1 ? hi1 : id == 2 ? hi2 : hi3;
+    const float l = id == 0 ? lo0 : id == 1 ? lo1 : id == 2 ? lo2 : lo3;
+    const float r = h - ((t * (s1 + s2) - l) - t);
+    float res = small ? t - t * (s1 + s2) : (hx < 0 ? -r : r);
+    if (ix < 0x31000000) res = x;
+    if (ix >= 0x4c000000) res = ix > 0x7f800000 ? x + x : (hx > 0 ? hi3 + lo3 : -hi3 - lo3);
+    return res;
 }
 
+// e_atan2f.c; x == 1 (atanf(y)) shares the one atanf with the general path (atanf(|y / x|))
 __device__ __forceinline__ float glibc_atan2f(float y, float x) {
     const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
                 pi_lo = -8.7422776573e-08f;
     const int32_t hx = (int32_t)__float_as_uint(x), ix = hx & 0x7fffffff;
     const int32_t hy = (int32_t)__float_as_uint(y), iy = hy & 0x7fffffff;
-    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
-    if (hx == 0x3f800000) return glibc_atanf(y);
+    const bool one = hx == 0x3f800000;
     const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
-    if (iy == 0) return m <= 1 ? y : (m == 2 ? pi + tiny : -pi - tiny);
-    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    const float za = glibc_atanf(one ? y : fabsf(y / x));
+    float z = k > 60 ? pi_o_2 + 0.5f * pi_lo : (hx < 0 && k < -60) ? 0.0f : za;
+    float res = m == 0 ? z : m == 1 ? __uint_as_float(__float_as_uint(z) ^ 0x80000000u)
+                       : m == 2 ? pi - (z - pi_lo) : (z - pi_lo) - pi;
+    // the special operands, in e_atan2f.c's order
+    if (iy == 0x7f800000) res = hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
     if (ix == 0x7f800000) {
         if (iy == 0x7f800000)
-            return m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny : m == 2 ? 3.0f * pi_o_4 + tiny : -3.0f * pi_o_4 - tiny;
-        return m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi + tiny : -pi - tiny;
+            res = m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny : m == 2 ? 3.0f * pi_o_4 + tiny : -3.0f * pi_o_4 - tiny;
+        else
+            res = m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi + tiny : -pi - tiny;
     }
-    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
-    const int32_t k = (iy - ix) >> 23;
-    float z;
-    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
-    else if (hx < 0 && k < -60) z = 0.0f;
-    else z = glibc_atanf(fabsf(y / x));
-    if (m == 0) return z;
-    if (m == 1) return __uint_as_float(__float_as_uint(z) ^ 0x80000000u);
-    if (m == 2) return pi - (z - pi_lo);
-    return (z - pi_lo) - pi;
+    if (ix == 0) res = hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (iy == 0) res = m <= 1 ? y : (m == 2 ? pi + tiny : -pi - tiny);
+    if (one) res = za;
+    if (ix > 0x7f800000 || iy > 0x7f800000) res = x + y;
+    return res;
 }
 
 // ---- screw, screw.hpp:98-150 at its constructor's constants (u, v, w = the axes, A = (0,0,-0.5),

@@ -579,6 +579,13 @@ void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
     wait_idle();
 }
 
+// diagnostics: IMPLISOLID_EVAL_WAVES=n asks the compiler for n waves per SIMD in the eval kernel
+static std::string eval_waves_attr() {
+    const char* e = std::getenv("IMPLISOLID_EVAL_WAVES");
+    if (!e || !*e) return "";
+    return " __attribute__((amdgpu_waves_per_eu(" + std::to_string(std::atoi(e)) + ")))";
+}
+
 std::string TreeJit::kernel_source(const Program& p, bool bake) {
     std::vector<Node> nodes;
     int next = 0;
@@ -606,7 +613,7 @@ std::string TreeJit::kernel_source(const Program& p, bool bake) {
       << "    __device__ __forceinline__ Iv operator()(Box p, uint64_t mi, uint64_t& m) const {\n"
       << "        return tree_iv(M, tab, tab_range, p, mi, m);\n    }\n};\n"
       << "}  // namespace impli\n"
-      << "extern \"C\" __global__ __launch_bounds__(" << kEvalBlock << ") void impli_eval_bricks(\n"
+      << "extern \"C\" __global__ __launch_bounds__(" << kEvalBlock << ")" << eval_waves_attr() << " void impli_eval_bricks(\n"
       << "    const float* M, const float* tab, impli::GridDesc g, impli::BrickGrid bg, const uint64_t* modes,\n"
       << "    const uint32_t* list, const uint32_t* count, float* field, void* signs, impli::ClaimCtx cc) {\n"
       << "    impli::eval_bricks_body(impli::JitEval{M, tab}, g, bg, cc, modes, list, count, field, signs);\n}\n"

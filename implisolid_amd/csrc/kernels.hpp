@@ -44,6 +44,8 @@ void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_
 void launch_signs_from_field(const GridDesc& g, const float* d_field, uint64_t* d_signs, hipStream_t s);
 void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit, const float* d_xyz, int64_t n,
                         float* d_f, float* d_grad /* nullable: values only */, hipStream_t s);
+// diagnostics: glibc sinf (0) / atanf (1) / atan2f (2) restatements on device operands
+void launch_libm_probe(int which, const float* d_a, const float* d_b, int64_t n, float* d_out, hipStream_t s);
 
 // K2 (count per group) and K2b (group bases + flat list of non-empty units)
 void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);

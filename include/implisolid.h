@@ -140,6 +140,10 @@ void implisolid_ob02_profile(int on);
 int implisolid_last_build_stats(double out[13]);
 /* evaluate n >= 0 points (no 50k limit) of the current set_object(); grad may be NULL */
 int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* grad_out);
+/* Additive, diagnostics: the device restatements of glibc 2.35 sinf (which 0: out = sinf(a)),
+   atanf (1) and atan2f (2: out = atan2f(a, b)) that the screw family calls (screw.hpp:20-36,
+   std::sin / std::atan2 on floats), on n host operands; 0 or -1 with implisolid_last_error() */
+int implisolid_debug_libm(int which, const float* a, const float* b, int64_t n, float* out);
 
 /* host-only: compile an MP5 tree to the node program; info = {n_instr, depth, n_mats, 0};
    mats_out receives n_mats inverse matrices (12 floats each, up to 256) */

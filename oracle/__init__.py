@@ -85,6 +85,8 @@ def lib():
         L.or_atan2f.restype = ctypes.c_float
         L.or_libm_check.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         L.or_libm_check.restype = ctypes.c_int64
+        L.or_libm_apply.argtypes = [ctypes.c_int, fp, fp, ctypes.c_int64, fp]
+        L.or_libm_apply.restype = None
         L.or_marching_cubes.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, ctypes.POINTER(OrMesh)]
         L.or_mesh_free.argtypes = [ctypes.POINTER(OrMesh)]
         L.or_mc_field.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, fp]
@@ -439,6 +441,16 @@ def libm_check(which, start, stride, count):
     """Mismatches of the restated glibc sinf (0) / atanf (1) over bit patterns start + k*stride,
     or atan2f (2) over `count` seeded random pairs, against this host's libm."""
     return int(lib().or_libm_check(int(which), int(start), int(stride), int(count)))
+
+
+def libm_apply(which, a, b=None):
+    """The restated glibc sinf (0) / atanf (1) / atan2f (2: atan2f(a, b)) on float32 arrays."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(a if b is None else b, dtype=np.float32)
+    out = np.empty_like(a)
+    fpp = ctypes.POINTER(ctypes.c_float)
+    lib().or_libm_apply(int(which), a.ctypes.data_as(fpp), b.ctypes.data_as(fpp), a.size, out.ctypes.data_as(fpp))
+    return out
 
 
 def srand(seed):

@@ -203,3 +203,10 @@ int64_t or_libm_check(int which, uint32_t start, uint32_t stride, uint64_t count
     }
     return bad;
 }
+
+/* the restated functions on arrays (which as above; b only for atan2f): the GPU test's checker
+   for the device restatement (implisolid_debug_libm) */
+void or_libm_apply(int which, const float* a, const float* b, int64_t n, float* out) {
+    for (int64_t i = 0; i < n; i++)
+        out[i] = which == 0 ? or_sinf(a[i]) : which == 1 ? or_atanf(a[i]) : or_atan2f(a[i], b[i]);
+}

@@ -89,6 +89,48 @@ def test_eval_points_bit_exact(impli, oracle, name):
         assert np.array_equal(g.view(np.uint32), g_ref.view(np.uint32)), np.flatnonzero((g != g_ref).any(1))[:10]
 
 
+def _same_bits(a, b):
+    return (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+
+
+def _pattern_windows(centres, half=20000):
+    return np.concatenate([np.arange(c - half, c + half, dtype=np.int64) for c in centres]).astype(np.uint32)
+
+
+def test_device_libm_bit_exact(impli, oracle):
+    """The screw family's glibc sinf / atanf / atan2f restatements on the device (branch-free
+    selections, one division) against the oracle's (pinned to the host glibc by test_cpu), over a
+    stride through every float pattern, dense windows around every range boundary, both signs,
+    and seeded atan2f pairs including x == 1, zeros, infinities and NaN."""
+    stride = np.arange(0, 1 << 32, 257, dtype=np.uint64).astype(np.uint32)
+    sin_b = [0x39800000, 0x3f490fdb, 0x42f00000, 0x7f800000]                      # 2^-12, pi/4, 120, inf
+    atan_b = [0x31000000, 0x3ee00000, 0x3f300000, 0x3f980000, 0x401c0000, 0x4c000000, 0x7f800000]
+    for which, bounds in ((0, sin_b), (1, atan_b)):
+        w = _pattern_windows(bounds)
+        pats = np.concatenate([stride, w, w | np.uint32(0x80000000)])
+        a = pats.view(np.float32)
+        got, ref = impli.debug_libm(which, a), oracle.libm_apply(which, a)
+        bad = ~_same_bits(got, ref)
+        assert not bad.any(), (which, pats[bad][:8], got[bad][:4], ref[bad][:4])
+    rng = np.random.default_rng(99)
+    n = 1 << 21
+    ys = [rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32),
+          rng.uniform(-4, 4, n).astype(np.float32), (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-40, 40, n)).astype(np.float32)]
+    xs = [rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32),
+          rng.uniform(-4, 4, n).astype(np.float32), (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-40, 40, n)).astype(np.float32)]
+    # |y / x| near atanf's boundaries, x == 1 (atanf(y) path), and the special operands
+    t = np.array([0x3ee00000, 0x3f300000, 0x3f980000, 0x401c0000], np.uint32).view(np.float32)
+    xr = rng.uniform(0.5, 2, n).astype(np.float32)
+    yr = (xr * rng.choice(t, n) * (1 + rng.uniform(-1e-6, 1e-6, n))).astype(np.float32) * rng.choice([-1, 1], n).astype(np.float32)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 1e-30, -1e-30, 1e30, -1e30, 2.0], np.float32)
+    gy, gx = np.meshgrid(sp, sp)
+    Y = np.concatenate(ys + [yr, yr, ys[2], gy.ravel()]).astype(np.float32)
+    X = np.concatenate(xs + [xr, -xr, np.ones(n, np.float32), gx.ravel()]).astype(np.float32)
+    got, ref = impli.debug_libm(2, Y, X), oracle.libm_apply(2, Y, X)
+    bad = ~_same_bits(got, ref)
+    assert not bad.any(), (Y[bad][:4], X[bad][:4], got[bad][:4], ref[bad][:4])
+
+
 def _has_twist(shape):
     return "screw" in json.dumps(shape)
 
