@@ -566,7 +566,9 @@ static int64_t jit_compile_kind(const char* shape_json, int kind, char* source_o
     g_last_error.clear();
     try {
         const Program p = compile_mp5(shape_json, false);
-        const std::string src = kind == TreeJit::kPoints ? TreeJit::point_source(p) : TreeJit::kernel_source(p);
+        // (bake mode 1, "always": the value-baked source of this object)
+        const std::string src = kind == TreeJit::kPoints ? TreeJit::point_source(p)
+                                                         : TreeJit::kernel_source(p, TreeJit::instance().bake() == TreeJit::kBakeAlways);
         if (source_out && capacity > 0) {
             const size_t n = std::min<size_t>(src.size(), (size_t)capacity - 1);
             std::memcpy(source_out, src.data(), n);

@@ -48,6 +48,20 @@ __device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, in
 // samples).  Sign-filled bricks never reach this kernel -- k_brick_fill wrote their constant sign
 // bits -- except claimed candidates (grid.hpp ClaimCtx), evaluated by the wave of the mixed brick
 // that claimed them, values only (their sign pieces are constant and already written).
+// both layers of a column: the evaluator's pair() when it has one (the JIT tree: one pass of the
+// tree code for both samples), else two calls
+template <class Eval>
+__device__ __forceinline__ auto eval_pair(const Eval& ev, uint64_t m, float x, float y, float z0, float z1, float& f0,
+                                          float& f1, int) -> decltype(ev.pair(m, x, y, z0, z1, f0, f1), void()) {
+    ev.pair(m, x, y, z0, z1, f0, f1);
+}
+template <class Eval>
+__device__ __forceinline__ void eval_pair(const Eval& ev, uint64_t m, float x, float y, float z0, float z1, float& f0,
+                                          float& f1, long) {
+    f0 = ev(m, x, y, z0);
+    f1 = ev(m, x, y, z1);
+}
+
 // one brick (b, its modes m) by the calling wave; neg[k]: layer k's sign bits, valid: the lanes
 // inside the grid
 template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
@@ -77,8 +91,8 @@ __device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g
         // chains per lane (a layer past the slab is evaluated at a clamped z and not stored)
         static_assert(!Pair || kBZ == 2, "the layer pair needs two layers per brick");
         const int l0 = bz * kBZ, l1 = l0 + 1;
-        const float f0 = ev(m, x, y, sample_z(g, l0));
-        const float f1 = ev(m, x, y, sample_z(g, l1 < layers ? l1 : l0));
+        float f0, f1;
+        eval_pair(ev, m, x, y, sample_z(g, l0), sample_z(g, l1 < layers ? l1 : l0), f0, f1, 0);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int layer = l0 + k;

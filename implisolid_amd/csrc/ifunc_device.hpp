@@ -207,14 +207,14 @@ __device__ __forceinline__ double div_sq_const(double a, double D, double R) {
 __device__ __forceinline__ float dm_f(float x, float y, float z) {
     const float r = 0.9f / 2, a = (float)(0.4 / 2), c = 1.f / (float)(1 / 0.2);
     const float a2 = a * a, b2 = a * a, c2 = c * c;
-    if (z > r) return r - z;
-    if (z < -r) return r + z;
     // a2 == b2 == c2 (object_factory.hpp:86-100): one constant, one reciprocal
     const double D = (double)a2, R = 1.0 / (double)a2;
     static_assert(0.2f * 0.2f == (float)(0.4 / 2) * (float)(0.4 / 2), "the checked constant");
+    // the body is computed for every sample and the caps selected after (no branch): the x and y
+    // terms of a brick's two layers are then one computation (JIT pair code)
     const double v = div_sq_const(sq_exact(x - 0.f), D, R) + div_sq_const(sq_exact(y - 0.f), (double)b2, R) -
                      div_sq_const(sq_exact(z - 0.f), (double)c2, R) - 1;
-    return (float)(-v);
+    return z > r ? r - z : z < -r ? r + z : (float)(-v);
 }
 __device__ __forceinline__ V3 dm_g(float x, float y, float z) {
     const float r = 0.9f / 2, a = (float)(0.4 / 2), c = 1.f / (float)(1 / 0.2);
@@ -368,6 +368,33 @@ __device__ __forceinline__ float screw_f(const float* __restrict__ prm, float x,
     const float ph = t / tw - theta / pi2;
     return (-r + r0) + delta * glibc_sinf(ph * 2 * pi);       // phi (screw.hpp:29-36)
 }
+// screw_f at two points (a brick's two layers): the same operations per point, one atan2f when
+// both points' (ab1, ab0) agree bit for bit (the screw axis is z: they do whenever the transforms
+// above keep x and y independent of z)
+__device__ __forceinline__ void screw_f2(const float* __restrict__ prm, float xa, float ya, float za, float xb, float yb,
+                                         float zb, float& fa, float& fb) {
+    const float tw = prm[0], r0 = prm[1], delta = prm[2];
+    const float pi = (float)3.1415926535897, pi2 = pi * 2;
+    float t[2], ab0[2], ab1[2], r[2];
+    const float X[2] = {xa, xb}, Y[2] = {ya, yb}, Z[2] = {za, zb};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float a0 = X[k] - 0.f, a1 = Y[k] - 0.f, a2 = Z[k] - (-0.5f);
+        t[k] = ((0.f + a0 * 0.f) + a1 * 0.f) + a2 * 1.f;
+        const float p0 = 0.f * t[k] + 0.f, p1 = 0.f * t[k] + 0.f, p2 = 1.f * t[k] + (-0.5f);
+        const float d0 = X[k] - p0, d1 = Y[k] - p1, d2 = Z[k] - p2;
+        ab0[k] = 0.f + (((0.f + 1.f * d0) + 0.f * d1) + 0.f * d2);
+        ab1[k] = 0.f + (((0.f + 0.f * d0) + 1.f * d1) + 0.f * d2);
+        r[k] = sqrtf(d0 * d0 + (d1 * d1 + d2 * d2));
+    }
+    const float th0 = glibc_atan2f(ab1[0], ab0[0]);
+    float th1 = th0;
+    if (__float_as_uint(ab0[1]) != __float_as_uint(ab0[0]) || __float_as_uint(ab1[1]) != __float_as_uint(ab1[0]))
+        th1 = glibc_atan2f(ab1[1], ab0[1]);
+    const float ph0 = t[0] / tw - th0 / pi2, ph1 = t[1] / tw - th1 / pi2;
+    fa = (-r[0] + r0) + delta * glibc_sinf(ph0 * 2 * pi);
+    fb = (-r[1] + r0) + delta * glibc_sinf(ph1 * 2 * pi);
+}
 // screw.hpp:152-160 (sympy gradient) at the same constants, with the C++ type of every
 // sub-expression: std::pow(float, 2) -> exact double square, atan2(float, float) -> atanf path,
 // cos(double) -> double cos (device libm; the only call not restated bit for bit), M_PI double.
@@ -413,6 +440,13 @@ __device__ __forceinline__ float lid_f(float z) {
 //      imp.min(tbb * -1) = std::min(screw, -lid); prm = {twist, r0, delta} | (next row) M^-1
 __device__ __forceinline__ float tbb_f(const float* __restrict__ prm, float x, float y, float z) {
     return stdmin(screw_f(prm, x, y, z), lid_f(z) * -1.f);
+}
+__device__ __forceinline__ void tbb_f2(const float* __restrict__ prm, float xa, float ya, float za, float xb, float yb,
+                                       float zb, float& fa, float& fb) {
+    float sa, sb;
+    screw_f2(prm, xa, ya, za, xb, yb, zb, sa, sb);
+    fa = stdmin(sa, lid_f(za) * -1.f);
+    fb = stdmin(sb, lid_f(zb) * -1.f);
 }
 // :142-166: the screw's gradient with its own M^-T (screw.hpp:476-486), replaced by (0, 0, -1)
 // where z' >= 0.5 and (0, 0, 1) where z' <= -0.5, whichever operand the min chose; the node's

@@ -25,6 +25,8 @@ namespace impli {
 
 #define IMPLI_HIP_THROW(x) do { if ((x) != hipSuccess) throw std::runtime_error(#x " failed"); } while (0)
 
+static const char* const kEvalWavesAttr = " __attribute__((amdgpu_waves_per_eu(8)))";
+
 namespace {
 
 // types and macros hipRTC does not provide (the headers skip their system includes under it)
@@ -208,6 +210,81 @@ struct Emitter {
             << " : " << right << ";\n";
         out << pad << "}\n";
         return f;
+    }
+};
+
+// The point tree at two samples of one column (a brick's two layers, same x and y) under the same
+// modes: each node's code for both samples in the same wave-uniform branches, so the two
+// dependency chains interleave and the compiler shares whatever does not depend on z (the screw
+// shares its atan2f through screw_f2 / tbb_f2).  Per sample, exactly the operations of emit().
+struct PairEmitter {
+    const std::vector<Node>& nodes;
+    const Program& prog;
+    bool bake;
+    std::ostringstream out;
+    int counter = 0;
+
+    // returns the variables holding f at sample a and at sample b
+    std::pair<std::string, std::string> emit(int i, const std::string& xa, const std::string& ya, const std::string& za,
+                                             const std::string& xb, const std::string& yb, const std::string& zb, int ind) {
+        const Node& n = nodes[i];
+        const int id = counter++;
+        const std::string pad(ind, ' ');
+        const std::string q = "q" + std::to_string(id), f = "f" + std::to_string(id);
+        const std::string qb = q + "b", fb = f + "b";
+        const float* mm = prog.mats[n.mat];
+        for (int s = 0; s < 2; ++s) {
+            const std::string& x = s ? xb : xa;
+            const std::string& y = s ? yb : ya;
+            const std::string& z = s ? zb : za;
+            out << pad << "const V3 " << (s ? qb : q) << " = V3{" << xform_row(mm, 12 * n.mat, x, y, z, bake) << ",\n"
+                << pad << "    " << xform_row(mm + 4, 12 * n.mat + 4, x, y, z, bake) << ",\n" << pad << "    "
+                << xform_row(mm + 8, 12 * n.mat + 8, x, y, z, bake) << "};\n";
+        }
+        if (n.leaf) {
+            if (n.type == NT_SCREW || n.type == NT_SCREW_TBB) {
+                out << pad << "float " << f << ", " << fb << ";\n" << pad
+                    << with_params(n.type == NT_SCREW ? "screw_f2(P, " : "tbb_f2(P, ", n.prm) << q << ".x, " << q << ".y, "
+                    << q << ".z, " << qb << ".x, " << qb << ".y, " << qb << ".z, " << f << ", " << fb << ");\n";
+                return {f, fb};
+            }
+            for (int s = 0; s < 2; ++s) {
+                const std::string& v = s ? qb : q;
+                std::string call = n.type == NT_LID         ? "lid_f(" + v + ".z)"
+                                   : n.type == NT_EXTRUSION ? with_params("extr_f(P, ", n.prm) + v + ".x, " + v + ".y)"
+                                                            : with_params(prim_call(n.type), n.prm) + v + ".x, " + v + ".y, " + v + ".z)";
+                out << pad << "const float " << (s ? fb : f) << " = " << call << ";\n";
+            }
+            return {f, fb};
+        }
+        const std::string m = "m" + std::to_string(id), a = "a" + std::to_string(id), b = "b" + std::to_string(id);
+        const std::string ab = a + "b", bb = b + "b";
+        out << pad << "float " << f << ", " << fb << ";\n" << pad << "{\n";
+        out << pad << "  const uint32_t " << m << " = mode_of(modes, " << n.csg << ");\n";
+        out << pad << "  float " << a << " = 0.f, " << b << " = 0.f, " << ab << " = 0.f, " << bb << " = 0.f;\n";
+        out << pad << "  if (" << m << " != PM_RIGHT) {\n";
+        const auto fa = emit(n.child[0], q + ".x", q + ".y", q + ".z", qb + ".x", qb + ".y", qb + ".z", ind + 4);
+        out << pad << "    " << a << " = " << fa.first << ";\n" << pad << "    " << ab << " = " << fa.second << ";\n"
+            << pad << "  }\n";
+        out << pad << "  if (" << m << " != PM_LEFT) {\n";
+        const auto fr = emit(n.child[1], q + ".x", q + ".y", q + ".z", qb + ".x", qb + ".y", qb + ".z", ind + 4);
+        out << pad << "    " << b << " = " << fr.first << ";\n" << pad << "    " << bb << " = " << fr.second << ";\n"
+            << pad << "  }\n";
+        for (int s = 0; s < 2; ++s) {
+            const std::string& A = s ? ab : a;
+            const std::string& B = s ? bb : b;
+            std::string sel, right = B;
+            if (n.type == NT_UNION) sel = "(" + A + " > " + B + ") ? " + A + " : " + B;
+            else if (n.type == NT_INTERSECTION) sel = "(" + A + " > " + B + ") ? " + B + " : " + A;
+            else {
+                sel = "(" + A + " < -" + B + ") ? " + A + " : -" + B;
+                right = "-" + B;
+            }
+            out << pad << "  " << (s ? fb : f) << " = (" << m << " == PM_BOTH) ? (" << sel << ") : (" << m
+                << " == PM_LEFT) ? " << A << " : " << right << ";\n";
+        }
+        out << pad << "}\n";
+        return {f, fb};
     }
 };
 
@@ -439,18 +516,37 @@ void TreeJit::build(Slot* slot) {
         if (prev != slot->device) IMPLI_HIP_THROW(hipSetDevice(slot->device));
         Kernels k;
         PointKernels pk;
-        bool ok = hipModuleLoadData(&slot->mod, code.data()) == hipSuccess;
-        if (ok && slot->kind == kBricks)
-            ok = hipModuleGetFunction(&k.bricks, slot->mod, "impli_eval_bricks") == hipSuccess &&
-                 hipModuleGetFunction(&k.coarse, slot->mod, "impli_coarse_modes") == hipSuccess &&
-                 hipModuleGetFunction(&k.refine, slot->mod, "impli_brick_refine") == hipSuccess;
-        if (ok && slot->kind == kPoints)
-            ok = hipModuleGetFunction(&pk.cnormals, slot->mod, "impli_pt_centroid_normals") == hipSuccess &&
-                 hipModuleGetFunction(&pk.prep, slot->mod, "impli_pt_project_prep") == hipSuccess &&
-                 hipModuleGetFunction(&pk.early, slot->mod, "impli_pt_project_early") == hipSuccess &&
-                 hipModuleGetFunction(&pk.late, slot->mod, "impli_pt_project_late") == hipSuccess &&
-                 hipModuleGetFunction(&pk.normals, slot->mod, "impli_pt_normals_at") == hipSuccess &&
-                 hipModuleGetFunction(&pk.points, slot->mod, "impli_pt_points") == hipSuccess;
+        auto load = [&](const std::vector<char>& co) {
+            bool ok = hipModuleLoadData(&slot->mod, co.data()) == hipSuccess;
+            if (ok && slot->kind == kBricks)
+                ok = hipModuleGetFunction(&k.bricks, slot->mod, "impli_eval_bricks") == hipSuccess &&
+                     hipModuleGetFunction(&k.coarse, slot->mod, "impli_coarse_modes") == hipSuccess &&
+                     hipModuleGetFunction(&k.refine, slot->mod, "impli_brick_refine") == hipSuccess;
+            if (ok && slot->kind == kPoints)
+                ok = hipModuleGetFunction(&pk.cnormals, slot->mod, "impli_pt_centroid_normals") == hipSuccess &&
+                     hipModuleGetFunction(&pk.prep, slot->mod, "impli_pt_project_prep") == hipSuccess &&
+                     hipModuleGetFunction(&pk.early, slot->mod, "impli_pt_project_early") == hipSuccess &&
+                     hipModuleGetFunction(&pk.late, slot->mod, "impli_pt_project_late") == hipSuccess &&
+                     hipModuleGetFunction(&pk.normals, slot->mod, "impli_pt_normals_at") == hipSuccess &&
+                     hipModuleGetFunction(&pk.points, slot->mod, "impli_pt_points") == hipSuccess;
+            return ok;
+        };
+        bool ok = load(code);
+        // the eval kernel asks for eight waves per SIMD; a tree whose code then spills to scratch is
+        // compiled again without the request (stored under the same source key: deterministic)
+        const size_t at = slot->src.find(" __attribute__((amdgpu_waves_per_eu(");
+        const size_t at_end = at == std::string::npos ? at : slot->src.find(")))", at);
+        int scratch = 0;
+        if (ok && slot->kind == kBricks && at_end != std::string::npos &&
+            hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, k.bricks) == hipSuccess && scratch > 0) {
+            (void)hipModuleUnload(slot->mod);
+            slot->mod = nullptr;
+            std::string plain = slot->src;
+            plain.erase(at, at_end + 3 - at);
+            code = compile(plain);
+            if (!disk_dir_.empty()) write_file_atomic(disk_dir_, name, code);
+            ok = load(code);
+        }
         if (prev != slot->device) (void)hipSetDevice(prev);
         if (!ok) throw std::runtime_error("hipModuleLoadData / hipModuleGetFunction failed");
         slot->k = k;
@@ -579,11 +675,15 @@ void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
     wait_idle();
 }
 
-// diagnostics: IMPLISOLID_EVAL_WAVES=n asks the compiler for n waves per SIMD in the eval kernel
+// The eval kernel's occupancy request: eight waves per SIMD (64 VGPRs).  The config-4 tree's pair
+// code needs 79 without it (six waves) and runs 1 us faster with it (22.6 -> 21.6 us, no scratch:
+// the compiler rematerialises and keeps more in SGPR lanes); build() drops the request for a tree
+// that would spill to scratch.  IMPLISOLID_EVAL_WAVES=n (diagnostics) asks for n, 0 for none.
 static std::string eval_waves_attr() {
     const char* e = std::getenv("IMPLISOLID_EVAL_WAVES");
-    if (!e || !*e) return "";
-    return " __attribute__((amdgpu_waves_per_eu(" + std::to_string(std::atoi(e)) + ")))";
+    if (!e || !*e) return kEvalWavesAttr;
+    const int n = std::atoi(e);
+    return n > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(n) + ")))" : "";
 }
 
 std::string TreeJit::kernel_source(const Program& p, bool bake) {
@@ -595,6 +695,8 @@ std::string TreeJit::kernel_source(const Program& p, bool bake) {
     const std::string f = em.emit(root, "x0", "y0", "z0", 4);
     IvEmitter iv{nodes, p, bake};
     const std::string r = iv.emit(root, "p0", 4);
+    PairEmitter pe{nodes, p, bake};
+    const auto f2 = pe.emit(root, "x0", "y0", "z0", "x0", "y0", "z1", 4);
     std::ostringstream s;
     if (const char* e = std::getenv("IMPLISOLID_EVAL_PAIR")) s << "#define IMPLI_EVAL_PAIR " << (e[0] == '1' ? 1 : 0) << "\n";
     s << kPrelude << "#include \"eval_bricks.hpp\"\n#include \"ifunc_interval.hpp\"\n#include \"brick_modes.hpp\"\n"
@@ -602,9 +704,16 @@ std::string TreeJit::kernel_source(const Program& p, bool bake) {
       << "__device__ __forceinline__ float tree_f(const float* __restrict__ M, const float* __restrict__ tab,\n"
       << "                                        uint64_t modes, float x0, float y0, float z0) {\n"
       << em.out.str() << "    return " << f << ";\n}\n"
+      << "__device__ __forceinline__ void tree_f2(const float* __restrict__ M, const float* __restrict__ tab,\n"
+      << "                                        uint64_t modes, float x0, float y0, float z0, float z1,\n"
+      << "                                        float& out0, float& out1) {\n"
+      << pe.out.str() << "    out0 = " << f2.first << ";\n    out1 = " << f2.second << ";\n}\n"
       << "struct JitEval {\n    const float* M;\n    const float* tab;\n"
       << "    __device__ __forceinline__ float operator()(uint64_t m, float x, float y, float z) const {\n"
-      << "        return tree_f(M, tab, m, x, y, z);\n    }\n};\n"
+      << "        return tree_f(M, tab, m, x, y, z);\n    }\n"
+      << "    __device__ __forceinline__ void pair(uint64_t m, float x, float y, float z0, float z1, float& f0,\n"
+      << "                                         float& f1) const {\n"
+      << "        tree_f2(M, tab, m, x, y, z0, z1, f0, f1);\n    }\n};\n"
       << "__device__ __forceinline__ Iv tree_iv(const float* __restrict__ M, const float* __restrict__ tab,\n"
       << "                                      float2 tab_range, Box p0, uint64_t modes_in, uint64_t& modes) {\n"
       << "    modes = modes_in;\n"
