@@ -566,6 +566,24 @@ def test_jit_tree_kernels_compile_for_gfx950(impli):
         n, secs, src = impli.jit_compile(shape)
         assert n > 1000 and "impli_eval_bricks" in src, src[:500]
         assert "impli_coarse_modes" in src and "impli_brick_refine" in src
+        # the brick pair's tree code (both layers in one pass) and the eval kernel's occupancy request
+        assert "tree_f2(M, tab, m, x, y, z0, z1, f0, f1)" in src
+        assert "__launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void impli_eval_bricks" in src
+
+
+def test_jit_pair_code_shares_the_screw_atan2f(impli):
+    """Host-only: a twist leaf's pair code calls screw_f2 (one atan2f for both layers when their
+    (ab1, ab0) agree); the baked source of an object holds the same calls with literal matrices."""
+    from implisolid_amd import scenes
+    shape = scenes.twist(1, 0, 0, 0)
+    _, _, src = impli.jit_compile(shape)
+    assert "screw_f2(M + " in src
+    impli.set_jit_bake(1)
+    try:
+        _, _, baked = impli.jit_compile(scenes.config3()[0])
+    finally:
+        impli.set_jit_bake(2)
+    assert "screw_f2(M + " in baked and "__builtin_bit_cast(float, 0x" in baked
 
 
 def test_headline_summary_oracle_regression(oracle):
