@@ -111,11 +111,14 @@ __device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
 // placed from the owner cell's fx/fy/fz (the reference's first emission), their ids go to vid3
 // (halo cells, below the slab's first emitted layer: ids only), active cells get a record
 // {L, ci, face base}.  (A separate one-lane-per-active-cell position pass measured 2 us slower.)
-__device__ __forceinline__ unsigned long long pack4(unsigned a, unsigned b, unsigned c, unsigned d) {
-    return (unsigned long long)a | ((unsigned long long)b << 16) | ((unsigned long long)c << 32) |
-           ((unsigned long long)d << 48);
+// a window's (owned edges <= 3, triangles <= 5, active <= 1) per cell, packed for one 32-bit scan:
+// over 64 cells the sums stay below 2^8 (192), 2^10 (320) and 2^7 (64)
+constexpr int kPackShift[3] = {0, 8, 18};
+constexpr unsigned kPackMask[3] = {0xffu, 0x3ffu, 0x7fu};
+__device__ __forceinline__ unsigned pack3(unsigned own, unsigned tri, unsigned act) {
+    return own | (tri << 8) | (act << 18);
 }
-__device__ __forceinline__ unsigned fld(unsigned long long p, int i) { return (unsigned)(p >> (16 * i)) & 0xffffu; }
+__device__ __forceinline__ unsigned fld(unsigned p, int i) { return (p >> kPackShift[i]) & kPackMask[i]; }
 
 // position of the r-th set bit of x (r < popcount(x))
 __device__ __forceinline__ int select_bit(uint64_t x, uint32_t r) {
@@ -203,9 +206,9 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
                 const unsigned c_nown = cw & 3u, c_ntri = (cw >> 2) & 7u;
                 const bool emit = has && z >= g.cz_emit;
                 const unsigned own = has ? c_nown : 0u, tri = emit ? c_ntri : 0u, act = (emit && c_ntri) ? 1u : 0u;
-                const unsigned long long p = pack4(own, tri, act, 0u);
-                const unsigned long long inc = wave_incl_scan<unsigned long long>(p, lane);
-                const unsigned long long pre = inc - p, tot = __shfl(inc, 63, 64);
+                const unsigned p = pack3(own, tri, act);
+                const unsigned inc = wave_incl_scan<unsigned>(p, lane);
+                const unsigned pre = inc - p, tot = __shfl(inc, 63, 64);
                 const uint32_t vrun = vrun0 + fld(pre, 0);
                 if (mine) {
                     const int y = (int)erow % g.m + 1;
