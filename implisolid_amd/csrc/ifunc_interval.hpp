@@ -200,9 +200,16 @@ __device__ __forceinline__ Iv dm_iv(Box p) {
     if (p.z.hi > r) { res = hull(res, sub(ivc(r), p.z)); any = true; }
     if (p.z.lo < -r) { res = hull(res, add(ivc(r), p.z)); any = true; }
     if (p.z.lo <= r && p.z.hi >= -r) {
-        const IvD v = subd(subd(addd(divcd(sq_exact_iv(sub(p.x, ivc(0.f))), (double)a2),
-                                     divcd(sq_exact_iv(sub(p.y, ivc(0.f))), (double)b2)),
-                               divcd(sq_exact_iv(sub(p.z, ivc(0.f))), (double)c2)),
+        // the endpoints are exact squares of floats (or 0): dm_f's one-correction-step quotient is
+        // the IEEE quotient for every one of them (tools/divconst_check.c), three f64 operations
+        // instead of a division sequence -- the bounds are bit for bit those of divcd
+        const double D = (double)a2, R = 1.0 / (double)a2;
+        static_assert(0.2f * 0.2f == (float)(0.4 / 2) * (float)(0.4 / 2), "the checked constant");
+        auto q = [&](IvD t) { return IvD{div_sq_const(t.lo, D, R), div_sq_const(t.hi, D, R)}; };
+        (void)b2;
+        (void)c2;
+        const IvD v = subd(subd(addd(q(sq_exact_iv(sub(p.x, ivc(0.f)))), q(sq_exact_iv(sub(p.y, ivc(0.f))))),
+                                q(sq_exact_iv(sub(p.z, ivc(0.f))))),
                           IvD{1., 1.});
         res = hull(res, tof(IvD{-v.hi, -v.lo}));
         any = true;
