@@ -5,7 +5,7 @@ most of the chip idle in its interval, fill, count and scan kernels).  The face 
 needs the counts of the slabs below it: each slab copies its counts into row s of one device
 array and records an event; slab s's stream waits for the events of slabs < s.  Prints the step
 time per S and checks that the concatenated slab meshes equal the one-slab mesh byte for byte.
-    python tools/streams_probe.py [S ...]
+    python tools/streams_probe.py [S ...] [--graph]   (--graph: each step replayed as one hipGraph)
 """
 import sys
 import time
@@ -18,7 +18,8 @@ from implisolid_amd import scenes
 
 
 def main():
-    Ss = [int(a) for a in sys.argv[1:]] or [1, 2, 3, 4]
+    use_graph = "--graph" in sys.argv
+    Ss = [int(a) for a in sys.argv[1:] if not a.startswith("--")] or [1, 2, 3, 4]
     dev = torch.device("cuda", 0)
     main_s = torch.cuda.current_stream(dev)
     shape, mc = scenes.config4(512)
@@ -70,11 +71,28 @@ def main():
         if grew:
             step()
         torch.cuda.synchronize(dev)
+        run = step
+        if use_graph:   # the whole multi-stream step as one graph: no host launch cost per kernel
+            graph = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream(dev)
+            cs.wait_stream(main_s)
+            outer = main_s
+            with torch.cuda.stream(cs):
+                main_s = cs
+                graph.capture_begin()
+                step()
+                graph.capture_end()
+            main_s = outer
+            main_s.wait_stream(cs)
+            run = graph.replay
+            for _ in range(3):
+                run()
+            torch.cuda.synchronize(dev)
         times = []
         for rep in range(3):
             t0 = time.perf_counter()
             for _ in range(50):
-                step()
+                run()
             torch.cuda.synchronize(dev)
             times.append((time.perf_counter() - t0) / 50 * 1e3)
         vs, fs = [], []
