@@ -51,9 +51,16 @@ __global__ __launch_bounds__(256) void k_eval_field(const Program* __restrict__ 
     field[w * (kBX * kBY) + lane] = f;   // eval_shape: field (zero) += value
 }
 
-template <int D>
+// A program pointer loaded from memory (ObjArgs::prog of a merged object stream) is generic: loads
+// through it are flat vector loads, so every instruction fetch of the interpreter was a memory round
+// trip and its fields and stack indices VGPR values.  The program is read-only during a launch, so
+// the merged kernels read it through the constant address space (scalar loads, uniform indices).
+typedef const __attribute__((address_space(4))) Program* ProgC;
+__device__ __forceinline__ ProgC prog_const(const Program* p) { return (ProgC)p; }
+
+template <int D, class ProgP = const Program*>
 struct InterpIv {   // the interval interpreter (ifunc_interval.hpp eval_iv)
-    const Program* prog;
+    ProgP prog;
     const float* tab;
     float2 tab_range;
     __device__ __forceinline__ Iv operator()(Box p, uint64_t modes_in, uint64_t& modes) const {
@@ -79,16 +86,110 @@ __global__ __launch_bounds__(256) void k_brick_refine(const Program* __restrict_
     brick_refine_body(InterpIv<D>{prog, tab, tab_range}, g, bg, cg, cmodes, clist, ccount, modes, cls);
 }
 
-template <int D>
+template <int D, class ProgP = const Program*>
 struct InterpEval {   // the node-program interpreter with per-brick operand skipping
-    const Program* prog;
+    ProgP prog;
     const float* tab;
     __device__ __forceinline__ float operator()(uint64_t m, float x, float y, float z) const {
         return eval_f_pruned<D>(prog, tab, m, x, y, z);
     }
 };
 
-template <int D>
+// A brick column's two samples in one pass of the interpreter: one instruction decode, one mode
+// test and one primitive dispatch serve both, and the two dependency chains sit in the same basic
+// blocks, so they interleave.  Per sample the operations are exactly eval_f_pruned's (bit-identical).
+__device__ __forceinline__ void prim_f2(int t, const float* __restrict__ tab, const float* __restrict__ prm, float x0,
+                                        float y0, float z0, float x1, float y1, float z1, float& a, float& b) {
+    switch (t) {
+        case NT_ELLIPSOID: a = egg_f(x0, y0, z0); b = egg_f(x1, y1, z1); return;
+        case NT_CUBE: a = cube_f(tab, x0, y0, z0); b = cube_f(tab, x1, y1, z1); return;
+        case NT_CYLINDER: a = cyl_f(x0, y0, z0); b = cyl_f(x1, y1, z1); return;
+        case NT_CONE: a = cone_f(x0, y0, z0); b = cone_f(x1, y1, z1); return;
+        case NT_HEART: a = heart_f(x0, y0, z0); b = heart_f(x1, y1, z1); return;
+        case NT_TORUS: a = torus_f(x0, y0, z0); b = torus_f(x1, y1, z1); return;
+        case NT_SCREW: a = screw_f(prm, x0, y0, z0); b = screw_f(prm, x1, y1, z1); return;
+        case NT_LID: a = lid_f(z0); b = lid_f(z1); return;
+        case NT_HALF_PLANE: a = hp_f(prm, x0, y0, z0); b = hp_f(prm, x1, y1, z1); return;
+        case NT_TETRA: a = tet_f(prm, x0, y0, z0); b = tet_f(prm, x1, y1, z1); return;
+        case NT_METABALLS: a = meta_f(prm, x0, y0, z0); b = meta_f(prm, x1, y1, z1); return;
+        case NT_EXTRUSION: a = extr_f(prm, x0, y0); b = extr_f(prm, x1, y1); return;
+        case NT_SCREW_TBB: a = tbb_f(prm, x0, y0, z0); b = tbb_f(prm, x1, y1, z1); return;
+        default: a = dm_f(x0, y0, z0); b = dm_f(x1, y1, z1); return;
+    }
+}
+
+template <int D, class ProgP>
+__device__ __forceinline__ void eval_f2_pruned(ProgP __restrict__ prog, const float* __restrict__ tab,
+                                               uint64_t modes, float x, float y, float z0, float z1, float& r0,
+                                               float& r1) {
+    float px0[D], py0[D], pz0[D], px1[D], py1[D], pz1[D], vf0[D], vf1[D];
+    int sp = 0, vp = 0;
+    px0[0] = x; py0[0] = y; pz0[0] = z0;
+    px1[0] = x; py1[0] = y; pz1[0] = z1;
+    const int n = prog->n_instr;
+    for (int pc = 0; pc < n; ++pc) {
+        const Instr I = instr_at(prog, pc);
+        if (I.skip_csg >= 0) {
+            const uint32_t m = mode_of(modes, I.skip_csg);
+            if (m == (I.skip_child ? (uint32_t)PM_LEFT : (uint32_t)PM_RIGHT)) {
+                pc = I.skip_to - 1;
+                continue;
+            }
+        }
+        if (I.op == OP_XFORM) {
+            const float* M = mat_row(prog, I.mat);
+            const V3 q0 = xform(M, px0[sp], py0[sp], pz0[sp]);
+            const V3 q1 = xform(M, px1[sp], py1[sp], pz1[sp]);
+            ++sp;
+            px0[sp] = q0.x; py0[sp] = q0.y; pz0[sp] = q0.z;
+            px1[sp] = q1.x; py1[sp] = q1.y; pz1[sp] = q1.z;
+        } else if (I.op == OP_PRIM) {
+            float a, b;
+            prim_f2(I.type, tab, mat_row(prog, I.prm), px0[sp], py0[sp], pz0[sp], px1[sp], py1[sp], pz1[sp], a, b);
+            vf0[vp] = a; vf1[vp] = b;
+            ++vp;
+            --sp;
+        } else {
+            --sp;
+            const uint32_t m = mode_of(modes, I.csg);
+            if (m == PM_BOTH) {
+                --vp;
+                const float a2 = vf0[vp], a1 = vf0[vp - 1], b2 = vf1[vp], b1 = vf1[vp - 1];
+                if (I.type == NT_UNION) {
+                    vf0[vp - 1] = (a1 > a2) ? a1 : a2; vf1[vp - 1] = (b1 > b2) ? b1 : b2;
+                } else if (I.type == NT_INTERSECTION) {
+                    vf0[vp - 1] = (a1 > a2) ? a2 : a1; vf1[vp - 1] = (b1 > b2) ? b2 : b1;
+                } else {
+                    vf0[vp - 1] = (a1 < -a2) ? a1 : -a2; vf1[vp - 1] = (b1 < -b2) ? b1 : -b2;
+                }
+            } else if (m == PM_RIGHT && I.type == NT_DIFFERENCE) {
+                vf0[vp - 1] = -vf0[vp - 1];
+                vf1[vp - 1] = -vf1[vp - 1];
+            }
+        }
+    }
+    r0 = vf0[0];
+    r1 = vf1[0];
+}
+
+template <int D, class ProgP = const Program*>
+struct InterpEval2 : InterpEval<D, ProgP> {   // the interpreter with the layer pair (eval_bricks.hpp eval_pair)
+    __device__ __forceinline__ void pair(uint64_t m, float x, float y, float z0, float z1, float& f0, float& f1) const {
+        eval_f2_pruned<D>(this->prog, this->tab, m, x, y, z0, z1, f0, f1);
+    }
+};
+
+// the interpreter's brick eval (merged streams, and single objects until their module is loaded):
+// both layers per pass unless IMPLISOLID_INTERP_PAIR=0
+static bool interp_pair() {
+    static const bool on = [] {
+        const char* s = std::getenv("IMPLISOLID_INTERP_PAIR");
+        return !(s && std::atoi(s) == 0);
+    }();
+    return on;
+}
+
+template <int D, bool Pair>
 __global__ __launch_bounds__(kEvalBlock) void k_eval_field_pruned(const Program* __restrict__ prog,
                                                            const float* __restrict__ tab, GridDesc g, BrickGrid bg,
                                                            const uint64_t* __restrict__ modes,
@@ -96,7 +197,8 @@ __global__ __launch_bounds__(kEvalBlock) void k_eval_field_pruned(const Program*
                                                            const uint32_t* __restrict__ count,
                                                            float* __restrict__ field, void* __restrict__ signs,
                                                            ClaimCtx cc) {
-    eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, cc, modes, list, count, field, signs);
+    if constexpr (Pair) eval_bricks_body(InterpEval2<D>{{prog, tab}}, g, bg, cc, modes, list, count, field, signs);
+    else eval_bricks_body(InterpEval<D>{prog, tab}, g, bg, cc, modes, list, count, field, signs);
 }
 
 // Per brick: its class (inherited from a sign-definite coarse box, or refined), the neighbour rule
@@ -328,7 +430,7 @@ template <int D>
 __global__ __launch_bounds__(256) void k_coarse_modes_b(const ObjArgs* __restrict__ objs, const float* __restrict__ tab,
                                                         float2 tab_range, GridDesc g, BrickGrid cg) {
     const ObjArgs& o = objs[blockIdx.y];
-    coarse_modes_body(InterpIv<D>{o.prog, tab, tab_range}, g, cg, o.cmodes, o.ccls, o.clist, o.counters);
+    coarse_modes_body(InterpIv<D, ProgC>{prog_const(o.prog), tab, tab_range}, g, cg, o.cmodes, o.ccls, o.clist, o.counters);
 }
 template <int D>
 __global__ __launch_bounds__(256) void k_brick_refine_b(const ObjArgs* __restrict__ objs, int n, const float* __restrict__ tab,
@@ -343,7 +445,7 @@ __global__ __launch_bounds__(256) void k_brick_refine_b(const ObjArgs* __restric
         const bool live = i < total;
         const int k = batch_object_of(s_pre, n, live ? i : 0u);
         const ObjArgs& o = objs[k];
-        brick_refine_item(InterpIv<D>{o.prog, tab, tab_range}, g, bg, cg, o.cmodes, o.clist, o.modes, o.cls,
+        brick_refine_item(InterpIv<D, ProgC>{prog_const(o.prog), tab, tab_range}, g, bg, cg, o.cmodes, o.clist, o.modes, o.cls,
                           live ? i - s_pre[k] : 0u, live);
     }
 }
@@ -354,7 +456,7 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill_b(const ObjArgs* __re
                     o.counters + kBrickListWord, static_cast<sign_piece_t*>(o.signs), o.counters + kCoarseListWord,
                     o.umark, o.mark_id);
 }
-template <int D>
+template <int D, bool Pair>
 __global__ __launch_bounds__(256) void k_eval_field_pruned_b(const ObjArgs* __restrict__ objs, int n,
                                                              const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
     __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
@@ -364,9 +466,9 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned_b(const ObjArgs* __re
         const int k = __builtin_amdgcn_readfirstlane(batch_object_of(s_pre, n, i));
         const ObjArgs& o = objs[k];
         const uint32_t li = i - s_pre[k];
-        // one layer at a time: the interpreter's node stacks are VGPR arrays, a layer pair doubles them
+        // Pair: both layers in one pass of the interpreter (InterpEval2; twice the node stacks in VGPRs)
         const ClaimCtx cc{o.fill, o.ccls, o.modes, o.cmodes, bg.nbx, bg.nbx * bg.nby};
-        eval_listed<InterpEval<D>, false>(InterpEval<D>{o.prog, tab}, g, bg, cc, o.blist[li], o.lmodes[li], o.field,
+        eval_listed<InterpEval2<D, ProgC>, Pair>(InterpEval2<D, ProgC>{{prog_const(o.prog), tab}}, g, bg, cc, o.blist[li], o.lmodes[li], o.field,
                                           static_cast<sign_piece_t*>(o.signs));
     }
 }
@@ -514,10 +616,20 @@ void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_
     if (bg.n_bricks <= 0) return;
     depth = eval_depth(depth);
     const unsigned eb = eval_bricks_grid(g);
-    if (depth <= 4) k_eval_field_pruned<4><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
-    else if (depth <= 8) k_eval_field_pruned<8><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
-    else if (depth <= 12) k_eval_field_pruned<12><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
-    else k_eval_field_pruned<16><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list, d_count, d_field, d_signs, cc);
+#define IMPLI_EVAL_PRUNED(DD)                                                                                      \
+    do {                                                                                                           \
+        if (interp_pair())                                                                                         \
+            k_eval_field_pruned<DD, true><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list,      \
+                                                                    d_count, d_field, d_signs, cc);                \
+        else                                                                                                       \
+            k_eval_field_pruned<DD, false><<<eb, kEvalBlock, 0, s>>>(d_prog, d_rabbit, g, bg, d_modes, d_list,     \
+                                                                     d_count, d_field, d_signs, cc);               \
+    } while (0)
+    if (depth <= 4) IMPLI_EVAL_PRUNED(4);
+    else if (depth <= 8) IMPLI_EVAL_PRUNED(8);
+    else if (depth <= 12) IMPLI_EVAL_PRUNED(12);
+    else IMPLI_EVAL_PRUNED(16);
+#undef IMPLI_EVAL_PRUNED
 }
 
 // flat merged kernels (refine, eval): a fixed grid over all objects' items
@@ -536,7 +648,10 @@ void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_r
         k_coarse_modes_b<DD><<<gc, 256, 0, s>>>(d_objs, d_rabbit, tab_range, g, cg);                       \
         k_brick_refine_b<DD><<<kBatchRefineBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, tab_range, g, bg, cg); \
         k_brick_fill_b<<<gf, kFillBlock, 0, s>>>(d_objs, g, bg, cg, sign_fill);                            \
-        k_eval_field_pruned_b<DD><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);            \
+        if (interp_pair())                                                                             \
+            k_eval_field_pruned_b<DD, true><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);  \
+        else                                                                                               \
+            k_eval_field_pruned_b<DD, false><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg); \
     } while (0)
     if (depth <= 4) IMPLI_BATCH_EVAL(4);
     else if (depth <= 8) IMPLI_BATCH_EVAL(8);

@@ -349,8 +349,26 @@ __device__ __forceinline__ uint32_t mode_of(uint64_t modes, int csg);
 // skipped and their decision kept.  The stacks are kept as separate scalar arrays (structure of
 // arrays) so that the uniform-index accesses stay in VGPRs (arrays of Iv structs were demoted to
 // scratch).
-template <int D>
-__device__ __forceinline__ Iv eval_iv(const Program* __restrict__ prog, const float* __restrict__ tab,
+// one instruction through any program pointer (field by field: an Instr in another address space
+// does not bind to the copy constructor's reference)
+template <class ProgP>
+__device__ __forceinline__ Instr instr_at(ProgP prog, int pc) {
+    const auto& s = prog->instr[pc];
+    Instr I;
+    I.op = s.op; I.type = s.type; I.mat = s.mat; I.csg = s.csg;
+    I.skip_csg = s.skip_csg; I.skip_child = s.skip_child; I.skip_to = s.skip_to; I.prm = s.prm;
+    return I;
+}
+
+// a matrix / parameter row as a generic pointer (after inlining, the address space is inferred
+// back from the cast, so constant-space rows are still read with scalar loads)
+template <class ProgP>
+__device__ __forceinline__ const float* mat_row(ProgP prog, int i) { return (const float*)prog->mats[i]; }
+
+// ProgP: the program pointer -- const Program*, or a constant-address-space pointer when it was
+// loaded from memory (merged object streams: scalar loads of the instructions, eval.hip ProgC)
+template <int D, class ProgP>
+__device__ __forceinline__ Iv eval_iv(ProgP __restrict__ prog, const float* __restrict__ tab,
                                       float2 tab_range, Box p0, uint64_t modes_in, uint64_t& modes) {
     float xl[D], xh[D], yl[D], yh[D], zl[D], zh[D], vl[D], vh[D];
     int sp = 0, vp = 0;
@@ -358,7 +376,7 @@ __device__ __forceinline__ Iv eval_iv(const Program* __restrict__ prog, const fl
     modes = modes_in;
     const int n = prog->n_instr;
     for (int pc = 0; pc < n; ++pc) {
-        const Instr I = prog->instr[pc];
+        const Instr I = instr_at(prog, pc);
         if (I.skip_csg >= 0) {
             const uint32_t m = mode_of(modes_in, I.skip_csg);
             if (m == (I.skip_child ? (uint32_t)PM_LEFT : (uint32_t)PM_RIGHT)) {
@@ -368,11 +386,11 @@ __device__ __forceinline__ Iv eval_iv(const Program* __restrict__ prog, const fl
         }
         const Box cur{Iv{xl[sp], xh[sp]}, Iv{yl[sp], yh[sp]}, Iv{zl[sp], zh[sp]}};
         if (I.op == OP_XFORM) {
-            const Box q = xform_iv(prog->mats[I.mat], cur);
+            const Box q = xform_iv(mat_row(prog, I.mat), cur);
             ++sp;
             xl[sp] = q.x.lo; xh[sp] = q.x.hi; yl[sp] = q.y.lo; yh[sp] = q.y.hi; zl[sp] = q.z.lo; zh[sp] = q.z.hi;
         } else if (I.op == OP_PRIM) {
-            const Iv r = prim_iv(I.type, tab, tab_range, prog->mats[I.prm], cur);
+            const Iv r = prim_iv(I.type, tab, tab_range, mat_row(prog, I.prm), cur);
             vl[vp] = r.lo; vh[vp] = r.hi;
             ++vp;
             --sp;
@@ -402,15 +420,15 @@ __device__ __forceinline__ uint32_t mode_of(uint64_t modes, int csg) {
 }
 
 // point interpreter that skips pruned operands; bit-identical to eval_f for points in the brick
-template <int D>
-__device__ __forceinline__ float eval_f_pruned(const Program* __restrict__ prog, const float* __restrict__ tab,
+template <int D, class ProgP>
+__device__ __forceinline__ float eval_f_pruned(ProgP __restrict__ prog, const float* __restrict__ tab,
                                                uint64_t modes, float x, float y, float z) {
     float px[D], py[D], pz[D], vf[D];
     int sp = 0, vp = 0;
     px[0] = x; py[0] = y; pz[0] = z;
     const int n = prog->n_instr;
     for (int pc = 0; pc < n; ++pc) {
-        const Instr I = prog->instr[pc];
+        const Instr I = instr_at(prog, pc);
         if (I.skip_csg >= 0) {
             const uint32_t m = mode_of(modes, I.skip_csg);
             if (m == (I.skip_child ? (uint32_t)PM_LEFT : (uint32_t)PM_RIGHT)) {
@@ -419,11 +437,11 @@ __device__ __forceinline__ float eval_f_pruned(const Program* __restrict__ prog,
             }
         }
         if (I.op == OP_XFORM) {
-            const V3 q = xform(prog->mats[I.mat], px[sp], py[sp], pz[sp]);
+            const V3 q = xform(mat_row(prog, I.mat), px[sp], py[sp], pz[sp]);
             ++sp;
             px[sp] = q.x; py[sp] = q.y; pz[sp] = q.z;
         } else if (I.op == OP_PRIM) {
-            vf[vp++] = prim_f(I.type, tab, prog->mats[I.prm], px[sp], py[sp], pz[sp]);
+            vf[vp++] = prim_f(I.type, tab, mat_row(prog, I.prm), px[sp], py[sp], pz[sp]);
             --sp;
         } else {
             --sp;
