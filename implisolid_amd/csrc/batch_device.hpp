@@ -11,15 +11,16 @@ namespace impli {
 // index over every object's items: each block loads the n list lengths, forms their exclusive prefix in LDS, and a
 // thread (refine) or wave (eval) finds the object of its item by binary search.
 constexpr int kMaxBatchObjects = 1024;
+// align: each object's range rounded up to a multiple of it (64: every wave holds one object)
 __device__ __forceinline__ uint32_t batch_prefix(const ObjArgs* __restrict__ objs, int n, int word, uint32_t mult,
-                                                 uint32_t cap, uint32_t* s_pre) {
+                                                 uint32_t cap, uint32_t* s_pre, uint32_t align = 1u) {
     __shared__ uint32_t s_part[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;   // 256 threads, up to 4 objects each
     uint32_t v[4], sum = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int o = 4 * t + k;
-        v[k] = o < n ? min(objs[o].counters[word], cap) * mult : 0u;
+        v[k] = o < n ? (min(objs[o].counters[word], cap) * mult + align - 1u) / align * align : 0u;
         sum += v[k];
     }
     uint32_t inc = sum;

@@ -111,8 +111,21 @@ __device__ __forceinline__ void coarse_modes_body(const IvEval& ev, const GridDe
 // layers are of that class, and a CSG operand pruned over all layers is pruned over the brick
 // (modes agreeing over the layers are kept, the others reset to both operands -- never less
 // pruning than the brick's own interval).
+//
+// WaveModes (merged object streams, whose waves each hold one object): the interval program starts
+// from the modes every live lane of the wave agrees on (the others reset to both operands), so the
+// interpreter's skips -- and with them its instruction fetch -- are wave-uniform.  Starting from
+// fewer skips never changes the field: a mode is only ever derived from the brick's own interval,
+// and a skipped operand's select would have returned the kept one exactly.
 constexpr int kRefineSplit = kBZ;
-template <class IvEval>
+#ifndef IMPLI_REFINE_WAVE_MODES   // the tree module's refine pass (JIT): per-lane modes measured as fast
+#define IMPLI_REFINE_WAVE_MODES 0
+#endif
+__device__ __forceinline__ uint64_t agreeing_modes(uint64_t m_and, uint64_t m_or) {
+    const uint64_t d = m_and ^ m_or;
+    return m_and & ~(((d | (d >> 1)) & 0x5555555555555555ull) * 3ull);
+}
+template <class IvEval, bool WaveModes = false>
 __device__ __forceinline__ void brick_refine_item(const IvEval& ev, const GridDesc& g, const BrickGrid& bg,
                                                   const BrickGrid& cg, const uint64_t* __restrict__ cmodes,
                                                   const uint32_t* __restrict__ clist, uint64_t* __restrict__ modes,
@@ -128,6 +141,17 @@ __device__ __forceinline__ void brick_refine_item(const IvEval& ev, const GridDe
     // the lane's layer (a brick past the slab's last layer repeats its last one)
     const int lz = min(q.z0 + (int)qd, q.z1);
     uint64_t m = cmodes[cb];
+    if constexpr (WaveModes) {
+        uint64_t wa = live ? m : ~0ull, wo = live ? m : 0ull;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            wa &= __shfl_xor(wa, o, 64);
+            wo |= __shfl_xor(wo, o, 64);
+        }
+        m = agreeing_modes(wa, wo);
+        m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
+            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)m);
+    }
     uint8_t c = sign_class(ev(sample_box(g, q.x0, q.x1, q.y0, q.y1, lz, lz), m, m));
     // combine the brick's lanes (consecutive lanes of one wave)
     uint64_t m_and = m, m_or = m;
@@ -140,16 +164,14 @@ __device__ __forceinline__ void brick_refine_item(const IvEval& ev, const GridDe
         c_and &= (uint32_t)__shfl_xor((int)c_and, o, 64);
         c_or |= (uint32_t)__shfl_xor((int)c_or, o, 64);
     }
-    const uint64_t d = m_and ^ m_or;
-    const uint64_t differ = ((d | (d >> 1)) & 0x5555555555555555ull) * 3ull;
-    m = m_and & ~differ;
+    m = agreeing_modes(m_and, m_or);
     c = c_and == c_or ? (uint8_t)c_and : (uint8_t)kBrickMixed;
     if (!ok || qd != 0) return;
     const int b = cx + cy * bg.nbx + bz * bg.nbx * bg.nby;
     modes[b] = m;
     cls[b] = sealed_class(g, c, q.x0, q.x1, q.y0, q.y1, q.z0, q.z1);
 }
-template <class IvEval>
+template <class IvEval, bool WaveModes = IMPLI_REFINE_WAVE_MODES != 0>
 __device__ __forceinline__ void brick_refine_body(const IvEval& ev, const GridDesc& g, const BrickGrid& bg,
                                                   const BrickGrid& cg, const uint64_t* __restrict__ cmodes,
                                                   const uint32_t* __restrict__ clist,
@@ -159,7 +181,7 @@ __device__ __forceinline__ void brick_refine_body(const IvEval& ev, const GridDe
     // the loop runs while any lane of the wave has an item: a brick's layer lanes shuffle together
     for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < total; i0 += gridDim.x * 256) {
         const uint32_t i = i0 + (threadIdx.x & 63u);
-        brick_refine_item(ev, g, bg, cg, cmodes, clist, modes, cls, i, i < total);
+        brick_refine_item<IvEval, WaveModes>(ev, g, bg, cg, cmodes, clist, modes, cls, i, i < total);
     }
 }
 

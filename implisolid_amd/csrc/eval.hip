@@ -83,7 +83,8 @@ __global__ __launch_bounds__(256) void k_brick_refine(const Program* __restrict_
                                                       const uint32_t* __restrict__ clist,
                                                       const uint32_t* __restrict__ ccount, uint64_t* __restrict__ modes,
                                                       uint8_t* __restrict__ cls) {
-    brick_refine_body(InterpIv<D>{prog, tab, tab_range}, g, bg, cg, cmodes, clist, ccount, modes, cls);
+    // wave-uniform starting modes: uniform skips, so the interpreter's instruction fetch stays scalar
+    brick_refine_body<InterpIv<D>, true>(InterpIv<D>{prog, tab, tab_range}, g, bg, cg, cmodes, clist, ccount, modes, cls);
 }
 
 template <int D, class ProgP = const Program*>
@@ -436,17 +437,18 @@ template <int D>
 __global__ __launch_bounds__(256) void k_brick_refine_b(const ObjArgs* __restrict__ objs, int n, const float* __restrict__ tab,
                                                         float2 tab_range, GridDesc g, BrickGrid bg, BrickGrid cg) {
     __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
-    const uint32_t total =
-        batch_prefix(objs, n, kCoarseListWord, (uint32_t)(kCZ * kRefineSplit), (uint32_t)cg.n_bricks, s_pre);
-    // whole waves iterate (a brick's layer lanes shuffle together); object ranges start at
-    // multiples of kRefineSplit, so a brick's lanes share their object
+    constexpr uint32_t kItems = kCZ * kRefineSplit;   // items per listed coarse box
+    const uint32_t total = batch_prefix(objs, n, kCoarseListWord, kItems, (uint32_t)cg.n_bricks, s_pre, 64u);
+    // whole waves iterate (a brick's layer lanes shuffle together); object ranges are padded to
+    // whole waves, so a wave's object, program and starting modes are uniform (WaveModes): the
+    // interval interpreter's instruction fetch is scalar and its skips do not diverge
     for (uint32_t i0 = blockIdx.x * 256 + (threadIdx.x & ~63u); i0 < total; i0 += gridDim.x * 256) {
-        const uint32_t i = i0 + (threadIdx.x & 63u);
-        const bool live = i < total;
-        const int k = batch_object_of(s_pre, n, live ? i : 0u);
+        const int k = __builtin_amdgcn_readfirstlane(batch_object_of(s_pre, n, i0));
         const ObjArgs& o = objs[k];
-        brick_refine_item(InterpIv<D, ProgC>{prog_const(o.prog), tab, tab_range}, g, bg, cg, o.cmodes, o.clist, o.modes, o.cls,
-                          live ? i - s_pre[k] : 0u, live);
+        const uint32_t i = i0 + (threadIdx.x & 63u) - s_pre[k];
+        const bool live = i < min(o.counters[kCoarseListWord], (uint32_t)cg.n_bricks) * kItems;
+        brick_refine_item<InterpIv<D, ProgC>, true>(InterpIv<D, ProgC>{prog_const(o.prog), tab, tab_range}, g, bg, cg,
+                                                    o.cmodes, o.clist, o.modes, o.cls, live ? i : 0u, live);
     }
 }
 __global__ __launch_bounds__(kFillBlock) void k_brick_fill_b(const ObjArgs* __restrict__ objs, GridDesc g, BrickGrid bg,

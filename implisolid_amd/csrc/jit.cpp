@@ -699,6 +699,8 @@ std::string TreeJit::kernel_source(const Program& p, bool bake) {
     const auto f2 = pe.emit(root, "x0", "y0", "z0", "x0", "y0", "z1", 4);
     std::ostringstream s;
     if (const char* e = std::getenv("IMPLISOLID_EVAL_PAIR")) s << "#define IMPLI_EVAL_PAIR " << (e[0] == '1' ? 1 : 0) << "\n";
+    if (const char* e = std::getenv("IMPLISOLID_REFINE_WAVE_MODES"))
+        s << "#define IMPLI_REFINE_WAVE_MODES " << (e[0] == '1' ? 1 : 0) << "\n";
     s << kPrelude << "#include \"eval_bricks.hpp\"\n#include \"ifunc_interval.hpp\"\n#include \"brick_modes.hpp\"\n"
       << "namespace impli {\nusing namespace dev;\n"
       << "__device__ __forceinline__ float tree_f(const float* __restrict__ M, const float* __restrict__ tab,\n"
