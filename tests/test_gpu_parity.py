@@ -833,6 +833,45 @@ def test_batch_stream_matches_oracle(impli, oracle, n_streams):
                 assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), (rep, i)
 
 
+_INTERP_SCRIPT = r"""
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import implisolid_amd as I
+from implisolid_amd import scenes
+objs = scenes.config5_objects(8, 48)
+shapes, mc = [o[0] for o in objs], objs[0][1]
+I.set_jit(0)
+out = []
+with I.Batch(shapes, mc, n_streams=0) as b:
+    b.run()
+    for i in range(len(shapes)):
+        v, f = b.download(i)
+        out.append(hashlib.sha256(v.tobytes() + f.tobytes()).hexdigest())
+v, f = I.make_geometry(scenes.config3_tree(), scenes.mc_settings(48, 1.0))
+out.append(hashlib.sha256(v.tobytes() + f.tobytes()).hexdigest())
+print(" ".join(out))
+"""
+
+
+def test_interpreter_switches_identical():
+    """The interpreter's diagnostic switch (IMPLISOLID_INTERP_PAIR=0: one layer per pass, read once
+    per process) gives the meshes of the default layer pair: merged object stream and a single
+    object on the interpreter kernels (set_jit(0)), each in a fresh process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for pair in ("1", "0"):
+        env = dict(os.environ, IMPLISOLID_INTERP_PAIR=pair)
+        r = subprocess.run([sys.executable, "-c", _INTERP_SCRIPT, root], env=env, capture_output=True,
+                           text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[pair] = r.stdout.split()
+    assert len(res["1"]) == 9 and res["1"] == res["0"]
+
+
 # ---- the bench's own workloads at their full sizes (tests/golden/make_headline.py) -----------------
 _HEADLINE = None
 
