@@ -38,7 +38,8 @@ ABI_SYMBOLS = [
     "implisolid_slab_create_range", "implisolid_slab_balance", "implisolid_cuts_from_layer_work", "implisolid_set_devices",
     "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
     "implisolid_set_progress_callback", "implisolid_ob02_profile", "implisolid_last_build_stats",
-    "implisolid_jit_compile_points", "implisolid_debug_libm",
+    "implisolid_jit_compile_points", "implisolid_debug_libm", "implisolid_slab_stats_n",
+    "implisolid_slab_kernel_times_each",
 ]
 
 # implisolid_progress_callback (include/implisolid.h): verts, n_verts, faces, n_faces,
@@ -116,6 +117,8 @@ def lib():
         "implisolid_jit_compile": ([c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)],
                                    ctypes.c_int64),
         "implisolid_slab_kernel_times": ([c_void_p, fp], c_int),
+        "implisolid_slab_kernel_times_each": ([c_void_p, fp], c_int),
+        "implisolid_slab_stats_n": ([c_void_p, ctypes.POINTER(ctypes.c_int64), c_int], c_int),
         "implisolid_srand": ([ctypes.c_uint], None),
         "implisolid_rand": ([], c_int),
         "implisolid_rand_skip": ([ctypes.c_uint64], None),
@@ -541,6 +544,9 @@ class Slab:
         return lib().implisolid_slab_field(self.h)
 
     KERNELS = ("brick_modes", "eval_field", "mc_count", "mc_scan", "mc_verts", "mc_faces")
+    # one figure per kernel (Engine::kernel_times_each); names as in the rocprofv3 kernel trace
+    EACH_KERNEL = ("impli_coarse_modes", "impli_brick_refine", "k_brick_fill", "impli_eval_bricks", "k_mc_count",
+                   "k_unit_scan", "k_mc_cells", "k_mc_faces")
 
     def set_timing(self, on=True):
         self._rc(lib().implisolid_slab_set_timing(self.h, 1 if on else 0))
@@ -551,11 +557,18 @@ class Slab:
         self._rc(lib().implisolid_slab_kernel_times(self.h, out))
         return dict(zip(self.KERNELS, [float(x) for x in out]))
 
+    def kernel_times_each(self):
+        """ms per kernel (coarse, refine and fill split out of the brick pass) of the last timed calls."""
+        out = (ctypes.c_float * 8)()
+        self._rc(lib().implisolid_slab_kernel_times_each(self.h, out))
+        return dict(zip(self.EACH_KERNEL, [float(x) for x in out]))
+
     def stats(self):
         """After count(): units, non-empty units, owned vertices, triangles, active cells, halo-owned,
         cells, mixed coarse boxes, halo-owned as the vertex pass reads it, unit parts."""
         out = (ctypes.c_int64 * 10)()
-        self._rc(lib().implisolid_slab_stats(self.h, out))
+        n = lib().implisolid_slab_stats_n(self.h, out, 10)
+        self._rc(-1 if n < 0 else 0)
         keys = ["units", "nonempty_units", "own", "tri", "act", "halo_own", "cells", "mixed_coarse_boxes",
                 "halo_own_verts_pass", "unit_parts"]
         return dict(zip(keys, [int(x) for x in out]))

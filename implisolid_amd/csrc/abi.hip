@@ -10,6 +10,8 @@
 
 #include "../../include/implisolid.h"
 #include "engine.hpp"
+#include "batch_device.hpp"
+#include "brick_modes.hpp"
 #include "jit.hpp"
 
 #include <chrono>
@@ -761,26 +763,31 @@ float* implisolid_slab_verts(implisolid_slab* s) { return s->engine.d_verts(); }
 int32_t* implisolid_slab_faces(implisolid_slab* s) { return s->engine.d_faces(); }
 float* implisolid_slab_field(implisolid_slab* s) { return s->engine.d_field(); }
 
-int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]) {
+int implisolid_slab_stats_n(implisolid_slab* s, int64_t* out, int n) {
+    constexpr int kStats = 10;
     try {
+        if (!out || n < 0) throw InputError("slab_stats: null output or negative length");
         uint32_t c[16];
         s->engine.raw_counters(c, 0);
         const GridDesc& g = s->engine.grid();
-        out[0] = n_units(g);
-        out[1] = c[6];   // non-empty units (c[0] counts their parts)
-        out[2] = c[2];
-        out[3] = c[3];
-        out[4] = c[4];
-        out[5] = c[5];
-        out[6] = g.n_cells;
-        out[7] = c[14];   // mixed coarse boxes of the last eval (the fill kernel's copy of [13])
-        out[8] = c[1];    // the vertex pass's copy of the halo count (mc_types.hpp counters)
-        out[9] = c[0];    // unit parts
+        const int64_t v[kStats] = {
+            n_units(g),
+            c[6],        // non-empty units (c[0] counts their parts)
+            c[2], c[3], c[4], c[5],
+            g.n_cells,
+            c[14],       // mixed coarse boxes of the last eval (the fill kernel's copy of [13])
+            c[1],        // the vertex pass's copy of the halo count (mc_types.hpp counters)
+            c[0]};       // unit parts
+        for (int k = 0; k < n && k < kStats; ++k) out[k] = v[k];
+        return kStats;
     } catch (const std::exception& e) {
         report(e.what(), false);
         return -1;
     }
-    return 0;
+}
+
+int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]) {   // the original 8 figures
+    return implisolid_slab_stats_n(s, out, 8) < 0 ? -1 : 0;
 }
 
 int implisolid_slab_used_jit(implisolid_slab* s) { return s->engine.used_baked() ? 2 : s->engine.used_jit() ? 1 : 0; }
@@ -798,6 +805,7 @@ void implisolid_jit_stats(int32_t out[4], double* compile_seconds) {
 
 int implisolid_slab_set_timing(implisolid_slab* s, int on) { SLAB_TRY(s->engine.set_timing(on != 0)) }
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]) { SLAB_TRY(s->engine.kernel_times(ms)) }
+int implisolid_slab_kernel_times_each(implisolid_slab* s, float ms[8]) { SLAB_TRY(s->engine.kernel_times_each(ms)) }
 
 int64_t implisolid_slab_read_signs(implisolid_slab* s, uint8_t* out, int64_t capacity) {
     try {
@@ -878,6 +886,19 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         // n_streams <= 0: merged launches (the interpreter kernels, every stage once for all
         // objects); otherwise one hipGraph per object (JIT tree kernels when enabled) over streams
         b->merged = n_streams <= 0 && Engine::pruning() > 0;
+        if (b->merged) {
+            // the merged kernels keep the objects' list prefix in LDS (kMaxBatchObjects entries) and
+            // index every object's refine items with one 32-bit flat index
+            if (n > kMaxBatchObjects)
+                throw InputError("implisolid_batch_create: merged launches hold at most " + std::to_string(kMaxBatchObjects) +
+                                 " objects; use n_streams >= 1 (per-object graphs) for larger batches");
+            const float* bx = st.box;
+            const GridDesc g = make_grid(st.resolution, bx, 1, st.resolution + 3, 1);
+            const uint64_t items = (uint64_t)n * (uint64_t)coarse_grid(g).n_bricks * kCZ * kRefineSplit;
+            if (items >= (1ull << 32))
+                throw InputError("implisolid_batch_create: " + std::to_string(n) + " objects at this resolution exceed the "
+                                 "merged refine pass's 32-bit item index; use fewer objects or n_streams >= 1");
+        }
         const auto t0 = std::chrono::steady_clock::now();
         if (Engine::pruning() > 0 && !b->merged) TreeJit::instance().precompile(progs, 16);
         b->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

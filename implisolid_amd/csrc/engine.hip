@@ -130,6 +130,17 @@ void Engine::set_timing(bool on) {
     timing_ = on;
 }
 
+void Engine::kernel_times_each(float out[kTimedEachKernel]) {
+    if (!ev_[0]) throw InputError("kernel timing was never enabled");
+    IMPLI_HIP(hipEventSynchronize(ev_[8]));
+    const int pairs[kTimedEachKernel][2] = {{0, 9}, {9, 10}, {10, 1}, {1, 2}, {3, 4}, {4, 5}, {6, 7}, {7, 8}};
+    for (int k = 0; k < kTimedEachKernel; ++k) {
+        float ms = 0.f;
+        IMPLI_HIP(hipEventElapsedTime(&ms, ev_[pairs[k][0]], ev_[pairs[k][1]]));
+        out[k] = ms;
+    }
+}
+
 void Engine::kernel_times(float out[kTimedKernels]) {
     if (!ev_[0]) throw InputError("kernel timing was never enabled");
     IMPLI_HIP(hipEventSynchronize(ev_[8]));
@@ -278,7 +289,8 @@ void Engine::eval_field(hipStream_t s) {
         ensure_jit();
         launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, cmodes_.as<uint64_t>(),
                            ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>(),
-                           modes_.as<uint64_t>(), cls_.as<uint8_t>(), s, &jit_iv_);
+                           modes_.as<uint64_t>(), cls_.as<uint8_t>(), s, &jit_iv_, timing_ ? ev_[9] : nullptr);
+        mark(10, s);
         uint32_t* d_count = counters_.as<uint32_t>() + kBrickListWord;
         launch_brick_fill(grid_, ccls_.as<uint8_t>(), cmodes_.as<uint64_t>(), cls_.as<uint8_t>(), modes_.as<uint64_t>(),
                           level >= 2, fill_.as<uint8_t>(), blist_.as<uint32_t>(), lmodes_.as<uint64_t>(), d_count,
@@ -300,6 +312,8 @@ void Engine::eval_field(hipStream_t s) {
     } else {
         marks_valid_ = false;   // dense field: MC counts every unit
         IMPLI_HIP(hipMemsetAsync(fill_.p, 0, (size_t)brick_grid(grid_).n_bricks, s));   // nothing filled
+        mark(9, s);
+        mark(10, s);
         mark(1, s);
         launch_eval_field(prog_.as<Program>(), depth_, rabbit_.as<float>(), grid_, field_.as<float>(), s);
         launch_signs_from_field(grid_, field_.as<float>(), signs_.as<uint64_t>(), s);

@@ -130,6 +130,10 @@ public:
     static constexpr int kTimedKernels = 6;
     void set_timing(bool on);
     void kernel_times(float out[kTimedKernels]);
+    // the same, one figure per kernel: coarse interval pass, brick refine, fill, field eval, MC
+    // count, unit scan, vertex emission (k_mc_cells), face emission (k_mc_faces)
+    static constexpr int kTimedEachKernel = 8;
+    void kernel_times_each(float out[kTimedEachKernel]);
     // raw device counters after count(): [active units, halo own, own, tri, act, halo] (blocking)
     void raw_counters(uint32_t out[16], hipStream_t stream);
     // brick statistics of the last pruned eval: [bricks, mixed, sign-filled]; blocking
@@ -162,7 +166,7 @@ private:
     DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, ulist_, upart_, umark_, counters_, lmodes_, vid3_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
-    hipEvent_t ev_[9] = {};
+    hipEvent_t ev_[11] = {};   // 0-8 phase boundaries, 9 after the coarse pass, 10 after refine
     void mark(int i, hipStream_t s) {
         if (timing_) IMPLI_HIP(hipEventRecord(ev_[i], s));
     }

@@ -557,9 +557,12 @@ BrickGrid coarse_grid(const GridDesc& g) {
 
 void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                         uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_counters, uint64_t* d_modes,
-                        uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit) {
+                        uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit, hipEvent_t after_coarse) {
     BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
-    if (bg.n_bricks <= 0) return;
+    if (bg.n_bricks <= 0) {
+        if (after_coarse) (void)hipEventRecord(after_coarse, s);
+        return;
+    }
     uint32_t* d_ccount = d_counters + kCoarseListWord;
     depth = eval_depth(depth);
     const unsigned tc = (unsigned)((cg.n_bricks + 255) / 256);
@@ -569,6 +572,7 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
         const float* d_mats = reinterpret_cast<const float*>(reinterpret_cast<const char*>(d_prog) + offsetof(Program, mats));
         void* ca[] = {&d_mats, &d_rabbit, &tab_range, &gg, &cg, &d_cmodes, &d_ccls, &d_clist, &d_counters};
         TreeJit::launch(jit->coarse, tc, ca, s, "impli_coarse_modes");
+        if (after_coarse) (void)hipEventRecord(after_coarse, s);
         void* ra[] = {&d_mats, &d_rabbit, &tab_range, &gg, &bg, &cg, &d_cmodes, &d_clist, &d_ccount, &d_modes, &d_cls};
         TreeJit::launch(jit->refine, tr, ra, s, "impli_brick_refine");
         return;
@@ -577,6 +581,7 @@ void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit,
     do {                                                                                                          \
         k_coarse_modes<DD><<<tc, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, cg, d_cmodes, d_ccls, d_clist,     \
                                               d_counters);                                                        \
+        if (after_coarse) (void)hipEventRecord(after_coarse, s);                                              \
         k_brick_refine<DD><<<tr, 256, 0, s>>>(d_prog, d_rabbit, tab_range, g, bg, cg, d_cmodes, d_clist, d_ccount, \
                                               d_modes, d_cls);                                                    \
     } while (0)

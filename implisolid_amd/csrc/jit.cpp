@@ -10,6 +10,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <atomic>
+#include <functional>
+#include <map>
+#include <mutex>
 #include <set>
 #include <sstream>
 #include <stdexcept>
@@ -450,18 +453,43 @@ double TreeJit::compile_seconds() const { return compile_us_.load() * 1e-6; }
 
 namespace {
 
-// FNV-1a over the source and the compile options: the disk cache key
-std::string source_hash(const std::string& src) {
-    uint64_t h = 1469598103934665603ull;
-    auto mix = [&h](const char* p, size_t n) {
-        for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)p[i]; h *= 1099511628211ull; }
-    };
-    mix(src.data(), src.size());
-    for (int k = 0; k < kJitNumHeaders; ++k) mix(kJitHeaderSources[k], std::strlen(kJitHeaderSources[k]));   // the headers it includes
-    const char* tag = "gfx950 -O3 -ffp-contract=off -std=c++17 v3";
-    mix(tag, std::strlen(tag));
+uint64_t fnv1a(const char* p, size_t n, uint64_t h = 1469598103934665603ull) {
+    for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)p[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+// the device's architecture string (gcnArchName), once per device
+std::string device_arch(int device) {
+    static std::mutex mu;
+    static std::map<int, std::string> names;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = names.find(device);
+    if (it != names.end()) return it->second;
+    hipDeviceProp_t prop{};
+    std::string name = hipGetDeviceProperties(&prop, device) == hipSuccess ? std::string(prop.gcnArchName) : "unknown";
+    names.emplace(device, name);
+    return name;
+}
+
+// FNV-1a over the source, the headers it includes, the compile options, the hipRTC version and
+// the device's architecture: the disk cache key
+std::string source_hash(const std::string& src, int device) {
+    uint64_t h = fnv1a(src.data(), src.size());
+    for (int k = 0; k < kJitNumHeaders; ++k) h = fnv1a(kJitHeaderSources[k], std::strlen(kJitHeaderSources[k]), h);
+    int major = 0, minor = 0;
+    (void)hiprtcVersion(&major, &minor);
+    const std::string tag = "--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 v4 hiprtc " + std::to_string(major) +
+                            "." + std::to_string(minor) + " " + device_arch(device);
+    h = fnv1a(tag.data(), tag.size(), h);
     char buf[32];
     std::snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
+    return buf;
+}
+
+// the integrity record stored beside a cached code object: its size and FNV-1a hash
+std::string code_meta(const std::vector<char>& code) {
+    char buf[64];
+    std::snprintf(buf, sizeof buf, "%zu %016llx", code.size(), (unsigned long long)fnv1a(code.data(), code.size()));
     return buf;
 }
 
@@ -481,7 +509,11 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
     std::string path;   // mkdir -p
     for (size_t i = 1; i <= dir.size(); ++i)
         if (i == dir.size() || dir[i] == '/') (void)::mkdir(dir.substr(0, i).c_str(), 0755);
-    const std::string tmp = dir + "/." + name + "." + std::to_string((long)::getpid()) + ".tmp";
+    // unique per process, thread and call: concurrent writers of one entry never share a temp file
+    static std::atomic<uint64_t> counter{0};
+    const std::string tmp = dir + "/." + name + "." + std::to_string((long)::getpid()) + "." +
+                            std::to_string(std::hash<std::thread::id>()(std::this_thread::get_id())) + "." +
+                            std::to_string(counter.fetch_add(1)) + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return;
     const bool ok = std::fwrite(data.data(), 1, data.size(), f) == data.size();
@@ -495,22 +527,31 @@ void TreeJit::build(Slot* slot) {
     const auto t0 = std::chrono::steady_clock::now();
     try {
         std::vector<char> code;
-        const std::string name = source_hash(slot->src) + ".co";
-        // the disk copy is only trusted with its source beside it (a hash collision cannot alias)
-        std::vector<char> src_on_disk;
+        const std::string name = source_hash(slot->src, slot->device) + ".co";
+        // the disk copy is only trusted with its source beside it (a hash collision cannot alias) and
+        // with its size and checksum matching the integrity record written after it
+        std::vector<char> src_on_disk, meta_on_disk;
+        bool from_disk = false;
         if (!disk_dir_.empty() && read_file(disk_dir_ + "/" + name, code) &&
             read_file(disk_dir_ + "/" + name + ".src", src_on_disk) &&
-            std::string(src_on_disk.begin(), src_on_disk.end()) == slot->src) {
+            std::string(src_on_disk.begin(), src_on_disk.end()) == slot->src &&
+            read_file(disk_dir_ + "/" + name + ".meta", meta_on_disk) &&
+            std::string(meta_on_disk.begin(), meta_on_disk.end()) == code_meta(code)) {
             ++n_disk_;
-        } else {
-            code = compile(slot->src);
+            from_disk = true;
+        }
+        auto compile_and_store = [&](const std::string& src) {
+            code = compile(src);
             compile_us_ += (int64_t)(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
             ++n_compiled_;
             if (!disk_dir_.empty()) {
                 write_file_atomic(disk_dir_, name + ".src", std::vector<char>(slot->src.begin(), slot->src.end()));
                 write_file_atomic(disk_dir_, name, code);
+                const std::string m = code_meta(code);
+                write_file_atomic(disk_dir_, name + ".meta", std::vector<char>(m.begin(), m.end()));
             }
-        }
+        };
+        if (!from_disk) compile_and_store(slot->src);
         int prev = 0;
         (void)hipGetDevice(&prev);
         if (prev != slot->device) IMPLI_HIP_THROW(hipSetDevice(slot->device));
@@ -532,6 +573,13 @@ void TreeJit::build(Slot* slot) {
             return ok;
         };
         bool ok = load(code);
+        if (!ok && from_disk) {   // a cached object that does not load: compile it again and rewrite the entry
+            if (slot->mod) (void)hipModuleUnload(slot->mod);
+            slot->mod = nullptr;
+            from_disk = false;
+            compile_and_store(slot->src);
+            ok = load(code);
+        }
         // the eval kernel asks for eight waves per SIMD; a tree whose code then spills to scratch is
         // compiled again without the request (stored under the same source key: deterministic)
         const size_t at = slot->src.find(" __attribute__((amdgpu_waves_per_eu(");
@@ -544,7 +592,11 @@ void TreeJit::build(Slot* slot) {
             std::string plain = slot->src;
             plain.erase(at, at_end + 3 - at);
             code = compile(plain);
-            if (!disk_dir_.empty()) write_file_atomic(disk_dir_, name, code);
+            if (!disk_dir_.empty()) {
+                write_file_atomic(disk_dir_, name, code);
+                const std::string m = code_meta(code);
+                write_file_atomic(disk_dir_, name + ".meta", std::vector<char>(m.begin(), m.end()));
+            }
             ok = load(code);
         }
         if (prev != slot->device) (void)hipSetDevice(prev);

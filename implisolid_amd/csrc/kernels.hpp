@@ -27,7 +27,8 @@ struct JitIntervalKernels {
 };
 void launch_brick_modes(const Program* d_prog, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                         uint64_t* d_cmodes, uint8_t* d_ccls, uint32_t* d_clist, uint32_t* d_counters, uint64_t* d_modes,
-                        uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit = nullptr);
+                        uint8_t* d_cls, hipStream_t s, const JitIntervalKernels* jit = nullptr,
+                        hipEvent_t after_coarse = nullptr /* recorded between the two kernels (timing) */);
 // K1b: neighbour rule -> fill[b], the list of bricks to evaluate, constant sign bits of the rest
 void launch_brick_fill(const GridDesc& g, const uint8_t* d_ccls, const uint64_t* d_cmodes, const uint8_t* d_cls,
                        const uint64_t* d_modes, int sign_fill, uint8_t* d_fill, uint32_t* d_list, uint64_t* d_lmodes,

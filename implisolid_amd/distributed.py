@@ -83,7 +83,12 @@ def gather_mesh(slab, gathered, rank, world, group=None, stream=0):
         v_loc = torch.empty(int(nv[rank]) * 3, dtype=torch.float32, device=dev)
         f_loc = torch.empty(int(nf[rank]) * 3, dtype=torch.int32, device=dev)
         slab.copy_mesh(v_loc.data_ptr(), f_loc.data_ptr(), int(nv[rank]), int(nf[rank]), stream)
-        torch.cuda.current_stream(dev).synchronize()
+        # the copy ran on `stream` (any caller stream, not necessarily torch's current one): wait
+        # for that stream before the send reads the buffers
+        if stream:
+            torch.cuda.ExternalStream(stream, device=dev).synchronize()
+        else:
+            torch.cuda.synchronize(dev)
     if rank != 0:   # empty parts are skipped on both sides (both know the sizes)
         works = [dist.isend(t, 0, group=group) for t in (v_loc, f_loc) if t.numel()]
         for w in works:

@@ -160,6 +160,19 @@ def config3(resolution=256):
                                                       qem=1, overall_repeats=3)
 
 
+def config3_shifted(resolution=256, shift=0.003):
+    """Config 3 with its box moved by a non-dyadic offset (every axis [-1 + shift, 1 + shift]).
+
+    On the dyadic box [-1, 1]^3 a double mushroom's singular point lands exactly on a grid sample:
+    the zero gradient there makes the reference's NaN normals, the average
+    edge length is NaN from the first repeat, make_alpha_list (centroids_projection.cpp:144-194)
+    returns an empty list and the projection keeps every centroid.  Shifted, no sample is singular,
+    every vertex stays finite, and the alpha search and the bisection run on every face."""
+    shape, mc = config3(resolution)
+    mc["box"] = {k: v + shift for k, v in mc["box"].items()}
+    return shape, mc
+
+
 def config4(resolution=512):
     """config 3's tree at 512^3, eval + MC (the Z-slab scaling workload)."""
     return config3_tree(), mc_settings(resolution, 1.0)

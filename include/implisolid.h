@@ -158,7 +158,10 @@ int implisolid_program_info(const char* shape_json, int ignore_root_matrix, int3
 
 /* Device-resident slab pipeline (benchmarks / multi-GPU Z-slab runs).  A slab engine owns the
    device buffers of one Z-slab of one object on the current HIP device.  `stream` is a
-   hipStream_t (may be NULL); nothing blocks except implisolid_slab_counts. */
+   hipStream_t (may be NULL).  The launches (eval, count, emit*, copy_*) are stream-ordered and do
+   not block; implisolid_slab_counts, _download, _stats* and _kernel_times* block on their stream;
+   the setup calls (create*, set_offsets) synchronise the device, since the buffers they reset or
+   write may still be read by kernels of an earlier call on another stream. */
 typedef struct implisolid_slab implisolid_slab;
 implisolid_slab* implisolid_slab_create(const char* shape_json, const char* mc_json, int rank, int nranks);
 /* async device-to-device copy of the slab's emitted mesh (nv vertices, nf faces, as counted) into
@@ -203,9 +206,11 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
  * [brick pass, field eval, MC count, unit scan, vertex emission, face emission] */
 int implisolid_slab_set_timing(implisolid_slab* s, int on);
 /* after count: [units, non-empty units, owned vertices (incl. halo), triangles, active cells,
- * halo-owned vertices, cells, mixed coarse boxes of the last eval, halo-owned vertices as the
- * vertex pass reads them (counter word 1, must equal [5]), unit parts] (blocking) */
-int implisolid_slab_stats(implisolid_slab* s, int64_t out[10]);
+ * halo-owned vertices, cells, mixed coarse boxes of the last eval] (blocking) */
+int implisolid_slab_stats(implisolid_slab* s, int64_t out[8]);
+/* the same figures, then [halo-owned vertices as the vertex pass reads them (counter word 1, must
+ * equal [5]), unit parts]: writes min(n, 10) values and returns how many exist (10), or -1 */
+int implisolid_slab_stats_n(implisolid_slab* s, int64_t* out, int n);
 /* the tree kernels the slab's last eval ran: 0 the interpreter, 1 the shape's JIT module, 2 the
  * object's baked JIT module */
 int implisolid_slab_used_jit(implisolid_slab* s);
@@ -225,6 +230,9 @@ void implisolid_jit_wait(void);
 /* [mode, bake, modules compiled, modules read from the disk cache], total compile seconds */
 void implisolid_jit_stats(int32_t out[4], double* compile_seconds);
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]);
+/* the same timing per kernel: [coarse interval pass, brick refine, brick fill, field eval, MC count,
+ * unit scan, vertex emission (k_mc_cells), face emission (k_mc_faces)] */
+int implisolid_slab_kernel_times_each(implisolid_slab* s, float ms[8]);
 /* blocking copy of the slab's sample signs (1: value < 0), n*n*layers bytes, x fastest; with
  * out == NULL returns the count.  At pruning level 2 sign-filled bricks keep no field values, so
  * this (not the field) is the complete sign information marching cubes uses. */

@@ -10,6 +10,9 @@ run alone takes ~16 s of CPU):
   config4_mc_r256   the same tree at R = 256, eval + MC                  (the metric's 256^3 point)
   config3_ob02_r256 config 3 (the tree, R = 256, MC + 3 x [resample, project, QEM])
   config2_ob02_r128 config 2 (sphere u rabbit, R = 128, MC + 3 x [resample, project, QEM])
+  config3s_ob02_r256 config 3 with its box shifted by 0.003 (scenes.config3_shifted): no singular
+                    sample, every vertex finite, so the alpha search and bisection run on every face
+  config5_mc_r128   config 5's 64 objects at 128^3, eval + MC: per object V / F and the SHA-256s
 
 Per configuration: V / F counts, SHA-256 of the face array, SHA-256 of the vertex array (for the
 bit-exact cases), the non-finite vertex rows (OB02 on the tree: reference behaviour at singular
@@ -18,7 +21,7 @@ with their values (the tolerance check for trees holding a twist, whose gradient
 cos).  OB02 meshes with more than 21 845 faces are past the reference's short edge-id wrap
 (DESIGN.md §5): the oracle, like the GPU, follows the intended semantics there.
 
-    python tests/golden/make_headline.py        # ~40 s
+    python tests/golden/make_headline.py        # adds missing entries; --all recomputes every one
 """
 import hashlib
 import json
@@ -46,6 +49,7 @@ def configs():
         "config4_mc_r256": scenes.config4(256),
         "config3_ob02_r256": scenes.config3(256),
         "config2_ob02_r128": scenes.config2(128),
+        "config3s_ob02_r256": scenes.config3_shifted(256),
     }
 
 
@@ -61,11 +65,32 @@ def summarize(v, f, seed):
     }, idx, v[idx]
 
 
+def config5_summary():
+    """Config 5's object stream: each of the 64 objects' eval + MC mesh (oracle.marching_cubes)."""
+    import oracle
+    from implisolid_amd import scenes
+    objs = scenes.config5_objects(64, 128)
+    rows = []
+    t0 = time.perf_counter()
+    for shape, mc in objs:
+        v, f = oracle.marching_cubes(oracle.mp5_to_nodes(json.dumps(shape)), 128, [-1.0, 1.0] * 3)
+        rows.append({"n_verts": int(v.shape[0]), "n_faces": int(f.shape[0]), "sha256_faces": sha(f), "sha256_verts": sha(v)})
+    return {"workload": "scenes.config5_objects(64, 128): eval + MC of each object, box [-1, 1]^3",
+            "objects": rows, "oracle_s": round(time.perf_counter() - t0, 1)}
+
+
 def main():
     import oracle
     oracle.build()
+    redo = "--all" in sys.argv
+    path_s, path_a = os.path.join(HERE, "headline_summaries.json"), os.path.join(HERE, "headline_samples.npz")
     out, arrays = {}, {}
+    if not redo and os.path.exists(path_s):
+        out = json.load(open(path_s))
+        arrays = dict(np.load(path_a))
     for k, (name, (shape, mc)) in enumerate(configs().items()):
+        if name in out:
+            continue
         t0 = time.perf_counter()
         v, f = oracle.polygonize(json.dumps(shape), json.dumps(mc))
         s, idx, vs = summarize(v, f, 20251015 + k)
@@ -73,9 +98,13 @@ def main():
         out[name] = s
         arrays[name + "_idx"], arrays[name + "_v"] = idx, vs
         print(name, s["n_verts"], s["n_faces"], "non-finite", len(s["nonfinite_rows"]), "%.1f s" % s["oracle_s"])
-    with open(os.path.join(HERE, "headline_summaries.json"), "w") as fh:
+    if "config5_mc_r128" not in out:
+        out["config5_mc_r128"] = config5_summary()
+        print("config5_mc_r128", sum(o["n_faces"] for o in out["config5_mc_r128"]["objects"]), "faces",
+              "%.1f s" % out["config5_mc_r128"]["oracle_s"])
+    with open(path_s, "w") as fh:
         json.dump(out, fh, indent=1)
-    np.savez_compressed(os.path.join(HERE, "headline_samples.npz"), **arrays)
+    np.savez_compressed(path_a, **arrays)
 
 
 if __name__ == "__main__":

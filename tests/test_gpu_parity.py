@@ -883,7 +883,8 @@ def _headline():
     return _HEADLINE
 
 
-@pytest.mark.parametrize("name", ["config4_mc_r512", "config4_mc_r256", "config3_ob02_r256", "config2_ob02_r128"])
+@pytest.mark.parametrize("name", ["config4_mc_r512", "config4_mc_r256", "config3_ob02_r256", "config3s_ob02_r256",
+                                  "config2_ob02_r128"])
 def test_headline_against_oracle_summary(impli, name):
     """The exact meshes bench.py times (config 4's tree at 512^3 and 256^3, eval + MC) and the OB02
     legs it reports (config 3 at 256^3, config 2 at 128^3, 3 repeats of resample + project + QEM),
@@ -905,6 +906,91 @@ def test_headline_against_oracle_summary(impli, name):
     assert np.abs(v[idx][ok].astype(np.float64) - vs[ok]).max(initial=0.0) < 1e-5
     tot = v[fin].astype(np.float64).sum(0)
     assert np.abs(tot - np.array(s["finite_sum"])).max() < 1e-5 * max(1, fin.sum())
+
+
+def _sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_config3_shifted_projection_live(impli):
+    """Config 3 at 256^3 on the shifted box (scenes.config3_shifted): the average edge length stays
+    finite, so the projection runs its alpha search and bisection on the faces (many evaluations
+    per face and repeat, not config 3's one), and the mesh is still the oracle's (faces SHA-256,
+    every vertex finite, sampled rows within 1e-5: the tree holds a twist)."""
+    summ, samples = _headline()
+    s = summ["config3s_ob02_r256"]
+    impli.ob02_profile(True)
+    try:
+        v, f = impli.make_geometry(s["shape"], s["mc"])
+        st = impli.last_build_stats()
+    finally:
+        impli.ob02_profile(False)
+    assert _sha(f) == s["sha256_faces"] and np.isfinite(v).all() and s["nonfinite_rows"] == []
+    idx, vs = samples["config3s_ob02_r256_idx"], samples["config3s_ob02_r256_v"]
+    assert np.abs(v[idx].astype(np.float64) - vs).max() < 1e-5
+    evals_per_face = st["projection_evals"] / (len(f) * s["mc"]["overall_repeats"])
+    assert evals_per_face > 10, evals_per_face
+
+
+@pytest.mark.parametrize("n_streams", [0, 8])
+def test_config5_stream_against_oracle_summary(impli, n_streams):
+    """Config 5 at its stated size: the 64 seeded objects at 128^3 (scenes.config5_objects(64, 128)),
+    eval + MC as one merged launch per stage (n_streams 0, the bench headline) and as per-object
+    hipGraphs over 8 streams: every object's faces and vertices byte-identical to the oracle's
+    (tests/golden/make_headline.py), on two replays."""
+    from implisolid_amd import scenes
+    summ, _ = _headline()
+    rows = summ["config5_mc_r128"]["objects"]
+    objs = scenes.config5_objects(64, 128)
+    shapes, mc = [o[0] for o in objs], objs[0][1]
+    with impli.Batch(shapes, mc, n_streams=n_streams) as b:
+        assert b.n == 64 and b.merged == (n_streams == 0)
+        for rep in range(2):
+            b.run()
+            for i, row in enumerate(rows):
+                v, f = b.download(i)
+                assert (len(v), len(f)) == (row["n_verts"], row["n_faces"]), (rep, i)
+                assert _sha(f) == row["sha256_faces"] and _sha(v) == row["sha256_verts"], (rep, i)
+
+
+@pytest.mark.parametrize("balanced", [True, False])
+def test_config4_eight_slabs_512(impli, balanced):
+    """BASELINE config 4's partition on one GPU: the 512^3 grid of config 4's tree as 8 Z-slabs
+    (balanced cuts from the interval pass, or equal layers), each with its recomputed halo layer
+    and global offsets: the concatenated mesh is the oracle's config4_mc_r512 byte for byte."""
+    from implisolid_amd import scenes
+    summ, _ = _headline()
+    s = summ["config4_mc_r512"]
+    shape, mc = scenes.config4(512)
+    assert shape == s["shape"]
+    cuts = impli.slab_balance(shape, mc, 8) if balanced else None
+    slabs = [impli.Slab(shape, mc, r, 8, cuts=cuts) for r in range(8)]
+    try:
+        counts = []
+        for sl in slabs:
+            sl.eval()
+            sl.count()
+            counts.append(sl.counts()[:2])
+        voff = np.concatenate([[0], np.cumsum([c[0] for c in counts])])
+        foff = np.concatenate([[0], np.cumsum([c[1] for c in counts])])
+        vs, fs = [], []
+        for r, sl in enumerate(slabs):
+            if cuts is not None:
+                assert (sl.cz_emit, sl.cz1) == (cuts[r], cuts[r + 1])
+            sl.set_offsets(int(voff[r]), int(foff[r]))
+            sl.emit()
+            nv, nf, of = sl.counts()
+            assert not of and (nf > 0 or cuts is None)   # equal slabs: the bottom ones may hold no surface
+            v, f = sl.download(nv, nf)
+            vs.append(v)
+            fs.append(f)
+    finally:
+        for sl in slabs:
+            sl.close()
+    v, f = np.concatenate(vs), np.concatenate(fs)
+    assert (len(v), len(f)) == (s["n_verts"], s["n_faces"])
+    assert _sha(f) == s["sha256_faces"] and _sha(v) == s["sha256_verts"]
 
 
 def test_rebuild_sequence_consistent(impli):

@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--R", type=int, default=512)
     ap.add_argument("--launches", type=int, default=4, help="dispatches per kernel of the R grid to average")
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--lib", help="the profiled library: its SHA-256 is recorded, so bench.py can tell whether the "
+                                  "traffic figures describe the library it runs")
     a = ap.parse_args()
     kib = 1024.0
     fr, fw = 2.0, 1.0   # MI355X_MICROARCH.md: FETCH_SIZE counts half of wide streaming reads
@@ -112,6 +114,9 @@ def main():
            "calibration": cal or "guide rule: FETCH_SIZE x2, WRITE_SIZE x1",
            "dropped_warmup_interpreter_kernels": dropped,
            "note": __doc__.strip().splitlines()[0]}
+    if a.lib:
+        import hashlib
+        out["lib_sha256"] = hashlib.sha256(open(a.lib, "rb").read()).hexdigest()
     json.dump(out, sys.stdout, indent=1)
     print()
 

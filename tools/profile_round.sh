@@ -19,8 +19,10 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$root/$out/
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$root/$out/cwrite" -o run -- python3 $B --prune 0 > "$out/cwrite.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU --output-format csv -d "$root/$out/sq" -o run -- python3 $B > "$out/sq.log" 2>&1
 python3 tools/pmc_valu.py "$out/sq" > "$out/valu.json"
+cp "$out/valu.json" profiles/valu_$tag.json
+cp "$out/trace/run_kernel_stats.csv" profiles/${tag}_kernel_stats.csv
 python3 tools/pmc_traffic.py --fetch "$out/fetch" --write "$out/write" --cal-fetch "$out/cfetch" --cal-write "$out/cwrite" \
-    --R 512 > "$out/traffic.json"
+    --R 512 --lib implisolid_amd/lib/libimplisolid_mi355x.so > "$out/traffic.json"
 cp "$out/traffic.json" profiles/traffic_$tag.json
 timeout -k 10 600 python3 bench.py > "$out/bench.log" 2>&1
 echo done
