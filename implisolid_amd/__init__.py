@@ -39,7 +39,10 @@ ABI_SYMBOLS = [
     "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
     "implisolid_set_progress_callback", "implisolid_ob02_profile", "implisolid_last_build_stats",
     "implisolid_jit_compile_points", "implisolid_debug_libm", "implisolid_slab_stats_n",
-    "implisolid_slab_kernel_times_each",
+    "implisolid_slab_kernel_times_each", "implisolid_debug_fold",
+    "implisolid_ob02_create", "implisolid_ob02_destroy", "implisolid_ob02_load", "implisolid_ob02_resample",
+    "implisolid_ob02_project", "implisolid_ob02_subdivide", "implisolid_ob02_counts", "implisolid_ob02_ranges",
+    "implisolid_ob02_get_verts", "implisolid_ob02_set_verts", "implisolid_ob02_download",
 ]
 
 # implisolid_progress_callback (include/implisolid.h): verts, n_verts, faces, n_faces,
@@ -87,6 +90,19 @@ def lib():
         "implisolid_last_error": ([], c_char_p), "implisolid_set_error_mode": ([c_int], None),
         "implisolid_eval_points": ([fp, ctypes.c_int64, fp, fp], c_int),
         "implisolid_debug_libm": ([c_int, fp, fp, ctypes.c_int64, fp], c_int),
+        "implisolid_debug_fold": ([fp, ctypes.c_int64, fp, ctypes.POINTER(ctypes.c_int64)], c_int),
+        "implisolid_ob02_create": ([c_char_p, c_char_p], c_void_p),
+        "implisolid_ob02_destroy": ([c_void_p], None),
+        "implisolid_ob02_load": ([c_void_p, c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                  ctypes.c_int64], c_int),
+        "implisolid_ob02_resample": ([c_void_p], c_int),
+        "implisolid_ob02_project": ([c_void_p], c_int),
+        "implisolid_ob02_subdivide": ([c_void_p, ctypes.c_float], c_int),
+        "implisolid_ob02_counts": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
+        "implisolid_ob02_ranges": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
+        "implisolid_ob02_get_verts": ([c_void_p, c_void_p], c_int),
+        "implisolid_ob02_set_verts": ([c_void_p, c_void_p], c_int),
+        "implisolid_ob02_download": ([c_void_p, fp, ip], c_int),
         "implisolid_program_info": ([c_char_p, c_int, ip, fp], c_int),
         "implisolid_slab_create": ([c_char_p, c_char_p, c_int, c_int], c_void_p),
         "implisolid_slab_destroy": ([c_void_p], None),
@@ -439,6 +455,19 @@ def debug_libm(which, a, b=None):
     return out
 
 
+def debug_fold(terms):
+    """Diagnostics: the projection's edge-length fold (s = 0; s += e[k], float, in order) on the
+    device, as build_geometry computes it; returns (sum, chunks taken from the chunk table)."""
+    e = np.ascontiguousarray(terms, dtype=np.float32).reshape(-1)
+    out = (ctypes.c_float * 1)()
+    tc = ctypes.c_int64(0)
+    fp = ctypes.POINTER(ctypes.c_float)
+    rc = lib().implisolid_debug_fold(e.ctypes.data_as(fp), e.size, out, ctypes.byref(tc))
+    if rc != 0:
+        raise ImplisolidError(last_error())
+    return np.float32(out[0]), int(tc.value)
+
+
 def program_info(shape, ignore_root_matrix=False):
     """Host-only: compile an MP5 tree; returns (n_instr, depth, n_mats, inverse matrices [n,12])."""
     L = lib()
@@ -613,6 +642,77 @@ class Slab:
         if self.h:
             lib().implisolid_slab_destroy(self.h)
             self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Ob02Shard:
+    """The OB02 loop on one Z-slab shard (include/implisolid.h implisolid_ob02_*): load the whole MC
+    mesh (device pointers) owning vertices [v0, v1); resample() / project() update the owned
+    vertices; get_verts / set_verts move the current vertices to and from a device buffer for the
+    exchange between steps (distributed.ob02_sharded drives the loop).  Every call blocks."""
+
+    def __init__(self, shape, mc_settings):
+        self.h = lib().implisolid_ob02_create(_s(shape), _s(mc_settings))
+        if not self.h:
+            raise ImplisolidError(last_error())
+
+    def _rc(self, rc):
+        if rc != 0:
+            raise ImplisolidError(last_error())
+
+    def load(self, d_verts, nv, d_faces, nf, v0, v1):
+        self._rc(lib().implisolid_ob02_load(self.h, ctypes.c_void_p(d_verts), int(nv), ctypes.c_void_p(d_faces), int(nf),
+                                            int(v0), int(v1)))
+
+    def resample(self):
+        self._rc(lib().implisolid_ob02_resample(self.h))
+
+    def project(self):
+        self._rc(lib().implisolid_ob02_project(self.h))
+
+    def subdivide(self, amplitude):
+        self._rc(lib().implisolid_ob02_subdivide(self.h, float(amplitude)))
+
+    def counts(self):
+        out = (ctypes.c_int64 * 2)()
+        self._rc(lib().implisolid_ob02_counts(self.h, out))
+        return int(out[0]), int(out[1])
+
+    def ranges(self):
+        """[v0, v1) owned vertices, [f0, f1) work faces, [c0, c1) centroid faces"""
+        out = (ctypes.c_int64 * 6)()
+        self._rc(lib().implisolid_ob02_ranges(self.h, out))
+        return tuple(int(x) for x in out)
+
+    def get_verts(self, d_dst):
+        self._rc(lib().implisolid_ob02_get_verts(self.h, ctypes.c_void_p(d_dst)))
+
+    def set_verts(self, d_src):
+        self._rc(lib().implisolid_ob02_set_verts(self.h, ctypes.c_void_p(d_src)))
+
+    def download(self):
+        nv, nf = self.counts()
+        v = np.empty((nv, 3), np.float32)
+        f = np.empty((nf, 3), np.int32)
+        self._rc(lib().implisolid_ob02_download(self.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                f.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return v, f
+
+    def close(self):
+        if self.h:
+            lib().implisolid_ob02_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
     def __del__(self):
         try:

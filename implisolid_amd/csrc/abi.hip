@@ -471,6 +471,33 @@ int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* gra
     return 0;
 }
 
+int implisolid_debug_fold(const float* terms, int64_t n, float* sum_out, int64_t* table_chunks) {
+    if (n < 0 || (n && !terms) || !sum_out) {
+        report("implisolid_debug_fold: bad arguments", false);
+        return -1;
+    }
+    try {
+        (void)engine();   // the device context
+        int tc = 0;
+        static long long st[6];
+        static int tr[256];
+        *sum_out = debug_fold(terms, n, &tc, st, tr);
+        if (std::getenv("IMPLISOLID_FOLD_TRACE")) {
+            for (int i = 0; i < 256 && i < st[0] + st[1] + st[2]; ++i)
+                std::fprintf(stderr, "%s k=%d E=%d\n", (tr[i] >> 28) == 1 ? "table" : "term ", tr[i] & 0xfffff,
+                             ((tr[i] >> 20) & 0xff) - 64);
+        }
+        if (std::getenv("IMPLISOLID_FOLD_STATS"))
+            std::fprintf(stderr, "fold n=%lld steps zero/serial %lld table %lld terms %lld global-term-loads %lld cycles stage %lld walk %lld\n",
+                         (long long)n, st[0], st[1], st[2], st[3], st[4], st[5]);
+        if (table_chunks) *table_chunks = tc;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
 int implisolid_debug_libm(int which, const float* a, const float* b, int64_t n, float* out) {
     if (which < 0 || which > 2 || n < 0 || (n && (!a || !out || (which == 2 && !b)))) {
         report("implisolid_debug_libm: bad arguments", false);
@@ -1047,6 +1074,117 @@ int implisolid_batch_download(implisolid_batch* b, int i, float* verts, int32_t*
         return -1;
     }
     return 0;
+}
+
+// ---- the OB02 loop on a Z-slab shard (one object per rank; Ob02::set_owned_vertices) -------------
+struct implisolid_ob02 {
+    std::unique_ptr<Engine> engine;
+    std::unique_ptr<Ob02> ob;
+    MCSettings st;
+    hipStream_t stream = nullptr;
+    ~implisolid_ob02() {
+        ob.reset();
+        engine.reset();
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+implisolid_ob02* implisolid_ob02_create(const char* shape_json, const char* mc_json) {
+    g_last_error.clear();
+    auto* h = new implisolid_ob02();
+    try {
+        h->st = parse_mc_settings(mc_json);
+        const Program p = compile_mp5(shape_json, h->st.ignore_root_matrix);
+        IMPLI_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->engine.reset(new Engine());
+        h->engine->set_object(p);
+        h->ob.reset(new Ob02(*h->engine, h->stream));
+        h->ob->capture_pointsets = false;
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        delete h;
+        return nullptr;
+    }
+    return h;
+}
+
+void implisolid_ob02_destroy(implisolid_ob02* h) {
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    delete h;
+}
+
+#define OB02_TRY(expr)                                 \
+    try {                                              \
+        expr;                                          \
+    } catch (const std::exception& e) {                \
+        report(e.what(), false);                       \
+        return -1;                                     \
+    }                                                  \
+    return 0;
+
+int implisolid_ob02_load(implisolid_ob02* h, const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, int64_t v0,
+                         int64_t v1) {
+    OB02_TRY({
+        if (nv < 0 || nf < 0 || (nv && !d_verts) || (nf && !d_faces)) throw InputError("implisolid_ob02_load: bad mesh");
+        IMPLI_HIP(hipDeviceSynchronize());   // the caller's copies of the mesh are complete
+        h->ob->load_mesh(d_verts, nv, d_faces, nf);
+        h->ob->set_owned_vertices(v0, v1);
+        IMPLI_HIP(hipStreamSynchronize(h->stream));
+    })
+}
+
+int implisolid_ob02_resample(implisolid_ob02* h) {
+    OB02_TRY({
+        h->ob->vertex_resampling(h->st.vresampl_c);
+        IMPLI_HIP(hipStreamSynchronize(h->stream));
+    })
+}
+
+int implisolid_ob02_project(implisolid_ob02* h) {
+    OB02_TRY({
+        h->ob->centroids_projection(h->st.qem != 0);
+        IMPLI_HIP(hipStreamSynchronize(h->stream));
+    })
+}
+
+int implisolid_ob02_subdivide(implisolid_ob02* h, float amplitude) {
+    OB02_TRY({
+        h->ob->subdivide(amplitude);
+        IMPLI_HIP(hipStreamSynchronize(h->stream));
+    })
+}
+
+int implisolid_ob02_counts(implisolid_ob02* h, int64_t out[2]) {
+    out[0] = h->ob->n_verts();
+    out[1] = h->ob->n_faces();
+    return 0;
+}
+
+int implisolid_ob02_ranges(implisolid_ob02* h, int64_t out[6]) {
+    h->ob->ranges(out);
+    return 0;
+}
+
+int implisolid_ob02_get_verts(implisolid_ob02* h, float* d_dst) {
+    OB02_TRY({
+        const int64_t nv = h->ob->n_verts();
+        if (nv) IMPLI_HIP(hipMemcpyAsync(d_dst, h->ob->d_verts(), (size_t)nv * 12, hipMemcpyDeviceToDevice, h->stream));
+        IMPLI_HIP(hipStreamSynchronize(h->stream));
+    })
+}
+
+int implisolid_ob02_set_verts(implisolid_ob02* h, const float* d_src) {
+    OB02_TRY({
+        const int64_t nv = h->ob->n_verts();
+        IMPLI_HIP(hipDeviceSynchronize());   // the caller's exchange into d_src is complete
+        if (nv) IMPLI_HIP(hipMemcpyAsync(h->ob->d_verts(), d_src, (size_t)nv * 12, hipMemcpyDeviceToDevice, h->stream));
+        IMPLI_HIP(hipStreamSynchronize(h->stream));
+    })
+}
+
+int implisolid_ob02_download(implisolid_ob02* h, float* verts, int32_t* faces) {
+    OB02_TRY(h->ob->fetch(verts, faces))
 }
 
 void implisolid_batch_destroy(implisolid_batch* b) {

@@ -411,9 +411,9 @@ __device__ __forceinline__ float kij(int64_t i, int64_t j, const float* __restri
 }
 
 __global__ void k_face_weights(const float* __restrict__ C, const float* __restrict__ N, const int32_t* __restrict__ fof,
-                               int64_t nf, float c, float* __restrict__ W) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= nf) return;
+                               int64_t i0, int64_t i1, float c, float* __restrict__ W) {   // faces [i0, i1)
+    const int64_t i = i0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= i1) return;
     float ki = 0;   // wi, vertex_resampling.hpp:79-91
     for (int j = 0; j < 3; ++j) ki += kij(i, fof[3 * i + j], C, N);
     W[i] = (float)(1.0 + (double)(c * ki));
@@ -435,6 +435,36 @@ __global__ void k_resample(const uint32_t* __restrict__ off, const int32_t* __re
         z += w * C[3 * fj + 2];
     }
     out[3 * v] = x; out[3 * v + 1] = y; out[3 * v + 2] = z;
+}
+
+// the faces [out[0], out[1]] touching a vertex in [v0, v1) (slab sharding): min / max face index
+__global__ void k_touch_range(const int32_t* __restrict__ f, int64_t nf, int64_t v0, int64_t v1,
+                              unsigned long long* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nf) return;
+    bool t = false;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) t = t || (f[3 * j + q] >= v0 && f[3 * j + q] < v1);
+    if (t) {
+        atomicMin(&out[0], (unsigned long long)j);
+        atomicMax(&out[1], (unsigned long long)j);
+    }
+}
+// ... and the min / max over those faces' edge neighbours (the faces the weights read)
+__global__ void k_fof_range(const int32_t* __restrict__ fof, int64_t j0, int64_t j1, unsigned long long* __restrict__ out) {
+    const int64_t j = j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= j1) return;
+    unsigned long long lo = (unsigned long long)j, hi = (unsigned long long)j;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int32_t g = fof[3 * j + q];
+        if (g >= 0) {
+            lo = (unsigned long long)g < lo ? (unsigned long long)g : lo;
+            hi = (unsigned long long)g > hi ? (unsigned long long)g : hi;
+        }
+    }
+    atomicMin(&out[2], lo);
+    atomicMax(&out[3], hi);
 }
 
 // ---- step 2 ----------------------------------------------------------------------------------
@@ -468,7 +498,8 @@ __global__ __launch_bounds__(256) void k_fold_chunk_sums(const float* __restrict
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) cs[c] = v;
 }
-__global__ __launch_bounds__(1024) void k_fold_bases(const double* __restrict__ cs, int64_t nc, int32_t* __restrict__ base) {
+__global__ __launch_bounds__(1024) void k_fold_bases(const double* __restrict__ cs, int64_t nc, int32_t* __restrict__ base,
+                                                    double* __restrict__ est) {
     __shared__ double s_w[16];
     __shared__ double s_carry;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -487,14 +518,23 @@ __global__ __launch_bounds__(1024) void k_fold_bases(const double* __restrict__ 
         __syncthreads();
         double off = s_carry;
         for (int k = 0; k < w; ++k) off += s_w[k];
-        if (i < nc) base[i] = fold_base(off + inc - v);   // the estimate of the sum before chunk i
+        if (i < nc) {
+            base[i] = fold_base(off + inc - v);   // the estimate of the sum before chunk i
+            est[i] = off + inc - v;
+        }
         __syncthreads();
         if (t == 1023) s_carry = off + inc;
         __syncthreads();
     }
+    if (t == 0) est[nc] = s_carry;
 }
+// hint[c] = 1: the walk will probably need chunk c's terms (the estimate is 0, the estimated sum
+// crosses a power of two inside the chunk, with a margin of 2^-7 for the float chain's drift from the
+// double estimate, or the chunk is flagged in the binades the estimate puts s in) -- k_fold_walk
+// stages those chunks' terms in LDS beforehand
 __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e, int64_t n, const int32_t* __restrict__ base,
-                                                    uint32_t* __restrict__ sum, uint8_t* __restrict__ flags) {
+                                                    const double* __restrict__ est, uint32_t* __restrict__ sum,
+                                                    uint8_t* __restrict__ flags, uint8_t* __restrict__ hint) {
     const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (c >= fold_chunks(n)) return;   // uniform per wave
@@ -505,6 +545,7 @@ __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e,
         bits[q] = k < n ? __float_as_uint(e[k]) : 0u;   // +0 past the end contributes nothing
     }
     const int E0 = base[c];
+    uint32_t fl34 = 0;
 #pragma unroll
     for (int b = 0; b < kFoldBinades; ++b) {
         uint32_t s = 0, f = 0;
@@ -523,6 +564,344 @@ __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e,
             sum[c * kFoldBinades + b] = s;
             flags[c * kFoldBinades + b] = (uint8_t)f;
         }
+        if (b == 3 || b == 4) fl34 |= f;
+    }
+    if (lane == 0) {
+        const double lo = est[c] * (1.0 - 0x1p-7), hi = est[c + 1] * (1.0 + 0x1p-7);
+        int elo = 0, ehi = 0;
+        (void)frexp(lo, &elo);
+        (void)frexp(hi, &ehi);
+        hint[c] = (uint8_t)(!(est[c] > 0.0) || elo != ehi || fl34 != 0 || !(hi < 0x1p100));
+    }
+}
+
+// The serial chain itself, walked on the device by one wave (no host round trip): the exact sum s
+// advances over whole chunks from the table, 64 chunks per wave step (the lanes' integer sums of the
+// binade s is in, prefix-summed; the run stops at the first chunk that is flagged, outside its
+// window, or would leave the binade), and inside a chunk the table could not take, over the terms
+// up to the next event (a tie, an unusable term, the binade's end: the same prefix over the terms'
+// rounded multiples of the spacing), the event term then added as the float add of the chain.  Every
+// step either adds exactly what the chain adds (fold.hpp) or is the chain's own float add, so the
+// result is the serial chain's bit for bit (fold_walk's semantics: the first NaN term decides the
+// result, quieted as x86's addss quiets it; after an inf only a NaN changes the sum).  Then the
+// average edge length and make_alpha_list (cp:144-194) for it, into FoldOut.
+__device__ __forceinline__ float quiet_nan_of(float x) { return __uint_as_float(__float_as_uint(x) | 0x400000u); }
+
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t x, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// Inclusive wave scan of u32 through DPP (gfx9: row_shr 1, 2, 4, 8 inside rows of 16 lanes, then
+// row_bcast 15 and 31 into the rows above): a few cycles per step, where a ds_bpermute shuffle
+// takes a round trip through LDS -- the walk is a chain of such scans
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return x;
+}
+__device__ __forceinline__ uint32_t lane_value(uint32_t x, int lane) {   // lane: wave-uniform
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, lane);
+}
+
+// make_alpha_list(avg, 0.001, avg, 20) (cp:144-194) as the host called it: at most kMaxHalvings
+// halvings (the reference loops forever on an infinite average; any finite one ends within 140)
+__device__ void alpha_list_dev(float avg, FoldOut* o) {
+    const float unit = avg, min_step = (float)(0.001 * 1.0);
+    float step = (float)(avg * 1.0);
+    int n = 0;
+    for (int h = 0; h < kMaxHalvings && step > min_step; ++h) {
+        step = (float)((double)step * 0.5);
+        const double q = floor((double)(avg / fabsf(step)) + 0.001);
+        // (int) of a double as x86's cvttsd2si: out of range or NaN gives INT_MIN
+        const int total = (q >= -2147483648.0 && q < 2147483648.0) ? (int)q : (int)0x80000000u;
+        const int ms = 20 < total ? 20 : total;
+        for (int i = 1; i < ms + 1; i += 2) {
+            const float alpha = (float)i * step;
+            o->alphas[n++] = alpha / unit;
+            o->alphas[n++] = -alpha / unit;
+        }
+    }
+    o->nal = n;
+}
+
+// One block: its waves stage a window of the table (kWalkWindow chunk rows) and the terms of the
+// window's hinted chunks (kWalkSlots of them) in LDS, then wave 0 walks the window from LDS; terms
+// of an unhinted chunk the walk needs are read from memory.
+constexpr int kWalkThreads = 1024, kWalkWindow = 1536, kWalkSlots = 40;
+
+// fold_term (fold.hpp) without branches, for the walk: the rounded multiple of the spacing
+// 2^(E-24) of a term, and whether the chain must add it as a float (a tie, a term too large,
+// negative, inf or NaN) -- the same values and the same "flagged" as fold_term's flags != 0
+__device__ __forceinline__ uint32_t walk_term(uint32_t bits, int E, bool& flag) {
+    const uint32_t ex = (bits >> 23) & 0xffu, frac = bits & 0x7fffffu, mag = bits & 0x7fffffffu;
+    const bool special = ex == 0xffu, neg = (bits >> 31) != 0u && mag != 0u, zero = mag == 0u;
+    const uint32_t M = frac | (ex ? 0x800000u : 0u);
+    const int sh = (ex ? (int)ex : 1) - 150 + 24 - E;
+    const int d = -sh;
+    const int dd = d < 1 ? 1 : (d > 25 ? 25 : d);
+    const uint32_t half = 1u << (dd - 1), rem = M & ((1u << dd) - 1u), rd = (M + half) >> dd;
+    const uint32_t up = M << (sh < 0 ? 0 : (sh > 7 ? 7 : sh));
+    const uint32_t upc = sh >= 8 || up >= kFoldCap ? kFoldCap : up;
+    const bool plain = !(zero || neg || special);
+    flag = special || neg || (!zero && sh >= 8) || (plain && sh < 0 && d <= 25 && rem == half);
+    return !plain ? 0u : sh >= 0 ? upc : (d > 25 ? 0u : rd);
+}
+
+__global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restrict__ e, int64_t n64,
+                                                            const int32_t* __restrict__ base, const uint32_t* __restrict__ sum,
+                                                            const uint8_t* __restrict__ flags, const uint8_t* __restrict__ hint,
+                                                            int64_t nf, FoldOut* __restrict__ out) {
+    __shared__ uint32_t w_sum[kWalkWindow * kFoldBinades];
+    __shared__ uint8_t w_flag[kWalkWindow * kFoldBinades];
+    __shared__ int32_t w_base[kWalkWindow];
+    __shared__ int16_t w_slot[kWalkWindow];
+    __shared__ int16_t w_slot_chunk[kWalkSlots];
+    __shared__ float w_terms[kWalkSlots][kFoldChunk];
+    __shared__ int w_nslots;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int n = (int)n64;   // < 2^31 (launch_fold checks)
+    const int nc = (int)fold_chunks(n64);
+    float s = 0.f;       // wave 0: the chain's exact value after term k - 1
+    int k = 0;
+    int table_chunks = 0;
+    bool done = false;   // wave 0: a NaN or an inf decided the result
+    int st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+    long long cyc_stage = 0, cyc_walk = 0;
+    for (int c0 = 0; c0 < nc; c0 += kWalkWindow) {
+        const long long tc0 = clock64();
+        const int wn = nc - c0 < kWalkWindow ? nc - c0 : kWalkWindow;
+        if (t == 0) w_nslots = 0;
+        __syncthreads();   // the previous window's walk is over
+        for (int i = t; i < wn; i += kWalkThreads) {
+            const int64_t c = c0 + i;
+            w_base[i] = base[c];
+#pragma unroll
+            for (int b = 0; b < kFoldBinades; ++b) {
+                w_sum[i * kFoldBinades + b] = sum[c * kFoldBinades + b];
+                w_flag[i * kFoldBinades + b] = flags[c * kFoldBinades + b];
+            }
+            int sl = -1;
+            if (hint[c]) {
+                sl = atomicAdd(&w_nslots, 1);
+                if (sl < kWalkSlots) w_slot_chunk[sl] = (int16_t)i;
+                else sl = -1;
+            }
+            w_slot[i] = (int16_t)sl;
+        }
+        __syncthreads();
+        const int ns = w_nslots < kWalkSlots ? w_nslots : kWalkSlots;
+        for (int i = t; i < ns * kFoldChunk; i += kWalkThreads) {
+            const int sl = i / kFoldChunk, j = i % kFoldChunk;
+            const int kk = (c0 + w_slot_chunk[sl]) * kFoldChunk + j;
+            w_terms[sl][j] = kk < n ? e[kk] : 0.f;
+        }
+        __syncthreads();
+        const long long tc1 = clock64();
+        cyc_stage += tc1 - tc0;
+        if (wid != 0) continue;
+        const int kend_w = (c0 + wn) * kFoldChunk < n ? (c0 + wn) * kFoldChunk : n;
+        while (!done && k < kend_w) {   // uniform over wave 0
+            // the walk's state is wave-uniform: kept in scalar registers, so its branches are scalar
+            k = __builtin_amdgcn_readfirstlane(k);
+            s = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s)));
+            if (!(s >= 0x1p-100f && s <= 0x1p100f)) {
+                ++st0;
+                if (s == 0.f) {   // 0 + (+-0) = +0: on to the first term of nonzero magnitude (or NaN)
+                    const int kk = k + lane;
+                    const bool in = kk < kend_w;
+                    const uint64_t m = __ballot(in && (__float_as_uint(e[in ? kk : k]) & 0x7fffffffu) != 0u);
+                    if (!m) {
+                        k = k + 64 < kend_w ? k + 64 : kend_w;
+                        continue;
+                    }
+                    k += __ffsll((unsigned long long)m) - 1;
+                } else if (s == INFINITY) {   // only a NaN term changes it: the first one decides
+                    for (; k < n; k += 64) {
+                        const int kk = k + lane;
+                        const float x = e[kk < n ? kk : 0];
+                        const uint64_t m = __ballot(kk < n && x != x);
+                        if (m) {
+                            s = quiet_nan_of(e[k + __ffsll((unsigned long long)m) - 1]);
+                            break;
+                        }
+                    }
+                    done = true;
+                    break;
+                }
+                // tiny, huge or negative, or the first nonzero term after zeros: one float add
+                const float x = e[k];
+                if (x != x) { s = quiet_nan_of(x); done = true; break; }
+                s = s + x;
+                ++k;
+                continue;
+            }
+            int E = 0;
+            (void)frexpf(s, &E);   // s in [2^(E-1), 2^E): spacing 2^(E-24)
+            E = __builtin_amdgcn_readfirstlane(E);
+            uint32_t su = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E));   // in [2^23, 2^24)
+            if ((k & (kFoldChunk - 1)) == 0) {   // whole chunks from the table, 4 per lane: 256 per step
+                if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (1 << 28) | k;
+                ++st1;
+                const int i0 = k / kFoldChunk - c0 + 4 * lane;
+                uint32_t v[4];
+                bool ok[4];
+                int bb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bb[j] = E - w_base[i0 + j < wn ? i0 + j : wn - 1];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int i = i0 + j < wn ? i0 + j : wn - 1;
+                    const bool inb = i0 + j < wn && bb[j] >= 0 && bb[j] < kFoldBinades;
+                    const int cell = i * kFoldBinades + (inb ? bb[j] : 0);
+                    v[j] = w_sum[cell];
+                    ok[j] = inb && w_flag[cell] == 0;
+                }
+                uint32_t T = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) T += ok[j] ? v[j] : 0u;   // below 2^26
+                // lanes clamped at 2^24 keep the scan below 2^30; such a lane holds the run's end
+                const uint32_t Tc = T < kFoldCap ? T : kFoldCap;
+                const uint32_t incl = wave_scan_dpp(Tc), excl = incl - Tc;
+                int first = 4;
+                uint32_t run = excl, before = excl;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t vj = ok[j] ? v[j] : 0u;
+                    if (first == 4 && (!ok[j] || su + run + vj >= kFoldCap)) { first = j; before = run; }
+                    run += vj;
+                }
+                const uint64_t lm = __ballot(first < 4);
+                const int L = lm ? __ffsll((unsigned long long)lm) - 1 : 63;
+                const int fb = lm ? 4 * L + (int)lane_value((uint32_t)first, L) : 256;
+                if (fb > 0) {
+                    const uint32_t tt = su + (lm ? lane_value(before, L) : lane_value(incl, 63));   // < 2^24: exact
+                    s = ldexpf((float)tt, E - 24);
+                    table_chunks += fb;
+                    k += fb * kFoldChunk;
+                    if (k >= kend_w) {
+                        if (k > n) k = n;
+                        continue;
+                    }
+                    // the chunk that ended the run goes term by term now (same binade: tt < 2^24)
+                    k = __builtin_amdgcn_readfirstlane(k);
+                    su = tt;
+                }
+            }
+            // the chunk's terms from k, 4 consecutive per lane, in order: their rounded multiples of the
+            // spacing in this binade, up to the first event; that term is added as the chain's float add,
+            // and if it was the crossing into the next binade, the chunk's run continues there in the
+            // same step (the terms' multiples of the next binade's spacing)
+            if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (2 << 28) | k | (E + 64) << 20;
+            ++st2;
+            const int kc = k & ~(kFoldChunk - 1);
+            const int kend = kc + kFoldChunk < n ? kc + kFoldChunk : n;
+            uint32_t q0[4], xb[4];
+            bool ev0[4];
+            // the chunk's terms: from LDS if it was staged (uniform: one chunk), else from memory, all
+            // four loads issued before any use
+            const int sl = __builtin_amdgcn_readfirstlane((int)w_slot[k / kFoldChunk - c0]);
+            if (sl >= 0) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int kk = k + 4 * lane + j;
+                    xb[j] = kk < kend ? __float_as_uint(w_terms[sl][kk & (kFoldChunk - 1)]) : 0u;
+                }
+            } else {
+                ++st3;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int kk = k + 4 * lane + j;
+                    xb[j] = __float_as_uint(e[kk < kend ? kk : k]);
+                    if (kk >= kend) xb[j] = 0u;
+                }
+            }
+            uint32_t T0 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                q0[j] = walk_term(xb[j], E, ev0[j]);   // a term past the chunk is +0: 0, no event
+                T0 += q0[j];                           // each q <= 2^24: below 2^26
+            }
+            // lane totals clamped at 2^24 keep the scan below 2^30; a lane whose terms reach that holds
+            // the first event, so every sum before it is exact
+            const uint32_t T0c = T0 < kFoldCap ? T0 : kFoldCap;
+            const uint32_t incl0 = wave_scan_dpp(T0c), excl0 = incl0 - T0c;
+            int first = 4;
+            uint32_t run = excl0, before = excl0, xe = 0;
+            bool flagged = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (first == 4 && (ev0[j] || su + run + q0[j] >= kFoldCap)) {
+                    first = j; before = run; xe = xb[j]; flagged = ev0[j];
+                }
+                run += q0[j];
+            }
+            const uint64_t lm = __ballot(first < 4);
+            if (!lm) {
+                s = ldexpf((float)(su + lane_value(incl0, 63)), E - 24);
+                k = kend;
+                continue;
+            }
+            const int L = __ffsll((unsigned long long)lm) - 1;
+            const int jf = (int)lane_value((uint32_t)first, L);
+            s = ldexpf((float)(su + lane_value(before, L)), E - 24);   // exact: the chain before the event
+            const int t1 = k + 4 * L + jf;
+            const float x = __uint_as_float(lane_value(xe, L));
+            if (x != x) { s = quiet_nan_of(x); done = true; break; }
+            s = s + x;   // the event term: the chain's own float add
+            const int kstep = k;
+            k = t1 + 1;
+            int E1 = 0;
+            (void)frexpf(s, &E1);
+            if (lane_value(flagged ? 1u : 0u, L) || E1 != E + 1 || !(s <= 0x1p100f) || k >= kend) continue;
+            // lookahead in binade E + 1 over the terms after the crossing
+            const uint32_t su1 = (uint32_t)ldexpf(s, 24 - E1);
+            uint32_t q1[4], T1 = 0;
+            bool ev1[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool after = kstep + 4 * lane + j > t1;
+                q1[j] = walk_term(after ? xb[j] : 0u, E1, ev1[j]);
+                T1 += q1[j];
+            }
+            const uint32_t T1c = T1 < kFoldCap ? T1 : kFoldCap;
+            const uint32_t incl1 = wave_scan_dpp(T1c), excl1 = incl1 - T1c;
+            int first1 = 4;
+            uint32_t r1 = excl1, before1 = excl1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (first1 == 4 && (ev1[j] || su1 + r1 + q1[j] >= kFoldCap)) { first1 = j; before1 = r1; }
+                r1 += q1[j];
+            }
+            const uint64_t lm1 = __ballot(first1 < 4);
+            if (!lm1) {
+                s = ldexpf((float)(su1 + lane_value(incl1, 63)), E1 - 24);
+                k = kend;
+                continue;
+            }
+            const int L1 = __ffsll((unsigned long long)lm1) - 1;
+            const int j1 = (int)lane_value((uint32_t)first1, L1);
+            s = ldexpf((float)(su1 + lane_value(before1, L1)), E1 - 24);   // exact: the chain before that event
+            k = kstep + 4 * L1 + j1;                                         // the next step starts at it
+        }
+        cyc_walk += clock64() - tc1;
+    }
+    if (t == 0) {
+        out->sum = s;
+        out->table_chunks = table_chunks;
+        out->steps[0] = st0; out->steps[1] = st1; out->steps[2] = st2; out->steps[3] = st3;
+        out->cycles[0] = cyc_stage; out->cycles[1] = cyc_walk;
+        const float avg = (float)((double)s / (3. * (double)nf));
+        out->avg = avg;
+        alpha_list_dev(avg, out);
     }
 }
 
@@ -637,9 +1016,10 @@ __device__ int jacobi_svd3(const float A[3][3], float thr, float S[3], float U[3
 // vertex_apply_qem (qem.hpp:321-599) with get_A_b (:256-316), one lane per vertex
 __global__ __launch_bounds__(256) void k_qem(float* __restrict__ verts, int64_t nv, const uint32_t* __restrict__ off,
                                              const int32_t* __restrict__ lst, const float* __restrict__ C,
-                                             const float* __restrict__ N, float maxd) {
+                                             const float* __restrict__ N, const FoldOut* __restrict__ fo) {
     const int64_t vi = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (vi >= nv) return;
+    const float maxd = fo->avg;   // the average edge length (k_fold_walk), in stream order
     float* v = verts + 3 * vi;
     const float ox = v[0], oy = v[1], oz = v[2];
     float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, b[3] = {0.f, 0.f, 0.f};
@@ -678,25 +1058,6 @@ __global__ __launch_bounds__(256) void k_qem(float* __restrict__ verts, int64_t 
 }
 
 // ---- host helpers ------------------------------------------------------------------------------
-// make_alpha_list cp:144-194
-std::vector<float> make_alpha_list(float initial_step, float min_step, float max_dist, int max_iter) {
-    std::vector<float> a;
-    const float unit = max_dist;
-    float step = initial_step;
-    while (step > min_step) {
-        step = (float)(step * 0.5);
-        const int total = (int)std::floor((double)(max_dist / std::fabs(step)) + 0.001);
-        const int ms = max_iter < total ? max_iter : total;
-        for (int i = 1; i < ms + 1; i += 2) {
-            const float alpha = (float)i * step;
-            a.push_back(alpha / unit);
-            a.push_back(-alpha / unit);
-        }
-        if (a.size() > 100000) break;   // guards a pathological max_dist
-    }
-    return a;
-}
-
 // boost::random::mt11213b (seed 12) + uniform_01<float>: make_random_pm1(n, 3, 1e-6)
 // (make_random_pm1.hpp:15-29): the twist in three runs (no index wrap inside), tempering of a
 // whole block at once, then uniform_01's rejection of draws that round to 1.0f
@@ -772,6 +1133,7 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     evals_ = 0;
     jit_launches_ = 0;
     avg_edge_ = 0.f;
+    avg_valid_ = true;
     for (double& t : stage_ms_) t = 0.0;
     Stage st(this, kStageTopology);
     IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 64, s));   // (unused), cap hits, evaluations
@@ -782,6 +1144,45 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     if (nf) IMPLI_HIP(hipMemcpyAsync(faces_.p, d_faces, (size_t)nf * 12, hipMemcpyDeviceToDevice, s));
     start_perturbations();   // host thread, overlaps the topology and resampling kernels
     build_topology();
+    own_v0_ = 0; own_v1_ = nv; wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
+    sharded_ = false;
+}
+
+void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
+    if (v0 < 0 || v1 < v0 || v1 > nv) throw InputError("ob02: owned vertex range outside the mesh");
+    if (!topo_valid_) build_topology();
+    own_v0_ = v0;
+    own_v1_ = v1;
+    sharded_ = !(v0 == 0 && v1 == nv);
+    if (!sharded_) {
+        wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
+        return;
+    }
+    DevBuf& r = scan_tmp_;   // scratch: 4 x u64 (only topology uses it, before this)
+    r.reserve(64);
+    const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
+    IMPLI_HIP(hipMemcpyAsync(r.p, init, sizeof init, hipMemcpyHostToDevice, s));
+    if (nf) k_touch_range<<<blocks_for(nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, v0, v1, r.as<unsigned long long>());
+    unsigned long long h[4];
+    IMPLI_HIP(hipMemcpyAsync(h, r.p, sizeof h, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    if (h[0] > h[1]) {   // no face touches the owned vertices
+        wf0_ = wf1_ = cf0_ = cf1_ = 0;
+        return;
+    }
+    wf0_ = (int64_t)h[0];
+    wf1_ = (int64_t)h[1] + 1;
+    IMPLI_HIP(hipMemcpyAsync(r.p, init, sizeof init, hipMemcpyHostToDevice, s));
+    k_fof_range<<<blocks_for(wf1_ - wf0_), 256, 0, s>>>(fof_.as<int32_t>(), wf0_, wf1_, r.as<unsigned long long>());
+    IMPLI_HIP(hipMemcpyAsync(h, r.p, sizeof h, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    cf0_ = (int64_t)h[2];
+    cf1_ = (int64_t)h[3] + 1;
+    IMPLI_HIP(hipGetLastError());
+}
+
+void Ob02::ranges(int64_t out[6]) const {
+    out[0] = own_v0_; out[1] = own_v1_; out[2] = wf0_; out[3] = wf1_; out[4] = cf0_; out[5] = cf1_;
 }
 
 EdgeTab Ob02::edge_table() {
@@ -867,14 +1268,13 @@ const std::map<std::string, std::vector<float>>& Ob02::pointsets() {
 
 Ob02::~Ob02() {
     if (pert_job_.valid()) pert_job_.wait();
-    if (norms_ready_) (void)hipEventDestroy(norms_ready_);
+    if (walk_done_) (void)hipEventDestroy(walk_done_);
     if (table_done_) (void)hipEventDestroy(table_done_);
-    if (copy_s_) (void)hipStreamDestroy(copy_s_);
-    host_norms_.release();
+    if (walk_s_) (void)hipStreamDestroy(walk_s_);
     dir_.release();
     evals_buf_.release();
     for (DevBuf* b : {&verts_, &faces_, &vnew_, &cen_, &nrm_, &w_, &fof_, &uoff_, &ulst_, &etab_, &deg_, &proj_, &grad_,
-                      &fn_, &norms_, &alphas_, &pert_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_, &fold_sum_})
+                      &fn_, &norms_, &pert_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_, &fold_sum_, &fold_out_})
         b->release();
     for (auto& kv : snaps_) kv.second.buf.release();
 }
@@ -884,71 +1284,129 @@ void Ob02::vertex_resampling(float c) {
     if (!topo_valid_) build_topology();
     Stage st(this, kStageResample);
     store_pointset("pre_resampling_vertices", verts_.as<float>(), nv, true);   // vertex_resampling.hpp:176-180
-    if (const TreeJit::PointKernels* pk = E.point_jit()) {
-        const float *m = E.d_mats(), *tab = E.d_rabbit(), *v = verts_.as<float>();
-        const int32_t* f = faces_.as<int32_t>();
-        float *C = cen_.as<float>(), *N = nrm_.as<float>();
-        void* args[] = {&m, &tab, &v, &f, &nf, &C, &N};
-        TreeJit::launch(pk->cnormals, blocks_for(nf), args, s, "impli_pt_centroid_normals");
-        ++jit_launches_;
-    } else {
-        DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), verts_.as<float>(),
-                     faces_.as<int32_t>(), nf, cen_.as<float>(), nrm_.as<float>());
+    // centroids and normals of faces [cf0, cf1), weights of [wf0, wf1), vertices [v0, v1) (the whole
+    // mesh unless sharded); per-face pointers are offset to the range's first face
+    const int64_t ncf = cf1_ - cf0_;
+    if (ncf > 0) {
+        if (const TreeJit::PointKernels* pk = E.point_jit()) {
+            const float *m = E.d_mats(), *tab = E.d_rabbit(), *v = verts_.as<float>();
+            const int32_t* f = faces_.as<int32_t>() + 3 * cf0_;
+            float *C = cen_.as<float>() + 3 * cf0_, *N = nrm_.as<float>() + 3 * cf0_;
+            int64_t n = ncf;
+            void* args[] = {&m, &tab, &v, &f, &n, &C, &N};
+            TreeJit::launch(pk->cnormals, blocks_for(ncf), args, s, "impli_pt_centroid_normals");
+            ++jit_launches_;
+        } else {
+            DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(ncf), 256, s, E.d_program(), E.d_rabbit(), verts_.as<float>(),
+                         faces_.as<int32_t>() + 3 * cf0_, ncf, cen_.as<float>() + 3 * cf0_, nrm_.as<float>() + 3 * cf0_);
+        }
     }
-    k_face_weights<<<blocks_for(nf), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(), nf, c, w_.as<float>());
-    k_resample<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), w_.as<float>(), cen_.as<float>(),
-                                              nv, vnew_.as<float>());
+    if (wf1_ > wf0_)
+        k_face_weights<<<blocks_for(wf1_ - wf0_), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(), wf0_,
+                                                                wf1_, c, w_.as<float>());
+    if (own_v1_ > own_v0_)
+        k_resample<<<blocks_for(own_v1_ - own_v0_), 256, 0, s>>>(uoff_.as<uint32_t>() + own_v0_, ulst_.as<int32_t>(),
+                                                                  w_.as<float>(), cen_.as<float>(), own_v1_ - own_v0_,
+                                                                  vnew_.as<float>() + 3 * own_v0_);
     std::swap(verts_, vnew_);
     IMPLI_HIP(hipGetLastError());
     store_pointset("post_resampling_vertices", verts_.as<float>(), nv, true);   // :207-211
 }
 
-// compute_average_edge_length (cp:70-82) is one serial float chain in face order: the terms are
-// computed on the device and copied to pinned host memory; the chain runs on the host (one GPU lane
-// adds a dependent term every ~4 cycles at 2.4 GHz, slower than a host core) while the GPU runs the
-// projection's prep pass, which does not need the average.
+// the fold's device buffers in one allocation: [sums u32 (cells) | bases i32 (chunks) | flags u8
+// (cells) | hints u8 (chunks)], then the chunks' double sums and the estimates (chunks + 1 each)
+struct FoldLayout {
+    int64_t chunks, cells;
+    size_t cs_off, est_off, bytes;
+    explicit FoldLayout(int64_t n) : chunks(fold_chunks(n)), cells(fold_chunks(n) * kFoldBinades) {
+        const size_t tab = (size_t)(cells + chunks) * 4 + (size_t)cells + (size_t)chunks;
+        cs_off = (tab + 15) & ~(size_t)15;
+        est_off = cs_off + (size_t)(chunks + 1) * 8;
+        bytes = est_off + (size_t)(chunks + 1) * 8;
+    }
+};
+
+// the table passes on `ts`, then the walk on `ws` after them (ws may be ts)
+void launch_fold(const float* d_terms, int64_t n, int64_t nf, char* d_tab, FoldOut* d_out, hipStream_t ts, hipStream_t ws,
+                 hipEvent_t table_done) {
+    if (n >= ((int64_t)1 << 31) - kFoldChunk) throw InputError("edge-length fold: more than 2^31 terms");
+    const FoldLayout L(n);
+    uint32_t* d_sum = reinterpret_cast<uint32_t*>(d_tab);
+    int32_t* d_base = reinterpret_cast<int32_t*>(d_sum + L.cells);
+    uint8_t* d_flags = reinterpret_cast<uint8_t*>(d_base + L.chunks);
+    uint8_t* d_hint = d_flags + L.cells;
+    double* d_cs = reinterpret_cast<double*>(d_tab + L.cs_off);
+    double* d_est = reinterpret_cast<double*>(d_tab + L.est_off);
+    if (L.cells) {
+        k_fold_chunk_sums<<<blocks_for(L.chunks * 64), 256, 0, ts>>>(d_terms, n, d_cs);
+        k_fold_bases<<<1, 1024, 0, ts>>>(d_cs, L.chunks, d_base, d_est);
+        k_fold_table<<<blocks_for(L.chunks * 64), 256, 0, ts>>>(d_terms, n, d_base, d_est, d_sum, d_flags, d_hint);
+    }
+    if (ws != ts) {
+        IMPLI_HIP(hipEventRecord(table_done, ts));
+        IMPLI_HIP(hipStreamWaitEvent(ws, table_done, 0));
+    }
+    k_fold_walk<<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_sum, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
+}
+
+// compute_average_edge_length (cp:70-82) is one serial float chain in face order.  The terms and
+// the fold's chunk table (fold.hpp) are computed on s; the walk (k_fold_walk, one wave) then runs
+// on a second stream while s runs the projection's prep pass, which does not need the average, and
+// s waits for the walk before the searches.  No host round trip: the average and the alpha list stay
+// in device memory (FoldOut) for the searches and QEM.
 void Ob02::start_edge_fold() {
     norms_.reserve((size_t)(nf + 1) * 12);
     k_edge_norms<<<blocks_for(nf), 256, 0, s>>>(verts_.as<float>(), faces_.as<int32_t>(), nf, norms_.as<float>());
-    // the chunk table of the serial fold (fold.hpp) and the terms themselves go to pinned memory
-    const int64_t chunks = fold_chunks(3 * nf), cells = chunks * kFoldBinades;
-    // the table, device and host alike: [sums (cells u32) | bases (chunks i32) | flags (cells u8)],
-    // then on the device the chunks' double sums; the host's pinned buffer holds the terms first
-    const size_t tab_bytes = (size_t)(cells + chunks) * 4 + (size_t)cells, cs_off = (tab_bytes + 15) & ~(size_t)15;
-    fold_sum_.reserve(cs_off + (size_t)(chunks + 1) * 8);
-    const size_t terms_bytes = ((size_t)nf * 12 + 15) & ~(size_t)15;
-    host_norms_.reserve(terms_bytes + tab_bytes + 16);
-    uint32_t* d_sum = fold_sum_.as<uint32_t>();
-    int32_t* d_base = reinterpret_cast<int32_t*>(d_sum + cells);
-    uint8_t* d_flags = reinterpret_cast<uint8_t*>(d_base + chunks);
-    double* d_cs = reinterpret_cast<double*>(fold_sum_.as<char>() + cs_off);
-    if (cells) {
-        k_fold_chunk_sums<<<blocks_for(chunks * 64), 256, 0, s>>>(norms_.as<float>(), 3 * nf, d_cs);
-        k_fold_bases<<<1, 1024, 0, s>>>(d_cs, chunks, d_base);
-        k_fold_table<<<blocks_for(chunks * 64), 256, 0, s>>>(norms_.as<float>(), 3 * nf, d_base, d_sum, d_flags);
-    }
-    // the copies run on their own stream, so the projection's prep pass (next on s) overlaps them
-    if (!copy_s_) IMPLI_HIP(hipStreamCreateWithFlags(&copy_s_, hipStreamNonBlocking));
+    const FoldLayout L(3 * nf);
+    fold_sum_.reserve(L.bytes);
+    fold_out_.reserve(sizeof(FoldOut));
+    if (!walk_s_) IMPLI_HIP(hipStreamCreateWithFlags(&walk_s_, hipStreamNonBlocking));
     if (!table_done_) IMPLI_HIP(hipEventCreateWithFlags(&table_done_, hipEventDisableTiming));
-    if (!norms_ready_) IMPLI_HIP(hipEventCreateWithFlags(&norms_ready_, hipEventDisableTiming));
-    IMPLI_HIP(hipEventRecord(table_done_, s));
-    IMPLI_HIP(hipStreamWaitEvent(copy_s_, table_done_, 0));
-    if (cells)
-        IMPLI_HIP(hipMemcpyAsync(host_norms_.as<char>() + terms_bytes, fold_sum_.p, tab_bytes, hipMemcpyDeviceToHost, copy_s_));
-    IMPLI_HIP(hipMemcpyAsync(host_norms_.p, norms_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, copy_s_));
-    IMPLI_HIP(hipEventRecord(norms_ready_, copy_s_));
+    if (!walk_done_) IMPLI_HIP(hipEventCreateWithFlags(&walk_done_, hipEventDisableTiming));
+    launch_fold(norms_.as<float>(), 3 * nf, nf, fold_sum_.as<char>(), fold_out_.as<FoldOut>(), s, walk_s_, table_done_);
+    IMPLI_HIP(hipEventRecord(walk_done_, walk_s_));
+    avg_valid_ = false;
 }
 
-float Ob02::finish_edge_fold() {
-    IMPLI_HIP(hipEventSynchronize(norms_ready_));
-    // the serial chain (the reference starts from an uninitialised float, F8a; defined as 0), from
-    // the device's chunk table: bit-identical (fold.hpp, tools/fold_check.cpp), a few chunks term
-    // by term
-    const int64_t chunks = fold_chunks(3 * nf), cells = chunks * kFoldBinades;
-    const uint32_t* sums = reinterpret_cast<const uint32_t*>(host_norms_.as<char>() + (((size_t)nf * 12 + 15) & ~(size_t)15));
-    const int32_t* bases = reinterpret_cast<const int32_t*>(sums + cells);
-    const float el = fold_walk(host_norms_.as<float>(), 3 * nf, bases, sums, reinterpret_cast<const uint8_t*>(bases + chunks));
-    return (float)((double)el / (3. * (double)nf));
+void Ob02::finish_edge_fold() {   // s waits for the walk (stream order, no host sync)
+    IMPLI_HIP(hipStreamWaitEvent(s, walk_done_, 0));
+}
+
+// the fold alone on given terms (diagnostics / tests): the same table kernels and walk as a
+// projection, on the null stream; returns the chain's sum and the chunks taken from the table
+float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* stats, int* trace) {
+    const FoldLayout L(n);
+    DevBuf terms, tab, fo;
+    terms.reserve((size_t)(n + 1) * 4);
+    tab.reserve(L.bytes);
+    fo.reserve(sizeof(FoldOut));
+    if (n) IMPLI_HIP(hipMemcpy(terms.p, h_terms, (size_t)n * 4, hipMemcpyHostToDevice));
+    launch_fold(terms.as<float>(), n, n, tab.as<char>(), fo.as<FoldOut>(), 0, 0, nullptr);
+    IMPLI_HIP(hipGetLastError());
+    FoldOut h;
+    IMPLI_HIP(hipMemcpy(&h, fo.p, offsetof(FoldOut, alphas), hipMemcpyDeviceToHost));
+    if (trace) std::memcpy(trace, h.trace, sizeof h.trace);
+    terms.release();
+    tab.release();
+    fo.release();
+    if (table_chunks) *table_chunks = h.table_chunks;
+    if (stats) {
+        for (int i = 0; i < 4; ++i) stats[i] = h.steps[i];
+        stats[4] = h.cycles[0];
+        stats[5] = h.cycles[1];
+    }
+    return h.sum;
+}
+
+float Ob02::last_average_edge() {   // blocking: the last fold's average, read back once
+    if (!avg_valid_ && fold_out_.p) {
+        FoldOut h;
+        IMPLI_HIP(hipMemcpyAsync(&h, fold_out_.p, offsetof(FoldOut, alphas), hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+        avg_edge_ = h.avg;
+        avg_valid_ = true;
+    }
+    return avg_edge_;
 }
 
 // make_random_pm1(nf, 3, 1e-6) (centroids_projection.cpp:239-262) is seeded afresh (seed 12) on
@@ -986,51 +1444,51 @@ void Ob02::centroids_projection(bool enable_qem) {
     pend_.reserve((size_t)(nf + 2) * 4);
     if (profile_) evals_buf_.reserve((size_t)(nf + 1) * 4);
     DevBuf& fcbuf = w_;   // f(centroid) per face; the resampling weights are dead here
+    // the work faces [wf0, wf1) (every face unless sharded): per-face pointers offset to the first
+    const int64_t j0 = wf0_, nw = wf1_ - wf0_;
     ProjArgs a{};
     a.v = verts_.as<float>();
-    a.f = faces_.as<int32_t>();
-    a.nf = nf;
-    a.out = proj_.as<float>();
-    a.fn = fn_.as<float>();
-    a.fc = fcbuf.as<float>();
-    a.pend = pend_.as<uint32_t>();
+    a.f = faces_.as<int32_t>() + 3 * j0;
+    a.nf = nw;
+    a.out = proj_.as<float>() + 3 * j0;
+    a.fn = fn_.as<float>() + 3 * j0;
+    a.fc = fcbuf.as<float>() + j0;
+    a.pend = pend_.as<uint32_t>() + j0;
     a.pend_count = misc_.as<uint32_t>();
     a.cap_hits = misc_.as<uint32_t>() + 1;
-    a.cen = cen_.as<float>();
-    a.dir = dir_.as<float>();
-    a.evals = profile_ ? evals_buf_.as<uint32_t>() : nullptr;
+    a.cen = cen_.as<float>() + 3 * j0;
+    a.dir = dir_.as<float>() + 3 * j0;
+    a.evals = profile_ ? evals_buf_.as<uint32_t>() + j0 : nullptr;
     const TreeJit::PointKernels* pk = E.point_jit();   // one choice for the whole projection
     const float *jm = E.d_mats(), *jtab = E.d_rabbit();
     void* jargs[] = {&jm, &jtab, &a};
-    if (pk) {
-        TreeJit::launch(pk->prep, blocks_for(nf), jargs, s, "impli_pt_project_prep");
+    if (nw <= 0) {
+        // no face touches this rank's vertices: nothing to project (the fold still ran, as on
+        // every rank)
+    } else if (pk) {
+        TreeJit::launch(pk->prep, blocks_for(nw), jargs, s, "impli_pt_project_prep");
         ++jit_launches_;
     } else {
-        DEPTH_LAUNCH(E.depth(), k_project_prep, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), a);
+        DEPTH_LAUNCH(E.depth(), k_project_prep, blocks_for(nw), 256, s, E.d_program(), E.d_rabbit(), a);
     }
     store_pointset("pre_p_centroids", cen_.as<float>(), nf, false);   // cp:1236-1238: the centroids
-    const float avg = finish_edge_fold();
-    avg_edge_ = avg;
-    alphas_host_ = make_alpha_list((float)(avg * 1.0), (float)(0.001 * 1.0), avg, 20);
-    alphas_.reserve((alphas_host_.size() + 1) * 4);
-    if (!alphas_host_.empty())
-        IMPLI_HIP(hipMemcpyAsync(alphas_.p, alphas_host_.data(), alphas_host_.size() * 4, hipMemcpyHostToDevice, s));
-    a.alphas = alphas_.as<float>();
-    a.nal = (int)alphas_host_.size();
-    a.max_dist = avg;
+    finish_edge_fold();
+    a.fold = fold_out_.as<FoldOut>();
     st.next(kStageProject);
-    const unsigned grid = blocks_for(nf * kProjGroup);
-    if (pk) TreeJit::launch(pk->early, grid, jargs, s, "impli_pt_project_early");
-    else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
+    const unsigned grid = blocks_for(nw * kProjGroup);
     // centroids left unresolved need the randomised directions (types 2-6): the late pass covers
     // every face and reads the early pass's per-face flags on the device (no host round trip)
-    a.pert = perturbations();
-    if (pk) TreeJit::launch(pk->late, grid, jargs, s, "impli_pt_project_late");
-    else DEPTH_LAUNCH(E.depth(), k_project_late, grid, 256, s, E.d_program(), E.d_rabbit(), a);
+    a.pert = perturbations() + 3 * j0;
+    if (nw > 0) {
+        if (pk) TreeJit::launch(pk->early, grid, jargs, s, "impli_pt_project_early");
+        else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
+        if (pk) TreeJit::launch(pk->late, grid, jargs, s, "impli_pt_project_late");
+        else DEPTH_LAUNCH(E.depth(), k_project_late, grid, 256, s, E.d_program(), E.d_rabbit(), a);
+    }
     IMPLI_HIP(hipGetLastError());
-    if (profile_) {   // the evaluations of this projection, summed on the host
-        std::vector<uint32_t> h((size_t)nf);
-        IMPLI_HIP(hipMemcpyAsync(h.data(), evals_buf_.p, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
+    if (profile_ && nw > 0) {   // the evaluations of this projection, summed on the host
+        std::vector<uint32_t> h((size_t)nw);
+        IMPLI_HIP(hipMemcpyAsync(h.data(), evals_buf_.as<uint32_t>() + j0, (size_t)nw * 4, hipMemcpyDeviceToHost, s));
         IMPLI_HIP(hipStreamSynchronize(s));
         for (uint32_t e : h) evals_ += e;
     }
@@ -1039,17 +1497,23 @@ void Ob02::centroids_projection(bool enable_qem) {
     if (enable_qem) {
         st.next(kStageQem);
         grad_.reserve((size_t)(nf + 1) * 12);
-        if (pk) {
-            const float* P = proj_.as<float>();
-            float* G = grad_.as<float>();
-            void* nargs[] = {&jm, &jtab, &P, &nf, &G};
-            TreeJit::launch(pk->normals, blocks_for(nf), nargs, s, "impli_pt_normals_at");
+        if (nw <= 0) {
+        } else if (pk) {
+            const float* P = proj_.as<float>() + 3 * j0;
+            float* G = grad_.as<float>() + 3 * j0;
+            int64_t n = nw;
+            void* nargs[] = {&jm, &jtab, &P, &n, &G};
+            TreeJit::launch(pk->normals, blocks_for(nw), nargs, s, "impli_pt_normals_at");
         } else {
-            DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nf), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>(), nf,
-                         grad_.as<float>());
+            DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nw), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>() + 3 * j0,
+                         nw, grad_.as<float>() + 3 * j0);
         }
-        if (nv) k_qem<<<blocks_for(nv), 256, 0, s>>>(verts_.as<float>(), nv, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
-                                                     proj_.as<float>(), grad_.as<float>(), avg);
+        // QEM of the owned vertices (all unless sharded), in place
+        const int64_t nov = own_v1_ - own_v0_;
+        if (nov > 0)
+            k_qem<<<blocks_for(nov), 256, 0, s>>>(verts_.as<float>() + 3 * own_v0_, nov, uoff_.as<uint32_t>() + own_v0_,
+                                                  ulst_.as<int32_t>(), proj_.as<float>(), grad_.as<float>(),
+                                                  fold_out_.as<FoldOut>());
         IMPLI_HIP(hipGetLastError());
         store_pointset("post_qem_verts", verts_.as<float>(), nv, false);
     }

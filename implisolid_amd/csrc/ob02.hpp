@@ -22,6 +22,19 @@ public:
     // takes a copy of the MC mesh (device pointers) and builds the face/vertex topology; resets
     // the point sets and counters, so one Ob02 serves many builds (its buffers are grow-only)
     void load_mesh(const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf);
+    // Z-slab sharding of the loop (one Ob02 per rank, each holding the whole mesh): this rank owns
+    // vertices [v0, v1) (its slab's).  Resampling and QEM then update only those; the per-face
+    // passes run over the faces touching them (the work faces, a contiguous range: faces are in
+    // z-major cell order and an owned vertex's faces lie in the slab's layers and the first layer
+    // above) and, for the resampling weights, their edge neighbours as well.  The edge-length fold
+    // runs over every face on every rank (the same serial chain, no exchange).  After each step
+    // that moves vertices the caller exchanges the owned ranges (set_verts) before the next step.
+    // Call after load_mesh; v0 = 0, v1 = nv restores the whole mesh.
+    void set_owned_vertices(int64_t v0, int64_t v1);
+    // [v0, v1, work faces f0, f1, centroid faces f0, f1]
+    void ranges(int64_t out[6]) const;
+    // device pointer of the current vertices (3 nv floats; valid until the next step)
+    float* d_verts() { return verts_.as<float>(); }
     // step 1: apply_vertex_resampling_to_MC_buffers__VMS (apply_v_s_to_mc_buffers.hpp:280-326)
     void vertex_resampling(float c);
     // step 2: centroids_projection (centroids_projection.cpp:1219-1311)
@@ -35,7 +48,8 @@ public:
     void fetch(float* verts, int32_t* faces);
     // host copies of the point sets stored since load_mesh (blocking)
     const std::map<std::string, std::vector<float>>& pointsets();
-    float last_average_edge() const { return avg_edge_; }
+    // the last projection's average edge length (blocking: read back from the device once)
+    float last_average_edge();
     // after read_counters(): bisections that hit the cap, implicit evaluations of the projection
     // (counted only while profiling)
     void read_counters();
@@ -58,7 +72,7 @@ private:
     void rand_tables(int64_t lanes);
     void add_rand_noise(float amplitude);
     void start_edge_fold();
-    float finish_edge_fold();
+    void finish_edge_fold();
     void start_perturbations();
     const float* perturbations();
     struct Stage {   // profiling scope: stage k from construction to next() / destruction
@@ -74,22 +88,25 @@ private:
     hipStream_t s;
     int64_t nv = 0, nf = 0;
     DevBuf verts_, faces_, vnew_, cen_, nrm_, w_, fof_, uoff_, ulst_, etab_, deg_, proj_, grad_, fn_, norms_,
-        alphas_, pert_, pend_, misc_, fnew_, rtab_, scan_tmp_;
+        pert_, pend_, misc_, fnew_, rtab_, scan_tmp_;
     bool topo_valid_ = false;
+    int64_t own_v0_ = 0, own_v1_ = 0;   // owned vertices
+    int64_t wf0_ = 0, wf1_ = 0;         // work faces: touching an owned vertex
+    int64_t cf0_ = 0, cf1_ = 0;         // faces whose centroid / normal the weights of the work faces read
+    bool sharded_ = false;
     int64_t rand_hi_rows_ = 0;
     float avg_edge_ = 0.f;
+    bool avg_valid_ = true;      // avg_edge_ holds the last fold's average (else read fold_out_)
     uint32_t cap_hits_ = 0;
     uint64_t evals_ = 0;
     int64_t jit_launches_ = 0;   // OB02 passes that ran the JIT point module (since load_mesh)
     bool profile_ = false;
     double stage_ms_[kStages] = {};
-    HostBuf host_norms_;                     // pinned: the edge-length terms and the fold's table (D2H)
     DevBuf fold_sum_;                        // the fold's chunk table (fold.hpp), built on the device
-    hipEvent_t norms_ready_ = nullptr;
-    hipStream_t copy_s_ = nullptr;           // the fold's D2H copies, beside the projection's prep pass
-    hipEvent_t table_done_ = nullptr;
+    DevBuf fold_out_;                        // FoldOut (ob02_device.hpp): sum, average, alpha list
+    hipStream_t walk_s_ = nullptr;           // the fold's walk, beside the projection's prep pass
+    hipEvent_t table_done_ = nullptr, walk_done_ = nullptr;
     DevBuf dir_, evals_buf_;
-    std::vector<float> alphas_host_;         // kept until the next projection (async H2D source)
     std::future<std::shared_ptr<const std::vector<float>>> pert_job_;
     std::shared_ptr<const std::vector<float>> pert_host_;
     int64_t pert_nf_ = -1;
@@ -101,5 +118,8 @@ private:
     std::map<std::string, Snapshot> snaps_;
     std::map<std::string, std::vector<float>> pointsets_;
 };
+
+// the edge-length fold alone on n host terms (diagnostics, tests): the device's serial-chain sum
+float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* stats = nullptr, int* trace = nullptr);
 
 }  // namespace impli

@@ -85,13 +85,28 @@ __device__ __forceinline__ V3 facet_normal(const float* __restrict__ v, const in
     return V3{x / n, y / n, z / n};
 }
 
+// The edge-length fold's result, written on the device by k_fold_walk (ob02.hip) and read by the
+// projection and QEM kernels in stream order (no host round trip): the serial sum, the average edge
+// length (compute_average_edge_length, cp:70-82) and make_alpha_list's list for it (cp:144-194;
+// at most 20 alphas per halving of the step, and at most kMaxHalvings halvings).
+constexpr int kMaxHalvings = 200;
+constexpr int kMaxAlphas = 20 * kMaxHalvings;
+struct FoldOut {
+    float sum;          // the serial float chain of the 3F edge lengths
+    float avg;          // (float)((double)sum / (3. * nf)): max_dist of the searches and QEM's clamp
+    int nal;            // alphas in the list
+    int table_chunks;   // chunks taken from the chunk table (statistics)
+    int steps[4];       // walk steps (statistics): zero-skip / serial terms, table runs, term runs, global term loads
+    long long cycles[2];   // staging, walking (clock64)
+    int trace[256];        // the walk's first steps (diagnostics): kind << 28 | term index
+    float alphas[kMaxAlphas];
+};
+
 struct ProjArgs {
     const float* v;
     const int32_t* f;
     int64_t nf;
-    const float* alphas;
-    int nal;
-    float max_dist;
+    const FoldOut* fold;    // alphas, their count and max_dist (the average edge length)
     const float* pert;      // type-2 perturbations (3 per centroid), only for the late pass
     float* out;             // projected centroids
     float* fn;              // facet normals (written by the early pass)
@@ -225,7 +240,7 @@ __device__ __forceinline__ bool try_direction(const Grp& g, const Ev& ev, V3 x, 
 
 // set_centers_on_surface (cp:421-594), the part before the searches: centroid, facet normal,
 // f(centroid) and the type-0 direction -normalise(grad) s_c; one lane per face.  Nothing here needs
-// the average edge length, so it runs while the host folds the edge lengths.
+// the average edge length, so it runs while k_fold_walk folds the edge lengths.
 template <class Ev>
 __device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& a) {
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -255,11 +270,14 @@ __device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs&
     const V3 d0{a.dir[3 * j], a.dir[3 * j + 1], a.dir[3 * j + 2]};
     const float fcv = a.fc[j];
     const float sc = get_sign(fcv);
+    const int nal = a.fold->nal;
+    const float max_dist = a.fold->avg;
+    const float* alphas = a.fold->alphas;
     uint32_t evals = 0;
     V3 best = x;
     float bf = fcv;
-    bool found = try_direction(g, ev, x, d0, sc, a.alphas, a.nal, a.max_dist, best, bf, evals);
-    if (!found) found = try_direction(g, ev, x, fnv, sc, a.alphas, a.nal < 10 ? a.nal : 10, a.max_dist, best, bf, evals);
+    bool found = try_direction(g, ev, x, d0, sc, alphas, nal, max_dist, best, bf, evals);
+    if (!found) found = try_direction(g, ev, x, fnv, sc, alphas, nal < 10 ? nal : 10, max_dist, best, bf, evals);
     if (found) finalize_g(g, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
     // unresolved faces are flagged for the late pass (a compacted list cost one same-address atomic
     // per wave: 258 us per pass when every face pends, as with a non-finite average edge length)
@@ -278,7 +296,9 @@ __device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& 
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const float fcv = a.fc[j];
     const float sc = get_sign(fcv);
-    const int n10 = a.nal < 10 ? a.nal : 10;
+    const float max_dist = a.fold->avg;
+    const float* alphas = a.fold->alphas;
+    const int n10 = a.fold->nal < 10 ? a.fold->nal : 10;
     const V3 pv{a.pert[3 * j], a.pert[3 * j + 1], a.pert[3 * j + 2]};
     V3 z = cross3(fnv, pv);               // cp:250-259, add_inplace is a no-op (F9)
     const float nz = norm2f(z.x, z.y, z.z);
@@ -287,11 +307,11 @@ __device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& 
     uint32_t evals = 0;
     V3 best = x;
     float bf = fcv;
-    bool found = try_direction(g, ev, x, z, sc, a.alphas, n10, a.max_dist, best, bf, evals);
-    if (!found) found = try_direction(g, ev, x, z2, sc, a.alphas, n10, a.max_dist, best, bf, evals);
+    bool found = try_direction(g, ev, x, z, sc, alphas, n10, max_dist, best, bf, evals);
+    if (!found) found = try_direction(g, ev, x, z2, sc, alphas, n10, max_dist, best, bf, evals);
     for (int ax = 0; ax < 3 && !found; ++ax) {
         const V3 d{ax == 0 ? 1.f : 0.f, ax == 1 ? 1.f : 0.f, ax == 2 ? 1.f : 0.f};
-        found = try_direction(g, ev, x, d, sc, a.alphas, n10, a.max_dist, best, bf, evals);
+        found = try_direction(g, ev, x, d, sc, alphas, n10, max_dist, best, bf, evals);
     }
     finalize_g(g, ev, x, fcv, found, found ? best : x, found ? bf : fcv, a.out + 3 * j, a, evals);
     if (a.evals && g.sub == 0) a.evals[j] += evals;

@@ -144,6 +144,11 @@ int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* gra
    atanf (1) and atan2f (2: out = atan2f(a, b)) that the screw family calls (screw.hpp:20-36,
    std::sin / std::atan2 on floats), on n host operands; 0 or -1 with implisolid_last_error() */
 int implisolid_debug_libm(int which, const float* a, const float* b, int64_t n, float* out);
+/* Additive, diagnostics: the edge-length fold of the projection (compute_average_edge_length,
+   centroids_projection.cpp:70-82: s = 0; s += e[k] in order, float) on n host terms, computed as
+   build_geometry computes it -- the chunk table and the device walk; *sum_out = s, *table_chunks
+   (may be NULL) = chunks the walk took from the table.  0, or -1 with implisolid_last_error(). */
+int implisolid_debug_fold(const float* terms, int64_t n, float* sum_out, int64_t* table_chunks);
 
 /* host-only: compile an MP5 tree to the node program; info = {n_instr, depth, n_mats, 0};
    mats_out receives n_mats inverse matrices (12 floats each, up to 256) */
@@ -258,6 +263,29 @@ int implisolid_batch_info(implisolid_batch* b, int32_t out[4], double* jit_secon
 int implisolid_batch_counts(implisolid_batch* b, int i, uint32_t out[3]);
 int implisolid_batch_download(implisolid_batch* b, int i, float* verts, int32_t* faces);
 void implisolid_batch_destroy(implisolid_batch* b);
+
+/* The OB02 loop (polygonizer steps 1-3, polygonizer_algorithm_ob02.hpp:74-157) on one Z-slab shard of
+ * a multi-GPU build: every rank loads the whole MC mesh (device pointers on the current device) and
+ * owns the vertices [v0, v1) of its slab.  resample / project (+ QEM per the mc settings) update only
+ * the owned vertices, evaluating the faces that touch them (and their edge neighbours for the
+ * resampling weights); the edge-length fold runs over every face on every rank.  After each step
+ * that moves vertices, the caller exchanges the owned ranges: get_verts copies the current
+ * vertices (3 nv floats) into a device buffer, set_verts takes them back.  Every call blocks;
+ * ranges = [v0, v1, work faces f0, f1, centroid faces f0, f1].  Results are byte-identical to the
+ * single-device loop.  0, or -1 with implisolid_last_error(). */
+typedef struct implisolid_ob02 implisolid_ob02;
+implisolid_ob02* implisolid_ob02_create(const char* shape_json, const char* mc_json);
+void implisolid_ob02_destroy(implisolid_ob02* h);
+int implisolid_ob02_load(implisolid_ob02* h, const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, int64_t v0,
+                         int64_t v1);
+int implisolid_ob02_resample(implisolid_ob02* h);
+int implisolid_ob02_project(implisolid_ob02* h);
+int implisolid_ob02_subdivide(implisolid_ob02* h, float amplitude);
+int implisolid_ob02_counts(implisolid_ob02* h, int64_t out[2]);
+int implisolid_ob02_ranges(implisolid_ob02* h, int64_t out[6]);
+int implisolid_ob02_get_verts(implisolid_ob02* h, float* d_dst);
+int implisolid_ob02_set_verts(implisolid_ob02* h, const float* d_src);
+int implisolid_ob02_download(implisolid_ob02* h, float* verts, int32_t* faces);
 
 #ifdef __cplusplus
 }

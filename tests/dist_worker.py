@@ -7,6 +7,11 @@ IMPLISOLID_DIST_BACKEND (gloo for the rehearsal, nccl = RCCL on a multi-GPU node
 bench.py's multi-GPU step on its Z-slab of config 3's tree (balanced cuts from one interval pass,
 eval, count, the count all-gather in flight while the vertex pass runs, the face pass with the
 gathered counts), then the mesh is gathered to rank 0, which writes it to OUT (.npz).
+
+With the flag "ob02" the scene is config 2 (sphere u rabbit, MC + 3 x [resample, project, QEM]): the
+slabs' MC meshes are all-gathered to every rank, the OB02 loop runs sharded by owned vertex ranges
+(distributed.ob02_sharded: the owned vertices all-gathered after every vertex-moving step) and rank 0
+writes the refined mesh.
 """
 import os
 import sys
@@ -24,7 +29,8 @@ def main():
     from implisolid_amd import scenes
 
     out_path, R = sys.argv[1], int(sys.argv[2])
-    balanced = len(sys.argv) > 3 and sys.argv[3] == "balanced"
+    balanced = "balanced" in sys.argv[3:]
+    ob02 = "ob02" in sys.argv[3:]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("IMPLISOLID_DIST_BACKEND", "nccl")
@@ -34,7 +40,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     else:
         dist.init_process_group(backend)
-    shape, mc = scenes.config3_tree(), scenes.mc_settings(R, 1.0)
+    shape, mc = scenes.config2(R) if ob02 else (scenes.config3_tree(), scenes.mc_settings(R, 1.0))
     cuts = D.balanced_cuts(shape, mc, world) if balanced else None
     slab = I.Slab(shape, mc, rank, world, cuts=cuts)
     sp = torch.cuda.current_stream(dev).cuda_stream
@@ -54,7 +60,11 @@ def main():
         slab.emit_faces(0, gath.data_ptr(), rank, sp)
         nv, nf, of = slab.counts(sp)
     assert not of
-    res = D.gather_mesh(slab, gath, rank, world)
+    if ob02:
+        V, F, voff, foff = D.allgather_mesh(slab, gath, rank, world, dev)
+        res = D.ob02_sharded(shape, mc, V, F, voff, rank, world)
+    else:
+        res = D.gather_mesh(slab, gath, rank, world)
     if rank == 0:
         v, f = res
         np.savez(out_path, verts=v, faces=f, cuts=np.asarray(cuts or [], np.int32), gathered=gath.cpu().numpy())

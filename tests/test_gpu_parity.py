@@ -135,6 +135,62 @@ def _has_twist(shape):
     return "screw" in json.dumps(shape)
 
 
+def _fold_arrays():
+    """Seeded edge-length-fold inputs in the spirit of tools/fold_check.cpp: typical edge lengths,
+    wide spreads, integer and half-integer terms (ties), zeros, subnormals, powers of two, binade
+    tops with terms at half the spacing, inf / NaN payloads, saturation past 2^24."""
+    rng = np.random.default_rng(20261017)
+    out = []
+    for t in range(48):
+        n = int(rng.uniform() * (5000 if t < 32 else 300000))
+        x = rng.uniform(size=n)
+        kind = t % 8
+        e = [0.0144 * (0.5 + x), np.exp2(-30.0 + 60.0 * x), np.floor(1 + 8 * x), np.floor(1 + 64 * x) * 0.5,
+             np.where(x < 0.3, 0.0, 1e-3 * x), np.where(x < 0.01, 1e-40 * x, 3.0 * x),
+             np.ldexp(1.0, (x * 40).astype(np.int64) - 20), x * x * 100.0][kind]
+        out.append(("random%d" % kind, e.astype(np.float32)))
+    for t in range(24):
+        E = 1 + int(rng.uniform() * 30)
+        u = np.ldexp(1.0, E - 24)
+        n = 1000 + int(rng.uniform() * 20000)
+        x = rng.uniform(size=n)
+        body = np.where(x < 0.5, u * (0.5 + (x * 8).astype(np.int64)), u * x * 3)
+        head = np.float32(np.ldexp(1.0, E) * (0.5 + 0.49 * rng.uniform()))
+        out.append(("ties", np.concatenate([[head], body]).astype(np.float32)))
+    out += [("empty", np.zeros(0, np.float32)), ("one", np.ones(1, np.float32)),
+            ("zeros", np.array([0.0, -0.0, 0.0], np.float32)), ("leading zeros", np.r_[np.zeros(5000), 0.01 * np.ones(700)].astype(np.float32))]
+    e = np.full(100000, 0.0144, np.float32)
+    e[50000] = np.inf
+    out.append(("inf", e.copy()))
+    e[70000] = np.nan
+    out.append(("inf+nan", e.copy()))
+    e[20000] = np.frombuffer(np.uint32(0x7f801234).tobytes(), np.float32)[0]   # signalling NaN, payload 0x1234
+    out.append(("nan payload", e.copy()))
+    out.append(("saturation", np.ones(3000000, np.float32)))
+    return out
+
+
+def test_device_edge_fold_matches_serial_chain(impli):
+    """The projection's average-edge-length fold (compute_average_edge_length, cp:70-82: s = 0;
+    s += e[k], float, in order) as the device computes it -- chunk table plus one-wave walk, no host
+    round trip -- against the serial float chain (numpy's add.accumulate is strictly sequential), bit
+    for bit; NaN results compared up to the quiet bit (x86 addss returns the NaN operand quieted)."""
+    for name, e in _fold_arrays():
+        ref = np.add.accumulate(e, dtype=np.float32)[-1] if e.size else np.float32(0.0)
+        got, _ = impli.debug_fold(e)
+        a, b = np.float32(ref).view(np.uint32), np.float32(got).view(np.uint32)
+        if np.isnan(ref):
+            assert np.isnan(got) and (int(a) | 0x400000) == (int(b) | 0x400000), (name, hex(int(a)), hex(int(b)))
+        else:
+            assert a == b, (name, e.size, float(ref), float(got))
+    # a typical mesh's terms: most chunks come from the table
+    e = _fold_arrays()[0][1]
+    big = np.tile(e, 100)
+    got, tc = impli.debug_fold(big)
+    assert np.float32(got).view(np.uint32) == np.add.accumulate(big, dtype=np.float32)[-1].view(np.uint32)
+    assert tc > 0.5 * (big.size // 256), tc
+
+
 def test_direct_eval_abi_matches_reference_semantics(impli, oracle):
     shape = TREES["union_sphere_cube"]
     pts = np.random.default_rng(5).uniform(-1, 1, size=(1000, 3)).astype(np.float32)
@@ -1063,6 +1119,84 @@ def test_multi_device_build_geometry(impli, oracle, devices):
         assert np.array_equal(v2.view(np.uint32), v1.view(np.uint32))
     finally:
         impli.set_devices(None)
+
+
+@pytest.mark.parametrize("world,balanced", [(2, True), (3, False)])
+def test_multiprocess_ob02_sharded_gloo(impli, oracle, tmp_path, world, balanced):
+    """OB02 on Z-slabs: `world` fresh processes build config 2 at R = 64 (sphere u rabbit, MC + 3 x
+    [resample, project, QEM]) -- their slabs' MC meshes all-gathered to every rank, then the OB02 loop
+    sharded by owned vertex ranges (each rank resamples and QEMs its slab's vertices over the faces
+    touching them; the edge-length fold on every rank; owned vertices all-gathered after every step
+    that moves them) -- and rank 0's refined mesh is the single-GPU oracle's byte for byte."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from implisolid_amd import scenes
+    R = 64
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    out = str(tmp_path / "mesh.npz")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IMPLISOLID_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "tests", "dist_worker.py"),
+           out, str(R), "ob02"] + (["balanced"] if balanced else [])
+    r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    g = np.load(out)
+    shape, mc = scenes.config2(R)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    assert np.array_equal(g["faces"], fr)
+    assert np.array_equal(g["verts"].view(np.uint32), vr.view(np.uint32))
+
+
+def test_ob02_shards_in_one_process(impli, oracle):
+    """The sharded OB02 loop without processes: config 2 at R = 48 as 3 and 5 vertex-range shards on
+    one GPU, stepped together with the owned ranges exchanged on the host after every vertex-moving
+    step -- the same mesh as build_geometry and the oracle, byte for byte; the shards' work-face
+    ranges cover their vertices' umbrellas and stay within the slabs plus one layer."""
+    import torch
+    from implisolid_amd import scenes
+    shape, mc = scenes.config2(48)
+    st = impli.parse_settings(mc)
+    v_mc, f_mc = impli.make_geometry(shape, scenes.mc_settings(48, 1.0))
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    for nshard in (3, 5):
+        nv, nf = len(v_mc), len(f_mc)
+        voff = np.linspace(0, nv, nshard + 1).astype(np.int64)
+        V = torch.from_numpy(v_mc.reshape(-1).copy()).cuda()
+        F = torch.from_numpy(f_mc.reshape(-1).copy()).cuda()
+        obs = [impli.Ob02Shard(shape, mc) for _ in range(nshard)]
+        for r, ob in enumerate(obs):
+            ob.load(V.data_ptr(), nv, F.data_ptr(), nf, int(voff[r]), int(voff[r + 1]))
+            v0, v1, w0, w1, c0, c1 = ob.ranges()
+            assert (v0, v1) == (voff[r], voff[r + 1]) and c0 <= w0 <= w1 <= c1
+        bufs = [torch.empty(nv * 3, dtype=torch.float32, device="cuda") for _ in obs]
+
+        def exchange():
+            full = torch.empty(nv * 3, dtype=torch.float32, device="cuda")
+            for r, ob in enumerate(obs):
+                ob.get_verts(bufs[r].data_ptr())
+                full[3 * voff[r]:3 * voff[r + 1]] = bufs[r][3 * voff[r]:3 * voff[r + 1]]
+            torch.cuda.synchronize()
+            for ob in obs:
+                ob.set_verts(full.data_ptr())
+
+        for rep in range(st["overall_repeats"]):
+            for _ in range(st["vresampl_iters"]):
+                for ob in obs:
+                    ob.resample()
+                exchange()
+            for ob in obs:
+                ob.project()
+            exchange()
+        v, f = obs[0].download()
+        for ob in obs:
+            ob.close()
+        assert np.array_equal(f, fr)
+        assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), nshard
 
 
 @pytest.mark.parametrize("world,balanced", [(2, True), (3, False)])

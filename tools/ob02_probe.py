@@ -21,7 +21,8 @@ def main():
     cases = [("config2 R128 MC only", scenes.union_sphere_cube(), scenes.mc_settings(128, 1.0)),
              ("config2 R128 MC+3xOB02", *scenes.config2(128)),
              ("config3 R256 MC only", scenes.config3_tree(), scenes.mc_settings(256, 1.0)),
-             ("config3 R256 MC+3xOB02", *scenes.config3(256))]
+             ("config3 R256 MC+3xOB02", *scenes.config3(256)),
+             ("config3s R256 MC+3xOB02 (shifted box: live projection)", *scenes.config3_shifted(256))]
     sub = dict(scenes.config2(128)[1])
     sub["subdiv"] = {"enabled": 1}
     sub["debug"] = {"post_subdiv_noise": 0.01}
