@@ -528,40 +528,90 @@ __global__ __launch_bounds__(1024) void k_fold_bases(const double* __restrict__ 
     }
     if (t == 0) est[nc] = s_carry;
 }
+// Inclusive wave scan of u32 through DPP (gfx9: row_shr 1, 2, 4, 8 inside rows of 16 lanes, then
+// row_bcast 15 and 31 into the rows above): a few cycles per step, where a ds_bpermute shuffle
+// takes a round trip through LDS -- the walk is a chain of such scans
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return x;
+}
+__device__ __forceinline__ uint32_t lane_value(uint32_t x, int lane) {   // lane: wave-uniform
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, lane);
+}
+
+// The same scan over FoldPair maps (fold.hpp), in lane order: x_l <- (lanes before) then x_l.
+// Lanes a DPP step does not reach read the identity (0, 0).
+__device__ __forceinline__ FoldPair dpp_pair(FoldPair x, int ctrl, int row_mask) {
+    FoldPair p;
+    switch (ctrl) {   // the control word must be a constant of the builtin
+        case 0x111: p.c0 = __builtin_amdgcn_update_dpp(0, (int)x.c0, 0x111, 0xf, 0xf, false);
+                    p.c1 = __builtin_amdgcn_update_dpp(0, (int)x.c1, 0x111, 0xf, 0xf, false); break;
+        case 0x112: p.c0 = __builtin_amdgcn_update_dpp(0, (int)x.c0, 0x112, 0xf, 0xf, false);
+                    p.c1 = __builtin_amdgcn_update_dpp(0, (int)x.c1, 0x112, 0xf, 0xf, false); break;
+        case 0x114: p.c0 = __builtin_amdgcn_update_dpp(0, (int)x.c0, 0x114, 0xf, 0xf, false);
+                    p.c1 = __builtin_amdgcn_update_dpp(0, (int)x.c1, 0x114, 0xf, 0xf, false); break;
+        case 0x118: p.c0 = __builtin_amdgcn_update_dpp(0, (int)x.c0, 0x118, 0xf, 0xf, false);
+                    p.c1 = __builtin_amdgcn_update_dpp(0, (int)x.c1, 0x118, 0xf, 0xf, false); break;
+        case 0x142: p.c0 = __builtin_amdgcn_update_dpp(0, (int)x.c0, 0x142, 0xa, 0xf, false);
+                    p.c1 = __builtin_amdgcn_update_dpp(0, (int)x.c1, 0x142, 0xa, 0xf, false); break;
+        case 0x143: p.c0 = __builtin_amdgcn_update_dpp(0, (int)x.c0, 0x143, 0xc, 0xf, false);
+                    p.c1 = __builtin_amdgcn_update_dpp(0, (int)x.c1, 0x143, 0xc, 0xf, false); break;
+        default:    p.c0 = __builtin_amdgcn_update_dpp(0, (int)x.c0, 0x138, 0xf, 0xf, false);   // wave_shr:1
+                    p.c1 = __builtin_amdgcn_update_dpp(0, (int)x.c1, 0x138, 0xf, 0xf, false); break;
+    }
+    (void)row_mask;
+    return p;
+}
+__device__ __forceinline__ FoldPair wave_scan_pairs(FoldPair x) {   // inclusive
+    x = fold_compose(dpp_pair(x, 0x111, 0xf), x);
+    x = fold_compose(dpp_pair(x, 0x112, 0xf), x);
+    x = fold_compose(dpp_pair(x, 0x114, 0xf), x);
+    x = fold_compose(dpp_pair(x, 0x118, 0xf), x);
+    x = fold_compose(dpp_pair(x, 0x142, 0xa), x);
+    x = fold_compose(dpp_pair(x, 0x143, 0xc), x);
+    return x;
+}
+__device__ __forceinline__ FoldPair wave_excl_pairs(FoldPair incl) { return dpp_pair(incl, 0x138, 0xf); }
+__device__ __forceinline__ uint32_t pair_apply(FoldPair p, uint32_t x) { return x + ((x & 1u) ? p.c1 : p.c0); }
+
 // hint[c] = 1: the walk will probably need chunk c's terms (the estimate is 0, the estimated sum
 // crosses a power of two inside the chunk, with a margin of 2^-7 for the float chain's drift from the
 // double estimate, or the chunk is flagged in the binades the estimate puts s in) -- k_fold_walk
 // stages those chunks' terms in LDS beforehand
 __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e, int64_t n, const int32_t* __restrict__ base,
-                                                    const double* __restrict__ est, uint32_t* __restrict__ sum,
+                                                    const double* __restrict__ est, FoldPair* __restrict__ pairs,
                                                     uint8_t* __restrict__ flags, uint8_t* __restrict__ hint) {
     const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (c >= fold_chunks(n)) return;   // uniform per wave
-    uint32_t bits[4];
+    uint32_t bits[4];   // lane l: the chunk's terms 4 l .. 4 l + 3 (the maps compose in term order)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const int64_t k = c * kFoldChunk + q * 64 + lane;
+        const int64_t k = c * kFoldChunk + 4 * lane + q;
         bits[q] = k < n ? __float_as_uint(e[k]) : 0u;   // +0 past the end contributes nothing
     }
     const int E0 = base[c];
     uint32_t fl34 = 0;
 #pragma unroll
     for (int b = 0; b < kFoldBinades; ++b) {
-        uint32_t s = 0, f = 0;
+        FoldPair p{0u, 0u};
+        uint32_t f = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             uint8_t fq;
-            s = fold_add(s, fold_term(bits[q], E0 + b, fq));
+            p = fold_compose(p, fold_pair_term(bits[q], E0 + b, fq));
             f |= fq;
         }
+        const FoldPair all = wave_scan_pairs(p);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            s = fold_add(s, (uint32_t)__shfl_xor((int)s, o, 64));
-            f |= (uint32_t)__shfl_xor((int)f, o, 64);
-        }
-        if (lane == 0) {
-            sum[c * kFoldBinades + b] = s;
+        for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o, 64);
+        if (lane == 63) {
+            pairs[c * kFoldBinades + b] = all;
             flags[c * kFoldBinades + b] = (uint8_t)f;
         }
         if (b == 3 || b == 4) fl34 |= f;
@@ -596,22 +646,6 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t x, int lane) {
     return x;
 }
 
-// Inclusive wave scan of u32 through DPP (gfx9: row_shr 1, 2, 4, 8 inside rows of 16 lanes, then
-// row_bcast 15 and 31 into the rows above): a few cycles per step, where a ds_bpermute shuffle
-// takes a round trip through LDS -- the walk is a chain of such scans
-__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-    return x;
-}
-__device__ __forceinline__ uint32_t lane_value(uint32_t x, int lane) {   // lane: wave-uniform
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, lane);
-}
-
 // make_alpha_list(avg, 0.001, avg, 20) (cp:144-194) as the host called it: at most kMaxHalvings
 // halvings (the reference loops forever on an infinite average; any finite one ends within 140)
 __device__ void alpha_list_dev(float avg, FoldOut* o) {
@@ -638,29 +672,11 @@ __device__ void alpha_list_dev(float avg, FoldOut* o) {
 // of an unhinted chunk the walk needs are read from memory.
 constexpr int kWalkThreads = 1024, kWalkWindow = 1536, kWalkSlots = 40;
 
-// fold_term (fold.hpp) without branches, for the walk: the rounded multiple of the spacing
-// 2^(E-24) of a term, and whether the chain must add it as a float (a tie, a term too large,
-// negative, inf or NaN) -- the same values and the same "flagged" as fold_term's flags != 0
-__device__ __forceinline__ uint32_t walk_term(uint32_t bits, int E, bool& flag) {
-    const uint32_t ex = (bits >> 23) & 0xffu, frac = bits & 0x7fffffu, mag = bits & 0x7fffffffu;
-    const bool special = ex == 0xffu, neg = (bits >> 31) != 0u && mag != 0u, zero = mag == 0u;
-    const uint32_t M = frac | (ex ? 0x800000u : 0u);
-    const int sh = (ex ? (int)ex : 1) - 150 + 24 - E;
-    const int d = -sh;
-    const int dd = d < 1 ? 1 : (d > 25 ? 25 : d);
-    const uint32_t half = 1u << (dd - 1), rem = M & ((1u << dd) - 1u), rd = (M + half) >> dd;
-    const uint32_t up = M << (sh < 0 ? 0 : (sh > 7 ? 7 : sh));
-    const uint32_t upc = sh >= 8 || up >= kFoldCap ? kFoldCap : up;
-    const bool plain = !(zero || neg || special);
-    flag = special || neg || (!zero && sh >= 8) || (plain && sh < 0 && d <= 25 && rem == half);
-    return !plain ? 0u : sh >= 0 ? upc : (d > 25 ? 0u : rd);
-}
-
 __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restrict__ e, int64_t n64,
-                                                            const int32_t* __restrict__ base, const uint32_t* __restrict__ sum,
+                                                            const int32_t* __restrict__ base, const FoldPair* __restrict__ pairs,
                                                             const uint8_t* __restrict__ flags, const uint8_t* __restrict__ hint,
                                                             int64_t nf, FoldOut* __restrict__ out) {
-    __shared__ uint32_t w_sum[kWalkWindow * kFoldBinades];
+    __shared__ FoldPair w_pair[kWalkWindow * kFoldBinades];
     __shared__ uint8_t w_flag[kWalkWindow * kFoldBinades];
     __shared__ int32_t w_base[kWalkWindow];
     __shared__ int16_t w_slot[kWalkWindow];
@@ -686,7 +702,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             w_base[i] = base[c];
 #pragma unroll
             for (int b = 0; b < kFoldBinades; ++b) {
-                w_sum[i * kFoldBinades + b] = sum[c * kFoldBinades + b];
+                w_pair[i * kFoldBinades + b] = pairs[c * kFoldBinades + b];
                 w_flag[i * kFoldBinades + b] = flags[c * kFoldBinades + b];
             }
             int sl = -1;
@@ -752,7 +768,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (1 << 28) | k;
                 ++st1;
                 const int i0 = k / kFoldChunk - c0 + 4 * lane;
-                uint32_t v[4];
+                FoldPair tp[4];
                 bool ok[4];
                 int bb[4];
 #pragma unroll
@@ -762,135 +778,108 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     const int i = i0 + j < wn ? i0 + j : wn - 1;
                     const bool inb = i0 + j < wn && bb[j] >= 0 && bb[j] < kFoldBinades;
                     const int cell = i * kFoldBinades + (inb ? bb[j] : 0);
-                    v[j] = w_sum[cell];
+                    tp[j] = w_pair[cell];
                     ok[j] = inb && w_flag[cell] == 0;
+                    if (!ok[j]) tp[j] = FoldPair{0u, 0u};
                 }
-                uint32_t T = 0;
+                FoldPair p{0u, 0u};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) T += ok[j] ? v[j] : 0u;   // below 2^26
-                // lanes clamped at 2^24 keep the scan below 2^30; such a lane holds the run's end
-                const uint32_t Tc = T < kFoldCap ? T : kFoldCap;
-                const uint32_t incl = wave_scan_dpp(Tc), excl = incl - Tc;
+                for (int j = 0; j < 4; ++j) p = fold_compose(p, tp[j]);
+                const FoldPair incl = wave_scan_pairs(p), excl = wave_excl_pairs(incl);
+                // the lanes' values from the exact start: the first chunk that is unusable or takes
+                // the value to 2^24 ends the run (every map before it exact: no clamped value yet)
+                uint32_t v = pair_apply(excl, su), before = v;
                 int first = 4;
-                uint32_t run = excl, before = excl;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const uint32_t vj = ok[j] ? v[j] : 0u;
-                    if (first == 4 && (!ok[j] || su + run + vj >= kFoldCap)) { first = j; before = run; }
-                    run += vj;
+                    if (first == 4) {
+                        const uint32_t v2 = pair_apply(tp[j], v);
+                        if (!ok[j] || v2 >= kFoldCap) { first = j; before = v; }
+                        else v = v2;
+                    }
                 }
                 const uint64_t lm = __ballot(first < 4);
                 const int L = lm ? __ffsll((unsigned long long)lm) - 1 : 63;
                 const int fb = lm ? 4 * L + (int)lane_value((uint32_t)first, L) : 256;
                 if (fb > 0) {
-                    const uint32_t tt = su + (lm ? lane_value(before, L) : lane_value(incl, 63));   // < 2^24: exact
-                    s = ldexpf((float)tt, E - 24);
+                    const uint32_t tt = lm ? lane_value(before, L) : pair_apply(FoldPair{lane_value(incl.c0, 63),
+                                                                                          lane_value(incl.c1, 63)}, su);
+                    s = ldexpf((float)tt, E - 24);   // < 2^24: exact in this binade
                     table_chunks += fb;
                     k += fb * kFoldChunk;
                     if (k >= kend_w) {
                         if (k > n) k = n;
                         continue;
                     }
-                    // the chunk that ended the run goes term by term now (same binade: tt < 2^24)
                     k = __builtin_amdgcn_readfirstlane(k);
-                    su = tt;
+                    su = tt;   // the chunk that ended the run goes term by term now (same binade)
                 }
             }
-            // the chunk's terms from k, 4 consecutive per lane, in order: their rounded multiples of the
-            // spacing in this binade, up to the first event; that term is added as the chain's float add,
-            // and if it was the crossing into the next binade, the chunk's run continues there in the
-            // same step (the terms' multiples of the next binade's spacing)
+            // the chunk the table could not take: its terms from k, 4 consecutive per lane, in order, as
+            // maps of the current binade (fold.hpp) up to the first event -- an unusable term, or the
+            // one that reaches the binade's end -- which is added as the chain's own float add; then on
+            // from the next term in the binade the sum is in now, within the same step
             if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (2 << 28) | k | (E + 64) << 20;
             ++st2;
             const int kc = k & ~(kFoldChunk - 1);
             const int kend = kc + kFoldChunk < n ? kc + kFoldChunk : n;
-            uint32_t q0[4], xb[4];
-            bool ev0[4];
+            uint32_t xb[4];
             // the chunk's terms: from LDS if it was staged (uniform: one chunk), else from memory, all
             // four loads issued before any use
             const int sl = __builtin_amdgcn_readfirstlane((int)w_slot[k / kFoldChunk - c0]);
             if (sl >= 0) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int kk = k + 4 * lane + j;
-                    xb[j] = kk < kend ? __float_as_uint(w_terms[sl][kk & (kFoldChunk - 1)]) : 0u;
-                }
+                for (int j = 0; j < 4; ++j) xb[j] = __float_as_uint(w_terms[sl][4 * lane + j]);
             } else {
                 ++st3;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int kk = k + 4 * lane + j;
-                    xb[j] = __float_as_uint(e[kk < kend ? kk : k]);
-                    if (kk >= kend) xb[j] = 0u;
+                    const int kk = kc + 4 * lane + j;
+                    xb[j] = __float_as_uint(e[kk < n ? kk : kc]);
                 }
             }
-            uint32_t T0 = 0;
+            for (;;) {   // segments of the chunk, each ending at an event
+                if (!(s >= 0x1p-100f && s <= 0x1p100f)) break;   // the outer loop's term-by-term paths
+                (void)frexpf(s, &E);
+                E = __builtin_amdgcn_readfirstlane(E);
+                su = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E));
+                FoldPair tp[4], p{0u, 0u};
+                bool bad[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                q0[j] = walk_term(xb[j], E, ev0[j]);   // a term past the chunk is +0: 0, no event
-                T0 += q0[j];                           // each q <= 2^24: below 2^26
-            }
-            // lane totals clamped at 2^24 keep the scan below 2^30; a lane whose terms reach that holds
-            // the first event, so every sum before it is exact
-            const uint32_t T0c = T0 < kFoldCap ? T0 : kFoldCap;
-            const uint32_t incl0 = wave_scan_dpp(T0c), excl0 = incl0 - T0c;
-            int first = 4;
-            uint32_t run = excl0, before = excl0, xe = 0;
-            bool flagged = false;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (first == 4 && (ev0[j] || su + run + q0[j] >= kFoldCap)) {
-                    first = j; before = run; xe = xb[j]; flagged = ev0[j];
+                for (int j = 0; j < 4; ++j) {
+                    const int kk = kc + 4 * lane + j;
+                    uint8_t fl = 0;
+                    const bool act = kk >= k && kk < kend;
+                    tp[j] = fold_pair_term(act ? xb[j] : 0u, E, fl);
+                    bad[j] = act && fl != 0;
+                    p = fold_compose(p, tp[j]);
                 }
-                run += q0[j];
-            }
-            const uint64_t lm = __ballot(first < 4);
-            if (!lm) {
-                s = ldexpf((float)(su + lane_value(incl0, 63)), E - 24);
-                k = kend;
-                continue;
-            }
-            const int L = __ffsll((unsigned long long)lm) - 1;
-            const int jf = (int)lane_value((uint32_t)first, L);
-            s = ldexpf((float)(su + lane_value(before, L)), E - 24);   // exact: the chain before the event
-            const int t1 = k + 4 * L + jf;
-            const float x = __uint_as_float(lane_value(xe, L));
-            if (x != x) { s = quiet_nan_of(x); done = true; break; }
-            s = s + x;   // the event term: the chain's own float add
-            const int kstep = k;
-            k = t1 + 1;
-            int E1 = 0;
-            (void)frexpf(s, &E1);
-            if (lane_value(flagged ? 1u : 0u, L) || E1 != E + 1 || !(s <= 0x1p100f) || k >= kend) continue;
-            // lookahead in binade E + 1 over the terms after the crossing
-            const uint32_t su1 = (uint32_t)ldexpf(s, 24 - E1);
-            uint32_t q1[4], T1 = 0;
-            bool ev1[4];
+                const FoldPair incl = wave_scan_pairs(p), excl = wave_excl_pairs(incl);
+                uint32_t v = pair_apply(excl, su), before = v, xe = 0;
+                int first = 4;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool after = kstep + 4 * lane + j > t1;
-                q1[j] = walk_term(after ? xb[j] : 0u, E1, ev1[j]);
-                T1 += q1[j];
+                for (int j = 0; j < 4; ++j) {
+                    if (first == 4) {
+                        const uint32_t v2 = pair_apply(tp[j], v);
+                        if (bad[j] || v2 >= kFoldCap) { first = j; before = v; xe = xb[j]; }
+                        else v = v2;
+                    }
+                }
+                const uint64_t lm = __ballot(first < 4);
+                if (!lm) {
+                    s = ldexpf((float)pair_apply(FoldPair{lane_value(incl.c0, 63), lane_value(incl.c1, 63)}, su), E - 24);
+                    k = kend;
+                    break;
+                }
+                const int L = __ffsll((unsigned long long)lm) - 1;
+                const int jf = (int)lane_value((uint32_t)first, L);
+                s = ldexpf((float)lane_value(before, L), E - 24);   // exact: the chain before the event
+                const float x = __uint_as_float(lane_value(xe, L));
+                k = kc + 4 * L + jf + 1;
+                if (x != x) { s = quiet_nan_of(x); done = true; break; }
+                s = s + x;   // the event term: the chain's own float add
+                if (k >= kend) break;
             }
-            const uint32_t T1c = T1 < kFoldCap ? T1 : kFoldCap;
-            const uint32_t incl1 = wave_scan_dpp(T1c), excl1 = incl1 - T1c;
-            int first1 = 4;
-            uint32_t r1 = excl1, before1 = excl1;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (first1 == 4 && (ev1[j] || su1 + r1 + q1[j] >= kFoldCap)) { first1 = j; before1 = r1; }
-                r1 += q1[j];
-            }
-            const uint64_t lm1 = __ballot(first1 < 4);
-            if (!lm1) {
-                s = ldexpf((float)(su1 + lane_value(incl1, 63)), E1 - 24);
-                k = kend;
-                continue;
-            }
-            const int L1 = __ffsll((unsigned long long)lm1) - 1;
-            const int j1 = (int)lane_value((uint32_t)first1, L1);
-            s = ldexpf((float)(su1 + lane_value(before1, L1)), E1 - 24);   // exact: the chain before that event
-            k = kstep + 4 * L1 + j1;                                         // the next step starts at it
         }
         cyc_walk += clock64() - tc1;
     }
@@ -1313,13 +1302,13 @@ void Ob02::vertex_resampling(float c) {
     store_pointset("post_resampling_vertices", verts_.as<float>(), nv, true);   // :207-211
 }
 
-// the fold's device buffers in one allocation: [sums u32 (cells) | bases i32 (chunks) | flags u8
+// the fold's device buffers in one allocation: [pairs (cells) | bases i32 (chunks) | flags u8
 // (cells) | hints u8 (chunks)], then the chunks' double sums and the estimates (chunks + 1 each)
 struct FoldLayout {
     int64_t chunks, cells;
     size_t cs_off, est_off, bytes;
     explicit FoldLayout(int64_t n) : chunks(fold_chunks(n)), cells(fold_chunks(n) * kFoldBinades) {
-        const size_t tab = (size_t)(cells + chunks) * 4 + (size_t)cells + (size_t)chunks;
+        const size_t tab = (size_t)cells * sizeof(FoldPair) + (size_t)chunks * 4 + (size_t)cells + (size_t)chunks;
         cs_off = (tab + 15) & ~(size_t)15;
         est_off = cs_off + (size_t)(chunks + 1) * 8;
         bytes = est_off + (size_t)(chunks + 1) * 8;
@@ -1331,8 +1320,8 @@ void launch_fold(const float* d_terms, int64_t n, int64_t nf, char* d_tab, FoldO
                  hipEvent_t table_done) {
     if (n >= ((int64_t)1 << 31) - kFoldChunk) throw InputError("edge-length fold: more than 2^31 terms");
     const FoldLayout L(n);
-    uint32_t* d_sum = reinterpret_cast<uint32_t*>(d_tab);
-    int32_t* d_base = reinterpret_cast<int32_t*>(d_sum + L.cells);
+    FoldPair* d_pair = reinterpret_cast<FoldPair*>(d_tab);
+    int32_t* d_base = reinterpret_cast<int32_t*>(d_pair + L.cells);
     uint8_t* d_flags = reinterpret_cast<uint8_t*>(d_base + L.chunks);
     uint8_t* d_hint = d_flags + L.cells;
     double* d_cs = reinterpret_cast<double*>(d_tab + L.cs_off);
@@ -1340,13 +1329,13 @@ void launch_fold(const float* d_terms, int64_t n, int64_t nf, char* d_tab, FoldO
     if (L.cells) {
         k_fold_chunk_sums<<<blocks_for(L.chunks * 64), 256, 0, ts>>>(d_terms, n, d_cs);
         k_fold_bases<<<1, 1024, 0, ts>>>(d_cs, L.chunks, d_base, d_est);
-        k_fold_table<<<blocks_for(L.chunks * 64), 256, 0, ts>>>(d_terms, n, d_base, d_est, d_sum, d_flags, d_hint);
+        k_fold_table<<<blocks_for(L.chunks * 64), 256, 0, ts>>>(d_terms, n, d_base, d_est, d_pair, d_flags, d_hint);
     }
     if (ws != ts) {
         IMPLI_HIP(hipEventRecord(table_done, ts));
         IMPLI_HIP(hipStreamWaitEvent(ws, table_done, 0));
     }
-    k_fold_walk<<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_sum, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
+    k_fold_walk<<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
 }
 
 // compute_average_edge_length (cp:70-82) is one serial float chain in face order.  The terms and

@@ -1,7 +1,8 @@
 // fold_check.cpp -- the chunk-table fold (implisolid_amd/csrc/fold.hpp) against the serial float
 // chain on many seeded arrays: typical edge lengths, wide log-uniform spreads, exact ties (integer
 // and half-integer terms near binade tops), zeros, subnormals, huge values, inf and NaN, sizes from
-// 0 to 10^6.  Prints "mismatches N"; the table is computed by the same fold_cell the device runs.
+// 0 to 10^6.  Prints "mismatches N"; the table is computed by the same fold_cell (term pairs,
+// ties to even as parity-dependent increments) the device's table kernel computes.
 //     g++ -O2 -ffp-contract=off -std=c++17 tools/fold_check.cpp -o fold_check && ./fold_check
 #include <cmath>
 #include <cstdint>
@@ -22,7 +23,7 @@ static float serial(const std::vector<float>& e) {
 static int64_t g_table_chunks = 0, g_chunks = 0;
 static float table_fold(const std::vector<float>& e) {
     const int64_t n = (int64_t)e.size(), nc = impli::fold_chunks(n);
-    std::vector<uint32_t> sum((size_t)(nc * impli::kFoldBinades));
+    std::vector<impli::FoldPair> sum((size_t)(nc * impli::kFoldBinades));
     std::vector<uint8_t> fl((size_t)(nc * impli::kFoldBinades));
     std::vector<int32_t> base((size_t)nc);
     double est = 0.0;   // the device's estimate: chunk sums in double, exclusive prefix
