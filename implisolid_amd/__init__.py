@@ -37,6 +37,7 @@ ABI_SYMBOLS = [
     "implisolid_batch_download", "implisolid_batch_destroy",
     "implisolid_slab_create_range", "implisolid_slab_balance", "implisolid_cuts_from_layer_work", "implisolid_set_devices",
     "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
+    "implisolid_set_jit_max_modules", "implisolid_jit_modules",
     "implisolid_set_progress_callback", "implisolid_ob02_profile", "implisolid_last_build_stats",
     "implisolid_jit_compile_points", "implisolid_debug_libm", "implisolid_slab_stats_n",
     "implisolid_slab_kernel_times_each", "implisolid_debug_fold",
@@ -152,6 +153,8 @@ def lib():
         "implisolid_set_jit_bake": ([c_int], None),
         "implisolid_jit_wait": ([], None),
         "implisolid_jit_stats": ([ip, ctypes.POINTER(ctypes.c_double)], None),
+        "implisolid_set_jit_max_modules": ([ctypes.c_int], None),
+        "implisolid_jit_modules": ([ip], None),
         "implisolid_set_progress_callback": ([PROGRESS_CALLBACK, c_void_p], None),
         "implisolid_ob02_profile": ([c_int], None),
         "implisolid_jit_compile_points": ([c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)],
@@ -254,7 +257,15 @@ def jit_stats():
     out = (ctypes.c_int32 * 4)()
     secs = ctypes.c_double(0)
     lib().implisolid_jit_stats(out, ctypes.byref(secs))
-    return {"mode": out[0], "bake": int(out[1]), "compiled": out[2], "disk_hits": out[3], "compile_s": secs.value}
+    mods = (ctypes.c_int32 * 3)()
+    lib().implisolid_jit_modules(mods)
+    return {"mode": out[0], "bake": int(out[1]), "compiled": out[2], "disk_hits": out[3], "compile_s": secs.value,
+            "modules": mods[0], "max_modules": mods[1], "evicted": mods[2]}
+
+
+def set_jit_max_modules(n):
+    """Bound the loaded tree modules (least recently requested unheld ones are unloaded past it)."""
+    lib().implisolid_set_jit_max_modules(int(n))
 
 
 def jit_compile(shape, points=False):

@@ -829,6 +829,13 @@ void implisolid_jit_stats(int32_t out[4], double* compile_seconds) {
     out[3] = j.disk_hits();
     if (compile_seconds) *compile_seconds = j.compile_seconds();
 }
+void implisolid_set_jit_max_modules(int n) { TreeJit::instance().set_max_modules(n); }
+void implisolid_jit_modules(int32_t out[3]) {
+    TreeJit& j = TreeJit::instance();
+    out[0] = j.modules();
+    out[1] = j.max_modules();
+    out[2] = j.evicted();
+}
 
 int implisolid_slab_set_timing(implisolid_slab* s, int on) { SLAB_TRY(s->engine.set_timing(on != 0)) }
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]) { SLAB_TRY(s->engine.kernel_times(ms)) }

@@ -159,6 +159,19 @@ Engine::~Engine() {
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
+    (void)hipDeviceSynchronize();   // (hipFree already waits; the modules' last launches are done)
+    release_jit();
+}
+
+void Engine::release_jit() {
+    TreeJit& J = TreeJit::instance();
+    J.release(jit_slot_);
+    J.release(bake_slot_);
+    J.release(pt_slot_);
+    jit_slot_ = bake_slot_ = pt_slot_ = nullptr;
+    jit_requested_ = bake_requested_ = pt_requested_ = false;
+    jit_fn_ = nullptr;
+    jit_iv_ = JitIntervalKernels{};
 }
 
 void Engine::set_object(const Program& prog) {
@@ -171,13 +184,8 @@ void Engine::set_object(const Program& prog) {
     depth_ = prog.max_depth;
     n_csg_ = prog.n_csg;
     prog_host_ = prog;
-    jit_requested_ = false;
-    jit_slot_ = nullptr;
-    bake_requested_ = false;
-    bake_slot_ = nullptr;
+    release_jit();
     evals_ = 0;
-    pt_requested_ = false;
-    pt_slot_ = nullptr;
     jit_fn_ = nullptr;
     have_object_ = true;
 }

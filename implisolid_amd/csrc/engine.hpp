@@ -160,6 +160,7 @@ private:
     bool marks_valid_ = false;      // the last eval was pruned: count only marked units
     JitIntervalKernels jit_iv_;
     void ensure_jit();
+    void release_jit();   // drop the module references (after the device has synchronised)
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false, probe_only_ = false;
     DevBuf prog_, rabbit_, cases_;

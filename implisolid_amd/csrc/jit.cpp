@@ -4,6 +4,7 @@
 
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -437,6 +438,7 @@ TreeJit& TreeJit::instance() {
 TreeJit::TreeJit() {
     if (const char* e = std::getenv("IMPLISOLID_JIT")) mode_.store(e[0] == '0' ? kOff : e[0] == '1' ? kSync : kAsync);
     if (const char* e = std::getenv("IMPLISOLID_JIT_BAKE")) set_bake(e[0] - '0');
+    if (const char* e = std::getenv("IMPLISOLID_JIT_MAX_MODULES")) set_max_modules(std::atoi(e));
     const char* d = std::getenv("IMPLISOLID_JIT_CACHE");
     if (d && (!std::strcmp(d, "off") || !std::strcmp(d, "0"))) {
         disk_dir_.clear();
@@ -657,6 +659,7 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
     (void)hipGetDevice(&dev);
     Slot* slot = nullptr;
     bool fresh = false;
+    std::vector<Slot*> evict;
     {
         std::lock_guard<std::mutex> lock(mu_);
         const std::string key = std::to_string(dev) + "\n" + src;
@@ -667,9 +670,11 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
             slot = new Slot();
             slot->kind = kind;
             slot->src = std::move(src);
+            slot->key = key;
             slot->device = dev;
             cache_.emplace(key, slot);
             fresh = true;
+            if ((int)cache_.size() > max_modules_) evict_locked(evict);
             if (m == kAsync && !stop_) {
                 queue_.push_back(slot);
                 if (workers_.empty()) {   // a small pool, started on first use
@@ -681,6 +686,12 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
             }
         }
     }
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        ++slot->refs;
+        slot->last_use = ++tick_;
+    }
+    unload(evict);
     if (fresh && m == kAsync) cv_.notify_one();
     if (fresh && (m == kSync || stop_)) build(slot);
     if (m == kSync) {   // a slot queued earlier in async mode: wait for it
@@ -688,6 +699,59 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
         idle_cv_.wait(lock, [slot] { return slot->ready.load() || slot->failed.load(); });
     }
     return slot;
+}
+
+void TreeJit::evict_locked(std::vector<Slot*>& out) {
+    // the least recently requested finished slots nobody holds, down to 3/4 of the bound (one
+    // eviction pays for many requests); queued or compiling slots are never taken
+    std::vector<Slot*> idle;
+    for (auto& kv : cache_) {
+        Slot* s = kv.second;
+        if (s->refs == 0 && (s->ready.load(std::memory_order_acquire) || s->failed.load(std::memory_order_acquire)))
+            idle.push_back(s);
+    }
+    std::sort(idle.begin(), idle.end(), [](const Slot* a, const Slot* b) { return a->last_use < b->last_use; });
+    const size_t target = (size_t)max_modules_ * 3 / 4;
+    for (Slot* s : idle) {
+        if (cache_.size() <= target) break;
+        cache_.erase(s->key);
+        out.push_back(s);
+    }
+}
+
+void TreeJit::unload(std::vector<Slot*>& slots) {
+    // nothing references these slots: their last users synchronised before releasing them, and the
+    // device is synchronised once more so no kernel of an unloaded module can still be in flight
+    if (slots.empty()) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    std::map<int, bool> synced;
+    for (Slot* s : slots) {
+        if (s->mod) {
+            if (!synced[s->device]) {
+                (void)hipSetDevice(s->device);
+                (void)hipDeviceSynchronize();
+                synced[s->device] = true;
+            }
+            (void)hipSetDevice(s->device);
+            (void)hipModuleUnload(s->mod);
+        }
+        delete s;
+        n_evicted_.fetch_add(1);
+    }
+    (void)hipSetDevice(prev);
+    slots.clear();
+}
+
+void TreeJit::release(Slot* slot) {
+    if (!slot) return;
+    std::lock_guard<std::mutex> lock(mu_);
+    if (slot->refs > 0) --slot->refs;
+}
+
+int TreeJit::modules() const {
+    std::lock_guard<std::mutex> lock(mu_);
+    return (int)cache_.size();
 }
 
 void TreeJit::wait_idle() {
@@ -700,7 +764,7 @@ void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
     // register and queue every program's module (async), then drain the queue with extra threads
     const int saved = mode();
     mode_.store(kAsync);
-    for (const Program& p : progs) (void)request(p, kBricks, bake() == kBakeAlways);
+    for (const Program& p : progs) release(request(p, kBricks, bake() == kBakeAlways));   // cached, not held
     mode_.store(saved);
     // let the pool drain the queue, with extra threads for a large batch
     std::vector<std::thread> extra;

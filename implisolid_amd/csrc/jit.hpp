@@ -49,8 +49,11 @@ public:
                       points = nullptr;
     };
     enum Kind { kBricks = 0, kPoints = 1 };
-    // One compiled module (one source on one device).  Slots live as long as the process; `ready`
-    // is set (release) once `k` holds the loaded kernels, `failed` if compilation or loading failed.
+    // One compiled module (one source on one device).  `ready` is set (release) once `k` holds the
+    // loaded kernels, `failed` if compilation or loading failed.  request() takes a reference and
+    // release() drops it; the cache holds at most max_modules() slots and, past that, unloads the
+    // least recently requested finished slots nobody references (IMPLISOLID_JIT_MAX_MODULES,
+    // default 1024; a long-lived service polygonising ever-new objects keeps bounded device memory).
     struct Slot {
         std::atomic<bool> ready{false}, failed{false};
         Kernels k;
@@ -58,7 +61,10 @@ public:
         int kind = kBricks;
         hipModule_t mod = nullptr;
         std::string src;
+        std::string key;
         int device = 0;
+        int refs = 0;             // guarded by mu_
+        uint64_t last_use = 0;    // request tick, guarded by mu_
     };
     // Modes (IMPLISOLID_JIT=0|1|2, implisolid_set_jit):
     //   0 off: the interpreter kernels only;
@@ -77,6 +83,12 @@ public:
     enum BakeMode { kBakeNever = 0, kBakeAlways = 1, kBakeHot = 2 };
     static constexpr int kBakeAfter = 4;
     Slot* request(const Program& p, int kind = kBricks, bool bake = false);
+    // drop a reference taken by request() (null is ignored); the caller launches nothing from the
+    // slot afterwards and has synchronised whatever it launched
+    void release(Slot* slot);
+    int modules() const;
+    int max_modules() const { return max_modules_; }
+    void set_max_modules(int n) { max_modules_ = n < 8 ? 8 : n; }
     // block until every scheduled compilation has finished (bench / batch setup)
     void wait_idle();
     // compile the modules of many programs (sync, up to `threads` host threads); request() then
@@ -100,6 +112,7 @@ public:
     void set_enabled(bool on) { set_mode(on ? kAsync : kOff); }
     int compiled() const { return n_compiled_.load(); }
     int disk_hits() const { return n_disk_.load(); }
+    int evicted() const { return n_evicted_.load(); }
     double compile_seconds() const;
 
 private:
@@ -107,7 +120,12 @@ private:
     void build(Slot* slot);            // compile (or read from disk) + load; sets ready / failed
     void worker();
     void shutdown();
-    std::mutex mu_;
+    void evict_locked(std::vector<Slot*>& out);   // pick slots to unload (mu_ held)
+    void unload(std::vector<Slot*>& slots);       // unload and free them (mu_ not held)
+    mutable std::mutex mu_;
+    uint64_t tick_ = 0;
+    int max_modules_ = 1024;
+    std::atomic<int> n_evicted_{0};
     std::condition_variable cv_, idle_cv_;
     std::unordered_map<std::string, Slot*> cache_;   // key: device + source
     std::deque<Slot*> queue_;

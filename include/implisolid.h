@@ -234,6 +234,12 @@ void implisolid_set_jit_bake(int mode);
 void implisolid_jit_wait(void);
 /* [mode, bake, modules compiled, modules read from the disk cache], total compile seconds */
 void implisolid_jit_stats(int32_t out[4], double* compile_seconds);
+/* bound on the loaded tree modules (IMPLISOLID_JIT_MAX_MODULES, default 1024, at least 8): past it
+ * the least recently requested modules no engine holds are unloaded (a later request recompiles or
+ * reads the disk cache).  Replaces nothing in mcc2.cpp: the reference interprets its trees. */
+void implisolid_set_jit_max_modules(int n);
+/* [modules resident, bound, modules unloaded so far] */
+void implisolid_jit_modules(int32_t out[3]);
 int implisolid_slab_kernel_times(implisolid_slab* s, float ms[6]);
 /* the same timing per kernel: [coarse interval pass, brick refine, brick fill, field eval, MC count,
  * unit scan, vertex emission (k_mc_cells), face emission (k_mc_faces)] */

@@ -349,6 +349,54 @@ def test_jit_field_matches_interpreter(impli, name, level):
         assert ba == bb
 
 
+def test_jit_module_bound_unloads_idle_modules(impli, oracle):
+    """The loaded-module bound: with one baked module per object and room for 8, polygonising 14
+    objects one after another unloads the least recently used idle modules (never one a live slab
+    holds); an object seen again is rebuilt (disk cache or hipRTC) with the same mesh, which is the
+    oracle's."""
+    import hashlib
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(32, 1.0)
+    shapes = [scenes.random_tree(515000 + k, 3) for k in range(14)]
+    impli.set_jit(1)
+    impli.set_jit_bake(1)
+    impli.set_jit_max_modules(8)
+    ev0 = impli.jit_stats()["evicted"]
+
+    def mesh(shape):
+        s = impli.Slab(shape, mc)
+        try:
+            nv, nf = s.run()
+            assert s.used_jit()
+            st = impli.jit_stats()
+            assert st["modules"] <= 9, st   # the bound, plus the module just requested
+            return s.download(nv, nf)
+        finally:
+            s.close()
+
+    try:
+        first = mesh(shapes[0])
+        held = impli.Slab(shapes[1], mc)   # a live slab's module is never unloaded
+        try:
+            held.run()
+            for sh in shapes[2:]:
+                mesh(sh)
+            assert impli.jit_stats()["evicted"] > ev0
+            nv, nf = held.run()            # its module is still loaded: no fault, same kernels
+            vh, fh = held.download(nv, nf)
+        finally:
+            held.close()
+        again = mesh(shapes[0])
+    finally:
+        impli.set_jit_max_modules(1024)
+        impli.set_jit(2)
+        impli.set_jit_bake(2)
+    for (v, f), sh in ((first, shapes[0]), (again, shapes[0]), ((vh, fh), shapes[1])):
+        vr, fr = oracle.polygonize(json.dumps(sh), json.dumps(mc))
+        assert np.array_equal(f, fr) and np.array_equal(v.view(np.uint32), vr.view(np.uint32))
+    assert hashlib.sha256(first[1].tobytes()).digest() == hashlib.sha256(again[1].tobytes()).digest()
+
+
 def test_jit_async_first_call_then_compiled(impli, oracle):
     """Async JIT (the default): a never-seen shape is polygonised at once with the interpreter
     kernels while its module compiles in the background; after jit_wait() the same slab's eval runs
