@@ -479,17 +479,17 @@ int implisolid_debug_fold(const float* terms, int64_t n, float* sum_out, int64_t
     try {
         (void)engine();   // the device context
         int tc = 0;
-        static long long st[6];
+        static long long st[11];
         static int tr[256];
         *sum_out = debug_fold(terms, n, &tc, st, tr);
         if (std::getenv("IMPLISOLID_FOLD_TRACE")) {
-            for (int i = 0; i < 256 && i < st[0] + st[1] + st[2]; ++i)
-                std::fprintf(stderr, "%s k=%d E=%d\n", (tr[i] >> 28) == 1 ? "table" : "term ", tr[i] & 0xfffff,
-                             ((tr[i] >> 20) & 0xff) - 64);
+            for (int i = 0; i < 256 && i < st[0] + st[1] + st[2] + st[6]; ++i)
+                std::fprintf(stderr, "%s k=%d E=%d\n", (tr[i] >> 28) == 1 ? "table" : (tr[i] >> 28) == 3 ? "jump " : (tr[i] >> 28) == 4 ? "fast+" : (tr[i] >> 28) == 5 ? "fast-" : (tr[i] >> 28) == 6 ? "fastX" : "term ",
+                             tr[i] & 0xfffff, ((tr[i] >> 20) & 0xff) - 64);
         }
         if (std::getenv("IMPLISOLID_FOLD_STATS"))
-            std::fprintf(stderr, "fold n=%lld steps zero/serial %lld table %lld terms %lld global-term-loads %lld cycles stage %lld walk %lld\n",
-                         (long long)n, st[0], st[1], st[2], st[3], st[4], st[5]);
+            std::fprintf(stderr, "fold n=%lld steps zero/serial %lld table %lld terms %lld global-term-loads %lld run-jumps %lld cycles stage %lld walk %lld (table %lld terms %lld) term parts: preamble %lld fast %lld\n",
+                         (long long)n, st[0], st[1], st[2], st[3], st[6], st[4], st[5], st[7], st[8], st[9], st[10]);
         if (table_chunks) *table_chunks = tc;
     } catch (const std::exception& e) {
         report(e.what(), false);

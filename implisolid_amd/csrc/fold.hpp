@@ -55,28 +55,31 @@ IMPLI_FOLD_HD inline FoldPair fold_compose(FoldPair f, FoldPair g) {
 // (>= 2^31 spacings), negative, inf or NaN, with kFoldNaN for NaN; e = M 2^(ex-150), M the 24-bit
 // significand
 IMPLI_FOLD_HD inline FoldPair fold_pair_term(uint32_t bits, int E, uint8_t& flags) {
+    // branch-free (every case computed, then selected: the walk runs this in a single wave's
+    // dependent chain, where divergent branches cost more than the arithmetic); 32-bit throughout:
+    // M < 2^24, so M << sh (sh < 8) < 2^31 and M + half (d <= 25) < 2^25
     const uint32_t ex = (bits >> 23) & 0xffu, frac = bits & 0x7fffffu;
-    flags = 0;
-    if (ex == 0xffu) { flags = frac ? (kFoldBad | kFoldNaN) : kFoldBad; return FoldPair{0u, 0u}; }   // NaN / inf
-    if (bits & 0x80000000u) {                      // negative (-0 contributes 0 exactly)
-        if (bits & 0x7fffffffu) flags = kFoldBad;
-        return FoldPair{0u, 0u};
-    }
-    if (ex == 0u && frac == 0u) return FoldPair{0u, 0u};   // +0
-    const uint64_t M = (uint64_t)(frac | (ex ? 0x800000u : 0u));
+    const bool special = ex == 0xffu;                   // NaN / inf
+    const bool neg = (bits >> 31) != 0u;
+    const bool zero = (bits & 0x7fffffffu) == 0u;       // +-0 contributes 0 exactly
+    const uint32_t M = frac | (ex ? 0x800000u : 0u);
     const int sh = (ex ? (int)ex : 1) - 150 + 24 - E;
-    if (sh >= 0) {
-        if (sh >= 8) { flags = kFoldBad; return FoldPair{kFoldCap, kFoldCap}; }   // >= 2^31
-        const uint32_t r = fold_sat((uint32_t)(M << sh));
-        return FoldPair{r, r};
-    }
     const int d = -sh;
-    if (d > 25) return FoldPair{0u, 0u};           // below half the spacing: adds nothing
-    const uint64_t half = (uint64_t)1 << (d - 1), rem = M & (((uint64_t)1 << d) - 1);
-    const uint32_t m = (uint32_t)(M >> d);
-    if (rem == half) return FoldPair{m + (m & 1u), m + 1u - (m & 1u)};   // a tie: to even
-    const uint32_t r = (uint32_t)((M + half) >> d);
-    return FoldPair{r, r};
+    const int dc = d < 1 ? 1 : (d > 25 ? 25 : d);
+    const uint32_t half = 1u << (dc - 1), rem = M & ((1u << dc) - 1u), m = M >> dc;
+    const bool tie = rem == half;                       // exactly half a spacing: to even
+    const uint32_t rr = (M + half) >> dc;
+    const uint32_t a0 = d > 25 ? 0u : (tie ? m + (m & 1u) : rr);   // below half the spacing: nothing
+    const uint32_t a1 = d > 25 ? 0u : (tie ? m + 1u - (m & 1u) : rr);
+    const bool big = sh >= 8;                           // >= 2^31 spacings
+    const uint32_t left = big ? kFoldCap : fold_sat(M << (sh < 0 ? 0 : (sh > 7 ? 7 : sh)));
+    const bool kill = special || neg || zero;
+    FoldPair p;
+    p.c0 = kill ? 0u : (sh >= 0 ? left : a0);
+    p.c1 = kill ? 0u : (sh >= 0 ? left : a1);
+    flags = special ? (frac ? (uint8_t)(kFoldBad | kFoldNaN) : kFoldBad)
+                    : ((zero || !(neg || big)) ? (uint8_t)0 : kFoldBad);
+    return p;
 }
 
 // the window base of a chunk from the estimate of the sum before it (frexp exponent minus 3; a

@@ -35,20 +35,28 @@ namespace impli {
 
 using namespace dev;
 
+// One 32-byte record per slot, so inserting or reading an edge touches one cache line (five
+// arrays of one field each made k_edge_insert / k_fof five scattered lines per half-edge).  All
+// fields start at 0 (one memset): key holds the edge key + 1 (0 = empty), first_inv the complement
+// of the lowest face (so its start value 0 means none and atomicMax takes the minimum).
+struct EdgeRec {
+    unsigned long long key;
+    uint32_t cnt;
+    uint32_t f2[2];      // the faces of the edge's first two insertions (cnt says which hold one)
+    uint32_t first_inv;  // ~(lowest face): non-manifold extras while inserting, every face after k_fof
+    uint32_t last;       // highest face, likewise
+    uint32_t pad;
+};
+static_assert(sizeof(EdgeRec) == 32, "one record per 32 bytes");
 struct EdgeTab {
-    unsigned long long* key;
-    uint32_t* first;
-    uint32_t* last;
-    uint32_t* cnt;
+    EdgeRec* rec;        // cap records
     uint32_t* slot_of;   // 3 * nf
-    uint32_t* f2;        // 2 * cap: the faces of an edge's first two insertions (cnt says which hold one)
     uint64_t mask;
 };
 
 
 namespace {
 
-constexpr uint64_t kEmpty = ~0ull;
 
 #define DEPTH_LAUNCH(depth, KERNEL, GRID, BLOCK, STREAM, ...)                              \
     do {                                                                                   \
@@ -182,18 +190,19 @@ __global__ void k_edge_insert(const int32_t* __restrict__ f, int64_t nf, int64_t
     const unsigned long long key = (e2 > e1) ? e1 + e2 * (uint64_t)nv : e2 + e1 * (uint64_t)nv;
     uint64_t s = (key * 0x9E3779B97F4A7C15ull >> 17) & t.mask;
     while (true) {
-        const unsigned long long prev = atomicCAS(&t.key[s], kEmpty, key);
-        if (prev == kEmpty || prev == key) break;
+        const unsigned long long prev = atomicCAS(&t.rec[s].key, 0ull, key + 1ull);
+        if (prev == 0ull || prev == key + 1ull) break;
         s = (s + 1) & t.mask;
     }
     // two atomics per half-edge: the arrival index keeps the first two faces (an edge of a closed
     // manifold mesh has exactly two); min / max over further ones only for non-manifold edges
-    const uint32_t k = atomicAdd(&t.cnt[s], 1u);
+    EdgeRec& r = t.rec[s];
+    const uint32_t k = atomicAdd(&r.cnt, 1u);
     if (k < 2) {
-        t.f2[2 * s + k] = (uint32_t)fi;
+        r.f2[k] = (uint32_t)fi;
     } else {
-        atomicMin(&t.first[s], (uint32_t)fi);
-        atomicMax(&t.last[s], (uint32_t)fi);
+        atomicMax(&r.first_inv, ~(uint32_t)fi);
+        atomicMax(&r.last, (uint32_t)fi);
     }
     t.slot_of[i] = (uint32_t)s;
 }
@@ -205,12 +214,13 @@ __global__ void k_fof(int64_t nf, EdgeTab t, int32_t* __restrict__ fof) {
     if (i >= 3 * nf) return;
     const uint32_t s = t.slot_of[i];
     const uint32_t fi = (uint32_t)(i / 3);
-    const uint32_t c = t.cnt[s], a = t.f2[2 * s], b = c >= 2 ? t.f2[2 * s + 1] : a;
+    EdgeRec& r = t.rec[s];
+    const uint32_t c = r.cnt, a = r.f2[0], b = c >= 2 ? r.f2[1] : a;
     // first / last face of the edge (the min / max words hold only non-manifold extras); every
     // half-edge of the slot stores the same values for the subdivision pass
-    const uint32_t first = min(min(a, b), t.first[s]), last = max(max(a, b), t.last[s]);
-    t.first[s] = first;
-    t.last[s] = last;
+    const uint32_t first = min(min(a, b), ~r.first_inv), last = max(max(a, b), r.last);
+    r.first_inv = ~first;
+    r.last = last;
     fof[i] = (int32_t)((first != fi) ? first : (c >= 2 ? last : 0u));
 }
 
@@ -219,7 +229,7 @@ __global__ void k_fof(int64_t nf, EdgeTab t, int32_t* __restrict__ fof) {
 // their edge over (face ascending; e01, e12, e20).  The first slot of an edge is in face
 // first[edge], at the lowest k of that face holding the edge.
 __device__ __forceinline__ bool first_slot(const EdgeTab& t, int64_t fi, int k, uint32_t s[3]) {
-    return t.first[s[k]] == (uint32_t)fi && (k < 1 || s[0] != s[k]) && (k < 2 || s[1] != s[k]);
+    return ~t.rec[s[k]].first_inv == (uint32_t)fi && (k < 1 || s[0] != s[k]) && (k < 2 || s[1] != s[k]);
 }
 
 __global__ void k_sub_count(int64_t nf, EdgeTab t, uint32_t* __restrict__ cnt) {
@@ -468,66 +478,65 @@ __global__ void k_fof_range(const int32_t* __restrict__ fof, int64_t j0, int64_t
 }
 
 // ---- step 2 ----------------------------------------------------------------------------------
-// compute_average_edge_length cp:70-82 terms, in the reference's order (summed serially on host)
-__global__ void k_edge_norms(const float* __restrict__ v, const int32_t* __restrict__ f, int64_t nf, float* __restrict__ o) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= nf) return;
-    const float* a = v + 3 * f[3 * j];
-    const float* b = v + 3 * f[3 * j + 1];
-    const float* c = v + 3 * f[3 * j + 2];
-    o[3 * j] = norm2f(a[0] - b[0], a[1] - b[1], a[2] - b[2]);
-    o[3 * j + 1] = norm2f(a[0] - c[0], a[1] - c[1], a[2] - c[2]);
-    o[3 * j + 2] = norm2f(c[0] - b[0], c[1] - b[1], c[2] - b[2]);
-}
 
-// the fold's chunk table (fold.hpp), three small passes: each chunk's terms summed in double (one
-// wave per chunk); the exclusive prefix of those sums (one block) -> each chunk's binade window;
-// the table cells of the window (one wave per chunk, 4 terms per lane, wave sums of the lanes'
-// saturating partial sums, flags OR-ed)
-__global__ __launch_bounds__(256) void k_fold_chunk_sums(const float* __restrict__ e, int64_t n, double* __restrict__ cs) {
+// the fold's chunk table (fold.hpp), two passes: each chunk's terms summed in double (one wave per
+// chunk, four chunks per block, the block's sum beside them) -- fused with the terms themselves when
+// they are the mesh's edge lengths; then the table (one wave per chunk, 4 terms per lane, wave sums
+// of the lanes' saturating partial sums, flags OR-ed), each block first summing the block sums
+// before it for its chunks' estimates (the sums of the terms before each chunk) and binade windows.
+// The estimates only choose windows and staging hints: the walk checks every step, so any close
+// double sum serves.
+constexpr int kFoldBlockChunks = 4;   // chunks per 256-thread block
+__device__ __forceinline__ void fold_block_sums(double v, int64_t c, int64_t nc, double* __restrict__ cs,
+                                                double* __restrict__ bs) {
+    __shared__ double s_cs[kFoldBlockChunks];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) {
+        if (c < nc) cs[c] = v;
+        s_cs[w] = c < nc ? v : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) bs[blockIdx.x] = ((s_cs[0] + s_cs[1]) + s_cs[2]) + s_cs[3];
+}
+__global__ __launch_bounds__(256) void k_fold_chunk_sums(const float* __restrict__ e, int64_t n, double* __restrict__ cs,
+                                                         double* __restrict__ bs) {
     const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
-    if (c >= fold_chunks(n)) return;   // uniform per wave
     double v = 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const int64_t k = c * kFoldChunk + q * 64 + lane;
+        const int64_t k = c * kFoldChunk + 4 * lane + q;
         if (k < n) v += (double)e[k];
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) cs[c] = v;
+    fold_block_sums(v, c, fold_chunks(n), cs, bs);
 }
-__global__ __launch_bounds__(1024) void k_fold_bases(const double* __restrict__ cs, int64_t nc, int32_t* __restrict__ base,
-                                                    double* __restrict__ est) {
-    __shared__ double s_w[16];
-    __shared__ double s_carry;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (t == 0) s_carry = 0.0;
-    __syncthreads();
-    for (int64_t i0 = 0; i0 < nc; i0 += 1024) {
-        const int64_t i = i0 + t;
-        const double v = i < nc ? cs[i] : 0.0;
-        double inc = v;
+// compute_average_edge_length cp:70-82 terms, in the reference's order: term 3j + r of face j is
+// |a - b|, |a - c|, |c - b| for r = 0, 1, 2; written and summed per chunk in one pass
+__global__ __launch_bounds__(256) void k_fold_edge_terms(const float* __restrict__ v, const int32_t* __restrict__ f,
+                                                         int64_t nf, float* __restrict__ o, double* __restrict__ cs,
+                                                         double* __restrict__ bs) {
+    const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t n = 3 * nf;
+    double acc = 0.0;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const double y = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += y;
+    for (int q = 0; q < 4; ++q) {
+        const int64_t k = c * kFoldChunk + 4 * lane + q;
+        if (k < n) {
+            const int64_t j = k / 3;
+            const int r = (int)(k - 3 * j);
+            const float* pa = v + 3 * f[3 * j + (r == 2 ? 2 : 0)];
+            const float* pb = v + 3 * f[3 * j + (r == 1 ? 2 : 1)];
+            const float x = norm2f(pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]);
+            o[k] = x;
+            acc += (double)x;
         }
-        if (lane == 63) s_w[w] = inc;
-        __syncthreads();
-        double off = s_carry;
-        for (int k = 0; k < w; ++k) off += s_w[k];
-        if (i < nc) {
-            base[i] = fold_base(off + inc - v);   // the estimate of the sum before chunk i
-            est[i] = off + inc - v;
-        }
-        __syncthreads();
-        if (t == 1023) s_carry = off + inc;
-        __syncthreads();
     }
-    if (t == 0) est[nc] = s_carry;
+    fold_block_sums(acc, c, fold_chunks(n), cs, bs);
 }
+
 // Inclusive wave scan of u32 through DPP (gfx9: row_shr 1, 2, 4, 8 inside rows of 16 lanes, then
 // row_bcast 15 and 31 into the rows above): a few cycles per step, where a ds_bpermute shuffle
 // takes a round trip through LDS -- the walk is a chain of such scans
@@ -583,19 +592,33 @@ __device__ __forceinline__ uint32_t pair_apply(FoldPair p, uint32_t x) { return 
 // crosses a power of two inside the chunk, with a margin of 2^-7 for the float chain's drift from the
 // double estimate, or the chunk is flagged in the binades the estimate puts s in) -- k_fold_walk
 // stages those chunks' terms in LDS beforehand
-__global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e, int64_t n, const int32_t* __restrict__ base,
-                                                    const double* __restrict__ est, FoldPair* __restrict__ pairs,
-                                                    uint8_t* __restrict__ flags, uint8_t* __restrict__ hint) {
+__global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e, int64_t n, const double* __restrict__ cs,
+                                                    const double* __restrict__ bs, int32_t* __restrict__ base,
+                                                    FoldPair* __restrict__ pairs, uint8_t* __restrict__ flags,
+                                                    uint8_t* __restrict__ hint) {
+    __shared__ double s_part[4];
     const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (c >= fold_chunks(n)) return;   // uniform per wave
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // the sum of the terms before this block's chunks: the block sums before it
+    double p = 0.0;
+    for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += 256) p += bs[b];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+    if (lane == 0) s_part[w] = p;
+    __syncthreads();
+    const int64_t nc = fold_chunks(n);
+    if (c >= nc) return;   // uniform per wave
+    double e0 = ((s_part[0] + s_part[1]) + s_part[2]) + s_part[3];
+    for (int q = 0; q < w; ++q) e0 += cs[(int64_t)blockIdx.x * kFoldBlockChunks + q];
+    const double est_c = e0, est_c1 = e0 + cs[c];
+    if (lane == 0) base[c] = fold_base(est_c);
     uint32_t bits[4];   // lane l: the chunk's terms 4 l .. 4 l + 3 (the maps compose in term order)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int64_t k = c * kFoldChunk + 4 * lane + q;
         bits[q] = k < n ? __float_as_uint(e[k]) : 0u;   // +0 past the end contributes nothing
     }
-    const int E0 = base[c];
+    const int E0 = fold_base(est_c);
     uint32_t fl34 = 0;
 #pragma unroll
     for (int b = 0; b < kFoldBinades; ++b) {
@@ -617,11 +640,11 @@ __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e,
         if (b == 3 || b == 4) fl34 |= f;
     }
     if (lane == 0) {
-        const double lo = est[c] * (1.0 - 0x1p-7), hi = est[c + 1] * (1.0 + 0x1p-7);
+        const double lo = est_c * (1.0 - 0x1p-7), hi = est_c1 * (1.0 + 0x1p-7);
         int elo = 0, ehi = 0;
         (void)frexp(lo, &elo);
         (void)frexp(hi, &ehi);
-        hint[c] = (uint8_t)(!(est[c] > 0.0) || elo != ehi || fl34 != 0 || !(hi < 0x1p100));
+        hint[c] = (uint8_t)(!(est_c > 0.0) || elo != ehi || fl34 != 0 || !(hi < 0x1p100));
     }
 }
 
@@ -670,19 +693,27 @@ __device__ void alpha_list_dev(float avg, FoldOut* o) {
 // One block: its waves stage a window of the table (kWalkWindow chunk rows) and the terms of the
 // window's hinted chunks (kWalkSlots of them) in LDS, then wave 0 walks the window from LDS; terms
 // of an unhinted chunk the walk needs are read from memory.
-constexpr int kWalkThreads = 1024, kWalkWindow = 1536, kWalkSlots = 40;
+constexpr int kWalkThreads = 1024, kWalkWindow = 1536, kWalkSlots = 40, kWalkB0 = 2, kWalkBins = kFoldBinades - kWalkB0;
 
 __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restrict__ e, int64_t n64,
                                                             const int32_t* __restrict__ base, const FoldPair* __restrict__ pairs,
                                                             const uint8_t* __restrict__ flags, const uint8_t* __restrict__ hint,
                                                             int64_t nf, FoldOut* __restrict__ out) {
-    __shared__ FoldPair w_pair[kWalkWindow * kFoldBinades];
-    __shared__ uint8_t w_flag[kWalkWindow * kFoldBinades];
+    // the table cells of binades base + kWalkB0 .. base + 5 (the chain stays within a factor 2 of
+    // the estimate: binades base + 3 and base + 4 in practice; a cell outside goes term by term)
+    __shared__ FoldPair w_pair[kWalkWindow * kWalkBins];
+    __shared__ uint8_t w_flag[kWalkWindow * kWalkBins];
     __shared__ int32_t w_base[kWalkWindow];
     __shared__ int16_t w_slot[kWalkWindow];
     __shared__ int16_t w_slot_chunk[kWalkSlots];
     __shared__ float w_terms[kWalkSlots][kFoldChunk];
+    // per staged chunk: the lanes' inclusive prefix maps in binade base + 3 and suffix maps in base + 4
+    // (4 terms per lane), and the lanes holding a term either binade cannot express
+    __shared__ FoldPair w_pre[kWalkSlots][2][64];
+    __shared__ uint64_t w_prebad[kWalkSlots][2];
     __shared__ int w_nslots;
+    __shared__ int w_wcnt[kWalkThreads / 64];
+    __shared__ int w_ready[kWalkSlots];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int n = (int)n64;   // < 2^31 (launch_fold checks)
     const int nc = (int)fold_chunks(n64);
@@ -690,40 +721,88 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
     int k = 0;
     int table_chunks = 0;
     bool done = false;   // wave 0: a NaN or an inf decided the result
-    int st0 = 0, st1 = 0, st2 = 0, st3 = 0;
-    long long cyc_stage = 0, cyc_walk = 0;
+    int st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0, st5 = 0;
+    long long cyc_stage = 0, cyc_walk = 0, cyc_table = 0, cyc_term = 0, cyc_pre = 0, cyc_fast = 0;
     for (int c0 = 0; c0 < nc; c0 += kWalkWindow) {
         const long long tc0 = clock64();
         const int wn = nc - c0 < kWalkWindow ? nc - c0 : kWalkWindow;
         if (t == 0) w_nslots = 0;
+        if (t < kWalkSlots) w_ready[t] = 0;
         __syncthreads();   // the previous window's walk is over
-        for (int i = t; i < wn; i += kWalkThreads) {
+        // the window's table rows, and slots for its hinted chunks in chunk order (the walk meets
+        // them in that order): a ballot per wave and the waves' counts before it
+        for (int i0 = 0; i0 < wn; i0 += kWalkThreads) {
+            const int i = i0 + t;
             const int64_t c = c0 + i;
-            w_base[i] = base[c];
+            bool h = false;
+            if (i < wn) {
+                w_base[i] = base[c];
 #pragma unroll
-            for (int b = 0; b < kFoldBinades; ++b) {
-                w_pair[i * kFoldBinades + b] = pairs[c * kFoldBinades + b];
-                w_flag[i * kFoldBinades + b] = flags[c * kFoldBinades + b];
+                for (int b = 0; b < kWalkBins; ++b) {
+                    w_pair[i * kWalkBins + b] = pairs[c * kFoldBinades + kWalkB0 + b];
+                    w_flag[i * kWalkBins + b] = flags[c * kFoldBinades + kWalkB0 + b];
+                }
+                h = hint[c] != 0;
             }
-            int sl = -1;
-            if (hint[c]) {
-                sl = atomicAdd(&w_nslots, 1);
-                if (sl < kWalkSlots) w_slot_chunk[sl] = (int16_t)i;
-                else sl = -1;
+            const uint64_t hm = __ballot(h);
+            if (lane == 0) w_wcnt[wid] = (int)__popcll((unsigned long long)hm);
+            __syncthreads();
+            int before = w_nslots;
+            for (int w = 0; w < wid; ++w) before += w_wcnt[w];
+            const int sl = before + (int)__popcll((unsigned long long)(hm & ((1ull << lane) - 1ull)));
+            if (i < wn) {
+                w_slot[i] = (int16_t)(h && sl < kWalkSlots ? sl : -1);
+                if (h && sl < kWalkSlots) w_slot_chunk[sl] = (int16_t)i;
             }
-            w_slot[i] = (int16_t)sl;
+            __syncthreads();
+            if (t == kWalkThreads - 1) w_nslots = before + (int)__popcll((unsigned long long)hm);
+            __syncthreads();
         }
-        __syncthreads();
         const int ns = w_nslots < kWalkSlots ? w_nslots : kWalkSlots;
-        for (int i = t; i < ns * kFoldChunk; i += kWalkThreads) {
-            const int sl = i / kFoldChunk, j = i % kFoldChunk;
-            const int kk = (c0 + w_slot_chunk[sl]) * kFoldChunk + j;
-            w_terms[sl][j] = kk < n ? e[kk] : 0.f;
+        cyc_stage += clock64() - tc0;
+        if (wid != 0) {
+            // waves 1.. stage the slots while wave 0 walks: a slot's terms, then its lanes' maps --
+            // prefix scan in base + 3, suffix scan in base + 4, what a term step entering the chunk at
+            // its start in base + 3 needs -- then its ready flag (the walk waits for it)
+            for (int sl = wid - 1; sl < ns; sl += kWalkThreads / 64 - 1) {
+                const int kk0 = (c0 + w_slot_chunk[sl]) * kFoldChunk + 4 * lane;
+                uint32_t tb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    tb[j] = kk0 + j < n ? __float_as_uint(e[kk0 + j]) : 0u;
+                    w_terms[sl][4 * lane + j] = __uint_as_float(tb[j]);
+                }
+                const int Eb = w_base[w_slot_chunk[sl]] + 3;
+                FoldPair p3{0u, 0u}, p4{0u, 0u};
+                uint32_t f3 = 0, f4 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint8_t fa, fb;
+                    p3 = fold_compose(p3, fold_pair_term(tb[j], Eb, fa));
+                    p4 = fold_compose(p4, fold_pair_term(tb[j], Eb + 1, fb));
+                    f3 |= fa;
+                    f4 |= fb;
+                }
+                w_pre[sl][0][lane] = wave_scan_pairs(p3);
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {   // suffix: lane l <- its group, then the lanes after it
+                    FoldPair y;
+                    y.c0 = (uint32_t)__shfl_down((int)p4.c0, d, 64);
+                    y.c1 = (uint32_t)__shfl_down((int)p4.c1, d, 64);
+                    if (lane + d < 64) p4 = fold_compose(p4, y);
+                }
+                w_pre[sl][1][lane] = p4;
+                const uint64_t b3 = __ballot(f3 != 0u), b4 = __ballot(f4 != 0u);
+                if (lane == 0) {
+                    w_prebad[sl][0] = b3;
+                    w_prebad[sl][1] = b4;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&w_ready[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            continue;
         }
-        __syncthreads();
         const long long tc1 = clock64();
-        cyc_stage += tc1 - tc0;
-        if (wid != 0) continue;
         const int kend_w = (c0 + wn) * kFoldChunk < n ? (c0 + wn) * kFoldChunk : n;
         while (!done && k < kend_w) {   // uniform over wave 0
             // the walk's state is wave-uniform: kept in scalar registers, so its branches are scalar
@@ -764,8 +843,9 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             (void)frexpf(s, &E);   // s in [2^(E-1), 2^E): spacing 2^(E-24)
             E = __builtin_amdgcn_readfirstlane(E);
             uint32_t su = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E));   // in [2^23, 2^24)
+            const long long tA = clock64();
             if ((k & (kFoldChunk - 1)) == 0) {   // whole chunks from the table, 4 per lane: 256 per step
-                if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (1 << 28) | k;
+                if (lane == 0 && st0 + st1 + st2 + st4 < 256) out->trace[st0 + st1 + st2 + st4] = (1 << 28) | k;
                 ++st1;
                 const int i0 = k / kFoldChunk - c0 + 4 * lane;
                 FoldPair tp[4];
@@ -776,8 +856,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int i = i0 + j < wn ? i0 + j : wn - 1;
-                    const bool inb = i0 + j < wn && bb[j] >= 0 && bb[j] < kFoldBinades;
-                    const int cell = i * kFoldBinades + (inb ? bb[j] : 0);
+                    const bool inb = i0 + j < wn && bb[j] >= kWalkB0 && bb[j] < kFoldBinades;
+                    const int cell = i * kWalkBins + (inb ? bb[j] - kWalkB0 : 0);
                     tp[j] = w_pair[cell];
                     ok[j] = inb && w_flag[cell] == 0;
                     if (!ok[j]) tp[j] = FoldPair{0u, 0u};
@@ -791,12 +871,12 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 uint32_t v = pair_apply(excl, su), before = v;
                 int first = 4;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (first == 4) {
-                        const uint32_t v2 = pair_apply(tp[j], v);
-                        if (!ok[j] || v2 >= kFoldCap) { first = j; before = v; }
-                        else v = v2;
-                    }
+                for (int j = 0; j < 4; ++j) {   // selects, no branches (one wave's dependent chain)
+                    const uint32_t v2 = pair_apply(tp[j], v);
+                    const bool live = first == 4, stop = live && (!ok[j] || v2 >= kFoldCap);
+                    before = stop ? v : before;
+                    first = stop ? j : first;
+                    v = (live && !stop) ? v2 : v;
                 }
                 const uint64_t lm = __ballot(first < 4);
                 const int L = lm ? __ffsll((unsigned long long)lm) - 1 : 63;
@@ -812,14 +892,17 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                         continue;
                     }
                     k = __builtin_amdgcn_readfirstlane(k);
+                    if (!lm) continue;   // the step's reach ended, not the run: another table step
                     su = tt;   // the chunk that ended the run goes term by term now (same binade)
                 }
             }
+            const long long tB = clock64();
+            cyc_table += tB - tA;
             // the chunk the table could not take: its terms from k, 4 consecutive per lane, in order, as
             // maps of the current binade (fold.hpp) up to the first event -- an unusable term, or the
             // one that reaches the binade's end -- which is added as the chain's own float add; then on
             // from the next term in the binade the sum is in now, within the same step
-            if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (2 << 28) | k | (E + 64) << 20;
+            if (lane == 0 && st0 + st1 + st2 + st4 < 256) out->trace[st0 + st1 + st2 + st4] = (2 << 28) | k | (E + 64) << 20;
             ++st2;
             const int kc = k & ~(kFoldChunk - 1);
             const int kend = kc + kFoldChunk < n ? kc + kFoldChunk : n;
@@ -828,6 +911,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             // four loads issued before any use
             const int sl = __builtin_amdgcn_readfirstlane((int)w_slot[k / kFoldChunk - c0]);
             if (sl >= 0) {
+                while (__hip_atomic_load(&w_ready[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                    __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) xb[j] = __float_as_uint(w_terms[sl][4 * lane + j]);
             } else {
@@ -838,7 +923,93 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     xb[j] = __float_as_uint(e[kk < n ? kk : kc]);
                 }
             }
-            for (;;) {   // segments of the chunk, each ending at an event
+            // Fast path: a staged chunk entered at its start with the sum in binade base + 3.  Its
+            // lanes' prefix maps (staged) give each lane's value before and after its group at once;
+            // the first lane whose group reaches 2^24 or holds an unusable term holds the event, found
+            // term by term inside that group; the event term is the chain's own float add; then the
+            // group's remaining terms and the later lanes' suffix map (staged, binade base + 4) finish
+            // the chunk if the sum is in base + 4 and nothing there saturates or is unusable.  Any
+            // other case continues with the segments below from where this stopped.
+            const long long tF = clock64();
+            cyc_pre += tF - tB;
+            if (sl >= 0 && k == kc && s >= 0x1p-100f && s <= 0x1p100f) {
+                int E1 = 0;
+                (void)frexpf(s, &E1);
+                E1 = __builtin_amdgcn_readfirstlane(E1);
+                const int ic = kc / kFoldChunk - c0;
+                if (E1 == w_base[ic] + 3) {
+                    const uint32_t x0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E1));
+                    // independent of the sum: the lane's term maps in E1 (its group's search) and, in
+                    // E1 + 1, the maps of its group's terms from each position to the group's end
+                    FoldPair t1[4], g2[5];
+                    uint32_t f1[4], b2[5];
+                    g2[4] = FoldPair{0u, 0u};
+                    b2[4] = 0u;
+#pragma unroll
+                    for (int j = 3; j >= 0; --j) {
+                        uint8_t fa, fb;
+                        t1[j] = fold_pair_term(xb[j], E1, fa);
+                        g2[j] = fold_compose(fold_pair_term(xb[j], E1 + 1, fb), g2[j + 1]);
+                        f1[j] = fa;
+                        b2[j] = b2[j + 1] | fb;
+                    }
+                    const FoldPair incl = w_pre[sl][0][lane];
+                    const FoldPair excl = lane ? w_pre[sl][0][lane - 1] : FoldPair{0u, 0u};
+                    const uint32_t vb = pair_apply(excl, x0), ve = pair_apply(incl, x0);
+                    const uint64_t lm = __ballot(((w_prebad[sl][0] >> lane) & 1ull) != 0ull || ve >= kFoldCap);
+                    if (lm) {
+                        const int L = __ffsll((unsigned long long)lm) - 1;
+                        // the later lanes' suffix map in E1 + 1 (staged), read while the group is searched
+                        const FoldPair sufL = L < 63 ? w_pre[sl][1][L + 1] : FoldPair{0u, 0u};
+                        const bool badL = L < 63 && (w_prebad[sl][1] >> (L + 1)) != 0ull;
+                        uint32_t v = vb, before = vb, xe = 0;
+                        int first = 4;
+                        FoldPair rest = g2[4];   // the group's terms after the event, in E1 + 1
+                        uint32_t rest_bad = 0u;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const uint32_t v2 = pair_apply(t1[j], v);
+                            const bool live = first == 4, stop = live && (f1[j] != 0u || v2 >= kFoldCap);
+                            before = stop ? v : before;
+                            xe = stop ? xb[j] : xe;
+                            rest = stop ? g2[j + 1] : rest;
+                            rest_bad = stop ? b2[j + 1] : rest_bad;
+                            first = stop ? j : first;
+                            v = (live && !stop) ? v2 : v;
+                        }
+                        const int jf = (int)lane_value((uint32_t)first, L);   // < 4: lane L holds the event
+                        const FoldPair restL{lane_value(rest.c0, L), lane_value(rest.c1, L)};
+                        const FoldPair tail = fold_compose(restL, sufL);      // the chunk after the event
+                        const bool tail_bad = badL || lane_value(rest_bad, L) != 0u;
+                        s = ldexpf((float)lane_value(before, L), E1 - 24);
+                        const float xv = __uint_as_float(lane_value(xe, L));
+                        k = kc + 4 * L + jf + 1;
+                        if (xv != xv) {
+                            s = quiet_nan_of(xv);
+                            done = true;
+                        } else {
+                            s = s + xv;   // the event term: the chain's own float add
+                            if (k < kend && s >= 0x1p-100f && s <= 0x1p100f) {
+                                int E2 = 0;
+                                (void)frexpf(s, &E2);
+                                E2 = __builtin_amdgcn_readfirstlane(E2);
+                                const uint32_t x2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E2));
+                                const uint32_t x4 = pair_apply(tail, x2);
+                                const bool ok2 = E2 == E1 + 1 && !tail_bad && x4 < kFoldCap;
+                                if (ok2) {
+                                    s = ldexpf((float)x4, E2 - 24);
+                                    k = kend;
+                                }
+                                st5 += ok2 ? 1 : 0;
+                            }
+                        }
+                        ++st4;
+                    }
+                }
+            }
+            const long long tG = clock64();
+            cyc_fast += tG - tF;
+            for (; !done && k < kend;) {   // segments of the chunk, each ending at an event
                 if (!(s >= 0x1p-100f && s <= 0x1p100f)) break;   // the outer loop's term-by-term paths
                 (void)frexpf(s, &E);
                 E = __builtin_amdgcn_readfirstlane(E);
@@ -858,12 +1029,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 uint32_t v = pair_apply(excl, su), before = v, xe = 0;
                 int first = 4;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (first == 4) {
-                        const uint32_t v2 = pair_apply(tp[j], v);
-                        if (bad[j] || v2 >= kFoldCap) { first = j; before = v; xe = xb[j]; }
-                        else v = v2;
-                    }
+                for (int j = 0; j < 4; ++j) {   // selects, no branches
+                    const uint32_t v2 = pair_apply(tp[j], v);
+                    const bool live = first == 4, stop = live && (bad[j] || v2 >= kFoldCap);
+                    before = stop ? v : before;
+                    xe = stop ? xb[j] : xe;
+                    first = stop ? j : first;
+                    v = (live && !stop) ? v2 : v;
                 }
                 const uint64_t lm = __ballot(first < 4);
                 if (!lm) {
@@ -880,6 +1052,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 s = s + x;   // the event term: the chain's own float add
                 if (k >= kend) break;
             }
+            cyc_term += clock64() - tB;
         }
         cyc_walk += clock64() - tc1;
     }
@@ -887,7 +1060,9 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
         out->sum = s;
         out->table_chunks = table_chunks;
         out->steps[0] = st0; out->steps[1] = st1; out->steps[2] = st2; out->steps[3] = st3;
-        out->cycles[0] = cyc_stage; out->cycles[1] = cyc_walk;
+        out->steps[4] = st4; out->steps[5] = st5;
+        out->cycles[0] = cyc_stage; out->cycles[1] = cyc_walk; out->cycles[2] = cyc_table; out->cycles[3] = cyc_term;
+        out->cycles[4] = cyc_pre; out->cycles[5] = cyc_fast;
         const float avg = (float)((double)s / (3. * (double)nf));
         out->avg = avg;
         alpha_list_dev(avg, out);
@@ -1177,14 +1352,10 @@ void Ob02::ranges(int64_t out[6]) const {
 EdgeTab Ob02::edge_table() {
     uint64_t cap = 1024;
     while (cap < (uint64_t)(4 * nf + 16)) cap <<= 1;
-    etab_.reserve((size_t)cap * (8 + 12 + 8) + (size_t)(3 * nf + 1) * 4);
+    etab_.reserve((size_t)cap * sizeof(EdgeRec) + (size_t)(3 * nf + 1) * 4);
     EdgeTab t;
-    t.key = etab_.as<unsigned long long>();
-    t.first = reinterpret_cast<uint32_t*>(t.key + cap);
-    t.last = t.first + cap;
-    t.cnt = t.last + cap;
-    t.slot_of = t.cnt + cap;
-    t.f2 = t.slot_of + (3 * nf + 1);
+    t.rec = etab_.as<EdgeRec>();
+    t.slot_of = reinterpret_cast<uint32_t*>(t.rec + cap);
     t.mask = cap - 1;
     return t;
 }
@@ -1204,9 +1375,7 @@ void Ob02::build_topology() {
     // faces of faces
     const EdgeTab t = edge_table();
     const uint64_t cap = t.mask + 1;
-    IMPLI_HIP(hipMemsetAsync(t.key, 0xff, (size_t)cap * 8, s));
-    IMPLI_HIP(hipMemsetAsync(t.first, 0xff, (size_t)cap * 4, s));
-    IMPLI_HIP(hipMemsetAsync(t.last, 0, (size_t)cap * 8, s));   // last + cnt
+    IMPLI_HIP(hipMemsetAsync(t.rec, 0, (size_t)cap * sizeof(EdgeRec), s));
     fof_.reserve((size_t)(3 * nf + 1) * 4);
     if (nf) {
         k_edge_insert<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, nv, t);
@@ -1315,9 +1484,10 @@ struct FoldLayout {
     }
 };
 
-// the table passes on `ts`, then the walk on `ws` after them (ws may be ts)
-void launch_fold(const float* d_terms, int64_t n, int64_t nf, char* d_tab, FoldOut* d_out, hipStream_t ts, hipStream_t ws,
-                 hipEvent_t table_done) {
+// the table passes on `ts`, then the walk on `ws` after them (ws may be ts); with d_verts the terms
+// are the mesh's edge lengths, computed into d_terms by the first pass
+void launch_fold(float* d_terms, int64_t n, int64_t nf, const float* d_verts, const int32_t* d_faces, char* d_tab,
+                 FoldOut* d_out, hipStream_t ts, hipStream_t ws, hipEvent_t table_done) {
     if (n >= ((int64_t)1 << 31) - kFoldChunk) throw InputError("edge-length fold: more than 2^31 terms");
     const FoldLayout L(n);
     FoldPair* d_pair = reinterpret_cast<FoldPair*>(d_tab);
@@ -1325,11 +1495,12 @@ void launch_fold(const float* d_terms, int64_t n, int64_t nf, char* d_tab, FoldO
     uint8_t* d_flags = reinterpret_cast<uint8_t*>(d_base + L.chunks);
     uint8_t* d_hint = d_flags + L.cells;
     double* d_cs = reinterpret_cast<double*>(d_tab + L.cs_off);
-    double* d_est = reinterpret_cast<double*>(d_tab + L.est_off);
+    double* d_bs = reinterpret_cast<double*>(d_tab + L.est_off);   // block sums (chunks / 4 + 1)
     if (L.cells) {
-        k_fold_chunk_sums<<<blocks_for(L.chunks * 64), 256, 0, ts>>>(d_terms, n, d_cs);
-        k_fold_bases<<<1, 1024, 0, ts>>>(d_cs, L.chunks, d_base, d_est);
-        k_fold_table<<<blocks_for(L.chunks * 64), 256, 0, ts>>>(d_terms, n, d_base, d_est, d_pair, d_flags, d_hint);
+        const unsigned blocks = blocks_for(L.chunks * 64);
+        if (d_verts) k_fold_edge_terms<<<blocks, 256, 0, ts>>>(d_verts, d_faces, nf, d_terms, d_cs, d_bs);
+        else k_fold_chunk_sums<<<blocks, 256, 0, ts>>>(d_terms, n, d_cs, d_bs);
+        k_fold_table<<<blocks, 256, 0, ts>>>(d_terms, n, d_cs, d_bs, d_base, d_pair, d_flags, d_hint);
     }
     if (ws != ts) {
         IMPLI_HIP(hipEventRecord(table_done, ts));
@@ -1345,14 +1516,14 @@ void launch_fold(const float* d_terms, int64_t n, int64_t nf, char* d_tab, FoldO
 // in device memory (FoldOut) for the searches and QEM.
 void Ob02::start_edge_fold() {
     norms_.reserve((size_t)(nf + 1) * 12);
-    k_edge_norms<<<blocks_for(nf), 256, 0, s>>>(verts_.as<float>(), faces_.as<int32_t>(), nf, norms_.as<float>());
     const FoldLayout L(3 * nf);
     fold_sum_.reserve(L.bytes);
     fold_out_.reserve(sizeof(FoldOut));
     if (!walk_s_) IMPLI_HIP(hipStreamCreateWithFlags(&walk_s_, hipStreamNonBlocking));
     if (!table_done_) IMPLI_HIP(hipEventCreateWithFlags(&table_done_, hipEventDisableTiming));
     if (!walk_done_) IMPLI_HIP(hipEventCreateWithFlags(&walk_done_, hipEventDisableTiming));
-    launch_fold(norms_.as<float>(), 3 * nf, nf, fold_sum_.as<char>(), fold_out_.as<FoldOut>(), s, walk_s_, table_done_);
+    launch_fold(norms_.as<float>(), 3 * nf, nf, verts_.as<float>(), faces_.as<int32_t>(), fold_sum_.as<char>(),
+                fold_out_.as<FoldOut>(), s, walk_s_, table_done_);
     IMPLI_HIP(hipEventRecord(walk_done_, walk_s_));
     avg_valid_ = false;
 }
@@ -1370,7 +1541,7 @@ float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* 
     tab.reserve(L.bytes);
     fo.reserve(sizeof(FoldOut));
     if (n) IMPLI_HIP(hipMemcpy(terms.p, h_terms, (size_t)n * 4, hipMemcpyHostToDevice));
-    launch_fold(terms.as<float>(), n, n, tab.as<char>(), fo.as<FoldOut>(), 0, 0, nullptr);
+    launch_fold(terms.as<float>(), n, n, nullptr, nullptr, tab.as<char>(), fo.as<FoldOut>(), 0, 0, nullptr);
     IMPLI_HIP(hipGetLastError());
     FoldOut h;
     IMPLI_HIP(hipMemcpy(&h, fo.p, offsetof(FoldOut, alphas), hipMemcpyDeviceToHost));
@@ -1383,6 +1554,11 @@ float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* 
         for (int i = 0; i < 4; ++i) stats[i] = h.steps[i];
         stats[4] = h.cycles[0];
         stats[5] = h.cycles[1];
+        stats[6] = h.steps[4] * 1000 + h.steps[5];
+        stats[7] = h.cycles[2];
+        stats[8] = h.cycles[3];
+        stats[9] = h.cycles[4];
+        stats[10] = h.cycles[5];
     }
     return h.sum;
 }

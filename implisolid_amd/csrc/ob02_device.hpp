@@ -96,8 +96,9 @@ struct FoldOut {
     float avg;          // (float)((double)sum / (3. * nf)): max_dist of the searches and QEM's clamp
     int nal;            // alphas in the list
     int table_chunks;   // chunks taken from the chunk table (statistics)
-    int steps[4];       // walk steps (statistics): zero-skip / serial terms, table runs, term runs, global term loads
-    long long cycles[2];   // staging, walking (clock64)
+    int steps[6];       // walk steps (statistics): zero-skip / serial terms, table runs, term runs, global term
+                        // loads, run jumps, (spare)
+    long long cycles[6];   // staging, walking, table steps, term steps, staging parts (clock64)
     int trace[256];        // the walk's first steps (diagnostics): kind << 28 | term index
     float alphas[kMaxAlphas];
 };
