@@ -65,6 +65,20 @@ void send_mesh_back_to_client(Ob02* ob, const CallSpecs& cs) {
 
 std::map<std::string, std::vector<float>> g_pointsets;   // pointset_set.hpp:8
 std::unique_ptr<Ob02> g_ob02;   // the refinement state of the last build
+// The point sets (get_pointset_*) live on the device in g_ob02's snapshots; they are copied to
+// g_pointsets only when asked for after a build (a D2H copy of every set per build cost ~0.25 ms)
+bool g_pointsets_dirty = false;
+void materialize_pointsets() {
+    if (!g_pointsets_dirty || !g_ob02) return;
+    // STORE_POINTSET (pointset_set.hpp:11-25) replaces; vertex_resampling.hpp:176-211 uses
+    // map::emplace on a never-cleared global, so the first resampling point sets persist
+    for (auto& kv : g_ob02->pointsets()) {
+        const bool first_wins = kv.first == "pre_resampling_vertices" || kv.first == "post_resampling_vertices";
+        if (first_wins && g_pointsets.count(kv.first)) continue;
+        g_pointsets[kv.first] = kv.second;
+    }
+    g_pointsets_dirty = false;
+}
 bool g_ob02_profile = false;
 
 struct EvalService {                 // ifunction_service, mcc2.cpp:699-705
@@ -217,6 +231,8 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
     Ob02& ob = *ob_ptr;
     send_mesh_back_to_client(&ob, cs);   // after polygonize_step_0 (mcc2.cpp:351)
     for (int rep = 0; rep < st.overall_repeats; ++rep) {
+        // a replacing point set keeps its last store: only the last repeat's need a snapshot
+        ob.capture_replace = rep == st.overall_repeats - 1;
         for (int i = 0; i < st.vresampl_iters; ++i) ob.vertex_resampling(st.vresampl_c);   // step 1
         send_mesh_back_to_client(&ob, cs);                                             // mcc2.cpp:372
         if (st.projection) {
@@ -236,13 +252,8 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
     g_state.verts.resize((size_t)nv * 3);
     g_state.faces.resize((size_t)nf * 3);
     ob.fetch(g_state.verts.data(), g_state.faces.data());
-    // STORE_POINTSET (pointset_set.hpp:11-25) replaces; vertex_resampling.hpp:176-211 uses
-    // map::emplace on a never-cleared global, so the first resampling point sets persist
-    for (auto& kv : ob.pointsets()) {
-        const bool first_wins = kv.first == "pre_resampling_vertices" || kv.first == "post_resampling_vertices";
-        if (first_wins && g_pointsets.count(kv.first)) continue;
-        g_pointsets[kv.first] = kv.second;
-    }
+    ob.capture_replace = true;
+    g_pointsets_dirty = true;              // copied to the host when asked for
     g_state.active = true;                 // polygonize_terminate, ob02:163-176
 }
 
@@ -577,10 +588,12 @@ int get_gradients_size(void) {
 }
 
 void* get_pointset_ptr(char* id) {
+    materialize_pointsets();
     auto it = g_pointsets.find(std::string(id));
     return it == g_pointsets.end() ? nullptr : it->second.data();
 }
 int get_pointset_size(char* id) {
+    materialize_pointsets();
     auto it = g_pointsets.find(std::string(id));
     return it == g_pointsets.end() ? 0 : (int)(it->second.size() / 3);
 }

@@ -1406,7 +1406,7 @@ void Ob02::scan(const uint32_t* in, uint32_t* out, int64_t n) {
 // when pointsets() is asked for
 void Ob02::store_pointset(const char* key, const float* d, int64_t n, bool keep_first) {
     if (!capture_pointsets) return;
-    if (keep_first && snaps_.count(key)) return;
+    if (keep_first ? snaps_.count(key) != 0 : !capture_replace) return;
     Snapshot& e = snaps_[key];
     e.buf.reserve((size_t)(n + 1) * 12);
     e.n = n;

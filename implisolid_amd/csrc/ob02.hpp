@@ -63,6 +63,7 @@ public:
     void set_profile(bool on) { profile_ = on; }
     const double* stage_ms() const { return stage_ms_; }
     bool capture_pointsets = true;
+    bool capture_replace = true;   // false: skip the replacing point sets (a later store overwrites them)
 
 private:
     void store_pointset(const char* key, const float* d, int64_t n, bool keep_first);
