@@ -32,10 +32,34 @@ void report(const std::string& msg, bool reference_aborts) {
     if (reference_aborts && g_error_mode == 0) std::abort();
 }
 
+// The host mesh of the last build, in pinned memory (D2H at full PCIe rate, where pageable memory
+// goes through the driver's staging copies) that resize() does not zero (a vector zero-filled 13 MB
+// per 512^3 build before the copy overwrote it).  Grow-only; kept until exit.
+template <class T>
+struct PinnedVec {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+    size_t size() const { return n; }
+    T* data() { return p; }
+    const T* data() const { return p; }
+    void resize(size_t m) {
+        if (m > cap) {
+            const size_t nc = std::max(m, cap + cap / 2);
+            T* q = nullptr;
+            if (hipHostMalloc((void**)&q, nc * sizeof(T), hipHostMallocDefault) != hipSuccess || !q)
+                throw HipError("host mesh: pinned allocation failed");
+            if (n) std::memcpy(q, p, n * sizeof(T));
+            if (p) (void)hipHostFree(p);
+            p = q;
+            cap = nc;
+        }
+        n = m;
+    }
+};
 struct GeometryState {               // state_t, mcc2.cpp:165-193
     bool active = false;
-    std::vector<float> verts;
-    std::vector<int32_t> faces;
+    PinnedVec<float> verts;
+    PinnedVec<int32_t> faces;
 };
 GeometryState g_state;
 
@@ -80,6 +104,7 @@ void materialize_pointsets() {
     g_pointsets_dirty = false;
 }
 bool g_ob02_profile = false;
+bool g_last_refined = false;   // the last build ran the refinement loop (implisolid_last_build_stats)
 
 struct EvalService {                 // ifunction_service, mcc2.cpp:699-705
     bool has_object = false;
@@ -126,7 +151,7 @@ std::vector<std::unique_ptr<SlabEngine>> g_slab_engines;
 // polygonize_step_0 on g_devices: balanced cuts (cached per object and grid), every slab evaluated
 // and counted on its device concurrently, vertex / face offsets from the counts (host), emission,
 // and the slabs' meshes copied into the host result at their offsets -- byte-identical to one GPU.
-void multi_device_mc(const Program& prog, const MCSettings& st, std::vector<float>& verts, std::vector<int32_t>& faces) {
+void multi_device_mc(const Program& prog, const MCSettings& st, PinnedVec<float>& verts, PinnedVec<int32_t>& faces) {
     DeviceGuard guard;
     const int n = (int)g_devices.size();
     while ((int)g_slab_engines.size() < n) {
@@ -204,7 +229,10 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         nf = (int64_t)g_state.faces.size() / 3;
         const bool refine = st.overall_repeats > 0 && (st.vresampl_iters > 0 || st.projection || st.subdiv);
         if (!refine) {
+            g_last_refined = false;
             send_mesh_back_to_client(nullptr, cs);   // mcc2.cpp:351
+            // the repeats of an empty loop still report after their (empty) resampling (:372)
+            for (int rep = 0; rep < st.overall_repeats; ++rep) send_mesh_back_to_client(nullptr, cs);
             g_state.active = true;
             return;
         }
@@ -224,11 +252,24 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         roctxRangePop();
         nv = c.n_verts();
         nf = c.n_faces();
+        const bool refine = st.overall_repeats > 0 && (st.vresampl_iters > 0 || st.projection || st.subdiv);
+        if (!refine) {   // the MC mesh is the result: straight to the host, no refinement state
+            g_state.verts.resize((size_t)nv * 3);
+            g_state.faces.resize((size_t)nf * 3);
+            E.download(g_state.verts.data(), g_state.faces.data(), c, s);
+            g_last_refined = false;
+            send_mesh_back_to_client(nullptr, cs);   // mcc2.cpp:351
+            // the repeats of an empty loop still report after their (empty) resampling (:372)
+            for (int rep = 0; rep < st.overall_repeats; ++rep) send_mesh_back_to_client(nullptr, cs);
+            g_state.active = true;
+            return;
+        }
         if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
         ob_ptr->set_profile(g_ob02_profile);
         ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf);
     }
     Ob02& ob = *ob_ptr;
+    g_last_refined = true;
     send_mesh_back_to_client(&ob, cs);   // after polygonize_step_0 (mcc2.cpp:351)
     for (int rep = 0; rep < st.overall_repeats; ++rep) {
         // a replacing point set keeps its last store: only the last repeat's need a snapshot
@@ -353,7 +394,7 @@ void implisolid_ob02_profile(int on) { g_ob02_profile = on != 0; }
 int implisolid_last_build_stats(double out[13]) {
     g_last_error.clear();
     for (int k = 0; k < 13; ++k) out[k] = 0.0;
-    if (!g_ob02) return 0;
+    if (!g_ob02 || !g_last_refined) return 0;
     try {
         g_ob02->read_counters();
         out[0] = g_ob02->bisection_cap_hits();

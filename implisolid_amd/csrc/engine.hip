@@ -159,8 +159,7 @@ Engine::~Engine() {
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
-    (void)hipDeviceSynchronize();   // (hipFree already waits; the modules' last launches are done)
-    release_jit();
+    release_jit();   // (hipFree above waited for the device: the modules' last launches are done)
 }
 
 void Engine::release_jit() {

@@ -1200,6 +1200,36 @@ def test_multiprocess_ob02_sharded_gloo(impli, oracle, tmp_path, world, balanced
     assert np.array_equal(g["verts"].view(np.uint32), vr.view(np.uint32))
 
 
+@pytest.mark.parametrize("mode", ["slabs", "ob02"])
+def test_rccl_world1_pipeline(impli, oracle, tmp_path, mode):
+    """The multi-GPU step over RCCL itself (backend "nccl"), on the one GPU a test box has: world 1
+    under torch.distributed.run -- the counts' all_gather_into_tensor in flight during the vertex pass,
+    the mesh gather to rank 0, and for OB02 the slab meshes' and the owned vertices' padded
+    all-gathers -- gives the oracle's mesh byte for byte.  (Point-to-point sends need a second GPU.)"""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from implisolid_amd import scenes
+    R = 64 if mode == "ob02" else 72
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    out = str(tmp_path / "mesh.npz")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IMPLISOLID_DIST_BACKEND="nccl", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "tests", "dist_worker.py"),
+           out, str(R)] + (["ob02"] if mode == "ob02" else [])
+    r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    g = np.load(out)
+    shape, mc = scenes.config2(R) if mode == "ob02" else (scenes.config3_tree(), scenes.mc_settings(R, 1.0))
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    assert np.array_equal(g["faces"], fr)
+    assert np.array_equal(g["verts"].view(np.uint32), vr.view(np.uint32))
+
+
 def test_ob02_shards_in_one_process(impli, oracle):
     """The sharded OB02 loop without processes: config 2 at R = 48 as 3 and 5 vertex-range shards on
     one GPU, stepped together with the owned ranges exchanged on the host after every vertex-moving
