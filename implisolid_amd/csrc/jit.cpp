@@ -20,7 +20,9 @@
 #include <thread>
 #include <vector>
 
+#include <dirent.h>
 #include <sys/stat.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include "generated/jit_headers.inc"
@@ -523,6 +525,34 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
     if (!ok || std::rename(tmp.c_str(), (dir + "/" + name).c_str()) != 0) std::remove(tmp.c_str());
 }
 
+// The disk cache keeps at most IMPLISOLID_JIT_CACHE_MAX code objects (default 2048): once per
+// process, before its first write, the least recently used entries beyond that (by modification
+// time; a disk hit refreshes it) are removed with their .src / .meta files, down to 3/4 of the cap.
+void trim_disk_cache(const std::string& dir) {
+    size_t cap = 2048;
+    if (const char* e = std::getenv("IMPLISOLID_JIT_CACHE_MAX")) cap = (size_t)std::max(16L, std::atol(e));
+    DIR* d = ::opendir(dir.c_str());
+    if (!d) return;
+    std::vector<std::pair<long long, std::string>> cos;   // (mtime ns, name)
+    while (const dirent* ent = ::readdir(d)) {
+        const std::string nm = ent->d_name;
+        if (nm.size() < 4 || nm.compare(nm.size() - 3, 3, ".co") != 0 || nm[0] == '.') continue;
+        struct stat st{};
+        if (::stat((dir + "/" + nm).c_str(), &st) != 0) continue;
+        cos.emplace_back((long long)st.st_mtim.tv_sec * 1000000000LL + st.st_mtim.tv_nsec, nm);
+    }
+    ::closedir(d);
+    if (cos.size() <= cap) return;
+    std::sort(cos.begin(), cos.end());
+    const size_t drop = cos.size() - cap * 3 / 4;
+    for (size_t i = 0; i < drop; ++i) {
+        const std::string base = dir + "/" + cos[i].second;
+        std::remove(base.c_str());
+        std::remove((base + ".src").c_str());
+        std::remove((base + ".meta").c_str());
+    }
+}
+
 }  // namespace
 
 void TreeJit::build(Slot* slot) {
@@ -541,12 +571,15 @@ void TreeJit::build(Slot* slot) {
             std::string(meta_on_disk.begin(), meta_on_disk.end()) == code_meta(code)) {
             ++n_disk_;
             from_disk = true;
+            (void)::utimes((disk_dir_ + "/" + name).c_str(), nullptr);   // recently used (trim order)
         }
         auto compile_and_store = [&](const std::string& src) {
             code = compile(src);
             compile_us_ += (int64_t)(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
             ++n_compiled_;
             if (!disk_dir_.empty()) {
+                static std::once_flag trimmed;
+                std::call_once(trimmed, [this] { trim_disk_cache(disk_dir_); });
                 write_file_atomic(disk_dir_, name + ".src", std::vector<char>(slot->src.begin(), slot->src.end()));
                 write_file_atomic(disk_dir_, name, code);
                 const std::string m = code_meta(code);

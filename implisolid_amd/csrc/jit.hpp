@@ -72,7 +72,8 @@ public:
     //   2 async (default): request() returns at once; compilation runs on background threads and the
     //     engine uses the interpreter kernels until the module is ready -- a never-seen shape costs
     //     no compile latency.  Code objects persist in a disk cache (IMPLISOLID_JIT_CACHE=<dir>,
-    //     default $XDG_CACHE_HOME or ~/.cache /implisolid_amd; "off" disables it).
+    //     default $XDG_CACHE_HOME or ~/.cache /implisolid_amd; "off" disables it), trimmed to the
+    //     IMPLISOLID_JIT_CACHE_MAX (2048) most recently used entries once per process.
     // Variants: shape modules keep the matrices as data (one module per tree shape); baked modules
     // hold the object's matrices as literals (one per object: no matrix loads on the dependency
     // chains, 5 % faster at 512^3).  Bake modes (IMPLISOLID_JIT_BAKE, implisolid_set_jit_bake):
