@@ -155,7 +155,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &vid3_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &vid3_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -229,6 +229,7 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     IMPLI_HIP(hipMemset(field_.p, 0, field_bytes));
     unit_cnt_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint4));
     unit_part_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint32_t));
+    unit_cmask_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint32_t));
     scan_blk_.reserve((size_t)(n_groups(grid_) + 1) * (kScanParts + 1) * sizeof(uint32_t));
     ulist_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint4));
     upart_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint32_t));
@@ -263,6 +264,7 @@ MCBuffers Engine::buffers() const {
 
     b.unit_cnt = unit_cnt_.as<uint4>();
     b.unit_part = unit_part_.as<uint32_t>();
+    b.unit_cmask = unit_cmask_.as<uint32_t>();
     b.scan_blk = scan_blk_.as<uint32_t>();
     b.ulist = ulist_.as<uint4>();
     b.upart = upart_.as<uint32_t>();

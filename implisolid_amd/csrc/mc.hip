@@ -109,10 +109,12 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 //      own, non-empty units), read by k_unit_scan.
 __device__ __forceinline__ void mc_count_body(const GridDesc& g, const MCBuffers& b) {
     __shared__ uint32_t s_u[kGroupUnits][4];
+    __shared__ uint32_t s_cm[kGroupUnits];   // per unit: its chunks holding non-trivial cells (bit c)
     __shared__ uint16_t s_fp[kGroupUnits * kMaxChunks];   // the group's candidate (unit, chunk) pairs
     __shared__ uint32_t s_nf;
     const int t = threadIdx.x, nt_ = blockDim.x;   // triangle counts: chunk_triangles (checked against the table)
     for (int k = t; k < 4 * kGroupUnits; k += nt_) (&s_u[0][0])[k] = 0u;
+    for (int k = t; k < kGroupUnits; k += nt_) s_cm[k] = 0u;
     if (t == 0) s_nf = 0u;
     const int64_t G = blockIdx.x;
     const int nch = n_chunks(g);
@@ -144,6 +146,7 @@ __device__ __forceinline__ void mc_count_body(const GridDesc& g, const MCBuffers
         load_chunk(g, b.signs, ok ? row0 + rb : 0, c, k);
         if (!ok) k.nt = 0;
         if (!k.nt) continue;
+        if (c < kChunkMaskBits) atomicOr(&s_cm[ui], 1u << c);
         // owned vertices = crossing owned edges (build_case_table checks the identity):
         // edge 5 = corners 5-6 (t01, t11), 6 = 6-7 (t11, s11), 10 = 2-6 (t10, t11)
         const unsigned own = (unsigned)(__popcll((unsigned long long)((k.t01 ^ k.t11) & k.nt)) +
@@ -178,6 +181,7 @@ __device__ __forceinline__ void mc_count_body(const GridDesc& g, const MCBuffers
         if (ne) {
             b.unit_cnt[G * kGroupUnits + pos] = make_uint4((uint32_t)t, eo, et, ea);
             b.unit_part[G * kGroupUnits + pos] = ep | (parts << 16);
+            b.unit_cmask[G * kGroupUnits + pos] = s_cm[t];
         }
         const uint32_t sums[kScanParts + 1] = {__shfl(eo + own, 63, 64), __shfl(et + tri, 63, 64),
                                                __shfl(ea + act, 63, 64), wave_sum(hal), __shfl(ep + parts, 63, 64),
@@ -209,6 +213,7 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
     if (nne == 0 && !last) return;   // uniform
     const uint4 e = b.unit_cnt[G * kGroupUnits + (t < (int)nne ? t : 0)];
     const uint32_t pp = b.unit_part[G * kGroupUnits + (t < (int)nne ? t : 0)];
+    const uint32_t cm = b.unit_cmask[G * kGroupUnits + (t < (int)nne ? t : 0)];
     uint32_t acc[kScanRows] = {0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll 4
     for (int64_t i = t; i < G; i += kScanBlock)
@@ -232,7 +237,7 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
         const uint32_t P = pp >> 16, at = s_base[4] + (pp & 0xffffu);
         for (uint32_t q = 0; q < P; ++q) {
             b.ulist[at + q] = ent;
-            b.upart[at + q] = q | (P << 8);
+            b.upart[at + q] = q | (P << 4) | (cm << 8);
         }
     }
     if (last && t == 0) {

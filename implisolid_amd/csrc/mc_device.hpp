@@ -158,8 +158,11 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
     const int items = kUnitRows * nch;
     {
         const uint4 ent = b.ulist[e];   // {unit, vbase, fbase, abase}
-        const uint32_t up = b.upart[e];   // part | parts << 8: this wave emits windows w % parts == part
-        const uint32_t part = up & 255u, parts = up >> 8;
+        // part | parts << 4 | chunk mask << 8: this wave emits windows w % parts == part; the unit's
+        // chunks without a non-trivial cell (k_mc_count) are not loaded
+        const uint32_t up = b.upart[e];
+        const uint32_t part = up & 15u, parts = (up >> 4) & 15u;
+        const uint32_t cmask = nch <= kChunkMaskBits ? up >> 8 : ~0u;
         const int64_t u = ent.x;
         uint32_t vrun0 = ent.y, frun0 = ent.z, arun0 = ent.w;
         uint32_t win = 0;   // 64-cell window index within the unit
@@ -169,7 +172,8 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
             k.nt = 0;
             if (i < items) {
                 const int64_t row = u * kUnitRows + i / nch;
-                if (row < rows) load_chunk(g, b.signs, row, i % nch, k);
+                const int c = i % nch;
+                if (row < rows && (c >= kChunkMaskBits || ((cmask >> c) & 1u))) load_chunk(g, b.signs, row, c, k);
             }
             const uint32_t cnt = (uint32_t)__popcll((unsigned long long)k.nt);
             const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);

@@ -27,16 +27,18 @@ constexpr int kScanParts = 5;          // group sums scanned: own, tri, act, hal
 // A non-empty unit with many active cells is handed to several waves ("parts"): part p of P takes
 // the unit's 64-cell windows w with w % P == p (the other windows only advance its bases).
 constexpr int kPartCells = 128;        // active cells per part
-constexpr int kMaxParts = 8;
+constexpr int kMaxParts = 8;          // (part and part count: 4 bits each in upart)
+constexpr int kChunkMaskBits = 24;     // chunks per row the vertex pass can skip by mask (R <= 1533)
 struct MCBuffers {
     const float* field;
     const uint64_t* signs;   // sign bitmap of the stored samples (grid.hpp)
     uint4* unit_cnt;         // per group, its non-empty units {unit in group, own, tri, act bases} (k_mc_count)
     uint32_t* unit_part;     // ... and their parts: in-group part base | part count << 16
+    uint32_t* unit_cmask;    // ... and their chunks holding non-trivial cells (bit c, c < kChunkMaskBits)
     uint32_t* scan_blk;      // [kScanParts + 1][n_groups]: group sums (own, tri, act, halo own, parts),
                              // then the group's non-empty unit count (not scanned)
     uint4* ulist;            // all parts of the non-empty units in order: {unit, vbase, fbase, abase}
-    uint32_t* upart;         // ... part index | part count << 8 (k_unit_scan)
+    uint32_t* upart;         // ... part index | part count << 4 | the unit's chunk mask << 8 (k_unit_scan)
     const uint32_t* umark;   // [unit][chunk]: the 64-cell chunks of a unit whose cells touch an evaluated
     uint32_t mark_id;        // brick hold mark_id (k_brick_fill); null: every chunk is counted (dense eval)
     uint32_t* counters;      // [0] unit parts, [1] halo own (read by the vertex pass), [2..5] totals
