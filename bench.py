@@ -229,6 +229,8 @@ def main():
     ap.add_argument("--skip-config5", action="store_true", help="do not time the 64-object stream (config 5)")
     ap.add_argument("--config5-streams", type=int, default=8)
     ap.add_argument("--skip-ob02", action="store_true", help="do not time build_geometry with the OB02 loop")
+    ap.add_argument("--skip-concurrent", action="store_true",
+                    help="do not time P concurrent builds of the headline object on P streams (serving throughput)")
     ap.add_argument("--bake", type=int, default=None,
                     help="tree modules with the matrices baked in: 0 never, 1 every object, 2 hot objects (library default)")
     ap.add_argument("--graph", action="store_true",
@@ -460,6 +462,73 @@ def main():
     rdense = None if (args.skip_256 or world > 1) else leg("union_scene", lambda: run(
         args.resolution, args.steps, args.warmup, scene=(scenes.union_sphere_cube(), scenes.mc_settings(args.resolution, 1.0))))
 
+    # serving throughput: P independent builds of the config-4 object, each with its own engine
+    # (buffers) on its own HIP stream, the P-stream step replayed as one hipGraph.  Every kernel of
+    # one build is latency-bound (few waves per SIMD, dependent memory round trips), so builds
+    # overlap.  Every build recomputes everything; each one's mesh is checked against the first.
+    def run_concurrent(R, P, steps):
+        shape, mc = scenes.config4(R)
+        slabs = [I.Slab(shape, mc) for _ in range(P)]
+        try:
+            streams = [torch.cuda.Stream(dev) for _ in range(P)]
+            ev_start, ev_end = torch.cuda.Event(), [torch.cuda.Event() for _ in range(P)]
+            main_s = torch.cuda.current_stream(dev)
+
+            def step(ms):
+                ev_start.record(ms)
+                for p in range(P):
+                    st = streams[p]
+                    st.wait_event(ev_start)
+                    slabs[p].eval(st.cuda_stream)
+                    slabs[p].count(st.cuda_stream)
+                    slabs[p].emit(0, st.cuda_stream)
+                    ev_end[p].record(st)
+                for p in range(P):
+                    ms.wait_event(ev_end[p])
+            for _ in range(3):
+                for _ in range(4):
+                    step(main_s)
+                I.jit_wait()
+            torch.cuda.synchronize(dev)
+            if any(sl.counts(0)[2] for sl in slabs):   # the first call sized the outputs
+                step(main_s)
+            torch.cuda.synchronize(dev)
+            graph = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream(dev)
+            cs.wait_stream(main_s)
+            with torch.cuda.stream(cs):
+                graph.capture_begin()
+                step(cs)
+                graph.capture_end()
+            main_s.wait_stream(cs)
+            for _ in range(3):
+                graph.replay()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                graph.replay()
+            torch.cuda.synchronize(dev)
+            ms = (time.perf_counter() - t0) / steps * 1e3 / P
+            meshes = []
+            for sl in slabs:
+                nv, nf, of = sl.counts(0)
+                if of:
+                    raise RuntimeError("concurrent builds: output overflow")
+                meshes.append(sl.download(nv, nf, 0))
+            v0, f0 = meshes[0]
+            same = all(v.shape == v0.shape and f.shape == f0.shape and np.array_equal(v.view(np.uint32), v0.view(np.uint32))
+                       and np.array_equal(f, f0) for v, f in meshes[1:])
+            return {"resolution": R, "builds": P, "ms_per_build": round(ms, 4),
+                    "value": round(R ** 3 / (ms * 1e-3) / 1e6, 2), "unit": "Mvoxels/s",
+                    "verts": int(len(v0)), "faces": int(len(f0)), "meshes_identical": bool(same)}
+        finally:
+            for sl in slabs:
+                sl.close()
+    conc = None
+    if world == 1 and not args.skip_concurrent:
+        conc = leg("concurrent", lambda: [run_concurrent(args.resolution, 4, args.steps)] +
+                   ([] if args.skip_256 or args.resolution == 256 else [run_concurrent(256, 8, args.steps)]))
+
     # config 5: a stream of 64 seeded random MP5 objects at 128^3, eval + MC, each object's
     # pipeline captured once in a hipGraph and replayed (objects round-robin over a few streams).
     # Headline: the interpreter kernels (no per-object compilation, so nothing is left out of the
@@ -685,7 +754,7 @@ def main():
     # average duration (engine HIP events on the launch stream, 5 extra steps after the timed
     # region: Slab.kernel_times_each).  Its `achieved` = its ALGORITHMIC bytes per launch over that
     # duration; algorithmic bytes per kernel:
-    #   impli_eval_bricks  4 B per evaluated sample (the listed + claimed bricks x 128 samples)
+    #   impli_eval_bricks  4 B per evaluated sample (the listed bricks x 128 samples; candidates' face layers not counted)
     #   k_brick_fill       the sign bitmap of the grid, 1 bit per stored sample
     #   k_mc_cells         20 B per vertex: its 12 B position + the 2 x 4 B field values of its edge
     #   k_mc_faces         12 B per face
@@ -835,6 +904,12 @@ def main():
         ms256 = r256["elapsed"] / args.steps * 1e3
         out["value_256"] = round(256 ** 3 / (ms256 * 1e-3) / 1e6, 2)
         out["ms_per_step_256"] = round(ms256, 4)
+    if conc:
+        out["concurrent_builds"] = {
+            "workload": "P independent builds of the config-4 object (own engine each) on P HIP streams, "
+                        "the P-stream step replayed as one hipGraph: serving throughput, every build "
+                        "recomputed (the headline above is one build at a time)",
+            "runs": conc}
     if c5:
         out["config5"] = c5
     if ob02:
