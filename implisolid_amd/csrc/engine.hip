@@ -195,6 +195,13 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
 
 void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool probe_only) {
     const SlabRange sr = slab_range(R, sr_in.z0, sr_in.z1);   // validated, 32-bit limits checked
+    // the same grid again (repeated builds of build_geometry): every buffer keeps its size and its
+    // invariants (umark ids only grow, the sign pieces past a row's last brick stay 0, counters are
+    // cleared in-kernel), so there is nothing to reset and nothing to wait for
+    if (have_grid_ && !probe_only && !probe_only_ && key_R_ == R && key_z0_ == sr.z0 && key_z1_ == sr.z1 &&
+        std::memcmp(key_box_, box, sizeof key_box_) == 0)
+        return;
+    key_R_ = -1;   // set again once the buffers below are valid
     // the buffers below are reset on the null stream, which a non-blocking caller stream does not
     // order against: no earlier kernel may still run, and the resets finish before the next launch
     IMPLI_HIP(hipDeviceSynchronize());
@@ -239,6 +246,10 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
                                (uint32_t)std::min<int64_t>(6 * m2, 1u << 31), 0});
     IMPLI_HIP(hipDeviceSynchronize());
     have_grid_ = true;
+    key_R_ = R;
+    key_z0_ = sr.z0;
+    key_z1_ = sr.z1;
+    std::memcpy(key_box_, box, sizeof key_box_);
 }
 
 bool Engine::ensure_capacity(const SlabCounts& c) {
@@ -477,17 +488,22 @@ void Engine::emit_faces(const uint32_t* d_offsets, const uint32_t* d_gathered, i
     IMPLI_HIP(hipGetLastError());
 }
 
+// the counter block's first kOverflowWord + 1 words in one copy into pinned memory (two copies into
+// pageable stack memory took ~60 us of staging per build)
+static_assert(kOverflowWord + 1 <= kCounterWords, "counter block layout");
 void Engine::raw_counters(uint32_t out[16], hipStream_t s) {
-    IMPLI_HIP(hipMemcpyAsync(out, counters_.p, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    hcounters_.reserve(kCounterWords * sizeof(uint32_t));
+    IMPLI_HIP(hipMemcpyAsync(hcounters_.p, counters_.p, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     IMPLI_HIP(hipStreamSynchronize(s));
+    std::memcpy(out, hcounters_.p, 16 * sizeof(uint32_t));
 }
 
 SlabCounts Engine::read_counts(hipStream_t s, bool* overflow) {
-    uint32_t h[16], of = 0;
-    IMPLI_HIP(hipMemcpyAsync(h, counters_.p, sizeof h, hipMemcpyDeviceToHost, s));
-    IMPLI_HIP(hipMemcpyAsync(&of, counters_.as<uint32_t>() + kOverflowWord, sizeof of, hipMemcpyDeviceToHost, s));
+    hcounters_.reserve(kCounterWords * sizeof(uint32_t));
+    IMPLI_HIP(hipMemcpyAsync(hcounters_.p, counters_.p, (kOverflowWord + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     IMPLI_HIP(hipStreamSynchronize(s));
-    if (overflow) *overflow = of != 0;
+    const uint32_t* h = hcounters_.as<uint32_t>();
+    if (overflow) *overflow = h[kOverflowWord] != 0;
     return SlabCounts{h[2], h[3], h[4], h[5]};
 }
 

@@ -163,6 +163,10 @@ private:
     void release_jit();   // drop the module references (after the device has synchronised)
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false, probe_only_ = false;
+    // the grid set_slab last built its buffers for: setting the same one again keeps them
+    int key_R_ = -1, key_z0_ = 0, key_z1_ = 0;
+    float key_box_[6] = {};
+    HostBuf hcounters_;   // pinned landing zone of read_counts / raw_counters (one small copy)
     DevBuf prog_, rabbit_, cases_;
     DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, vid3_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;

@@ -1290,8 +1290,9 @@ Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
 void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_) {
     nv = nv_;
     nf = nf_;
-    for (auto& kv : snaps_) kv.second.buf.release();
-    snaps_.clear();
+    // the snapshots' device buffers are kept for the next build's stores (a hipFree per set per
+    // build cost 80-380 us of device-wide synchronisation)
+    for (auto& kv : snaps_) kv.second.valid = false;
     pointsets_.clear();
     cap_hits_ = 0;
     evals_ = 0;
@@ -1406,16 +1407,20 @@ void Ob02::scan(const uint32_t* in, uint32_t* out, int64_t n) {
 // when pointsets() is asked for
 void Ob02::store_pointset(const char* key, const float* d, int64_t n, bool keep_first) {
     if (!capture_pointsets) return;
-    if (keep_first ? snaps_.count(key) != 0 : !capture_replace) return;
+    auto it = snaps_.find(key);
+    const bool stored = it != snaps_.end() && it->second.valid;
+    if (keep_first ? stored : !capture_replace) return;
     Snapshot& e = snaps_[key];
     e.buf.reserve((size_t)(n + 1) * 12);
     e.n = n;
+    e.valid = true;
     if (n) IMPLI_HIP(hipMemcpyAsync(e.buf.p, d, (size_t)n * 12, hipMemcpyDeviceToDevice, s));
 }
 
 const std::map<std::string, std::vector<float>>& Ob02::pointsets() {
     pointsets_.clear();
     for (auto& kv : snaps_) {
+        if (!kv.second.valid) continue;
         std::vector<float>& h = pointsets_[kv.first];
         h.resize((size_t)kv.second.n * 3);
         if (kv.second.n) IMPLI_HIP(hipMemcpyAsync(h.data(), kv.second.buf.p, (size_t)kv.second.n * 12, hipMemcpyDeviceToHost, s));

@@ -115,6 +115,7 @@ private:
     struct Snapshot {
         DevBuf buf;
         int64_t n = 0;
+        bool valid = false;   // stored since the last load_mesh (the buffer is kept across builds)
     };
     std::map<std::string, Snapshot> snaps_;
     std::map<std::string, std::vector<float>> pointsets_;
