@@ -75,8 +75,10 @@ __global__ void k_degree(const int32_t* __restrict__ f, int64_t n3, uint32_t* __
     if (i < n3) atomicAdd(&deg[f[i]], 1u);
 }
 
-// exclusive scan of n uint32 into out[0..n] (one workgroup of 1024 lanes)
-__global__ __launch_bounds__(1024) void k_scan_u32(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, int64_t n) {
+// exclusive scan of n uint32 into out[0..n] (one workgroup of 1024 lanes); zero_in: in[] is left
+// zeroed (read exactly once more by its own thread: the next pass's counters need no memset)
+__global__ __launch_bounds__(1024) void k_scan_u32(uint32_t* __restrict__ in, uint32_t* __restrict__ out, int64_t n,
+                                                   int zero_in) {
     __shared__ uint32_t s_w[16];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int64_t chunk = (n + 1023) / 1024;
@@ -100,6 +102,7 @@ __global__ __launch_bounds__(1024) void k_scan_u32(const uint32_t* __restrict__ 
         const uint32_t v = in[i];
         out[i] = run;
         run += v;
+        if (zero_in) in[i] = 0u;
     }
     if (t == 0) out[n] = tot;
 }
@@ -138,8 +141,8 @@ __global__ __launch_bounds__(256) void k_scan_tile_sums(const uint32_t* __restri
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(256) void k_scan_tiles(const uint32_t* __restrict__ in, int64_t n, const uint32_t* __restrict__ offs,
-                                                    uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ in, int64_t n, const uint32_t* __restrict__ offs,
+                                                    uint32_t* __restrict__ out, int zero_in) {
     __shared__ uint32_t s_w[4];
     const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
     uint32_t v[kScanPer], a = 0;
@@ -152,10 +155,25 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const uint32_t* __restrict__
     uint32_t run = offs[blockIdx.x] + block_excl_scan256(a, s_w, total);
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-        if (base + k < n) out[base + k] = run;
+        if (base + k < n) {
+            out[base + k] = run;
+            if (zero_in) in[base + k] = 0u;
+        }
         run += v[k];
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = offs[blockIdx.x] + total;
+}
+
+// load_mesh in one launch: the mesh into the refinement state's buffers, the degree counters and
+// the misc words zeroed (a memset and two copies were three host launch costs on the sync's heels)
+__global__ __launch_bounds__(256) void k_load_mesh(float* __restrict__ v, const float* __restrict__ sv, int64_t nv3,
+                                                   int32_t* __restrict__ f, const int32_t* __restrict__ sf, int64_t nf3,
+                                                   uint32_t* __restrict__ deg, int64_t ndeg, uint32_t* __restrict__ misc) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nv3) v[i] = sv[i];
+    if (i < nf3) f[i] = sf[i];
+    if (i < ndeg) deg[i] = 0u;
+    if (i < 16) misc[i] = 0u;
 }
 
 __global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const uint32_t* __restrict__ off,
@@ -168,10 +186,33 @@ __global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const
 }
 
 // make_neighbour_faces_of_vertex lists faces in ascending order: sort each small umbrella
+// (an umbrella of up to kSortRegs faces is sorted in registers: one load and one store per entry,
+// where the in-memory insertion sort was a chain of dependent global loads)
+constexpr int kSortRegs = 12;
 __global__ void k_sort_umbrella(const uint32_t* __restrict__ off, int32_t* __restrict__ lst, int64_t nv) {
     const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (v >= nv) return;
     const uint32_t a = off[v], e = off[v + 1];
+    if (e - a <= (uint32_t)kSortRegs) {
+        const int n = (int)(e - a);
+        int32_t r[kSortRegs];
+#pragma unroll
+        for (int k = 0; k < kSortRegs; ++k) r[k] = k < n ? lst[a + k] : 0x7fffffff;
+        // odd-even transposition sort of the fixed-size array (the padding sorts last)
+#pragma unroll
+        for (int pass = 0; pass < kSortRegs; ++pass) {
+#pragma unroll
+            for (int k = pass & 1; k + 1 < kSortRegs; k += 2) {
+                const int32_t lo = min(r[k], r[k + 1]), hi = max(r[k], r[k + 1]);
+                r[k] = lo;
+                r[k + 1] = hi;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSortRegs; ++k)
+            if (k < n) lst[a + k] = r[k];
+        return;
+    }
     for (uint32_t i = a + 1; i < e; ++i) {
         const int32_t x = lst[i];
         uint32_t j = i;
@@ -222,6 +263,41 @@ __global__ void k_fof(int64_t nf, EdgeTab t, int32_t* __restrict__ fof) {
     r.first_inv = ~first;
     r.last = last;
     fof[i] = (int32_t)((first != fi) ? first : (c >= 2 ? last : 0u));
+}
+
+// build_faces_of_faces from the umbrellas, no edge table: the faces holding edge {a, b} are the
+// faces of a's umbrella (ascending; a face appears once per occurrence of a) that have a half-edge
+// {a, b} -- in a triangle any two of its vertices form an edge.  first / last / count are the edge
+// table's (k_edge_insert + k_fof: min and max face over the edge's half-edges, and their number), so
+// fof is the same for every mesh, degenerate faces included.  One thread per half-edge walks a's
+// umbrella (~6 faces): 2 dependent L2 loads per face instead of a hash insert with two atomics per
+// half-edge and the table's clear (76 us -> see DESIGN "OB02 on the GPU").
+__global__ __launch_bounds__(256) void k_fof_umbrella(const int32_t* __restrict__ f, int64_t nf,
+                                                      const uint32_t* __restrict__ off, const int32_t* __restrict__ lst,
+                                                      int32_t* __restrict__ fof) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * nf) return;
+    const int64_t fi = i / 3;
+    const int k = (int)(i - 3 * fi);
+    const int32_t a = f[i], b = f[3 * fi + (k == 2 ? 0 : k + 1)];
+    uint32_t first = 0xffffffffu, last = 0u, c = 0u;
+    int32_t prev = -1;
+    const uint32_t p1 = off[a + 1];
+    for (uint32_t p = off[a]; p < p1; ++p) {
+        const int32_t g = lst[p];
+        if (g == prev) continue;   // a degenerate face lists a twice: count its half-edges once
+        prev = g;
+        const int32_t x = f[3 * (int64_t)g], y = f[3 * (int64_t)g + 1], z = f[3 * (int64_t)g + 2];
+        const uint32_t n = (uint32_t)((x == a && y == b) || (x == b && y == a)) +
+                           (uint32_t)((y == a && z == b) || (y == b && z == a)) +
+                           (uint32_t)((z == a && x == b) || (z == b && x == a));
+        if (n) {
+            c += n;
+            first = min(first, (uint32_t)g);
+            last = max(last, (uint32_t)g);
+        }
+    }
+    fof[i] = (int32_t)((first != (uint32_t)fi) ? first : (c >= 2 ? last : 0u));
 }
 
 // ---- step 3: my_subdiv_ (centroids_projection.cpp:1314-1367) -----------------------------------
@@ -1301,14 +1377,17 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     avg_valid_ = true;
     for (double& t : stage_ms_) t = 0.0;
     Stage st(this, kStageTopology);
-    IMPLI_HIP(hipMemsetAsync(misc_.p, 0, 64, s));   // (unused), cap hits, evaluations
     verts_.reserve((size_t)(nv + 1) * 12);
     vnew_.reserve((size_t)(nv + 1) * 12);
     faces_.reserve((size_t)(nf + 1) * 12);
-    if (nv) IMPLI_HIP(hipMemcpyAsync(verts_.p, d_verts, (size_t)nv * 12, hipMemcpyDeviceToDevice, s));
-    if (nf) IMPLI_HIP(hipMemcpyAsync(faces_.p, d_faces, (size_t)nf * 12, hipMemcpyDeviceToDevice, s));
+    deg_.reserve((size_t)(nv + 1) * 4);
+    // the mesh copied, the degree counters and misc ((unused), cap hits, evaluations) zeroed
+    const int64_t nmax = std::max<int64_t>(std::max<int64_t>(3 * nv, 3 * nf), nv + 1);
+    k_load_mesh<<<blocks_for(std::max<int64_t>(nmax, 16)), 256, 0, s>>>(verts_.as<float>(), d_verts, 3 * nv, faces_.as<int32_t>(),
+                                                                       d_faces, 3 * nf, deg_.as<uint32_t>(), nv + 1,
+                                                                       misc_.as<uint32_t>());
     start_perturbations();   // host thread, overlaps the topology and resampling kernels
-    build_topology();
+    build_topology(true);
     own_v0_ = 0; own_v1_ = nv; wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
     sharded_ = false;
 }
@@ -1361,27 +1440,23 @@ EdgeTab Ob02::edge_table() {
     return t;
 }
 
-void Ob02::build_topology() {
+void Ob02::build_topology(bool deg_zeroed) {
     // umbrellas
     deg_.reserve((size_t)(nv + 1) * 4);
     uoff_.reserve((size_t)(nv + 2) * 4);
     ulst_.reserve((size_t)(3 * nf + 1) * 4);
-    IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
+    if (!deg_zeroed) IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
     if (nf) k_degree<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
-    scan(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv);
-    IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
+    scan(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv, true);   // deg_ left zeroed: the fill counters
     if (nf) k_fill_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(),
                                                              deg_.as<uint32_t>(), ulst_.as<int32_t>());
     if (nv) k_sort_umbrella<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), nv);
-    // faces of faces
-    const EdgeTab t = edge_table();
-    const uint64_t cap = t.mask + 1;
-    IMPLI_HIP(hipMemsetAsync(t.rec, 0, (size_t)cap * sizeof(EdgeRec), s));
+    // faces of faces, from the umbrellas (the edge table is built only for subdivision)
     fof_.reserve((size_t)(3 * nf + 1) * 4);
-    if (nf) {
-        k_edge_insert<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, nv, t);
-        k_fof<<<blocks_for(3 * nf), 256, 0, s>>>(nf, t, fof_.as<int32_t>());
-    }
+    if (nf)
+        k_fof_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
+                                                          fof_.as<int32_t>());
+    etab_valid_ = false;
     cen_.reserve((size_t)(nf + 1) * 12);
     nrm_.reserve((size_t)(nf + 1) * 12);
     w_.reserve((size_t)(nf + 1) * 4);
@@ -1389,18 +1464,18 @@ void Ob02::build_topology() {
     topo_valid_ = true;
 }
 
-void Ob02::scan(const uint32_t* in, uint32_t* out, int64_t n) {
+void Ob02::scan(uint32_t* in, uint32_t* out, int64_t n, bool zero_in) {
     const int64_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles <= 1) {
-        k_scan_u32<<<1, 1024, 0, s>>>(in, out, n);
+        k_scan_u32<<<1, 1024, 0, s>>>(in, out, n, zero_in ? 1 : 0);
         return;
     }
     scan_tmp_.reserve((size_t)(2 * tiles + 2) * 4);
     uint32_t* sums = scan_tmp_.as<uint32_t>();
     uint32_t* offs = sums + tiles + 1;
     k_scan_tile_sums<<<(unsigned)tiles, 256, 0, s>>>(in, n, sums);
-    k_scan_u32<<<1, 1024, 0, s>>>(sums, offs, tiles);
-    k_scan_tiles<<<(unsigned)tiles, 256, 0, s>>>(in, n, offs, out);
+    k_scan_u32<<<1, 1024, 0, s>>>(sums, offs, tiles, 0);
+    k_scan_tiles<<<(unsigned)tiles, 256, 0, s>>>(in, n, offs, out, zero_in ? 1 : 0);
 }
 
 // STORE_POINTSET: a device snapshot now (stream-ordered, no host sync), copied to the host only
@@ -1784,6 +1859,12 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
     if (nf) {
         const EdgeTab t = edge_table();
         const uint64_t cap = t.mask + 1;
+        if (!etab_valid_) {   // the edge table of the current faces: half-edge slots, first / last faces
+            IMPLI_HIP(hipMemsetAsync(t.rec, 0, (size_t)cap * sizeof(EdgeRec), s));
+            k_edge_insert<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, nv, t);
+            k_fof<<<blocks_for(3 * nf), 256, 0, s>>>(nf, t, fof_.as<int32_t>());   // fof unchanged: same values
+            etab_valid_ = true;
+        }
         DevBuf& cnt = w_;                   // per-face new midpoints (resampling weights are dead here)
         deg_.reserve((size_t)(nf + 2) * 4);
         pend_.reserve((size_t)(cap + 1) * 4);
@@ -1806,6 +1887,7 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
         nv = nvt;
         nf = 4 * nf;
         topo_valid_ = false;
+        etab_valid_ = false;
     }
     add_rand_noise(amplitude);
 }

@@ -67,8 +67,8 @@ public:
 
 private:
     void store_pointset(const char* key, const float* d, int64_t n, bool keep_first);
-    void build_topology();
-    void scan(const uint32_t* in, uint32_t* out, int64_t n);   // exclusive, out[n] = total
+    void build_topology(bool deg_zeroed = false);   // deg_zeroed: deg_[0..nv] already 0 (load_mesh)
+    void scan(uint32_t* in, uint32_t* out, int64_t n, bool zero_in = false);   // exclusive, out[n] = total; zero_in: in[] left 0
     EdgeTab edge_table();
     void rand_tables(int64_t lanes);
     void add_rand_noise(float amplitude);
@@ -91,6 +91,7 @@ private:
     DevBuf verts_, faces_, vnew_, cen_, nrm_, w_, fof_, uoff_, ulst_, etab_, deg_, proj_, grad_, fn_, norms_,
         pert_, pend_, misc_, fnew_, rtab_, scan_tmp_;
     bool topo_valid_ = false;
+    bool etab_valid_ = false;   // the edge table (subdivision only) matches the current faces
     int64_t own_v0_ = 0, own_v1_ = 0;   // owned vertices
     int64_t wf0_ = 0, wf1_ = 0;         // work faces: touching an owned vertex
     int64_t cf0_ = 0, cf1_ = 0;         // faces whose centroid / normal the weights of the work faces read
