@@ -1506,9 +1506,9 @@ const std::map<std::string, std::vector<float>>& Ob02::pointsets() {
 
 Ob02::~Ob02() {
     if (pert_job_.valid()) pert_job_.wait();
-    if (walk_done_) (void)hipEventDestroy(walk_done_);
-    if (table_done_) (void)hipEventDestroy(table_done_);
-    if (walk_s_) (void)hipStreamDestroy(walk_s_);
+    if (prep_done_) (void)hipEventDestroy(prep_done_);
+    if (mesh_ready_) (void)hipEventDestroy(mesh_ready_);
+    if (side_s_) (void)hipStreamDestroy(side_s_);
     dir_.release();
     evals_buf_.release();
     for (DevBuf* b : {&verts_, &faces_, &vnew_, &cen_, &nrm_, &w_, &fof_, &uoff_, &ulst_, &etab_, &deg_, &proj_, &grad_,
@@ -1589,27 +1589,32 @@ void launch_fold(float* d_terms, int64_t n, int64_t nf, const float* d_verts, co
     k_fold_walk<<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
 }
 
-// compute_average_edge_length (cp:70-82) is one serial float chain in face order.  The terms and
-// the fold's chunk table (fold.hpp) are computed on s; the walk (k_fold_walk, one wave) then runs
-// on a second stream while s runs the projection's prep pass, which does not need the average, and
-// s waits for the walk before the searches.  No host round trip: the average and the alpha list stay
-// in device memory (FoldOut) for the searches and QEM.
-void Ob02::start_edge_fold() {
+// compute_average_edge_length (cp:70-82) is one serial float chain in face order.  The terms, the
+// fold's chunk table (fold.hpp) and the walk (k_fold_walk, one wave) run on s, back to back; the
+// projection's prep pass, which does not need the average, runs meanwhile on a side stream (from
+// the mesh as s left it), and s waits for it before the searches.  The walk is the long one, so
+// the searches follow it in s's own order (a wait on the walk from another stream cost ~13 us of
+// cross-stream signalling per repeat).  No host round trip: the average and the alpha list stay in
+// device memory (FoldOut) for the searches and QEM.
+hipStream_t Ob02::start_edge_fold() {
     norms_.reserve((size_t)(nf + 1) * 12);
     const FoldLayout L(3 * nf);
     fold_sum_.reserve(L.bytes);
     fold_out_.reserve(sizeof(FoldOut));
-    if (!walk_s_) IMPLI_HIP(hipStreamCreateWithFlags(&walk_s_, hipStreamNonBlocking));
-    if (!table_done_) IMPLI_HIP(hipEventCreateWithFlags(&table_done_, hipEventDisableTiming));
-    if (!walk_done_) IMPLI_HIP(hipEventCreateWithFlags(&walk_done_, hipEventDisableTiming));
+    if (!side_s_) IMPLI_HIP(hipStreamCreateWithFlags(&side_s_, hipStreamNonBlocking));
+    if (!mesh_ready_) IMPLI_HIP(hipEventCreateWithFlags(&mesh_ready_, hipEventDisableTiming));
+    if (!prep_done_) IMPLI_HIP(hipEventCreateWithFlags(&prep_done_, hipEventDisableTiming));
+    IMPLI_HIP(hipEventRecord(mesh_ready_, s));
+    IMPLI_HIP(hipStreamWaitEvent(side_s_, mesh_ready_, 0));
     launch_fold(norms_.as<float>(), 3 * nf, nf, verts_.as<float>(), faces_.as<int32_t>(), fold_sum_.as<char>(),
-                fold_out_.as<FoldOut>(), s, walk_s_, table_done_);
-    IMPLI_HIP(hipEventRecord(walk_done_, walk_s_));
+                fold_out_.as<FoldOut>(), s, s, nullptr);
     avg_valid_ = false;
+    return side_s_;   // the prep pass goes here
 }
 
-void Ob02::finish_edge_fold() {   // s waits for the walk (stream order, no host sync)
-    IMPLI_HIP(hipStreamWaitEvent(s, walk_done_, 0));
+void Ob02::finish_edge_fold() {   // s waits for the prep pass (stream order, no host sync)
+    IMPLI_HIP(hipEventRecord(prep_done_, side_s_));
+    IMPLI_HIP(hipStreamWaitEvent(s, prep_done_, 0));
 }
 
 // the fold alone on given terms (diagnostics / tests): the same table kernels and walk as a
@@ -1682,7 +1687,7 @@ void Ob02::centroids_projection(bool enable_qem) {
     if (!nf) return;
     if (!topo_valid_) build_topology();
     Stage st(this, kStageEdgeFold);
-    start_edge_fold();
+    const hipStream_t ps = start_edge_fold();   // the prep pass's stream
     proj_.reserve((size_t)(nf + 1) * 12);
     fn_.reserve((size_t)(nf + 1) * 12);
     dir_.reserve((size_t)(nf + 1) * 12);
@@ -1711,13 +1716,13 @@ void Ob02::centroids_projection(bool enable_qem) {
         // no face touches this rank's vertices: nothing to project (the fold still ran, as on
         // every rank)
     } else if (pk) {
-        TreeJit::launch(pk->prep, blocks_for(nw), jargs, s, "impli_pt_project_prep");
+        TreeJit::launch(pk->prep, blocks_for(nw), jargs, ps, "impli_pt_project_prep");
         ++jit_launches_;
     } else {
-        DEPTH_LAUNCH(E.depth(), k_project_prep, blocks_for(nw), 256, s, E.d_program(), E.d_rabbit(), a);
+        DEPTH_LAUNCH(E.depth(), k_project_prep, blocks_for(nw), 256, ps, E.d_program(), E.d_rabbit(), a);
     }
-    store_pointset("pre_p_centroids", cen_.as<float>(), nf, false);   // cp:1236-1238: the centroids
     finish_edge_fold();
+    store_pointset("pre_p_centroids", cen_.as<float>(), nf, false);   // cp:1236-1238: the centroids
     a.fold = fold_out_.as<FoldOut>();
     st.next(kStageProject);
     const unsigned grid = blocks_for(nw * kProjGroup);

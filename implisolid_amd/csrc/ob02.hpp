@@ -72,7 +72,7 @@ private:
     EdgeTab edge_table();
     void rand_tables(int64_t lanes);
     void add_rand_noise(float amplitude);
-    void start_edge_fold();
+    hipStream_t start_edge_fold();
     void finish_edge_fold();
     void start_perturbations();
     const float* perturbations();
@@ -106,8 +106,8 @@ private:
     double stage_ms_[kStages] = {};
     DevBuf fold_sum_;                        // the fold's chunk table (fold.hpp), built on the device
     DevBuf fold_out_;                        // FoldOut (ob02_device.hpp): sum, average, alpha list
-    hipStream_t walk_s_ = nullptr;           // the fold's walk, beside the projection's prep pass
-    hipEvent_t table_done_ = nullptr, walk_done_ = nullptr;
+    hipStream_t side_s_ = nullptr;           // the projection's prep pass, beside the fold's walk on s
+    hipEvent_t mesh_ready_ = nullptr, prep_done_ = nullptr;
     DevBuf dir_, evals_buf_;
     std::future<std::shared_ptr<const std::vector<float>>> pert_job_;
     std::shared_ptr<const std::vector<float>> pert_host_;
