@@ -125,9 +125,13 @@ struct ProjArgs {
 // its slowest centroid's chain of evaluations.  A group of kProjGroup lanes evaluates kProjGroup
 // alphas at once (the first hit in list order wins) and kBisLevels bisection levels at once (the
 // decision tree of the next levels, then the serial path through it), so the chains are shorter and
-// the wave is filled: the result is the serial one exactly.
-constexpr int kProjGroup = 8;
-constexpr int kBisLevels = 3;
+// the wave is filled: the result is the serial one exactly.  Group size (round 3, A/B on config 2 /
+// 3 / 3s with tools/ab_ob02_variants.sh, two alternating rounds): 4 lanes and 2 levels per round
+// 1.51-1.52 ms for config3s against 1.66-1.76 with 8 and 3 (fewer evaluations past the hit, and
+// 3 instead of 7 per two levels), 2 and 1 1.72-1.74, 16 and 4 1.88; configs 2 and 3 within noise.
+// The searches are throughput-bound at this size (90 k faces), not chain-bound.
+constexpr int kProjGroup = 4;
+constexpr int kBisLevels = 2;
 static_assert((1 << kBisLevels) - 1 <= kProjGroup && 64 % kProjGroup == 0, "bisection tree fits the group");
 
 struct Grp {   // a centroid's lanes inside the wave (control flow is uniform per group)
