@@ -22,6 +22,7 @@ the CPU baseline (the oracle restatement, single thread, on a bounded sample of 
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -773,20 +774,34 @@ def main():
     import glob
     import hashlib
 
-    def newest(pattern):
-        fs = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
-        if not fs:
-            return None, None
-        try:
-            return os.path.basename(fs[-1]), json.load(open(fs[-1]))
-        except Exception:
-            return None, None
-    tname, tj = newest("traffic_r*.json")
+    def tag_key(path):   # r03w < r03z < r03aa < r03ab: round, then suffix length, then suffix
+        m = re.match(r"\D*_r(\d+)([a-z]*)\.json$", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    lib_sha = hashlib.sha256(open(I.LIB_PATH, "rb").read()).hexdigest()
+
+    def newest(pattern, prefer_sha=None):
+        fs = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=tag_key)
+        docs = []
+        for f in fs:
+            try:
+                docs.append((os.path.basename(f), json.load(open(f))))
+            except Exception:
+                pass
+        if prefer_sha:   # the profile of this very library, if one is committed
+            for name, doc in reversed(docs):
+                if isinstance(doc, dict) and doc.get("lib_sha256") == prefer_sha:
+                    return name, doc
+        return docs[-1] if docs else (None, None)
+    tname, tj = newest("traffic_r*.json", lib_sha)
     if not (tj and tj.get("workload_R") == R and tj.get("tree_seed") == scenes.CONFIG3_SEED):
         tname, tj = None, None
-    lib_sha = hashlib.sha256(open(I.LIB_PATH, "rb").read()).hexdigest()
     traffic_current = bool(tj and tj.get("lib_sha256") == lib_sha)
     vname, vj = newest("valu_r*.json")
+    if tname:   # the VALU pass of the same profiling run as the traffic, when there is one
+        vpath = os.path.join(ROOT, "profiles", tname.replace("traffic_", "valu_"))
+        if os.path.exists(vpath):
+            vname, vj = os.path.basename(vpath), json.load(open(vpath))
     traffic = tj.get("pipeline_bytes") if tj else None
     k_traffic = {k: v["bytes"] for k, v in tj.get("kernels", {}).items()} if tj else {}
     valu = vj.get("kernels", {}) if vj else {}
