@@ -11,7 +11,7 @@ out=gpurun_out/$tag
 mkdir -p "$out"
 root=$(pwd)
 export TMPDIR=/tmp
-B="bench.py --steps 10 --warmup 4 --no-cpu-baseline --skip-256 --skip-config5 --skip-ob02"
+B="bench.py --steps 10 --warmup 4 --no-cpu-baseline --skip-256 --skip-config5 --skip-ob02 --skip-concurrent"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/trace" -o run -- python3 $B > "$out/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$root/$out/fetch" -o run -- python3 $B > "$out/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$root/$out/write" -o run -- python3 $B > "$out/write.log" 2>&1
