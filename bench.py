@@ -755,7 +755,7 @@ def main():
     # average duration (engine HIP events on the launch stream, 5 extra steps after the timed
     # region: Slab.kernel_times_each).  Its `achieved` = its ALGORITHMIC bytes per launch over that
     # duration; algorithmic bytes per kernel:
-    #   impli_eval_bricks  4 B per evaluated sample (the listed bricks x 128 samples; candidates' face layers not counted)
+    #   impli_eval_bricks  4 B per evaluated sample (the listed + claimed bricks x 128 samples)
     #   k_brick_fill       the sign bitmap of the grid, 1 bit per stored sample
     #   k_mc_cells         20 B per vertex: its 12 B position + the 2 x 4 B field values of its edge
     #   k_mc_faces         12 B per face

@@ -121,6 +121,10 @@ constexpr int kRefineSplit = kBZ;
 #ifndef IMPLI_REFINE_WAVE_MODES   // the tree module's refine pass (JIT): per-lane modes measured as fast
 #define IMPLI_REFINE_WAVE_MODES 0
 #endif
+__device__ __forceinline__ uint64_t agreeing_modes(uint64_t m_and, uint64_t m_or) {
+    const uint64_t d = m_and ^ m_or;
+    return m_and & ~(((d | (d >> 1)) & 0x5555555555555555ull) * 3ull);
+}
 template <class IvEval, bool WaveModes = false>
 __device__ __forceinline__ void brick_refine_item(const IvEval& ev, const GridDesc& g, const BrickGrid& bg,
                                                   const BrickGrid& cg, const uint64_t* __restrict__ cmodes,

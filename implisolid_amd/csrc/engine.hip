@@ -65,7 +65,7 @@ void Engine::brick_stats(int64_t out[3], hipStream_t s) {
     int64_t mixed = 0, filled = 0;
     for (int b = 0; b < bg.n_bricks; ++b) {
         mixed += (f[b] & 3) == kBrickMixed;
-        filled += ((f[b] >> 4) & 3) != 0;   // candidates: at most their face layers were evaluated
+        filled += ((f[b] >> 4) & 3) != 0 && !(f[b] & kBrickClaimed);   // claimed candidates were evaluated
     }
     out[0] = bg.n_bricks;
     out[1] = pruning() > 0 ? mixed : bg.n_bricks;

@@ -388,7 +388,7 @@ __device__ __forceinline__ void brick_fill_body(const GridDesc& g, const BrickGr
 #pragma unroll
         for (int j = 0; j < kFillP; ++j) {
             if (!((emask >> j) & 1u)) continue;
-            // mixed-class bricks evaluate their candidate neighbours' face layers after their own evaluation
+            // mixed-class bricks claim their candidate neighbours after their own evaluation
             list[i] = (uint32_t)(b0 + j) | ((own[j] & 3u) == kBrickMixed && sign_fill ? kListCheck : 0u);
             lmodes[i] = lm[j];
             ++i;

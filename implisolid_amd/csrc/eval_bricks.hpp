@@ -46,9 +46,8 @@ __device__ __forceinline__ void brick_of(int b, const BrickGrid& bg, int& bx, in
 // k_brick_fill, modes[i] the listed brick's pruning modes): every sample is evaluated with
 // `ev(modes, x, y, z)`, stored, and its sign bit set (wave ballot: 64 bits = kBY rows x kBX
 // samples).  Sign-filled bricks never reach this kernel -- k_brick_fill wrote their constant sign
-// bits -- except the face layers of candidates (grid.hpp ClaimCtx) next to a mixed brick whose face
-// samples differ from them, evaluated by that brick's wave, values only (their sign pieces are
-// constant and already written).
+// bits -- except claimed candidates (grid.hpp ClaimCtx), evaluated by the wave of the mixed brick
+// that claimed them, values only (their sign pieces are constant and already written).
 // both layers of a column: the evaluator's pair() when it has one (the JIT tree: one pass of the
 // tree code for both samples), else two calls
 template <class Eval>
@@ -124,162 +123,77 @@ __device__ __forceinline__ void eval_one_brick(const Eval& ev, const GridDesc& g
     }
 }
 
-// modes every one of a set of pruning-mode words agrees on (m_and / m_or: their AND / OR); the
-// others revert to "both operands" -- never less pruning than any member's box allows
-__device__ __forceinline__ uint64_t agreeing_modes(uint64_t m_and, uint64_t m_or) {
-    const uint64_t d = m_and ^ m_or;
-    return m_and & ~(((d | (d >> 1)) & 0x5555555555555555ull) * 3ull);
-}
-
-// fill byte of brick a (wave-uniform) through the scalar cache: nothing writes fill[] during the
-// eval, so the six neighbours' bytes are loaded into SGPRs before the brick's tree code runs
-__device__ __forceinline__ uint32_t fill_byte_uniform(const uint8_t* fill, int a) {
-    typedef const __attribute__((address_space(4))) uint32_t* CU32;
-    const uint32_t w = *(CU32)(fill + (a & ~3));
-    return (w >> (8 * (a & 3))) & 0xffu;
-}
-__device__ __forceinline__ uint64_t u64_uniform(const uint64_t* p, int i) {
-    typedef const __attribute__((address_space(4))) uint64_t* CU64;
-    return *(CU64)(p + i);
-}
-
-// Face neighbour d (= -x, +x, -y, +y, -z, +z) of brick b, or -1 outside the slab's brick grid.
-__device__ __forceinline__ int face_neighbour(const BrickGrid& bg, int b, int bx, int by, int bz, int d) {
-    const int ax = d >> 1, up = d & 1;
-    const int c = ax == 0 ? bx : ax == 1 ? by : bz;
-    const int lim = ax == 0 ? bg.nbx : ax == 1 ? bg.nby : bg.nbz;
-    if (up ? c + 1 >= lim : c == 0) return -1;
-    const int step = ax == 0 ? 1 : ax == 1 ? bg.nbx : bg.nbx * bg.nby;
-    return up ? b + step : b - step;
-}
-
-// Candidate faces of a just evaluated mixed brick (bit d: direction d): neighbours that are
-// candidates (grid.hpp) of sign s such that some sample of this brick on the shared face has the
-// other sign -- a cell edge across the face changes sign there, so marching cubes reads the
-// candidate's value at its end.  Such an edge ends on the candidate's face layer next to this
-// brick, and that layer is all marching cubes can read of it: every other edge it has runs inside
-// the candidate (one sign) or crosses into another neighbour -- of its own class, or mixed, whose
-// wave evaluates the layer on its side.  So each face is this brick's own business: no claims.
-// fa[d]: the neighbours' fill bytes (0 where there is none).
-__device__ __forceinline__ uint32_t candidate_faces(const GridDesc& g, int bz, const uint32_t fa[6],
-                                                    const uint64_t neg[kBZ], uint64_t valid) {
+// The face neighbours of a just evaluated mixed brick that it claims (bit d: direction d = -x, +x,
+// -y, +y, -z, +z): candidates (grid.hpp) of sign s such that some sample of this brick on the
+// shared face has the other sign -- a cell edge across the face changes sign there, so marching
+// cubes reads the candidate's value -- and that no other wave claimed first (atomic on the fill
+// byte).  Face samples are the lanes of the face column / row in both layers, or a whole layer.
+__device__ __forceinline__ uint32_t claim_neighbours(const GridDesc& g, const BrickGrid& bg, const ClaimCtx& cc, int b,
+                                                     const uint64_t neg[kBZ], uint64_t valid) {
     static_assert(kBZ == 2, "face masks of two-layer bricks");
+    int bx, by, bz;
+    brick_of(b, bg, bx, by, bz);
     const int layers = g.fz1 - g.fz0;
     const bool has1 = bz * kBZ + 1 < layers;
     uint64_t col0 = 0, row0 = (1ull << kBX) - 1ull;
 #pragma unroll
     for (int r = 0; r < kBY; ++r) col0 |= 1ull << (r * kBX);
     const uint64_t colL = col0 << (kBX - 1), rowL = row0 << (kBX * (kBY - 1));
-    uint32_t need = 0;
+    uint32_t claimed = 0;
 #pragma unroll
     for (int d = 0; d < 6; ++d) {
-        if (!(fa[d] & kBrickCandidate)) continue;
         const int ax = d >> 1, up = d & 1;
+        const int c = ax == 0 ? bx : ax == 1 ? by : bz;
+        const int lim = ax == 0 ? bg.nbx : ax == 1 ? bg.nby : bg.nbz;
+        if (up ? c + 1 >= lim : c == 0) continue;
+        const int step = ax == 0 ? 1 : ax == 1 ? bg.nbx : bg.nbx * bg.nby;
+        const int a = up ? b + step : b - step;
+        const uint32_t fa = cc.fill[a];
+        if (!(fa & kBrickCandidate)) continue;
         uint64_t f0, f1;
         if (ax == 0) f0 = f1 = up ? colL : col0;
         else if (ax == 1) f0 = f1 = up ? rowL : row0;
         else { f0 = up ? 0ull : ~0ull; f1 = up ? ~0ull : 0ull; }
         f0 &= valid;
         f1 = has1 ? (f1 & valid) : 0ull;
-        const bool aneg = (fa[d] & 3u) == kBrickNeg;
+        const bool aneg = (fa & 3u) == kBrickNeg;
         const uint64_t differ = aneg ? ((~neg[0] & f0) | (~neg[1] & f1)) : ((neg[0] & f0) | (neg[1] & f1));
-        if (differ) need |= 1u << d;
+        if (!differ) continue;
+        uint32_t old = 0;
+        const int sh = 8 * (a & 3);
+        if ((threadIdx.x & 63) == 0) old = atomicOr(reinterpret_cast<uint32_t*>(cc.fill + (a & ~3)), (uint32_t)kBrickClaimed << sh);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (!((old >> sh) & kBrickClaimed)) claimed |= 1u << d;
     }
-    return need;
+    return claimed;
 }
 
-// pruning modes of brick a: its refined modes if its coarse box is mixed, else the box's
-__device__ __forceinline__ uint64_t brick_modes_of(const BrickGrid& bg, const ClaimCtx& cc, int a) {
-    int cx, cy, cz;
-    brick_of(a, bg, cx, cy, cz);
-    const int cb = cx + cy * cc.cnbx + (cz / kCZ) * cc.cplane;
-    return fill_byte_uniform(cc.ccls, cb) == kBrickMixed ? u64_uniform(cc.bmodes, a) : u64_uniform(cc.cmodes, cb);
-}
-
-// The candidate face layers of `need`, values only (their sign pieces are constant and already
-// written), in at most two passes of the tree code with the modes all their candidates agree on:
-//   x / y faces: lanes 8 d + c, column c of face d's layer (both sample layers of the brick's pair);
-//   z faces: lane = the brick's (x, y), the pair = the -z candidate's top layer and the +z
-//   candidate's bottom layer.
-// Two mixed bricks may write a sample on a candidate's edge both: the same value bit for bit.
-template <class Eval, bool Pair>
-__device__ __forceinline__ void eval_candidate_faces(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
-                                                     const ClaimCtx& cc, int b, uint32_t need,
-                                                     float* __restrict__ field) {
-    const int lane = threadIdx.x & 63;
-    const int n = g.n, layers = g.fz1 - g.fz0;
-    int bx, by, bz;
-    brick_of(b, bg, bx, by, bz);
-    const int l0 = bz * kBZ;
-#pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t sel = need & (pass == 0 ? 0xfu : 0x30u);
-        if (!sel) continue;
-        uint64_t m_and = ~0ull, m_or = 0ull;
-        for (uint32_t r = sel; r; r &= r - 1u) {
-            const uint64_t m = brick_modes_of(bg, cc, face_neighbour(bg, b, bx, by, bz, __builtin_ctz(r)));
-            m_and &= m;
-            m_or |= m;
-        }
-        const uint64_t m = agreeing_modes(m_and, m_or);
-        int sx, sy, za, zb;
-        bool on_a, on_b;
-        if (pass == 0) {
-            const int d = lane >> 3, c = lane & 7;
-            const bool face = d < 4 && ((sel >> d) & 1u);
-            sx = d == 0 ? bx * kBX - 1 : d == 1 ? bx * kBX + kBX : bx * kBX + c;
-            sy = d == 2 ? by * kBY - 1 : d == 3 ? by * kBY + kBY : by * kBY + c;
-            on_a = face && sx < n && sy < n;
-            on_b = on_a && l0 + 1 < layers;
-            za = l0;
-            zb = l0 + 1 < layers ? l0 + 1 : l0;
-        } else {
-            sx = bx * kBX + (lane % kBX);
-            sy = by * kBY + (lane / kBX);
-            const bool ok = sx < n && sy < n;
-            on_a = ok && ((sel >> 4) & 1u);
-            on_b = ok && ((sel >> 5) & 1u);
-            za = on_a ? l0 - 1 : l0 + kBZ;
-            zb = on_b ? l0 + kBZ : l0 - 1;
-        }
-        const bool on = on_a || on_b;
-        const int cx = on ? sx : 0, cy = on ? sy : 0;
-        float f0, f1;
-        if constexpr (Pair) {
-            eval_pair(ev, m, sample_xy(g, 0, cx), sample_xy(g, 1, cy), sample_z(g, za), sample_z(g, zb), f0, f1, 0);
-        } else {
-            f0 = ev(m, sample_xy(g, 0, cx), sample_xy(g, 1, cy), sample_z(g, za));
-            f1 = ev(m, sample_xy(g, 0, cx), sample_xy(g, 1, cy), sample_z(g, zb));
-        }
-        const bool sealed_col = sealed_xy(g, cx) || sealed_xy(g, cy);
-        if (on_a) field[field_index(g, cx, cy, za)] = (sealed_col || sealed_z(g, za)) ? kSealed : 0.f + f0;
-        if (on_b) field[field_index(g, cx, cy, zb)] = (sealed_col || sealed_z(g, zb)) ? kSealed : 0.f + f1;
-    }
-}
-
-// a listed entry: the brick, then (mixed bricks) the layers of its candidate neighbours it needs.
-// The neighbours' fill bytes are loaded (scalar) before the brick's own tree code runs.
+// a listed entry: the brick, then (mixed bricks) the candidates it claimed, with their own modes --
+// one loop around a single copy of the tree code
 template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
 __device__ __forceinline__ void eval_listed(const Eval& ev, const GridDesc& g, const BrickGrid& bg, const ClaimCtx& cc,
                                             uint32_t entry, uint64_t m64, float* __restrict__ field,
                                             sign_piece_t* __restrict__ signs) {
     const int b = (int)(entry & ~kListCheck);
     const bool check = (entry & kListCheck) && cc.fill;
-    uint32_t fa[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-    int bx, by, bz;
-    brick_of(b, bg, bx, by, bz);
-    if (check) {
-#pragma unroll
-        for (int d = 0; d < 6; ++d) {
-            const int a = face_neighbour(bg, b, bx, by, bz, d);
-            fa[d] = a >= 0 ? fill_byte_uniform(cc.fill, a) : 0u;
-        }
+    int cur = b;
+    uint64_t mcur = m64;
+    uint32_t claimed = 0;
+    for (bool first = true;; first = false) {
+        uint64_t neg[kBZ], valid;
+        eval_one_brick<Eval, Pair>(ev, g, bg, cur, mcur, field, signs, first, neg, valid);
+        if (first && check) claimed = claim_neighbours(g, bg, cc, b, neg, valid);
+        if (!claimed) break;
+        const int d = __builtin_ctz(claimed);
+        claimed &= claimed - 1u;
+        const int ax = d >> 1, up = d & 1;
+        const int step = ax == 0 ? 1 : ax == 1 ? bg.nbx : bg.nbx * bg.nby;
+        cur = up ? b + step : b - step;
+        int cx, cy, cz;
+        brick_of(cur, bg, cx, cy, cz);
+        const int cb = cx + cy * cc.cnbx + (cz / kCZ) * cc.cplane;
+        mcur = cc.ccls[cb] == kBrickMixed ? cc.bmodes[cur] : cc.cmodes[cb];
     }
-    uint64_t neg[kBZ], valid;
-    eval_one_brick<Eval, Pair>(ev, g, bg, b, m64, field, signs, true, neg, valid);
-    if (!check) return;
-    const uint32_t need = candidate_faces(g, bz, fa, neg, valid);
-    if (need) eval_candidate_faces<Eval, Pair>(ev, g, bg, cc, b, need, field);
 }
 
 template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>

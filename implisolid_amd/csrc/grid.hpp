@@ -46,16 +46,15 @@ static_assert(kBX * kBY == 64 && (kBX == 8 || kBX == 16 || kBX == 32), "a brick 
 constexpr int kBrickListWord = 12, kCoarseListWord = 13, kOverflowWord = 16, kCounterWords = 32;
 enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBrickNoFill = 4 };
 // fill[b] (written by the pruned eval) = class | fill class << 4 | flags.  Fill class kBrickPos /
-// kBrickNeg: the brick's sign pieces are constant (no cell corner in it needs its exact value,
-// except a candidate's face layers next to a mixed neighbour) -- 0: listed, evaluated.
+// kBrickNeg: the brick's sign pieces are constant (no cell corner in it needs its exact value unless
+// it is a claimed candidate) -- 0: listed, evaluated.
 //   kBrickCandidate: sign-definite, and every face neighbour of another class is of mixed class.
-//     Its values are needed only on the face layer next to a mixed neighbour whose face samples
-//     take the other sign: that neighbour's wave checks this after its own evaluation and
-//     evaluates the layer (eval_bricks.hpp eval_candidate_faces).
-//   kBrickClaimed: no longer set (candidates are never claimed; kept for the fill byte's layout).
+//     Its values are needed only where a mixed neighbour's face samples take the other sign: the
+//     mixed neighbour's wave checks that after its own evaluation and evaluates the candidate.
+//   kBrickClaimed: set (atomically) by the first such wave.
 enum BrickFlag : uint8_t { kBrickCandidate = 8, kBrickClaimed = 0x80 };
 struct BrickGrid { int nbx, nby, nbz, n_bricks; };
-// what a listed mixed brick's wave needs to find and evaluate its candidates' face layers
+// what a listed mixed brick's wave needs to find and evaluate its claimed neighbours
 struct ClaimCtx {
     uint8_t* fill;            // null: no candidates (every brick that needs values is listed)
     const uint8_t* ccls;      // coarse classes: a brick of a mixed coarse box has refined modes
@@ -63,7 +62,7 @@ struct ClaimCtx {
     const uint64_t* cmodes;   // per-coarse-box modes
     int cnbx, cplane;         // coarse grid: boxes per row, per layer
 };
-// list entry: brick index | kListCheck if the brick is of mixed class (its wave evaluates candidate faces)
+// list entry: brick index | kListCheck if the brick is of mixed class (its wave claims candidates)
 constexpr uint32_t kListCheck = 0x80000000u;
 
 // Field storage, brick-major: brick (bx, by, bz) of the slab's brick grid holds its kBX x kBY x kBZ

@@ -249,8 +249,7 @@ int implisolid_slab_kernel_times_each(implisolid_slab* s, float ms[8]);
  * this (not the field) is the complete sign information marching cubes uses. */
 int64_t implisolid_slab_read_signs(implisolid_slab* s, uint8_t* out, int64_t capacity);
 /* bricks of the last slab eval: out = [bricks, mixed-sign bricks, sign-filled bricks] (blocking);
- * sign-filled = no value computed (neighbour candidates included: at most their face layers next to a
- * mixed brick are evaluated) */
+ * sign-filled = no value computed (claimed neighbour candidates, which were evaluated, excluded) */
 int implisolid_slab_brick_stats(implisolid_slab* s, int64_t out[3]);
 
 /* Object stream (BASELINE config 5): n objects polygonised with the same mc settings, each with
