@@ -29,6 +29,13 @@ import time
 import numpy as np
 
 T_START = time.perf_counter()   # the bench's total wall time is reported from here (legs_wall_s)
+
+
+def progress(what):
+    """A progress line on stderr (rank 0): a cold box compiles every tree module on first use, and
+    a run that prints nothing for minutes reads as hung.  The JSON line stays alone on stdout."""
+    if os.environ.get("RANK", "0") == "0":
+        print("bench: %s (%.1f s)" % (what, time.perf_counter() - T_START), file=sys.stderr, flush=True)
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -448,6 +455,7 @@ def main():
     legs = {}
 
     def leg(name, fn):
+        progress("%s ..." % name)
         t0 = time.perf_counter()
         r = fn()
         legs[name] = round(time.perf_counter() - t0, 2)
@@ -627,6 +635,7 @@ def main():
     # module compiles in the background): build_geometry (eval + MC, host-resident result) of fresh
     # random trees at R 32 and 128, against the oracle on one host core for the same call
     first = None
+    progress("first_call ...")
     t_leg = time.perf_counter()
     if world == 1 and not args.skip_ob02:
         import oracle
@@ -651,6 +660,7 @@ def main():
     # end-to-end build_geometry of the config-4 tree (eval + MC) through the C ABI,
     # to a host-resident mesh (PCIe included), at 256^3 and 512^3 -- the reference's unit of work
     e2e = None
+    progress("end_to_end ...")
     t_leg = time.perf_counter()
     if world == 1 and not args.skip_ob02:
         e2e = {}
@@ -670,6 +680,7 @@ def main():
     # configs 2 and 3 through the C ABI: build_geometry (MC + 3 x [resample, project, QEM]) to a
     # host-resident mesh, PCIe included; the oracle times config 2 on one host core beside it
     ob02 = None
+    progress("ob02 ...")
     t_leg = time.perf_counter()
     # config 3 on its dyadic box keeps every centroid (NaN average edge length from the reference's
     # NaN normals at a singular sample); on the box shifted by 0.003 the alpha
@@ -724,6 +735,7 @@ def main():
             # and face identity of the GPU result against it
             import oracle
             oracle.build()
+            progress("ob02_cpu_oracle ...")
             t_leg = time.perf_counter()
             for key, (shape, mc) in ob02_legs:
                 v, f = I.make_geometry(shape, mc)
@@ -937,6 +949,7 @@ def main():
         out["first_call"] = dict(first, workload="never-seen random 10-leaf trees, build_geometry eval+MC, "
                                                  "async JIT (interpreter kernels on the first call)")
     if world == 1 and not args.no_cpu_baseline:
+        progress("cpu_baseline ...")
         t0 = time.perf_counter()
         out["cpu_baseline"], (Rs, v_ref, f_ref) = cpu_baseline(main_run["shape"])
         legs["cpu_baseline"] = round(time.perf_counter() - t0, 2)
@@ -947,6 +960,7 @@ def main():
     else:
         out["cpu_baseline"] = None
     if c5 and not args.no_cpu_baseline:
+        progress("config5_cpu_baseline ...")
         t0 = time.perf_counter()
         c5["cpu_baseline"] = config5_cpu_baseline()
         legs["config5_cpu_baseline"] = round(time.perf_counter() - t0, 2)
