@@ -13,7 +13,8 @@ layer below its slab; the only exchange in the step is an all-gather of the per-
 counts, overlapped with the vertex pass, which gives every rank its global numbering offsets on the
 device.  After the timed steps the mesh is gathered to rank 0 (distributed.gather_mesh, timed as
 "gather_ms") and checked against the oracle's summary of the same workload.  Weak scaling (the grid
-grown to R_N = R N^(1/3), ~R^3 voxels per rank) is reported beside it; --weak swaps the two.
+grown to R_N = round(R N^(1/3)), ~R^3 voxels per rank: 645^3 / 813^3 / 1024^3 at 2 / 4 / 8 ranks) is
+reported beside it, gathered and checked the same way; --weak swaps the two.
 
 Prints ONE JSON line (rank 0).  Extra fields: per-kernel times from HIP events on the launch
 stream, the HBM roofline of the eval+MC kernel sequence (SURVEY.md 8d's algorithmic bytes), and
@@ -124,9 +125,21 @@ def config5_cpu_baseline(n_objects=64):
     cores = max(1, min(cores, n_objects))
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
-    with ctx.Pool(cores) as pool:
+    pool = ctx.Pool(cores)
+    try:
         rows = pool.map(_c5_oracle_object, range(n_objects), chunksize=1)
+        pool.close()
+    finally:
+        pool.terminate()
+        pool.join()   # every worker reaped before the bench goes on
     wall = time.perf_counter() - t0
+    # the spawn context started multiprocessing's resource tracker for the pool's semaphores: stop
+    # it now, so the bench leaves no child process behind (BENCH_r03 recorded one at its end)
+    try:
+        from multiprocessing import resource_tracker
+        resource_tracker._resource_tracker._stop()
+    except Exception:
+        pass
     one = sum(r[1] for r in rows)
     return {"value": round(n_objects / wall, 2), "unit": "objects/s", "cores": cores, "kind": "port",
             "sample": "oracle restatement (C): all %d config-5 objects at 128^3, eval+MC, one object per task on "
@@ -229,10 +242,10 @@ def main():
     ap.add_argument("--skip-256", action="store_true", help="do not also time R=256")
     ap.add_argument("--prune", type=int, default=None, help="pruning level 0/1/2 (default: library default 2)")
     ap.add_argument("--weak", action="store_true",
-                    help="N > 1: the headline is weak scaling (R N^(1/3), ~R^3 voxels per rank): the default")
-    ap.add_argument("--strong", action="store_true",
-                    help="N > 1: the headline is strong scaling of the R grid (BASELINE config 4) instead; "
-                         "the other is reported beside it either way")
+                    help="N > 1: the headline is weak scaling (R_N = R N^(1/3), ~R^3 voxels per rank) instead of "
+                         "strong scaling of the R grid (BASELINE config 4, the default); the other is reported "
+                         "beside it either way, both with the gathered mesh checked against the oracle")
+    ap.add_argument("--strong", action="store_true", help="N > 1: strong scaling headline (the default; kept for scripts)")
     ap.add_argument("--equal-slabs", action="store_true", help="N > 1: equal-layer slabs instead of balanced cuts")
     ap.add_argument("--skip-config5", action="store_true", help="do not time the 64-object stream (config 5)")
     ap.add_argument("--config5-streams", type=int, default=8)
@@ -448,10 +461,11 @@ def main():
         slab.close()
         return info
 
-    # N > 1: the headline is weak scaling (R_N = R N^(1/3), ~R^3 voxels per rank: the per-GPU work
-    # stays that of one GPU, task contract 5) and strong scaling of config 4 (the R grid over N GPUs,
-    # BASELINE config 4) is reported beside it, with the gather to rank 0 and its parity (--strong
-    # swaps them)
+    # N > 1: the headline is strong scaling of config 4 (the R grid over N GPUs, BASELINE config 4);
+    # weak scaling (R_N = R N^(1/3), ~R^3 voxels per rank: the per-GPU work stays that of one GPU) is
+    # reported beside it (--weak swaps them).  Both gather their mesh to rank 0 after the timed steps
+    # and check it against the oracle's summary of the same grid (tests/golden/make_headline.py holds
+    # config4_mc_r512 / r645 / r813 / r1024)
     legs = {}
 
     def leg(name, fn):
@@ -460,12 +474,12 @@ def main():
         r = fn()
         legs[name] = round(time.perf_counter() - t0, 2)
         return r
-    weak = world > 1 and not args.strong
+    weak = world > 1 and args.weak and not args.strong
     R_weak = int(round(args.resolution * world ** (1.0 / 3.0)))
-    main_run = leg("headline", lambda: run(R_weak if weak else args.resolution, args.steps, args.warmup, gather=not weak))
+    main_run = leg("headline", lambda: run(R_weak if weak else args.resolution, args.steps, args.warmup, gather=True))
     side_run = None
     if world > 1:
-        side_run = leg("side", lambda: run(args.resolution if weak else R_weak, args.steps, args.warmup, gather=weak))
+        side_run = leg("side", lambda: run(args.resolution if weak else R_weak, args.steps, args.warmup, gather=True))
     r256 = leg("r256", lambda: run(256, args.steps, args.warmup)) if (not args.skip_256 and args.resolution != 256 and world == 1) else None
     # a dense-surface data point: config 2's scene (sphere u rabbit, ~1.5 M vertices) at the same R
     rdense = None if (args.skip_256 or world > 1) else leg("union_scene", lambda: run(
@@ -666,9 +680,15 @@ def main():
         e2e = {}
         for Re in (256, 512):
             shape, mc = scenes.config4(Re)
-            I.make_geometry(shape, mc)
+            # warm: the object turns hot after a few builds (bake mode 2) and its baked module
+            # compiles on host threads; builds timed beside that compile read up to 2x slower
+            # (BENCH_r03: median 1.89 vs min 0.92 ms), so the timed builds start once it is loaded
+            for _ in range(2):
+                for _ in range(5):
+                    I.make_geometry(shape, mc)
+                I.jit_wait()
             ts = []
-            for _ in range(5):
+            for _ in range(7):
                 t0 = time.perf_counter()
                 v, f = I.make_geometry(shape, mc)
                 ts.append(time.perf_counter() - t0)
@@ -884,7 +904,11 @@ def main():
                    "mixed_coarse_boxes": main_run["stats"]["mixed_coarse_boxes"]},
         "mc": {"units": main_run["stats"]["units"], "nonempty_units": main_run["stats"]["nonempty_units"],
                "active_cells": main_run["stats"]["act"]},
-        "roofline": {"bound": "hbm", "kernel": dom, "dominant_kernel": dom,
+        # bound: what the counters show.  The path is elementwise / scan / gather work priced against
+        # HBM (roofline_class), but every kernel of the pruned pass is latency- or issue-bound:
+        # the pass moves 0.14 of peak by its counter bytes (pass_frac) and the dominant kernel's
+        # VALU is mostly idle
+        "roofline": {"bound": "latency", "roofline_class": "hbm", "kernel": dom, "dominant_kernel": dom,
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": k_traffic.get(dom), "traffic_source": tname, "traffic_current": traffic_current,
@@ -895,6 +919,9 @@ def main():
                      "valu_source": vname,
                      "per_kernel": per_kernel,
                      "kernel_share": {k: round(v / max(1e-9, sum(each.values())), 3) for k, v in each.items()},
+                     "pass_frac": round(pass_achieved / HBM_PEAK_GBS, 4) if pass_achieved else None,
+                     "pass_frac_note": "the whole eval+MC pass: PMC counter bytes of its kernels over their time "
+                                       "(the honest pass figure; pass.effective_frac is the dense-equivalent, > 1)",
                      "pass": {"kernels": "the eval+MC kernel sequence (8 kernels), HIP events around eval / count+scan / emit",
                               "launch_ms": round(t_kern * 1e3, 4), "traffic": traffic,
                               "achieved": round(pass_achieved, 1) if pass_achieved else None,

@@ -988,7 +988,11 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
                                  "merged refine pass's 32-bit item index; use fewer objects or n_streams >= 1");
         }
         const auto t0 = std::chrono::steady_clock::now();
-        if (Engine::pruning() > 0 && !b->merged) TreeJit::instance().precompile(progs, 16);
+        struct Held {   // precompile()'s references, dropped once the engines hold their own
+            std::vector<TreeJit::Slot*> s;
+            ~Held() { for (auto* x : s) TreeJit::instance().release(x); }
+        } held;
+        if (Engine::pruning() > 0 && !b->merged) held.s = TreeJit::instance().precompile(progs, 16);
         b->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         const int ns = b->merged ? 1 : std::max(1, std::min(n_streams, 8));
         for (int k = 0; k < ns; ++k) {

@@ -187,6 +187,7 @@ void Engine::set_object(const Program& prog) {
     evals_ = 0;
     jit_fn_ = nullptr;
     have_object_ = true;
+    ++obj_gen_;   // the grid's buffers hold the previous object's field and signs: set_slab resets them
 }
 
 void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
@@ -195,11 +196,13 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
 
 void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool probe_only) {
     const SlabRange sr = slab_range(R, sr_in.z0, sr_in.z1);   // validated, 32-bit limits checked
-    // the same grid again (repeated builds of build_geometry): every buffer keeps its size and its
-    // invariants (umark ids only grow, the sign pieces past a row's last brick stay 0, counters are
-    // cleared in-kernel), so there is nothing to reset and nothing to wait for
+    // the same grid and object again (repeated builds of build_geometry): every buffer keeps its size
+    // and its invariants (umark ids only grow, the sign pieces past a row's last brick stay 0,
+    // counters are cleared in-kernel), so there is nothing to reset and nothing to wait for.  A new
+    // object on the same grid resets the field (unlisted bricks read as 0) and the sign bitmap
+    // (bricks the new object leaves unlisted must not keep the old object's signs).
     if (have_grid_ && !probe_only && !probe_only_ && key_R_ == R && key_z0_ == sr.z0 && key_z1_ == sr.z1 &&
-        std::memcmp(key_box_, box, sizeof key_box_) == 0)
+        key_obj_gen_ == obj_gen_ && std::memcmp(key_box_, box, sizeof key_box_) == 0)
         return;
     key_R_ = -1;   // set again once the buffers below are valid
     // the buffers below are reset on the null stream, which a non-blocking caller stream does not
@@ -249,6 +252,7 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     key_R_ = R;
     key_z0_ = sr.z0;
     key_z1_ = sr.z1;
+    key_obj_gen_ = obj_gen_;
     std::memcpy(key_box_, box, sizeof key_box_);
 }
 
@@ -306,7 +310,7 @@ void Engine::eval_field(hipStream_t s) {
     counters_fresh_ = true;
     mark(0, s);
     if (level > 0) {
-        ensure_jit();
+        ensure_jit(s);
         launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, cmodes_.as<uint64_t>(),
                            ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>(),
                            modes_.as<uint64_t>(), cls_.as<uint8_t>(), s, &jit_iv_, timing_ ? ev_[9] : nullptr);
@@ -345,7 +349,7 @@ void Engine::eval_field(hipStream_t s) {
 void Engine::interval_pass(hipStream_t s) {
     if (!have_grid_ || !have_object_) throw InputError("engine: object and grid must be set before the interval pass");
     if (brick_grid(grid_).n_bricks <= 0) return;
-    ensure_jit();
+    ensure_jit(s);
     launch_brick_modes(prog_.as<Program>(), depth_, rabbit_.as<float>(), tab_range_, grid_, cmodes_.as<uint64_t>(),
                        ccls_.as<uint8_t>(), clist_.as<uint32_t>(), counters_.as<uint32_t>(), modes_.as<uint64_t>(),
                        cls_.as<uint8_t>(), s, &jit_iv_);
@@ -411,26 +415,26 @@ const float* Engine::d_mats() const {
     return reinterpret_cast<const float*>(prog_.as<char>() + offsetof(Program, mats));
 }
 
-const TreeJit::PointKernels* Engine::point_jit() {
+const TreeJit::PointKernels* Engine::point_jit(hipStream_t s) {
     if (!pt_requested_) {
-        pt_slot_ = TreeJit::instance().request(prog_host_, TreeJit::kPoints);
+        pt_slot_ = TreeJit::instance().request(prog_host_, TreeJit::kPoints, false, s);
         pt_requested_ = true;
     }
     return (pt_slot_ && pt_slot_->ready.load(std::memory_order_acquire)) ? &pt_slot_->pk : nullptr;
 }
 
-void Engine::ensure_jit() {
+void Engine::ensure_jit(hipStream_t s) {
     // the object's tree module is requested once (TreeJit: compiled now, or on a background thread
     // while the interpreter kernels run); every eval uses it as soon as it is loaded
     TreeJit& J = TreeJit::instance();
     if (!jit_requested_) {
-        jit_slot_ = J.request(prog_host_, TreeJit::kBricks, J.bake() == TreeJit::kBakeAlways);
+        jit_slot_ = J.request(prog_host_, TreeJit::kBricks, J.bake() == TreeJit::kBakeAlways, s);
         jit_requested_ = true;
     }
     // a hot object (evaluated kBakeAfter times since set_object) gets its baked module
     if (++evals_ >= TreeJit::kBakeAfter && !bake_requested_ && allow_hot_bake_ && J.bake() == TreeJit::kBakeHot &&
         jit_slot_) {
-        bake_slot_ = J.request(prog_host_, TreeJit::kBricks, true);
+        bake_slot_ = J.request(prog_host_, TreeJit::kBricks, true, s);
         bake_requested_ = true;
     }
     const TreeJit::Slot* use = bake_slot_ && bake_slot_->ready.load(std::memory_order_acquire) ? bake_slot_
@@ -547,7 +551,7 @@ ObjArgs Engine::obj_args() const {
 
 void Engine::eval_points(const float* d_xyz, int64_t n, float* d_f, float* d_grad, hipStream_t s) {
     if (!have_object_) throw InputError("engine: no object set");
-    if (const TreeJit::PointKernels* pk = point_jit()) {
+    if (const TreeJit::PointKernels* pk = point_jit(s)) {
         if (n <= 0) return;
         const float* m = d_mats();
         const float* tab = rabbit_.as<float>();

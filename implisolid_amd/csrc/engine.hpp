@@ -113,7 +113,7 @@ public:
     const float* d_mats() const;
     // the object's point module (OB02 passes, direct evaluation): requested on first use (compiled
     // in the background in async mode); null until loaded -- the interpreter kernels run meanwhile
-    const TreeJit::PointKernels* point_jit();
+    const TreeJit::PointKernels* point_jit(hipStream_t s = nullptr);
 
     DevBuf& scratch(int k) { return scratch_[k]; }
     // engines whose kernels are captured once (object streams): no switch to a baked module later
@@ -159,12 +159,13 @@ private:
     uint32_t mark_id_ = 0;          // id of the last pruned eval's unit marks (umark_)
     bool marks_valid_ = false;      // the last eval was pruned: count only marked units
     JitIntervalKernels jit_iv_;
-    void ensure_jit();
+    void ensure_jit(hipStream_t s = nullptr);
     void release_jit();   // drop the module references (after the device has synchronised)
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false, probe_only_ = false;
     // the grid set_slab last built its buffers for: setting the same one again keeps them
     int key_R_ = -1, key_z0_ = 0, key_z1_ = 0;
+    uint64_t obj_gen_ = 0, key_obj_gen_ = ~0ull;   // set_object's generation / the one the grid's buffers hold
     float key_box_[6] = {};
     HostBuf hcounters_;   // pinned landing zone of read_counts / raw_counters (one small copy)
     DevBuf prog_, rabbit_, cases_;

@@ -678,7 +678,21 @@ void TreeJit::shutdown() {   // at exit: drop queued work, finish what is compil
     workers_.clear();
 }
 
-TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
+// A caller stream being captured into a graph (torch.cuda.CUDAGraph captures in global mode) must
+// not see the device synchronisation an unload needs: eviction then waits for a request made outside
+// a capture.  Only the caller's own stream is asked (querying the null stream during a capture would
+// itself invalidate it); a null caller stream is taken as not capturing.
+bool TreeJit::defer_eviction(hipStream_t stream) {
+    if (!stream) return false;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return st != hipStreamCaptureStatusNone;
+}
+
+TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake, hipStream_t stream) {
     const int m = mode();
     if (m == kOff) return nullptr;
     std::string src;
@@ -707,7 +721,13 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
             slot->device = dev;
             cache_.emplace(key, slot);
             fresh = true;
-            if ((int)cache_.size() > max_modules_) evict_locked(evict);
+        }
+        // the reference is taken under the same lock as the lookup: a slot found here is held
+        // before any other request can evict it (evict_locked takes only slots with refs == 0)
+        ++slot->refs;
+        slot->last_use = ++tick_;
+        if ((int)cache_.size() > max_modules_.load()) evict_locked(evict, defer_eviction(stream));
+        if (fresh) {
             if (m == kAsync && !stop_) {
                 queue_.push_back(slot);
                 if (workers_.empty()) {   // a small pool, started on first use
@@ -719,14 +739,15 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
             }
         }
     }
-    {
-        std::lock_guard<std::mutex> lock(mu_);
-        ++slot->refs;
-        slot->last_use = ++tick_;
-    }
     unload(evict);
     if (fresh && m == kAsync) cv_.notify_one();
-    if (fresh && (m == kSync || stop_)) build(slot);
+    if (fresh && (m == kSync || stop_)) {
+        build(slot);
+        // another thread's sync request for the same source waits on idle_cv_ (the lock orders the
+        // notification after its predicate check)
+        { std::lock_guard<std::mutex> lock(mu_); }
+        idle_cv_.notify_all();
+    }
     if (m == kSync) {   // a slot queued earlier in async mode: wait for it
         std::unique_lock<std::mutex> lock(mu_);
         idle_cv_.wait(lock, [slot] { return slot->ready.load() || slot->failed.load(); });
@@ -734,9 +755,15 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake) {
     return slot;
 }
 
-void TreeJit::evict_locked(std::vector<Slot*>& out) {
+void TreeJit::evict_locked(std::vector<Slot*>& out, bool defer) {
     // the least recently requested finished slots nobody holds, down to 3/4 of the bound (one
-    // eviction pays for many requests); queued or compiling slots are never taken
+    // eviction pays for many requests); queued or compiling slots are never taken.  Deferred (a
+    // graph capture is in progress): nothing is taken now; the next request outside a capture
+    // trims the cache.
+    if (defer) {
+        ++n_deferred_;
+        return;
+    }
     std::vector<Slot*> idle;
     for (auto& kv : cache_) {
         Slot* s = kv.second;
@@ -763,7 +790,10 @@ void TreeJit::unload(std::vector<Slot*>& slots) {
         if (s->mod) {
             if (!synced[s->device]) {
                 (void)hipSetDevice(s->device);
-                (void)hipDeviceSynchronize();
+                const hipError_t e = hipDeviceSynchronize();
+                if (e != hipSuccess)   // an earlier kernel's fault surfaces here: report it where it shows
+                    std::fprintf(stderr, "implisolid: device synchronisation before a module unload failed: %s\n",
+                                 hipGetErrorString(e));
                 synced[s->device] = true;
             }
             (void)hipSetDevice(s->device);
@@ -792,12 +822,16 @@ void TreeJit::wait_idle() {
     idle_cv_.wait(lock, [this] { return queue_.empty() && busy_ == 0; });
 }
 
-void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
-    if (mode() == kOff) return;
+std::vector<TreeJit::Slot*> TreeJit::precompile(const std::vector<Program>& progs, int threads) {
+    if (mode() == kOff) return {};
     // register and queue every program's module (async), then drain the queue with extra threads
     const int saved = mode();
     mode_.store(kAsync);
-    for (const Program& p : progs) release(request(p, kBricks, bake() == kBakeAlways));   // cached, not held
+    // the slots stay held (returned to the caller, who releases them once the batch's engines have
+    // taken their own references):
+    // a batch larger than the module bound must not evict its own early modules before its warm run
+    std::vector<Slot*> held;
+    for (const Program& p : progs) held.push_back(request(p, kBricks, bake() == kBakeAlways));
     mode_.store(saved);
     // let the pool drain the queue, with extra threads for a large batch
     std::vector<std::thread> extra;
@@ -822,6 +856,7 @@ void TreeJit::precompile(const std::vector<Program>& progs, int threads) {
     });
     for (auto& t : extra) t.join();
     wait_idle();
+    return held;
 }
 
 // The eval kernel's occupancy request: eight waves per SIMD (64 VGPRs).  The config-4 tree's pair

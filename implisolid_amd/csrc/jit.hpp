@@ -83,18 +83,23 @@ public:
     enum Mode { kOff = 0, kSync = 1, kAsync = 2 };
     enum BakeMode { kBakeNever = 0, kBakeAlways = 1, kBakeHot = 2 };
     static constexpr int kBakeAfter = 4;
-    Slot* request(const Program& p, int kind = kBricks, bool bake = false);
+    // `stream`: the caller's launch stream; while it is being captured into a graph no module is
+    // unloaded (an unload synchronises the device), the cache is trimmed by a later request
+    Slot* request(const Program& p, int kind = kBricks, bool bake = false, hipStream_t stream = nullptr);
     // drop a reference taken by request() (null is ignored); the caller launches nothing from the
     // slot afterwards and has synchronised whatever it launched
     void release(Slot* slot);
     int modules() const;
-    int max_modules() const { return max_modules_; }
-    void set_max_modules(int n) { max_modules_ = n < 8 ? 8 : n; }
+    int max_modules() const { return max_modules_.load(); }
+    void set_max_modules(int n) { max_modules_.store(n < 8 ? 8 : n); }
+    int deferred_evictions() const { return n_deferred_.load(); }
     // block until every scheduled compilation has finished (bench / batch setup)
     void wait_idle();
     // compile the modules of many programs (sync, up to `threads` host threads); request() then
-    // finds them ready
-    void precompile(const std::vector<Program>& progs, int threads);
+    // finds them ready.  Returns one reference per program (null where JIT is off or the source
+    // failed), which the caller releases once its engines hold their own: until then the module
+    // bound cannot evict them.
+    std::vector<Slot*> precompile(const std::vector<Program>& progs, int threads);
 
     // launch the compiled brick kernel (same contract as launch_eval_field_pruned's 2nd kernel)
     static void launch_bricks(hipFunction_t fn, const float* d_mats, const float* d_rabbit, const GridDesc& g,
@@ -121,12 +126,13 @@ private:
     void build(Slot* slot);            // compile (or read from disk) + load; sets ready / failed
     void worker();
     void shutdown();
-    void evict_locked(std::vector<Slot*>& out);   // pick slots to unload (mu_ held)
+    void evict_locked(std::vector<Slot*>& out, bool defer);   // pick slots to unload (mu_ held)
+    static bool defer_eviction(hipStream_t stream);           // is the caller's stream capturing?
     void unload(std::vector<Slot*>& slots);       // unload and free them (mu_ not held)
     mutable std::mutex mu_;
     uint64_t tick_ = 0;
-    int max_modules_ = 1024;
-    std::atomic<int> n_evicted_{0};
+    std::atomic<int> max_modules_{1024};
+    std::atomic<int> n_evicted_{0}, n_deferred_{0};
     std::condition_variable cv_, idle_cv_;
     std::unordered_map<std::string, Slot*> cache_;   // key: device + source
     std::deque<Slot*> queue_;

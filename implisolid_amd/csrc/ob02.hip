@@ -1526,7 +1526,7 @@ void Ob02::vertex_resampling(float c) {
     // mesh unless sharded); per-face pointers are offset to the range's first face
     const int64_t ncf = cf1_ - cf0_;
     if (ncf > 0) {
-        if (const TreeJit::PointKernels* pk = E.point_jit()) {
+        if (const TreeJit::PointKernels* pk = E.point_jit(s)) {
             const float *m = E.d_mats(), *tab = E.d_rabbit(), *v = verts_.as<float>();
             const int32_t* f = faces_.as<int32_t>() + 3 * cf0_;
             float *C = cen_.as<float>() + 3 * cf0_, *N = nrm_.as<float>() + 3 * cf0_;
@@ -1709,7 +1709,7 @@ void Ob02::centroids_projection(bool enable_qem) {
     a.cen = cen_.as<float>() + 3 * j0;
     a.dir = dir_.as<float>() + 3 * j0;
     a.evals = profile_ ? evals_buf_.as<uint32_t>() + j0 : nullptr;
-    const TreeJit::PointKernels* pk = E.point_jit();   // one choice for the whole projection
+    const TreeJit::PointKernels* pk = E.point_jit(s);   // one choice for the whole projection
     const float *jm = E.d_mats(), *jtab = E.d_rabbit();
     void* jargs[] = {&jm, &jtab, &a};
     if (nw <= 0) {
@@ -1893,6 +1893,10 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
         nf = 4 * nf;
         topo_valid_ = false;
         etab_valid_ = false;
+        // the new vertices and faces are covered by later steps: the ranges become the whole mesh
+        // (a sharded caller sets its owned vertices of the subdivided mesh again)
+        own_v0_ = 0; own_v1_ = nv; wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
+        sharded_ = false;
     }
     add_rand_noise(amplitude);
 }

@@ -8,6 +8,9 @@ run alone takes ~16 s of CPU):
 
   config4_mc_r512   config 3/4's twist tree, R = 512, eval + MC          (the bench headline)
   config4_mc_r256   the same tree at R = 256, eval + MC                  (the metric's 256^3 point)
+  config4_mc_r645 / r813 / r1024   the same tree at bench.py's weak-scaling grids for 2 / 4 / 8
+                    ranks (R_N = round(512 N^(1/3))), eval + MC; r1024 also pins the one-GPU test
+                    of the eight balanced slabs of the 1024^3 grid
   config3_ob02_r256 config 3 (the tree, R = 256, MC + 3 x [resample, project, QEM])
   config2_ob02_r128 config 2 (sphere u rabbit, R = 128, MC + 3 x [resample, project, QEM])
   config3s_ob02_r256 config 3 with its box shifted by 0.003 (scenes.config3_shifted): no singular
@@ -47,6 +50,10 @@ def configs():
     return {
         "config4_mc_r512": scenes.config4(512),
         "config4_mc_r256": scenes.config4(256),
+        # the weak-scaling grids of bench.py at N = 2, 4, 8 ranks: R_N = round(512 N^(1/3))
+        "config4_mc_r645": scenes.config4(645),
+        "config4_mc_r813": scenes.config4(813),
+        "config4_mc_r1024": scenes.config4(1024),
         "config3_ob02_r256": scenes.config3(256),
         "config2_ob02_r128": scenes.config2(128),
         "config3s_ob02_r256": scenes.config3_shifted(256),

@@ -397,6 +397,70 @@ def test_jit_module_bound_unloads_idle_modules(impli, oracle):
     assert hashlib.sha256(first[1].tobytes()).digest() == hashlib.sha256(again[1].tobytes()).digest()
 
 
+def test_jit_module_bound_two_threads(impli, oracle):
+    """The module bound under concurrent requests: two host threads polygonise 10
+    different objects each through their own slabs (ctypes drops the GIL inside the library), with
+    one baked module per object and room for 8.  A request that finds its slot takes the reference
+    under the lookup's lock, so another thread's eviction can never unload a module in use: every
+    mesh is the oracle's."""
+    import threading
+    from implisolid_amd import scenes
+    mc = scenes.mc_settings(32, 1.0)
+    shapes = [[scenes.random_tree(616000 + 100 * t + k, 3) for k in range(10)] for t in range(2)]
+    out = [[None] * 10 for _ in range(2)]
+    errs = []
+
+    def work(t):
+        try:
+            for k, sh in enumerate(shapes[t]):
+                for _ in range(2):   # the second pass finds the slot (or a rebuilt one) in the cache
+                    s = impli.Slab(sh, mc)
+                    try:
+                        nv, nf = s.run()
+                        out[t][k] = s.download(nv, nf)
+                    finally:
+                        s.close()
+        except Exception as e:   # reported by the main thread
+            errs.append(e)
+
+    impli.set_jit(1)
+    impli.set_jit_bake(1)
+    impli.set_jit_max_modules(8)
+    try:
+        th = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        impli.set_jit_max_modules(1024)
+        impli.set_jit(2)
+        impli.set_jit_bake(2)
+    assert not errs, errs
+    for t in range(2):
+        for k, sh in enumerate(shapes[t]):
+            vr, fr = oracle.polygonize(json.dumps(sh), json.dumps(mc))
+            v, f = out[t][k]
+            assert np.array_equal(f, fr) and np.array_equal(v.view(np.uint32), vr.view(np.uint32)), (t, k)
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_same_grid_new_object_resets_buffers(impli, oracle, level):
+    """build_geometry of one object, then of another on the same grid: the engine keeps
+    an unchanged grid's buffers only while the object is unchanged too, so the second object never
+    reads the first one's signs (at pruning level 1 the unlisted bricks' sign words are not
+    rewritten).  Both meshes, and the first object's again, are the oracle's."""
+    from implisolid_amd import scenes
+    impli.set_pruning(level)
+    try:
+        mc = scenes.mc_settings(56, 1.0)
+        a, b = scenes.union_sphere_cube(), scenes.config3()[0]
+        for sh in (a, b, a, b):
+            _mc_compare(impli, oracle, sh, mc)
+    finally:
+        impli.set_pruning(2)
+
+
 def test_jit_async_first_call_then_compiled(impli, oracle):
     """Async JIT (the default): a never-seen shape is polygonised at once with the interpreter
     kernels while its module compiles in the background; after jit_wait() the same slab's eval runs
@@ -1093,18 +1157,21 @@ def test_config5_stream_against_oracle_summary(impli, n_streams):
                 assert _sha(f) == row["sha256_faces"] and _sha(v) == row["sha256_verts"], (rep, i)
 
 
-@pytest.mark.parametrize("balanced", [True, False])
-def test_config4_eight_slabs_512(impli, balanced):
-    """BASELINE config 4's partition on one GPU: the 512^3 grid of config 4's tree as 8 Z-slabs
-    (balanced cuts from the interval pass, or equal layers), each with its recomputed halo layer
-    and global offsets: the concatenated mesh is the oracle's config4_mc_r512 byte for byte."""
+@pytest.mark.parametrize("R,nslabs,balanced", [(512, 8, True), (512, 8, False), (645, 2, True), (813, 4, True),
+                                                (1024, 8, True)])
+def test_config4_slabs_against_summary(impli, R, nslabs, balanced):
+    """bench.py's N-GPU partitions on one GPU: config 4's grid as N Z-slabs (balanced cuts from the
+    interval pass, or equal layers), each with its recomputed halo layer and global offsets; the
+    concatenated mesh is the oracle's config4_mc_r<R> byte for byte.  512^3 over 8 slabs is the
+    strong-scaling headline (BASELINE config 4); 645^3 / 813^3 / 1024^3 over 2 / 4 / 8 slabs are the
+    weak-scaling runs (R_N = round(512 N^(1/3)))."""
     from implisolid_amd import scenes
     summ, _ = _headline()
-    s = summ["config4_mc_r512"]
-    shape, mc = scenes.config4(512)
+    s = summ["config4_mc_r%d" % R]
+    shape, mc = scenes.config4(R)
     assert shape == s["shape"]
-    cuts = impli.slab_balance(shape, mc, 8) if balanced else None
-    slabs = [impli.Slab(shape, mc, r, 8, cuts=cuts) for r in range(8)]
+    cuts = impli.slab_balance(shape, mc, nslabs) if balanced else None
+    slabs = [impli.Slab(shape, mc, r, nslabs, cuts=cuts) for r in range(nslabs)]
     try:
         counts = []
         for sl in slabs:
