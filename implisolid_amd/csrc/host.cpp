@@ -94,9 +94,12 @@ MCSettings parse_mc_settings(const char* text) {
     std::memcpy(s.box, box, sizeof box);
     {   // :193-206 resolution must be an integer-valued number
         const float r = d.get_float("resolution", -1.f);
-        int ri = (int)r;
+        // a value no int holds (or NaN) is not an integer resolution: converting it would be
+        // undefined behaviour (the reference's cast is; found by the host sanitizer run)
+        const bool fits = r > -2147483648.f && r < 2147483648.f;
+        int ri = fits ? (int)r : 0;
         if (ri == -1) ri = 28;
-        if ((float)ri != r) why += "  err3 (resolution must be integer)";
+        if (!fits || (float)ri != r) why += "  err3 (resolution must be integer)";
         s.resolution = ri;
         if (s.resolution <= 2) why += "  err4 (resolution must be > 2)";
     }
@@ -263,6 +266,7 @@ struct Builder {
     static int extrusion_params(const Json& d, float* out) {
         float fs;
         if (!d.get_float("size", &fs)) throw InputError("extrusion: missing \"size\"");
+        if (!(fs > -2147483648.f && fs < 2147483648.f)) throw InputError("extrusion: Invalid size");   // no int holds it
         const int size = (int)fs;
         if (size < 3) throw InputError("extrusion: Invalid size");
         if (size > 40) throw InputError("extrusion: size above 40 is not supported");
@@ -470,9 +474,13 @@ Program compile_mp5(const char* shape_json, bool ignore_root_matrix) {
     return compile_mp5(d, ignore_root_matrix);
 }
 
+// the largest resolution the settings parser accepts (the reference's dim_t, polygoniser_settings.hpp)
+constexpr int kMaxResolution = 65535;
+
 SlabRange slab_range(int R, int z0, int z1) {
+    if (R < 1 || R > kMaxResolution) throw InputError("slab_range: resolution out of range");
     const int layers = (R + 5) - 3;   // cell layers 1 .. res-3
-    if (R < 1 || z0 < 1 || z1 <= z0 || z1 > layers + 1) throw InputError("slab_range: bad layer range");
+    if (z0 < 1 || z1 <= z0 || z1 > layers + 1) throw InputError("slab_range: bad layer range");
     SlabRange r{z0, z1, z0 > 1 ? 1 : 0};
     // 32-bit indexing of one slab (mc_types.hpp / mc_device.hpp): the cell id L of a slab's cells
     // (halo layer included) is a uint32, and so are vertex ids, face rows and the MC counters.
@@ -484,7 +492,7 @@ SlabRange slab_range(int R, int z0, int z1) {
 }
 
 SlabRange slab_partition(int R, int rank, int nranks) {
-    if (R < 1 || nranks < 1 || rank < 0 || rank >= nranks) throw InputError("slab_partition: bad arguments");
+    if (R < 1 || R > kMaxResolution || nranks < 1 || rank < 0 || rank >= nranks) throw InputError("slab_partition: bad arguments");
     const int layers = (R + 5) - 3;   // cell layers 1 .. res-3
     if (nranks > layers) throw InputError("slab_partition: more slabs than cell layers");
     const int base = layers / nranks, extra = layers % nranks;

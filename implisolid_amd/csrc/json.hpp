@@ -7,6 +7,8 @@
 // get<>(path, default) then returns the default), and a bool read accepts true/false/1/0.
 // This DOM keeps the same model: scalars are text, conversions happen at the accessor.
 #pragma once
+#include <cerrno>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -98,8 +100,10 @@ public:
         std::string t = trim(text);
         if (t.empty()) return false;
         char* end = nullptr;
+        errno = 0;
         long v = std::strtol(t.c_str(), &end, 10);
         if (end != t.c_str() + t.size()) return false;
+        if (errno == ERANGE || v < INT_MIN || v > INT_MAX) return false;   // a stream read into int fails too
         *out = (int)v;
         return true;
     }
@@ -110,9 +114,21 @@ private:
         return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
     }
 
+    // nesting bound: the parser recurses per array / object level, so untrusted input could
+    // otherwise exhaust the stack (the MP5 compiler itself stops at kMaxDepth levels of nodes)
+    static constexpr int kMaxNesting = 256;
+
     struct Parser {
         const char* c;
         const char* e;
+        int nest = 0;
+        struct Level {
+            Parser* p;
+            explicit Level(Parser* q) : p(q) {
+                if (++p->nest > kMaxNesting) p->fail("nested too deeply");
+            }
+            ~Level() { --p->nest; }
+        };
         void ws() { while (c < e && (*c == ' ' || *c == '\t' || *c == '\n' || *c == '\r')) ++c; }
         [[noreturn]] void fail(const char* m) { throw JsonError(std::string("JSON parse error: ") + m); }
         Json value() {
@@ -171,6 +187,7 @@ private:
             return out;
         }
         Json array() {
+            Level lv(this);
             Json j;
             j.kind = Array;
             ++c;
@@ -186,6 +203,7 @@ private:
             return j;
         }
         Json object() {
+            Level lv(this);
             Json j;
             j.kind = Object;
             ++c;

@@ -128,6 +128,7 @@ static float rabbit_at(int idx) {
         default: return 0.f;
     }
 }
+static int trunc_index(float v) { return v == v ? (int)v : 0; }
 static float cube_f(const float p[3]) {
     const int sx = IMPLI_RABBIT_NX, sy = IMPLI_RABBIT_NY, sz = IMPLI_RABBIT_NZ;
     const float gs = bitsf(IMPLI_RABBIT_GRID_SIZE_BITS);
@@ -139,9 +140,13 @@ static float cube_f(const float p[3]) {
     } else if (oy + gs * (float)sy < Y || Y < oy) {
     } else if (oz + gs * (float)sz < Z || Z < oz) {
     } else {
-        int xg = (int)((X - ox) / gs);
-        int yg = (int)((Y - oy) / gs);
-        int zg = (int)((Z - oz) / gs);
+        /* a NaN coordinate passes the bounds test and reaches the conversion, which is undefined
+           behaviour in the reference (cube.hpp:222-224); the value is NaN whatever the index
+           (xd is NaN), so the index is taken as 0, the device conversion's result (found by the
+           sanitizer run, tests/test_sanitize.py) */
+        int xg = trunc_index((X - ox) / gs);
+        int yg = trunc_index((Y - oy) / gs);
+        int zg = trunc_index((Z - oz) / gs);
         float xl = ox + (float)xg * gs;
         float yl = oy + (float)yg * gs;
         float zl = oz + (float)zg * gs;

@@ -31,6 +31,9 @@
  */
 #include "oracle.h"
 
+#include <limits.h>
+
+#define MAX_ALPHA_HALVINGS 200   /* ob02_device.hpp kMaxHalvings */
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -195,9 +198,15 @@ static int make_alpha_list(float initial_step, float min_step, float max_dist, i
     int cap = 64, n = 0;
     float* a = (float*)malloc(sizeof(float) * cap);
     float unit = max_dist, step = initial_step;
-    while (step > min_step) {
+    int halvings = 0;
+    /* the reference loops forever on an infinite average; the library stops after
+       MAX_ALPHA_HALVINGS halvings (any finite average ends within 140) */
+    while (step > min_step && halvings++ < MAX_ALPHA_HALVINGS) {
         step = (float)(step * 0.5);
-        int total = (int)floor((double)(max_dist / fabsf(step)) + 0.001);
+        const double q = floor((double)(max_dist / fabsf(step)) + 0.001);
+        /* (int) of a double as x86's cvttsd2si, the reference build's conversion: out of range or
+           NaN gives INT_MIN (undefined behaviour in C, so spelled out; found by the sanitizer run) */
+        int total = (q >= -2147483648.0 && q < 2147483648.0) ? (int)q : INT_MIN;
         int ms = (max_iter < total) ? max_iter : total;
         for (int i = 1; i < ms + 1; i += 2) {
             float alpha = (float)i * step;
