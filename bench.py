@@ -632,7 +632,63 @@ def main():
             if rank == 0:
                 out_["parity"] = headline_parity("config3s_ob02_r256", *res)
             return out_
-        ob02_sharded = leg("ob02_sharded", run_ob02_sharded)
+        try:
+            ob02_sharded = leg("ob02_sharded", run_ob02_sharded)
+        except Exception as exc:   # reported, never the reason the bench line is lost
+            ob02_sharded = {"error": repr(exc)[:300]}
+
+    # N = 1: the sharded OB02 loop's 8-rank critical path, estimated on this GPU: config 3
+    # on the shifted box at 256^3, its MC mesh owned by the 8 balanced slabs' vertex ranges, every
+    # shard stepped one at a time (distributed.ob02_shards_local, HIP events on the shard's stream)
+    # with the exchanges of distributed.ob02_plan as device copies.  The 8-rank loop time is the sum
+    # over steps of the slowest shard, plus the exchanges priced by a stated model (the all-gather's
+    # bytes over xGMI); the same loop on one shard is the single-GPU figure beside it.
+    ob02_est = None
+    if world == 1 and not args.skip_ob02:
+        def run_ob02_estimate(n=8):
+            from implisolid_amd import distributed as D
+            shape, mc = scenes.config3_shifted(256)
+            cuts = D.balanced_cuts(shape, mc, n)
+            nvs = []
+            for r in range(n):
+                sl = I.Slab(shape, mc, r, n, cuts=cuts)
+                nvs.append(sl.run()[0])
+                sl.close()
+            mc_only = dict(mc, vresampl={"iters": 0, "c": 1.0}, projection={"enabled": 0}, qem={"enabled": 0},
+                           subdiv={"enabled": 0})
+            v_mc, f_mc = I.make_geometry(shape, mc_only)
+            assert sum(nvs) == len(v_mc)
+            V = torch.from_numpy(v_mc.reshape(-1).copy()).to(dev)
+            F = torch.from_numpy(f_mc.reshape(-1).copy()).to(dev)
+            voff = np.concatenate([[0], np.cumsum(nvs)]).astype(np.int64)
+            D.ob02_shards_local(shape, mc, V, F, voff, timing=True)   # warm (point modules, tables)
+            I.jit_wait()
+            v, f, st8 = D.ob02_shards_local(shape, mc, V, F, voff, timing=True)
+            _, _, st1 = D.ob02_shards_local(shape, mc, V, F, [0, len(v_mc)], timing=True)
+            crit = sum(max(x["shard_ms"]) for x in st8["steps"])
+            one = sum(max(x["shard_ms"]) for x in st1["steps"])
+            # exchange model: RCCL all-gather / p2p on one node, 25 us per exchange + the bytes a rank
+            # receives at 50 GB/s (a conservative share of its xGMI links; not measured here)
+            nbytes = st8["exchange_bytes"]
+            per_rank = [b / n for b in nbytes]
+            ex_ms = sum(0.025 + pb / 50e9 * 1e3 for pb in per_rank)
+            return {"workload": "config 3 on the shifted box (scenes.config3_shifted) at 256^3, 3 x [resample, project, "
+                                "QEM], the MC mesh's vertices owned by the 8 balanced Z-slabs",
+                    "shards": n, "owned_verts": nvs, "steps": [x["step"] + ":" + str(x["exchange"]) for x in st8["steps"]],
+                    "loop_compute_ms_8": round(crit, 4), "loop_compute_ms_1": round(one, 4),
+                    "step_max_ms": [max(x["shard_ms"]) for x in st8["steps"]],
+                    "attach_ms_max_8": max(st8["attach_ms"]), "attach_ms_1": st1["attach_ms"][0],
+                    "exchange_bytes_per_rank": [round(b) for b in per_rank],
+                    "exchange_model_ms": round(ex_ms, 4),
+                    "exchange_model": "25 us latency per exchange + received bytes at 50 GB/s per rank (a model, not "
+                                      "measured: one GPU here)",
+                    "estimate_ms_8": round(crit + ex_ms + max(st8["attach_ms"]), 4),
+                    "single_ms": round(one + st1["attach_ms"][0], 4),
+                    "parity": headline_parity("config3s_ob02_r256", v, f)}
+        try:
+            ob02_est = leg("ob02_sharded_estimate", run_ob02_estimate)
+        except Exception as exc:   # an estimate, never the reason the bench line is lost
+            ob02_est = {"error": repr(exc)[:300]}
 
     c5 = None
     if world == 1 and not args.skip_config5:
@@ -970,6 +1026,8 @@ def main():
         out["ob02"] = ob02
     if ob02_sharded:
         out["ob02_sharded"] = ob02_sharded
+    if ob02_est:
+        out["ob02_sharded_estimate"] = ob02_est
     if e2e:
         out["end_to_end"] = dict(e2e, workload="config4 tree, build_geometry (eval + MC) to host-resident verts/faces")
     if first:
