@@ -44,6 +44,8 @@ ABI_SYMBOLS = [
     "implisolid_ob02_create", "implisolid_ob02_destroy", "implisolid_ob02_load", "implisolid_ob02_resample",
     "implisolid_ob02_project", "implisolid_ob02_subdivide", "implisolid_ob02_counts", "implisolid_ob02_ranges",
     "implisolid_ob02_get_verts", "implisolid_ob02_set_verts", "implisolid_ob02_download",
+    "implisolid_ob02_attach", "implisolid_ob02_stream", "implisolid_ob02_resample_async", "implisolid_ob02_project_async",
+    "implisolid_ob02_unpack", "implisolid_ob02_halo",
 ]
 
 # implisolid_progress_callback (include/implisolid.h): verts, n_verts, faces, n_faces,
@@ -104,6 +106,13 @@ def lib():
         "implisolid_ob02_get_verts": ([c_void_p, c_void_p], c_int),
         "implisolid_ob02_set_verts": ([c_void_p, c_void_p], c_int),
         "implisolid_ob02_download": ([c_void_p, fp, ip], c_int),
+        "implisolid_ob02_attach": ([c_void_p, c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int64, c_void_p], c_int),
+        "implisolid_ob02_stream": ([c_void_p], c_void_p),
+        "implisolid_ob02_resample_async": ([c_void_p], c_int),
+        "implisolid_ob02_project_async": ([c_void_p], c_int),
+        "implisolid_ob02_unpack": ([c_void_p, c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), c_int, c_int], c_int),
+        "implisolid_ob02_halo": ([c_void_p, ctypes.POINTER(ctypes.c_int64)], c_int),
         "implisolid_program_info": ([c_char_p, c_int, ip, fp], c_int),
         "implisolid_slab_create": ([c_char_p, c_char_p, c_int, c_int], c_void_p),
         "implisolid_slab_destroy": ([c_void_p], None),
@@ -699,6 +708,35 @@ class Ob02Shard:
         out = (ctypes.c_int64 * 6)()
         self._rc(lib().implisolid_ob02_ranges(self.h, out))
         return tuple(int(x) for x in out)
+
+    # stream-ordered form (implisolid_ob02_attach ...): nothing below blocks the host
+    def attach(self, d_verts, nv, d_faces, nf, v0, v1, after_stream=0):
+        """The caller's device vertex array becomes the working one (updated in place; keep it alive);
+        the handle's stream is ordered after `after_stream` by an event."""
+        self._rc(lib().implisolid_ob02_attach(self.h, ctypes.c_void_p(d_verts), int(nv), ctypes.c_void_p(d_faces), int(nf),
+                                              int(v0), int(v1), ctypes.c_void_p(after_stream)))
+
+    def stream(self):
+        """The handle's HIP stream (an int for torch.cuda.ExternalStream)."""
+        return int(lib().implisolid_ob02_stream(self.h) or 0)
+
+    def resample_async(self):
+        self._rc(lib().implisolid_ob02_resample_async(self.h))
+
+    def project_async(self):
+        self._rc(lib().implisolid_ob02_project_async(self.h))
+
+    def unpack(self, d_rows, row_len, voff, rank):
+        """Copy every rank's row but `rank`'s (all-gathered owned ranges, equal rows of row_len floats)
+        into the vertex array, on the handle's stream."""
+        arr = (ctypes.c_int64 * len(voff))(*[int(x) for x in voff])
+        self._rc(lib().implisolid_ob02_unpack(self.h, ctypes.c_void_p(d_rows), int(row_len), arr, len(voff) - 1, int(rank)))
+
+    def halo(self):
+        """[h0, h1): the vertices the next resampling reads."""
+        out = (ctypes.c_int64 * 2)()
+        self._rc(lib().implisolid_ob02_halo(self.h, out))
+        return int(out[0]), int(out[1])
 
     def get_verts(self, d_dst):
         self._rc(lib().implisolid_ob02_get_verts(self.h, ctypes.c_void_p(d_dst)))

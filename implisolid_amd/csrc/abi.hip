@@ -1147,9 +1147,11 @@ struct implisolid_ob02 {
     std::unique_ptr<Ob02> ob;
     MCSettings st;
     hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;   // implisolid_ob02_attach: orders the stream after the caller's
     ~implisolid_ob02() {
         ob.reset();
         engine.reset();
+        if (ev) (void)hipEventDestroy(ev);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -1199,6 +1201,32 @@ int implisolid_ob02_load(implisolid_ob02* h, const float* d_verts, int64_t nv, c
     })
 }
 
+int implisolid_ob02_attach(implisolid_ob02* h, float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, int64_t v0,
+                           int64_t v1, void* after_stream) {
+    OB02_TRY({
+        if (nv < 0 || nf < 0 || (nv && !d_verts) || (nf && !d_faces)) throw InputError("implisolid_ob02_attach: bad mesh");
+        // stream-ordered after the caller's stream (its copies of the mesh), no device synchronisation
+        if (!h->ev) IMPLI_HIP(hipEventCreateWithFlags(&h->ev, hipEventDisableTiming));
+        IMPLI_HIP(hipEventRecord(h->ev, (hipStream_t)after_stream));
+        IMPLI_HIP(hipStreamWaitEvent(h->stream, h->ev, 0));
+        h->ob->load_mesh(d_verts, nv, d_faces, nf, d_verts);
+        h->ob->set_owned_vertices(v0, v1);
+    })
+}
+
+void* implisolid_ob02_stream(implisolid_ob02* h) { return h ? (void*)h->stream : nullptr; }
+
+int implisolid_ob02_resample_async(implisolid_ob02* h) { OB02_TRY(h->ob->vertex_resampling(h->st.vresampl_c)) }
+
+int implisolid_ob02_project_async(implisolid_ob02* h) { OB02_TRY(h->ob->centroids_projection(h->st.qem != 0)) }
+
+int implisolid_ob02_unpack(implisolid_ob02* h, const float* d_rows, int64_t row_len, const int64_t* voff, int world, int self) {
+    OB02_TRY({
+        if (world < 1 || !voff || (!d_rows && world > 1)) throw InputError("implisolid_ob02_unpack: bad arguments");
+        h->ob->unpack_ranges(d_rows, row_len, std::vector<int64_t>(voff, voff + world + 1), self);
+    })
+}
+
 int implisolid_ob02_resample(implisolid_ob02* h) {
     OB02_TRY({
         h->ob->vertex_resampling(h->st.vresampl_c);
@@ -1227,7 +1255,17 @@ int implisolid_ob02_counts(implisolid_ob02* h, int64_t out[2]) {
 }
 
 int implisolid_ob02_ranges(implisolid_ob02* h, int64_t out[6]) {
-    h->ob->ranges(out);
+    int64_t r[8];
+    h->ob->ranges(r);
+    for (int k = 0; k < 6; ++k) out[k] = r[k];
+    return 0;
+}
+
+int implisolid_ob02_halo(implisolid_ob02* h, int64_t out[2]) {
+    int64_t r[8];
+    h->ob->ranges(r);
+    out[0] = r[6];
+    out[1] = r[7];
     return 0;
 }
 

@@ -25,9 +25,10 @@ void DevBuf::reserve(size_t n) {
     bytes = want;
 }
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    if (p && !ext) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
+    ext = false;
 }
 
 void HostBuf::reserve(size_t n) {
@@ -155,7 +156,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &vid3_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &vidc_, &vid_halo_, &items_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -243,8 +244,9 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     scan_blk_.reserve((size_t)(n_groups(grid_) + 1) * (kScanParts + 1) * sizeof(uint32_t));
     ulist_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint4));
     upart_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint32_t));
-    vid3_.reserve((size_t)grid_.n_cells * 3 * sizeof(uint32_t));
     const int64_t m2 = (int64_t)grid_.m * grid_.m;
+    items_.reserve((size_t)(n_rows(grid_) * n_chunks(grid_) + 1) * sizeof(uint4));
+    if (grid_.cz_emit > grid_.cz0) vid_halo_.reserve((size_t)m2 * 3 * sizeof(uint32_t));   // the halo layer's cells
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
                                (uint32_t)std::min<int64_t>(6 * m2, 1u << 31), 0});
     IMPLI_HIP(hipDeviceSynchronize());
@@ -269,6 +271,7 @@ bool Engine::ensure_capacity(const SlabCounts& c) {
     grow(verts_, cap_v_, (int64_t)c.n_verts() + 1, 3 * sizeof(float));
     grow(faces_, cap_f_, (int64_t)c.n_faces() + 1, 3 * sizeof(int32_t));
     grow(records_, cap_rec_, (int64_t)c.act_total + 1, sizeof(uint4));
+    vidc_.reserve((size_t)cap_rec_ * 3 * sizeof(uint32_t));   // one owned-id triple per record
     return grew;
 }
 
@@ -286,7 +289,9 @@ MCBuffers Engine::buffers() const {
     b.umark = marks_valid_ ? umark_.as<uint32_t>() : nullptr;
     b.mark_id = mark_id_;
     b.counters = counters_.as<uint32_t>();
-    b.vid3 = vid3_.as<uint32_t>();
+    b.vidc = vidc_.as<uint32_t>();
+    b.vid_halo = grid_.cz_emit > grid_.cz0 ? vid_halo_.as<uint32_t>() : nullptr;
+    b.items = items_.as<uint4>();
     b.records = records_.as<uint4>();
     b.verts = verts_.as<float>();
     b.faces = faces_.as<int32_t>();

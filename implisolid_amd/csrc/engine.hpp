@@ -21,8 +21,15 @@ void hip_check(hipError_t e, const char* what);
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool ext = false;   // caller-owned memory (attach): never freed; a reserve past it allocates anew
     void reserve(size_t n);
     void release();
+    void attach(void* q, size_t n) {
+        release();
+        p = q;
+        bytes = n;
+        ext = true;
+    }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -169,7 +176,7 @@ private:
     float key_box_[6] = {};
     HostBuf hcounters_;   // pinned landing zone of read_counts / raw_counters (one small copy)
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, vid3_, records_, verts_, faces_;
+    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, vidc_, vid_halo_, items_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
     hipEvent_t ev_[11] = {};   // 0-8 phase boundaries, 9 after the coarse pass, 10 after refine

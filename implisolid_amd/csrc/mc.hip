@@ -18,10 +18,12 @@
 //   K2b k_unit_scan: per group, its global bases (sum of the groups before it) and its non-empty
 //       units in order in the flat list.
 //   K3 k_mc_cells : per unit, the non-trivial cells in cell order (selected in parallel): owned
-//                   vertex positions (field values read only at crossing edges), the dense
-//                   vid3[cell][slot] table, records {cell, case, face base} of the active cells.
-//   K4 k_mc_faces : per active cell, gathers the vertex ids of its triangle corners from vid3 of
-//                   the owner cells.
+//                   vertex positions (field values read only at crossing edges), records {cell,
+//                   case, face base, row} of the active cells with their owned-id triples beside
+//                   them (record order), and the item table (per row and 64-cell chunk: the mask
+//                   and first record index of its non-trivial cells).
+//   K4 k_mc_faces : per active cell, gathers the vertex ids of its triangle corners from the
+//                   owner cells' triples, found by record index through the item table.
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
@@ -266,32 +268,60 @@ static_assert(kFacesBlocks % 8 == 0, "k_mc_faces' XCD remap needs a multiple of 
 __constant__ uint8_t c_edge_owner_idx[12] = {5, 4, 4, 6, 2, 0, 0, 1, 3, 2, 0, 1};
 __constant__ uint8_t c_edge_slot[12] = {1, 0, 1, 0, 1, 0, 1, 0, 2, 2, 2, 2};
 
-struct __attribute__((packed, aligned(4))) IdTriple { uint32_t a, b, c; };
-
 // K4: one lane per active cell, XCD-aware (the dispatcher puts block b on XCD b % 8, so XCD x takes
 // the x-th eighth of the records in cell order and the owner cells it gathers from stay in its L2).
-// A lane loads the owned-id triples of the owner cells its case uses -- one 12-byte load per owner,
-// at most 7, instead of one load per triangle corner (up to 15) -- spreads them to the 12 edges in
-// LDS, and writes each triangle as one 12-byte store.  (Vector-memory issue, not bytes, bounded the
-// corner-per-load version: 3 % VALU, 53 % of wave time ready but not issued.)
+// A lane needs the owned-id triples of the owner cells its case uses (at most 7).  They are stored
+// densely in record order (vidc), so an owner is found by its record index:
+//   - the cell itself: its own record i;
+//   - the -x neighbour: record i - 1 (the cell just before it in cell order is non-trivial: it owns
+//     a crossing edge);
+//   - the others (rows -1, -m, -m-1): the owner's item (row, 64-cell chunk) holds the record index of
+//     its first non-trivial cell and their mask, so the index is that base plus the popcount of the
+//     mask below the owner's bit;
+//   - an owner in the halo layer (the slab's recomputed layer below its first emitted one) has no
+//     record: its triple is read by cell id from vid_halo.
+// Every address is formed before any load is used (a load under a divergent branch waits alone);
+// an owner the case does not use reads the cell's own triple.  The 12 edges' ids go to LDS, and each
+// triangle is one 12-byte store.
 // one active-cell record i of a slab: its triangles with the vertex ids of their corners
-__device__ __forceinline__ void face_record(const CaseInfo* s_case, uint32_t (*s_w)[256], const uint32_t off[7],
+__device__ __forceinline__ void face_record(const CaseInfo* s_case, uint32_t (*s_w)[256], const GridDesc& g,
                                             const MCBuffers& b, uint32_t Voff, uint32_t i) {
     const int t = threadIdx.x;
-    const uint32_t* __restrict__ vid3 = b.vid3;
     const uint4 r = b.records[i];
-    const uint32_t L = r.x, ci = r.y, fbase = r.z;
+    const uint32_t L = r.x, ci = r.y, fbase = r.z, row = r.w;
     const CaseInfo& C = s_case[ci];
     const int ntri = C.ntri;
     if (fbase + ntri > (uint64_t)b.cap_f) { *b.overflow = 1u; return; }
-    // every owner's triple loaded unconditionally (an owner the case does not use re-reads the
-    // cell's own triple), all before any use; the owners a case uses always exist
     const uint32_t need = C.owners;
-    IdTriple w[7];
+    const uint32_t m = (uint32_t)g.m, nch = (uint32_t)n_chunks(g);
+    const uint32_t xs = L - row * m;   // x - 1 of the cell
+    const bool halo = g.cz_emit > g.cz0 && b.vid_halo;   // rows [0, m) are the halo layer
+    // owners 2..6: (row offset, x offset) = -y, -x-y, -z, -y-z, -x-z
+    const uint32_t drow[5] = {1u, 1u, m, m + 1u, m};
+    const uint32_t dx[5] = {0u, 1u, 0u, 0u, 1u};
+    uint4 it[5];
+    uint32_t ro[5], xo[5];
 #pragma unroll
-    for (int o = 0; o < 7; ++o) {
-        const uint32_t cell = ((need >> o) & 1u) ? L - off[o] : L;
-        w[o] = *reinterpret_cast<const IdTriple*>(vid3 + (size_t)cell * 3);
+    for (int q = 0; q < 5; ++q) {
+        const bool use = (need >> (q + 2)) & 1u;
+        ro[q] = use ? row - drow[q] : row;
+        xo[q] = use ? xs - dx[q] : xs;
+        it[q] = b.items[(size_t)ro[q] * nch + (xo[q] >> 6)];
+    }
+    const IdTriple* vidc = reinterpret_cast<const IdTriple*>(b.vidc);
+    IdTriple w[7];
+    w[0] = vidc[i];
+    w[1] = vidc[((need >> 1) & 1u) ? i - 1u : i];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const bool use = (need >> (q + 2)) & 1u;
+        const uint64_t nt = (uint64_t)it[q].x | ((uint64_t)it[q].y << 32);
+        const uint32_t j = xo[q] & 63u;
+        const uint32_t idx = it[q].z + (uint32_t)__popcll((unsigned long long)(nt & ((1ull << j) - 1ull)));
+        const bool in_halo = use && halo && ro[q] < m;
+        const IdTriple* p = in_halo ? reinterpret_cast<const IdTriple*>(b.vid_halo) + (ro[q] * m + xo[q])
+                                    : vidc + (use && idx < (uint64_t)b.cap_rec ? idx : i);
+        w[q + 2] = *p;
     }
 #pragma unroll
     for (int e = 0; e < 12; ++e) {
@@ -315,9 +345,6 @@ __device__ __forceinline__ void mc_faces_body(const CaseInfo* __restrict__ cases
     const int t = threadIdx.x;
     s_case[t] = cases[t];
     __syncthreads();
-    const int64_t m = g.m;
-    const uint32_t off[7] = {0u, 1u, (uint32_t)m, (uint32_t)(m + 1), (uint32_t)(m * m), (uint32_t)(m * m + m),
-                             (uint32_t)(m * m + 1)};
     const uint32_t n_rec = b.counters[4];
     const uint32_t lim = n_rec < (uint64_t)b.cap_rec ? n_rec : (uint32_t)b.cap_rec;
     uint32_t Voff = b.offsets ? b.offsets[0] : 0u;
@@ -325,7 +352,7 @@ __device__ __forceinline__ void mc_faces_body(const CaseInfo* __restrict__ cases
         for (int r = 0; r < b.rank; ++r) Voff += b.gathered[4 * r] - b.gathered[4 * r + 3];
     const uint32_t nb = gridDim.x, lb = (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u;
     const uint32_t per = (lim + nb - 1u) / nb, i_end = min(lim, (lb + 1u) * per);
-    for (uint32_t i = lb * per + t; i < i_end; i += 256) face_record(s_case, s_w, off, b, Voff, i);
+    for (uint32_t i = lb * per + t; i < i_end; i += 256) face_record(s_case, s_w, g, b, Voff, i);
 }
 
 __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
@@ -363,15 +390,12 @@ __global__ __launch_bounds__(256) void k_mc_faces_b(const CaseInfo* __restrict__
     const int t = threadIdx.x;
     s_case[t] = cases[t];
     const uint32_t total = batch_prefix(objs, n, 4, 1u, 0xffffffffu, s_pre);   // counters[4]: active cells
-    const int64_t m = g.m;
-    const uint32_t off[7] = {0u, 1u, (uint32_t)m, (uint32_t)(m + 1), (uint32_t)(m * m), (uint32_t)(m * m + m),
-                             (uint32_t)(m * m + 1)};
     for (uint32_t gi = blockIdx.x * 256 + t; gi < total; gi += gridDim.x * 256) {
         const int k = batch_object_of(s_pre, n, gi);
         const MCBuffers& b = objs[k].mc;
         const uint32_t i = gi - s_pre[k];
         if (i >= (uint64_t)b.cap_rec) { *b.overflow = 1u; continue; }
-        face_record(s_case, s_w, off, b, b.offsets ? b.offsets[0] : 0u, i);
+        face_record(s_case, s_w, g, b, b.offsets ? b.offsets[0] : 0u, i);
     }
 }
 

@@ -16,6 +16,9 @@ __device__ __forceinline__ T wave_incl_scan(T x, int lane) {
     return x;
 }
 
+// three owned-edge vertex ids, one 12-byte access
+struct __attribute__((packed, aligned(4))) IdTriple { uint32_t a, b, c; };
+
 // 64 consecutive cells of one cell row, as sign bits.  For cell j (x = 64 c + 1 + j) the corners
 // are stored samples x-1 and x of the rows (y, z), (y+1, z), (y, z+1), (y+1, z+1): bit j of s.. and
 // t.. (t = s shifted by one sample).  nt marks the non-trivial cells (corner signs not all equal).
@@ -108,7 +111,7 @@ __device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
 // K3: one wave per unit.  Lanes find the non-trivial cells of their (row, chunk) items; the cells
 // are then taken in cell order, 64 at a time: a wave scan of (owned edges, triangles, active)
 // gives every cell its vertex / face / record base; owned vertices are
-// placed from the owner cell's fx/fy/fz (the reference's first emission), their ids go to vid3
+// placed from the owner cell's fx/fy/fz (the reference's first emission), their ids go beside the records (vidc)
 // (halo cells, below the slab's first emitted layer: ids only), active cells get a record
 // {L, ci, face base}.  (A separate one-lane-per-active-cell position pass measured 2 us slower.)
 // a window's (owned edges <= 3, triangles <= 5, active <= 1) per cell, packed for one 32-bit scan:
@@ -170,14 +173,25 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
             const int i = i0 + lane;
             ChunkBits k;
             k.nt = 0;
+            k.z = 0;
+            const int64_t irow = u * kUnitRows + i / nch;
+            const int ic = i % nch;
             if (i < items) {
-                const int64_t row = u * kUnitRows + i / nch;
-                const int c = i % nch;
-                if (row < rows && (c >= kChunkMaskBits || ((cmask >> c) & 1u))) load_chunk(g, b.signs, row, c, k);
+                if (irow < rows && (ic >= kChunkMaskBits || ((cmask >> ic) & 1u))) load_chunk(g, b.signs, irow, ic, k);
             }
             const uint32_t cnt = (uint32_t)__popcll((unsigned long long)k.nt);
             const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);
             const uint32_t total = __shfl(incl, 63, 64);
+            // the item table (faces find an owner cell's record through it): an emitted item's
+            // non-trivial cells and the record index of its first one (every emitted non-trivial cell
+            // is active); written once, by the unit's first part
+            {
+                const bool emit_item = k.nt != 0 && k.z >= g.cz_emit;
+                const uint32_t acnt = emit_item ? cnt : 0u;
+                const uint32_t aincl = wave_incl_scan<uint32_t>(acnt, lane);
+                if (part == 0 && emit_item)
+                    b.items[(size_t)irow * nch + ic] = make_uint4((uint32_t)k.nt, (uint32_t)(k.nt >> 32), arun0 + aincl - acnt, 0u);
+            }
             __builtin_amdgcn_wave_barrier();   // the previous batch's LDS reads are done
             bits[0][lane] = k.s00; bits[1][lane] = k.t00; bits[2][lane] = k.s10; bits[3][lane] = k.t10;
             bits[4][lane] = k.s01; bits[5][lane] = k.t01; bits[6][lane] = k.s11; bits[7][lane] = k.t11;
@@ -234,6 +248,10 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
                     const float f5 = (sx1 || sy0 || sz1) ? kSealed : r5;
                     const float f6 = (sx0 || sy1 || sz1) ? kSealed : r6;
                     const float f3 = (sx1 || sy1 || sz0) ? kSealed : r3;
+                    // the cell's owned ids (slot order 5, 6, 10; an unused slot's word is never read)
+                    uint32_t ids[3];
+#pragma unroll
+                    for (int slot = 0; slot < 3; ++slot) ids[slot] = vrun + (uint32_t)((cw >> (5 + 3 * slot)) & 7u) - 1u - H;
                     if (has && own) {
                         const float fx = ((float)x + g.i0[0]) * g.w[0];
                         const float fy = ((float)y + g.i0[1]) * g.w[1];
@@ -242,10 +260,8 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
 #pragma unroll
                         for (int slot = 0; slot < 3; ++slot) {
                             const int r = (int)((cw >> (5 + 3 * slot)) & 7u) - 1;
-                            if (r < 0) continue;
-                            const uint32_t out = vrun + (uint32_t)r - H;
-                            b.vid3[(size_t)L * 3 + slot] = out;
-                            if (!emit) continue;
+                            if (r < 0 || !emit) continue;
+                            const uint32_t out = ids[slot];
                             if (out >= (uint64_t)b.cap_v) { *b.overflow = 1u; continue; }
                             float px, py, pz;
                             if (slot == 0) { const float mu = (0.f - f5) / (f7 - f5); px = fx2; py = fy + mu * g.w[1]; pz = fz2; }
@@ -253,12 +269,19 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
                             else { const float mu = (0.f - f3) / (f7 - f3); px = fx2; py = fy2; pz = fz + mu * g.w[2]; }
                             b.verts[3 * (size_t)out] = px; b.verts[3 * (size_t)out + 1] = py; b.verts[3 * (size_t)out + 2] = pz;
                         }
+                        // a halo cell's ids (the layer below the slab's first emitted one), by cell id
+                        if (!emit && b.vid_halo)
+                            *reinterpret_cast<IdTriple*>(b.vid_halo + (size_t)L * 3) = IdTriple{ids[0], ids[1], ids[2]};
                     }
-                }
-                if (mine && act) {
-                    const uint32_t arun = arun0 + fld(pre, 2);
-                    if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), 0u);
-                    else *b.overflow = 1u;
+                    if (act) {   // an active cell: its record and its ids, at its record index
+                        const uint32_t arun = arun0 + fld(pre, 2);
+                        if (arun < (uint64_t)b.cap_rec) {
+                            b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), (uint32_t)erow);
+                            *reinterpret_cast<IdTriple*>(b.vidc + (size_t)arun * 3) = IdTriple{ids[0], ids[1], ids[2]};
+                        } else {
+                            *b.overflow = 1u;
+                        }
+                    }
                 }
                 vrun0 += fld(tot, 0);
                 frun0 += fld(tot, 1);

@@ -43,8 +43,13 @@ struct MCBuffers {
     uint32_t mark_id;        // brick hold mark_id (k_brick_fill); null: every chunk is counted (dense eval)
     uint32_t* counters;      // [0] unit parts, [1] halo own (read by the vertex pass), [2..5] totals
                              // own/tri/act/halo (copied as one block; [5] == [1]), [6] non-empty units
-    uint32_t* vid3;          // 3 * n_cells: slab-local vertex ids (vid - H, mod 2^32); faces add Voff
-    uint4* records;          // active cells: {L, ci, fbase, 0}
+    uint32_t* vidc;          // 3 * cap_rec: per active cell (record order) the slab-local ids (vid - H, mod
+                             // 2^32) of its owned edges 5, 6, 10 (unused slots undefined); faces add Voff
+    uint32_t* vid_halo;      // 3 * m^2: the same per cell of the halo layer (cell id L < m^2), written
+                             // only where the cell owns a vertex (null: the slab has no halo layer)
+    uint4* items;            // [row][chunk]: {non-trivial cell mask lo, hi, record index of the item's first
+                             // non-trivial cell, 0}, written for the emitted items holding non-trivial cells
+    uint4* records;          // active cells: {L, ci, fbase, cell row}
     float* verts;            // 3 * cap_v
     int32_t* faces;          // 3 * cap_f
     int64_t cap_v, cap_f, cap_rec;

@@ -536,6 +536,22 @@ __global__ void k_touch_range(const int32_t* __restrict__ f, int64_t nf, int64_t
         atomicMax(&out[1], (unsigned long long)j);
     }
 }
+// the lowest and highest vertex of faces [j0, j1) (out[0], out[1])
+__global__ void k_face_vertex_range(const int32_t* __restrict__ f, int64_t j0, int64_t j1, unsigned long long* __restrict__ out) {
+    const int64_t j = j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= j1) return;
+    unsigned long long lo = ~0ull, hi = 0ull;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int32_t v = f[3 * j + q];
+        if (v >= 0) {
+            lo = (unsigned long long)v < lo ? (unsigned long long)v : lo;
+            hi = (unsigned long long)v > hi ? (unsigned long long)v : hi;
+        }
+    }
+    atomicMin(&out[0], lo);
+    atomicMax(&out[1], hi);
+}
 // ... and the min / max over those faces' edge neighbours (the faces the weights read)
 __global__ void k_fof_range(const int32_t* __restrict__ fof, int64_t j0, int64_t j1, unsigned long long* __restrict__ out) {
     const int64_t j = j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1363,9 +1379,16 @@ Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
     misc_.reserve(512);
 }
 
-void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_) {
+void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_, float* d_work) {
     nv = nv_;
     nf = nf_;
+    if (d_work) {   // the caller's vertex array is the working one (sharded loop): no copy
+        verts_.attach(d_work, (size_t)(nv + 1) * 12);
+        d_verts = d_work;
+    } else if (verts_.ext) {
+        verts_.release();   // a previous attach: own buffer again
+    }
+    if (vnew_.ext) vnew_.release();   // (a subdivision's swap left a caller's array here)
     // the snapshots' device buffers are kept for the next build's stores (a hipFree per set per
     // build cost 80-380 us of device-wide synchronisation)
     for (auto& kv : snaps_) kv.second.valid = false;
@@ -1377,18 +1400,19 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     avg_valid_ = true;
     for (double& t : stage_ms_) t = 0.0;
     Stage st(this, kStageTopology);
-    verts_.reserve((size_t)(nv + 1) * 12);
-    vnew_.reserve((size_t)(nv + 1) * 12);
+    if (!verts_.ext) verts_.reserve((size_t)(nv + 1) * 12);
     faces_.reserve((size_t)(nf + 1) * 12);
     deg_.reserve((size_t)(nv + 1) * 4);
     // the mesh copied, the degree counters and misc ((unused), cap hits, evaluations) zeroed
     const int64_t nmax = std::max<int64_t>(std::max<int64_t>(3 * nv, 3 * nf), nv + 1);
-    k_load_mesh<<<blocks_for(std::max<int64_t>(nmax, 16)), 256, 0, s>>>(verts_.as<float>(), d_verts, 3 * nv, faces_.as<int32_t>(),
+    k_load_mesh<<<blocks_for(std::max<int64_t>(nmax, 16)), 256, 0, s>>>(verts_.as<float>(), d_verts,
+                                                                       verts_.as<float>() == d_verts ? 0 : 3 * nv, faces_.as<int32_t>(),
                                                                        d_faces, 3 * nf, deg_.as<uint32_t>(), nv + 1,
                                                                        misc_.as<uint32_t>());
     start_perturbations();   // host thread, overlaps the topology and resampling kernels
     build_topology(true);
     own_v0_ = 0; own_v1_ = nv; wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
+    hv0_ = 0; hv1_ = nv;
     sharded_ = false;
 }
 
@@ -1400,6 +1424,7 @@ void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
     sharded_ = !(v0 == 0 && v1 == nv);
     if (!sharded_) {
         wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
+        hv0_ = 0; hv1_ = nv;
         return;
     }
     DevBuf& r = scan_tmp_;   // scratch: 4 x u64 (only topology uses it, before this)
@@ -1412,6 +1437,8 @@ void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
     IMPLI_HIP(hipStreamSynchronize(s));
     if (h[0] > h[1]) {   // no face touches the owned vertices
         wf0_ = wf1_ = cf0_ = cf1_ = 0;
+        hv0_ = v0;
+        hv1_ = v1;
         return;
     }
     wf0_ = (int64_t)h[0];
@@ -1422,11 +1449,50 @@ void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
     IMPLI_HIP(hipStreamSynchronize(s));
     cf0_ = (int64_t)h[2];
     cf1_ = (int64_t)h[3] + 1;
+    // the vertices the next resampling reads: those of the centroid faces (its one-ring halo)
+    IMPLI_HIP(hipMemcpyAsync(r.p, init, sizeof init, hipMemcpyHostToDevice, s));
+    k_face_vertex_range<<<blocks_for(cf1_ - cf0_), 256, 0, s>>>(faces_.as<int32_t>(), cf0_, cf1_, r.as<unsigned long long>());
+    IMPLI_HIP(hipMemcpyAsync(h, r.p, sizeof h, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    hv0_ = std::min<int64_t>((int64_t)h[0], v0);
+    hv1_ = std::max<int64_t>((int64_t)h[1] + 1, v1);
     IMPLI_HIP(hipGetLastError());
 }
 
-void Ob02::ranges(int64_t out[6]) const {
+// every rank's owned range, all-gathered into equal padded rows (row r: rank r's 3 (v1 - v0)
+// floats), unpacked into this rank's vertex array except its own range (one kernel on the stream)
+__global__ void k_unpack_ranges(float* __restrict__ v, const float* __restrict__ rows, int64_t row_len,
+                                const int64_t* __restrict__ voff, int world, int self) {
+    const int r = blockIdx.y;
+    if (r == self) return;
+    const int64_t n = 3 * (voff[r + 1] - voff[r]);
+    float* dst = v + 3 * voff[r];
+    const float* src = rows + (int64_t)r * row_len;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+void Ob02::unpack_ranges(const float* d_rows, int64_t row_len, const std::vector<int64_t>& voff, int self) {
+    const int world = (int)voff.size() - 1;
+    if (world < 1 || voff.back() != nv || self < 0 || self >= world) throw InputError("ob02: bad owned ranges");
+    int64_t longest = 0;
+    for (int r = 0; r < world; ++r) {
+        if (voff[r + 1] < voff[r] || 3 * (voff[r + 1] - voff[r]) > row_len) throw InputError("ob02: bad owned ranges");
+        longest = std::max<int64_t>(longest, voff[r + 1] - voff[r]);
+    }
+    voff_dev_.reserve(voff.size() * sizeof(int64_t));
+    // pinned staging, so the upload is stream-ordered without a host synchronisation
+    voff_host_.reserve(voff.size() * sizeof(int64_t));
+    std::memcpy(voff_host_.p, voff.data(), voff.size() * sizeof(int64_t));
+    IMPLI_HIP(hipMemcpyAsync(voff_dev_.p, voff_host_.p, voff.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    const unsigned bx = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (3 * longest + 255) / 256), 1024);
+    k_unpack_ranges<<<dim3(bx, (unsigned)world), 256, 0, s>>>(verts_.as<float>(), d_rows, row_len, voff_dev_.as<int64_t>(),
+                                                               world, self);
+    IMPLI_HIP(hipGetLastError());
+}
+
+void Ob02::ranges(int64_t out[8]) const {
     out[0] = own_v0_; out[1] = own_v1_; out[2] = wf0_; out[3] = wf1_; out[4] = cf0_; out[5] = cf1_;
+    out[6] = hv0_; out[7] = hv1_;
 }
 
 EdgeTab Ob02::edge_table() {
@@ -1542,11 +1608,13 @@ void Ob02::vertex_resampling(float c) {
     if (wf1_ > wf0_)
         k_face_weights<<<blocks_for(wf1_ - wf0_), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(), wf0_,
                                                                 wf1_, c, w_.as<float>());
+    // in place: the new positions are weighted sums of the centroids alone (vertex_resampling.hpp
+    // :93-141), which were computed above, so nothing reads the old positions any more and the
+    // vertex buffer stays the same (a sharded caller's exchange writes into it directly)
     if (own_v1_ > own_v0_)
         k_resample<<<blocks_for(own_v1_ - own_v0_), 256, 0, s>>>(uoff_.as<uint32_t>() + own_v0_, ulst_.as<int32_t>(),
                                                                   w_.as<float>(), cen_.as<float>(), own_v1_ - own_v0_,
-                                                                  vnew_.as<float>() + 3 * own_v0_);
-    std::swap(verts_, vnew_);
+                                                                  verts_.as<float>() + 3 * own_v0_);
     IMPLI_HIP(hipGetLastError());
     store_pointset("post_resampling_vertices", verts_.as<float>(), nv, true);   // :207-211
 }
@@ -1889,6 +1957,7 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
         IMPLI_HIP(hipGetLastError());
         std::swap(verts_, vnew_);
         std::swap(faces_, fnew_);
+        if (vnew_.ext) vnew_.release();   // never reuse a caller's attached array as scratch
         nv = nvt;
         nf = 4 * nf;
         topo_valid_ = false;
@@ -1896,6 +1965,7 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
         // the new vertices and faces are covered by later steps: the ranges become the whole mesh
         // (a sharded caller sets its owned vertices of the subdivided mesh again)
         own_v0_ = 0; own_v1_ = nv; wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
+        hv0_ = 0; hv1_ = nv;
         sharded_ = false;
     }
     add_rand_noise(amplitude);

@@ -21,7 +21,10 @@ public:
     Ob02& operator=(const Ob02&) = delete;
     // takes a copy of the MC mesh (device pointers) and builds the face/vertex topology; resets
     // the point sets and counters, so one Ob02 serves many builds (its buffers are grow-only)
-    void load_mesh(const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf);
+    // d_work (optional): the caller's vertex array (3 nv floats, kept alive by the caller until the
+    // next load) becomes the working one in place -- the steps update it and a sharded caller's
+    // exchange writes into it directly; d_verts is then ignored
+    void load_mesh(const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, float* d_work = nullptr);
     // Z-slab sharding of the loop (one Ob02 per rank, each holding the whole mesh): this rank owns
     // vertices [v0, v1) (its slab's).  Resampling and QEM then update only those; the per-face
     // passes run over the faces touching them (the work faces, a contiguous range: faces are in
@@ -31,8 +34,15 @@ public:
     // that moves vertices the caller exchanges the owned ranges (set_verts) before the next step.
     // Call after load_mesh; v0 = 0, v1 = nv restores the whole mesh.
     void set_owned_vertices(int64_t v0, int64_t v1);
-    // [v0, v1, work faces f0, f1, centroid faces f0, f1]
-    void ranges(int64_t out[6]) const;
+    // [v0, v1, work faces f0, f1, centroid faces f0, f1, halo vertices h0, h1]: [h0, h1) are the
+    // vertices the next resampling reads (those of the centroid faces), so after a step only they
+    // must be current before another resampling (the edge-length fold reads every vertex)
+    void ranges(int64_t out[8]) const;
+    // the exchange after a vertex-moving step: rows holds every rank's owned range (row r: rank r's
+    // 3 (voff[r+1] - voff[r]) floats at r row_len), copied into the vertex array except row `self`,
+    // on the stream (no host synchronisation)
+    void unpack_ranges(const float* d_rows, int64_t row_len, const std::vector<int64_t>& voff, int self);
+    hipStream_t stream() const { return s; }
     // device pointer of the current vertices (3 nv floats; valid until the next step)
     float* d_verts() { return verts_.as<float>(); }
     // step 1: apply_vertex_resampling_to_MC_buffers__VMS (apply_v_s_to_mc_buffers.hpp:280-326)
@@ -95,6 +105,9 @@ private:
     int64_t own_v0_ = 0, own_v1_ = 0;   // owned vertices
     int64_t wf0_ = 0, wf1_ = 0;         // work faces: touching an owned vertex
     int64_t cf0_ = 0, cf1_ = 0;         // faces whose centroid / normal the weights of the work faces read
+    int64_t hv0_ = 0, hv1_ = 0;         // vertices of those faces (the next resampling's input)
+    DevBuf voff_dev_;                   // unpack_ranges: the ranks' vertex offsets
+    HostBuf voff_host_;
     bool sharded_ = false;
     int64_t rand_hi_rows_ = 0;
     float avg_edge_ = 0.f;

@@ -155,52 +155,207 @@ def _allgather_segments(local, offs, world, group=None):
     return torch.cat([out[r, :n[r]] for r in range(world)])
 
 
-def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_step=None):
-    """The OB02 loop (grand_algorithm's order, mcc2.cpp:309-444 / polygonizer_algorithm_ob02.hpp:74-157:
-    overall_repeats x [vresampl.iters x resampling; projection (+ QEM)]; subdivision on the last
-    repeat) over Z-slab shards: every rank holds the whole mesh and owns its slab's vertices
-    [voff[rank], voff[rank + 1]); after each step that moves vertices the owned ranges are
-    all-gathered (12 B per vertex), so every rank starts the next step from the same mesh.
-    Subdivision runs once on rank 0 after the loop (it reads every face).  Returns rank 0's final
-    (verts, faces) numpy arrays, None elsewhere; byte-identical to the single-device loop."""
+def ob02_plan(st):
+    """The OB02 loop's steps in grand_algorithm's order (mcc2.cpp:309-444, polygonizer_algorithm_ob02.hpp
+    :74-157): overall_repeats x [vresampl.iters x resampling ("R"); projection ("P", + QEM)], and the
+    exchange each vertex-moving step needs before the next step that reads vertices:
+      - before a resampling, only its halo (the vertices of the faces whose centroids its weights
+        read, Ob02Shard.halo()): "halo";
+      - before a projection (the edge-length fold reads every vertex) or at the end: "full".
+    A projection without QEM moves no vertex (exchange None).  Returns [(step, exchange), ...]."""
+    steps = []
+    for _ in range(st["overall_repeats"]):
+        steps += ["R"] * st["vresampl_iters"]
+        if st["projection"]:
+            steps.append("P")
+    out = []
+    for k, step in enumerate(steps):
+        moves = step == "R" or st["qem"]
+        nxt = next((x for x in steps[k + 1:] if x == "R" or x == "P"), None)
+        out.append((step, None if not moves else "halo" if nxt == "R" else "full"))
+    # a step that moves nothing leaves the previous exchange's coverage; the step after a "halo"
+    # exchange is always a resampling, which reads only the halo
+    return out
+
+
+def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_step=None, halo=True):
+    """The OB02 loop (ob02_plan) over Z-slab shards: every rank holds the whole mesh and owns its
+    slab's vertices [voff[rank], voff[rank + 1]).  Stream-ordered: the loop runs on the shard's HIP
+    stream (Ob02Shard.attach / resample_async / project_async) with no host synchronisation per
+    step, on a copy of V that is the shard's working vertex array in place.  After a vertex-moving
+    step the owned ranges are exchanged into that array on the same stream:
+      - "full": every rank's owned range padded to one equal row, one all-gather (RCCL), unpacked by
+        one kernel (Ob02Shard.unpack);
+      - "halo" (halo=True, before a resampling): point-to-point sends of the owned vertices each
+        neighbour's next resampling reads (its one-ring halo), batched (RCCL group).
+    Subdivision runs once on rank 0 after the loop (it reads every face).  gloo (the CPU-side
+    rehearsal) stages the same exchanges through host copies.  Returns rank 0's final (verts,
+    faces) numpy arrays, None elsewhere; byte-identical to the single-device loop."""
+    import numpy as np
+    import implisolid_amd as I
+    st = I.parse_settings(mc_settings)
+    device = V.device
+    cuda = device.type == "cuda"
+    gloo = dist.get_backend(group) == "gloo"
+    nv, nf = V.numel() // 3, F.numel() // 3
+    voff = [int(x) for x in voff]
+    v0, v1 = voff[rank], voff[rank + 1]
+    W = V.clone()   # the working array (updated in place)
+    ob = I.Ob02Shard(shape, mc_settings)
+    try:
+        cur = torch.cuda.current_stream(device) if cuda else None
+        ob.attach(W.data_ptr(), nv, F.data_ptr(), nf, v0, v1, cur.cuda_stream if cur is not None else 0)
+        s_ob = torch.cuda.ExternalStream(ob.stream(), device=device) if cuda else None
+        # every rank's halo (host, once)
+        h = torch.tensor(list(ob.halo()), dtype=torch.int64, device=device if not gloo else "cpu")
+        hs = [torch.zeros_like(h) for _ in range(world)]
+        dist.all_gather(hs, h, group=group)
+        H = [(int(x[0]), int(x[1])) for x in hs]
+        m = 3 * max(1, max(voff[r + 1] - voff[r] for r in range(world)))
+
+        def full_exchange():
+            if gloo:
+                s_ob.synchronize()
+                own = torch.zeros(m, dtype=torch.float32)
+                own[:3 * (v1 - v0)] = W[3 * v0:3 * v1].cpu()
+                parts = [torch.empty(m, dtype=torch.float32) for _ in range(world)]
+                dist.all_gather(parts, own, group=group)
+                rows = torch.stack(parts).to(device)
+                torch.cuda.current_stream(device).synchronize()
+                ob.unpack(rows.data_ptr(), m, voff, rank)
+                s_ob.synchronize()
+                return
+            with torch.cuda.stream(s_ob):
+                own = torch.zeros(m, dtype=torch.float32, device=device)
+                own[:3 * (v1 - v0)].copy_(W[3 * v0:3 * v1])
+                rows = torch.empty(world, m, dtype=torch.float32, device=device)
+                dist.all_gather_into_tensor(rows, own, group=group)
+                ob.unpack(rows.data_ptr(), m, voff, rank)
+
+        def halo_exchange():
+            sends, recvs = [], []
+            for q in range(world):
+                if q == rank:
+                    continue
+                a, b = max(v0, H[q][0]), min(v1, H[q][1])          # my owned vertices q reads
+                if a < b:
+                    sends.append((q, a, b))
+                a, b = max(voff[q], H[rank][0]), min(voff[q + 1], H[rank][1])   # q's that I read
+                if a < b:
+                    recvs.append((q, a, b))
+            if gloo:
+                s_ob.synchronize()
+                host = W.cpu()
+                ops = [dist.P2POp(dist.isend, host[3 * a:3 * b].clone(), q, group=group) for q, a, b in sends]
+                got = [(a, b, torch.empty(3 * (b - a), dtype=torch.float32)) for q, a, b in recvs]
+                ops += [dist.P2POp(dist.irecv, t, q, group=group) for (q, _, _), (_, _, t) in zip(recvs, got)]
+                for r in (dist.batch_isend_irecv(ops) if ops else []):
+                    r.wait()
+                for a, b, t in got:
+                    W[3 * a:3 * b].copy_(t.to(device))
+                torch.cuda.current_stream(device).synchronize()
+                return
+            ops = [dist.P2POp(dist.isend, W[3 * a:3 * b], q, group=group) for q, a, b in sends]
+            ops += [dist.P2POp(dist.irecv, W[3 * a:3 * b], q, group=group) for q, a, b in recvs]
+            if not ops:
+                return
+            with torch.cuda.stream(s_ob):
+                for r in dist.batch_isend_irecv(ops):
+                    r.wait()
+
+        plan = ob02_plan(st)
+        reps = st["overall_repeats"]
+        per_rep = len(plan) // reps if reps else 0
+        for k, (step, ex) in enumerate(plan):
+            if step == "R":
+                ob.resample_async()
+            else:
+                ob.project_async()
+            if ex == "full" or (ex == "halo" and not halo):
+                full_exchange()
+            elif ex == "halo":
+                halo_exchange()
+            if on_step and per_rep:
+                on_step({"R": "resample", "P": "project"}[step], k // per_rep)
+        if st["subdiv"] and st["overall_repeats"] >= 1 and rank == 0:   # polygonize_step_3, last repeat: noise x 10
+            ob.subdivide(float(st["post_subdiv_noise"]) * 10.0)
+        if rank == 0:
+            return ob.download()
+        if cuda:
+            s_ob.synchronize()
+        return None
+    finally:
+        ob.close()
+
+
+def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
+    """The sharded loop of ob02_sharded with every shard in this process, on one GPU (tests and the
+    bench's 8-rank estimate): shard r owns [voff[r], voff[r + 1]) and steps on its own HIP stream;
+    the exchanges of ob02_plan are device copies between the shards' arrays (full: every owned range
+    to every shard; halo: each shard's halo from its owners).  timing=True: every shard's step is
+    timed with HIP events on its stream, run one shard at a time (so the shards do not share the
+    GPU), giving each step's slowest shard.  Returns (shard 0's final verts, faces, stats)."""
+    import numpy as np
     import implisolid_amd as I
     st = I.parse_settings(mc_settings)
     device = V.device
     nv, nf = V.numel() // 3, F.numel() // 3
-    v0, v1 = int(voff[rank]), int(voff[rank + 1])
-    ob = I.Ob02Shard(shape, mc_settings)
+    voff = [int(x) for x in voff]
+    n = len(voff) - 1
+    Ws = [V.clone() for _ in range(n)]
+    obs = [I.Ob02Shard(shape, mc_settings) for _ in range(n)]
+    stats = {"steps": [], "exchange_bytes": []}
     try:
-        if device.type == "cuda":
+        import time
+        cur = torch.cuda.current_stream(device)
+        torch.cuda.synchronize(device)
+        attach_ms = []
+        for r, ob in enumerate(obs):   # one at a time: each shard's load + topology + ranges
+            t0 = time.perf_counter()
+            ob.attach(Ws[r].data_ptr(), nv, F.data_ptr(), nf, voff[r], voff[r + 1], cur.cuda_stream)
+            torch.cuda.ExternalStream(ob.stream(), device=device).synchronize()
+            attach_ms.append((time.perf_counter() - t0) * 1e3)
+        stats["attach_ms"] = [round(t, 4) for t in attach_ms]
+        streams = [torch.cuda.ExternalStream(ob.stream(), device=device) for ob in obs]
+        H = [ob.halo() for ob in obs]
+        stats["halo"] = H
+
+        def exchange(kind):
+            for s in streams:
+                s.synchronize()
+            moved = 0
+            for r in range(n):
+                for q in range(n):
+                    if q == r:
+                        continue
+                    a, b = voff[q], voff[q + 1]
+                    if kind == "halo":
+                        a, b = max(a, H[r][0]), min(b, H[r][1])
+                    if a < b:
+                        Ws[r][3 * a:3 * b].copy_(Ws[q][3 * a:3 * b])
+                        moved += 12 * (b - a)
             torch.cuda.synchronize(device)
-        ob.load(V.data_ptr(), nv, F.data_ptr(), nf, v0, v1)
-        buf = torch.empty(nv * 3, dtype=torch.float32, device=device)
+            return moved
 
-        def exchange():
-            ob.get_verts(buf.data_ptr())
-            own = buf[3 * v0:3 * v1]
-            src = own if dist.get_backend(group) != "gloo" else own.cpu()
-            full = _allgather_segments(src, voff * 3, world, group).to(device)
-            buf.copy_(full)
-            if device.type == "cuda":
-                torch.cuda.synchronize(device)
-            ob.set_verts(buf.data_ptr())
-
-        reps = st["overall_repeats"]
-        for rep in range(reps):
-            for _ in range(st["vresampl_iters"]):
-                ob.resample()
-                exchange()
-            if on_step:
-                on_step("resample", rep)
-            if st["projection"]:
-                ob.project()
-                if st["qem"]:
-                    exchange()
-                if on_step:
-                    on_step("project", rep)
-            if st["subdiv"] and (reps <= 1 or rep == reps - 1):
-                if rank == 0:   # polygonize_step_3: noise on the last repeat, scaled by 10
-                    ob.subdivide(float(st["post_subdiv_noise"]) * 10.0 if rep == reps - 1 else 0.0)
-        return ob.download() if rank == 0 else None
+        for step, ex in ob02_plan(st):
+            times = []
+            for r, ob in enumerate(obs):
+                if timing:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(streams[r])
+                ob.resample_async() if step == "R" else ob.project_async()
+                if timing:
+                    e1.record(streams[r])
+                    e1.synchronize()
+                    times.append(e0.elapsed_time(e1))
+            if ex:
+                stats["exchange_bytes"].append(exchange("full" if ex == "full" or not halo else "halo"))
+            stats["steps"].append({"step": step, "exchange": ex if (halo or ex is None) else "full",
+                                   "shard_ms": [round(t, 4) for t in times]})
+        if st["subdiv"] and st["overall_repeats"] >= 1:
+            obs[0].subdivide(float(st["post_subdiv_noise"]) * 10.0)
+        v, f = obs[0].download()
+        return v, f, stats
     finally:
-        ob.close()
+        for ob in obs:
+            ob.close()

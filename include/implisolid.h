@@ -292,6 +292,27 @@ int implisolid_ob02_ranges(implisolid_ob02* h, int64_t out[6]);
 int implisolid_ob02_get_verts(implisolid_ob02* h, float* d_dst);
 int implisolid_ob02_set_verts(implisolid_ob02* h, const float* d_src);
 int implisolid_ob02_download(implisolid_ob02* h, float* verts, int32_t* faces);
+/* Stream-ordered form of the same loop (distributed.ob02_sharded): no host synchronisation per step.
+ *   attach: like load, ordered after `after_stream` by an event (no device synchronisation), and
+ *     d_verts (3 nv floats, the caller's, kept alive until destroy or the next attach/load) becomes
+ *     the working vertex array itself: the steps update it in place and the caller's exchange
+ *     writes the other ranks' ranges into it.  Two small read-backs size the shard's ranges.
+ *   stream: the handle's HIP stream; the caller enqueues its collectives on it (and orders its
+ *     own streams after it).
+ *   resample_async / project_async: the steps, enqueued on that stream.
+ *   unpack: after an all-gather of every rank's owned range into equal rows (row r = rank r's
+ *     3 (voff[r+1] - voff[r]) floats at d_rows + r row_len; voff: host int64[world + 1]), one kernel
+ *     on the stream copies every row but `self` into the vertex array.
+ *   halo: [h0, h1), the vertices the next resampling reads (those of the faces whose centroids its
+ *     weights use): between a QEM and a resampling only they must be exchanged; the edge-length
+ *     fold of a projection reads every vertex. */
+int implisolid_ob02_attach(implisolid_ob02* h, float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, int64_t v0,
+                           int64_t v1, void* after_stream);
+void* implisolid_ob02_stream(implisolid_ob02* h);
+int implisolid_ob02_resample_async(implisolid_ob02* h);
+int implisolid_ob02_project_async(implisolid_ob02* h);
+int implisolid_ob02_unpack(implisolid_ob02* h, const float* d_rows, int64_t row_len, const int64_t* voff, int world, int self);
+int implisolid_ob02_halo(implisolid_ob02* h, int64_t out[2]);
 
 #ifdef __cplusplus
 }

@@ -1379,6 +1379,48 @@ def test_ob02_shards_in_one_process(impli, oracle):
         assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), nshard
 
 
+@pytest.mark.parametrize("nshard,halo,scene", [(3, True, "config2_48"), (5, True, "config2_48"), (8, True, "config2_48"),
+                                               (5, False, "config2_48"), (8, True, "config3s_64"), (4, True, "subdiv_40")])
+def test_ob02_stream_ordered_shards(impli, oracle, nshard, halo, scene):
+    """The stream-ordered sharded loop (distributed.ob02_shards_local: every shard attached to its own
+    copy of the mesh, stepped on its own stream without host synchronisation, the exchanges of
+    ob02_plan -- the one-ring halo before a resampling, every owned range before a projection and
+    at the end -- as device copies) is build_geometry's mesh and the oracle's, byte for byte, at 3 to
+    8 shards, with and without the halo-only exchanges, with subdivision after the loop."""
+    import torch
+    from implisolid_amd import distributed as D
+    from implisolid_amd import scenes
+    if scene == "config2_48":
+        shape, mc = scenes.config2(48)
+    elif scene == "config3s_64":
+        shape, mc = scenes.config3_shifted(64)
+    else:
+        shape, mc = scenes.config2(40)
+        mc = dict(mc, subdiv={"enabled": 1})
+    v_mc, f_mc = impli.make_geometry(shape, dict(mc, vresampl={"iters": 0, "c": 1.0}, projection={"enabled": 0},
+                                                 qem={"enabled": 0}, subdiv={"enabled": 0}))
+    impli.srand(4711)   # subdivision noise: glibc rand() from the same state on both sides
+    oracle.srand(4711)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    nv = len(v_mc)
+    voff = np.linspace(0, nv, nshard + 1).astype(np.int64)
+    V = torch.from_numpy(v_mc.reshape(-1).copy()).cuda()
+    F = torch.from_numpy(f_mc.reshape(-1).copy()).cuda()
+    plan = D.ob02_plan(impli.parse_settings(mc))
+    assert plan and plan[-1][1] in ("full", None)
+    v, f, stats = D.ob02_shards_local(shape, mc, V, F, voff, halo=halo)
+    assert np.array_equal(f, fr)
+    fin = np.isfinite(vr).all(1)
+    assert np.array_equal(np.isfinite(v).all(1), fin)
+    if _has_twist(shape):   # the twist's gradient goes through the double cos (GRAD_TOL, DESIGN.md section 4)
+        assert np.abs(v[fin] - vr[fin]).max(initial=0.0) < 1e-5
+    else:
+        assert np.array_equal(v[fin].view(np.uint32), vr[fin].view(np.uint32)), (nshard, halo, scene)
+    if halo and any(ex == "halo" for _, ex in plan):
+        full = 12 * nv * (nshard - 1) / nshard * nshard   # bytes a full exchange moves
+        assert min(stats["exchange_bytes"]) < full / 4    # the halo exchanges move a fraction
+
+
 @pytest.mark.parametrize("world,balanced", [(2, True), (3, False)])
 def test_multiprocess_slabs_gloo(impli, oracle, tmp_path, world, balanced):
     """`world` fresh processes (torch.distributed.run, all on this box's GPU, gloo backend) run the
