@@ -12,6 +12,7 @@ the median duration of every kernel over its direct and replayed steps is printe
 (the slab's kernel critical path: the kernels run back to back on one stream).
 """
 import csv
+import re
 import statistics
 import sys
 
@@ -21,10 +22,13 @@ SHORT = {"impli_coarse_modes": "coarse", "k_coarse_modes": "coarse", "impli_bric
 ORDER = ["coarse", "refine", "fill", "eval", "count", "scan", "cells", "faces"]
 
 
+SHORT["k_eval_field_pruned"] = "eval"
+_PAT = re.compile(r"\b(" + "|".join(sorted(SHORT, key=len, reverse=True)) + r")\b")
+
+
 def short(name):
-    base = name.split("(")[0].split("<")[0].strip()
-    base = base.split("::")[-1]
-    return SHORT.get(base)
+    m = _PAT.search(name)
+    return SHORT[m.group(1)] if m else None
 
 
 def main():
