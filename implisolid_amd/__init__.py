@@ -171,7 +171,14 @@ def lib():
         "implisolid_last_build_stats": ([ctypes.POINTER(ctypes.c_double)], c_int),
     }
     for name, (args, res) in sig.items():
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:
+            # an older experimental build (IMPLISOLID_LIB, same-box A/B runs) lacks the newest entry
+            # points: only its callers fail; the in-tree library exports every one (test_cpu)
+            if os.environ.get("IMPLISOLID_LIB"):
+                continue
+            raise
         f.argtypes = args
         f.restype = res
     L.implisolid_set_error_mode(1)   # Python callers get exceptions instead of abort()

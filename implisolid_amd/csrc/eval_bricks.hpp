@@ -139,31 +139,51 @@ __device__ __forceinline__ uint32_t claim_neighbours(const GridDesc& g, const Br
 #pragma unroll
     for (int r = 0; r < kBY; ++r) col0 |= 1ull << (r * kBX);
     const uint64_t colL = col0 << (kBX - 1), rowL = row0 << (kBX * (kBY - 1));
-    uint32_t claimed = 0;
+    // the six neighbours' fill bytes, loaded together (a neighbour outside the grid reads the
+    // brick's own byte, which is never a candidate: it is listed); one memory round trip instead of
+    // one per direction
+    int an[6];
+    uint32_t fa[6];
 #pragma unroll
     for (int d = 0; d < 6; ++d) {
         const int ax = d >> 1, up = d & 1;
         const int c = ax == 0 ? bx : ax == 1 ? by : bz;
         const int lim = ax == 0 ? bg.nbx : ax == 1 ? bg.nby : bg.nbz;
-        if (up ? c + 1 >= lim : c == 0) continue;
         const int step = ax == 0 ? 1 : ax == 1 ? bg.nbx : bg.nbx * bg.nby;
-        const int a = up ? b + step : b - step;
-        const uint32_t fa = cc.fill[a];
-        if (!(fa & kBrickCandidate)) continue;
+        const bool in = up ? c + 1 < lim : c > 0;
+        an[d] = in ? (up ? b + step : b - step) : b;
+        fa[d] = cc.fill[an[d]];
+    }
+    // the directions to claim: a candidate neighbour with a differing sample on the shared face
+    uint32_t want = 0;
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const int ax = d >> 1, up = d & 1;
         uint64_t f0, f1;
         if (ax == 0) f0 = f1 = up ? colL : col0;
         else if (ax == 1) f0 = f1 = up ? rowL : row0;
         else { f0 = up ? 0ull : ~0ull; f1 = up ? ~0ull : 0ull; }
         f0 &= valid;
         f1 = has1 ? (f1 & valid) : 0ull;
-        const bool aneg = (fa & 3u) == kBrickNeg;
+        const bool aneg = (fa[d] & 3u) == kBrickNeg;
         const uint64_t differ = aneg ? ((~neg[0] & f0) | (~neg[1] & f1)) : ((neg[0] & f0) | (neg[1] & f1));
-        if (!differ) continue;
-        uint32_t old = 0;
-        const int sh = 8 * (a & 3);
-        if ((threadIdx.x & 63) == 0) old = atomicOr(reinterpret_cast<uint32_t*>(cc.fill + (a & ~3)), (uint32_t)kBrickClaimed << sh);
-        old = __builtin_amdgcn_readfirstlane(old);
-        if (!((old >> sh) & kBrickClaimed)) claimed |= 1u << d;
+        if ((fa[d] & kBrickCandidate) && an[d] != b && differ) want |= 1u << d;
+    }
+    want = __builtin_amdgcn_readfirstlane(want);
+    if (!want) return 0u;
+    // the claims' atomics issued together by lane 0, their results read after (first claimer wins)
+    uint32_t old[6];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        old[d] = 0u;
+        if (((want >> d) & 1u) && (threadIdx.x & 63) == 0)
+            old[d] = atomicOr(reinterpret_cast<uint32_t*>(cc.fill + (an[d] & ~3)), (uint32_t)kBrickClaimed << (8 * (an[d] & 3)));
+    }
+    uint32_t claimed = 0;
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        const uint32_t o = __builtin_amdgcn_readfirstlane(old[d]);
+        if (((want >> d) & 1u) && !((o >> (8 * (an[d] & 3))) & kBrickClaimed)) claimed |= 1u << d;
     }
     return claimed;
 }

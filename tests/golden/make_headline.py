@@ -25,6 +25,9 @@ cos).  OB02 meshes with more than 21 845 faces are past the reference's short ed
 (DESIGN.md §5): the oracle, like the GPU, follows the intended semantics there.
 
     python tests/golden/make_headline.py        # adds missing entries; --all recomputes every one
+
+headline_ob02_verts.npz holds the full vertex arrays of the two OB02 meshes of the twist tree
+(config3_ob02_r256, config3s_ob02_r256) for the every-row tolerance check.
 """
 import hashlib
 import json
@@ -105,6 +108,19 @@ def main():
         out[name] = s
         arrays[name + "_idx"], arrays[name + "_v"] = idx, vs
         print(name, s["n_verts"], s["n_faces"], "non-finite", len(s["nonfinite_rows"]), "%.1f s" % s["oracle_s"])
+    # the full vertex arrays of the OB02 meshes of trees with a twist (their vertices are compared to
+    # 1e-5, the twist's gradient going through the double cos): every row, not only the samples
+    path_v = os.path.join(HERE, "headline_ob02_verts.npz")
+    full = dict(np.load(path_v)) if (not redo and os.path.exists(path_v)) else {}
+    for name in ("config3_ob02_r256", "config3s_ob02_r256"):
+        if name in full:
+            continue
+        shape, mc = out[name]["shape"], out[name]["mc"]
+        v, f = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+        assert sha(f) == out[name]["sha256_faces"]
+        full[name] = v
+        print(name, "full vertex array", v.shape)
+    np.savez_compressed(path_v, **full)
     if "config5_mc_r128" not in out:
         out["config5_mc_r128"] = config5_summary()
         print("config5_mc_r128", sum(o["n_faces"] for o in out["config5_mc_r128"]["objects"]), "faces",

@@ -621,3 +621,21 @@ def test_divconst_identity_exhaustive(tmp_path):
                     "-o", exe, "-lm"], check=True)
     r = subprocess.run([exe, str(min(8, os.cpu_count() or 1))], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout + r.stderr
+
+
+def test_ob02_exchange_plan(impli):
+    """distributed.ob02_plan (the sharded OB02 loop's exchanges): after a vertex-moving step, the
+    one-ring halo when the next step is a resampling (it reads only the vertices of the faces whose
+    centroids its weights use), every owned range when the next is a projection (the edge-length
+    fold reads every edge) and at the end (rank 0 returns the whole mesh); a projection without
+    QEM moves nothing."""
+    from implisolid_amd import distributed as D
+    from implisolid_amd import scenes
+    st = impli.parse_settings(scenes.config2(64)[1])   # 3 x [1 resampling, projection + QEM]
+    assert D.ob02_plan(st) == [("R", "full"), ("P", "halo"), ("R", "full"), ("P", "halo"), ("R", "full"), ("P", "full")]
+    two = impli.parse_settings(scenes.mc_settings(32, 1.0, vresampl_iters=2, vresampl_c=0.4, projection=1, qem=0,
+                                                  overall_repeats=2))
+    assert D.ob02_plan(two) == [("R", "halo"), ("R", "full"), ("P", None), ("R", "halo"), ("R", "full"), ("P", None)]
+    proj_only = impli.parse_settings(scenes.mc_settings(32, 1.0, projection=1, qem=1, overall_repeats=2))
+    assert D.ob02_plan(proj_only) == [("P", "full"), ("P", "full")]
+    assert D.ob02_plan(impli.parse_settings(scenes.mc_settings(32, 1.0))) == []

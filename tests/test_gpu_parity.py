@@ -1092,8 +1092,9 @@ def test_headline_against_oracle_summary(impli, name):
     """The exact meshes bench.py times (config 4's tree at 512^3 and 256^3, eval + MC) and the OB02
     legs it reports (config 3 at 256^3, config 2 at 128^3, 3 repeats of resample + project + QEM),
     against the oracle's summaries: faces byte-identical (SHA-256); vertices bit-identical where the
-    tree has no twist, else every sampled row within the north star's 1e-5 and the finite-vertex
-    sum within 1e-5 per vertex; the reference's non-finite rows at the same rows."""
+    tree has no twist, else every vertex row within the north star's 1e-5 (the oracle's full arrays,
+    headline_ob02_verts.npz) and the finite-vertex sum within 1e-5 per vertex; the reference's
+    non-finite rows at the same rows."""
     import hashlib
     summ, samples = _headline()
     s = summ[name]
@@ -1107,6 +1108,13 @@ def test_headline_against_oracle_summary(impli, name):
         assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"]
     ok = np.isfinite(vs).all(1)
     assert np.abs(v[idx][ok].astype(np.float64) - vs[ok]).max(initial=0.0) < 1e-5
+    full = np.load(_golden("headline_ob02_verts.npz"))
+    if name in full.files:   # the twist tree's OB02 meshes: every row, not only the samples
+        vr = full[name]
+        assert np.array_equal(np.isfinite(vr).all(1), fin)
+        d = np.abs(v[fin].astype(np.float64) - vr[fin])
+        assert d.max(initial=0.0) < 1e-5, d.max()
+        assert (d == 0).all(1).mean() > 0.999   # bit-identical but where the device cos rounds apart
     tot = v[fin].astype(np.float64).sum(0)
     assert np.abs(tot - np.array(s["finite_sum"])).max() < 1e-5 * max(1, fin.sum())
 
