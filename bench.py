@@ -298,8 +298,8 @@ def main():
             cuts = D.balanced_cuts(shape, mc, world)
             t_cut = time.perf_counter() - t0
         slab = I.Slab(shape, mc, rank, world, cuts=cuts)
-        cnt = torch.zeros(4, dtype=torch.int32, device=dev)
         gath = torch.zeros(world, 4, dtype=torch.int32, device=dev)
+        totals = D.counts_tensor(slab, dev) if backend == "nccl" else None
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
 
         def step(e=None):
@@ -309,13 +309,18 @@ def main():
             slab.count(sp)
             if e: e[2].record(stream)
             if world > 1:
-                # the 16 B/rank count all-gather runs while the vertex pass (slab-local ids) does;
+                # the vertex pass (slab-local ids), then the 16 B/rank count all-gather on the same
+                # stream, straight from the engine's counters (D.gather_counts_inline: an async
+                # gather on RCCL's own stream cost 16 us more per step in cross-stream events);
                 # the face pass forms this slab's vertex offset from the gathered counts
-                slab.copy_counts(cnt.data_ptr(), sp)
-                work = D.gather_counts_async(cnt, gath)
                 slab.emit_verts(sp)
-                if work is not None:
-                    work.wait()
+                if totals is not None:
+                    D.gather_counts_inline(totals, gath)
+                else:   # gloo rehearsal: host round trip of a copy
+                    cnt = torch.zeros(4, dtype=torch.int32, device=dev)
+                    slab.copy_counts(cnt.data_ptr(), sp)
+                    torch.cuda.synchronize(dev)
+                    D.gather_counts_inline(cnt, gath)
                 slab.emit_faces(0, gath.data_ptr(), rank, sp)
             else:
                 slab.emit(0, sp)

@@ -36,6 +36,29 @@ def gather_counts_async(local_counts, out, group=None):
     return dist.all_gather_into_tensor(out, local_counts, group=group, async_op=True)
 
 
+def counts_tensor(slab, device):
+    """The slab's totals block (its counter words [2, 6): own incl. halo, faces, active cells,
+    halo own -- the copy_counts layout) as an int32[4] tensor over the engine's own memory, no copy
+    (``__cuda_array_interface__``).  Valid while the slab lives; every count() rewrites it."""
+    class _Totals:
+        __cuda_array_interface__ = {"shape": (4,), "typestr": "<i4", "data": (slab.counters_ptr() + 8, False),
+                                    "version": 3, "strides": None}
+    return torch.as_tensor(_Totals(), device=device)
+
+
+def gather_counts_inline(totals, out, group=None):
+    """All-gather the per-rank counts into `out` (int32[world, 4]) on the caller's current stream
+    (a blocking-style collective: RCCL enqueues it on the launch stream; the host does not wait).
+    Measured on one MI355X (world 1, 1/8 of config 4 at 512^3, tools/step_host_probe.py): the
+    async form on the process group's own stream with copy_counts cost 21.6 us per step over the
+    kernels (cross-stream events), this one 5.3 us (profiles/r04d_step_host_probe.json)."""
+    if dist.get_backend(group) == "gloo":   # gloo: host tensors round trip (tests on the CPU)
+        parts = list(out.unbind(0))
+        dist.all_gather(parts, totals, group=group)
+        return
+    dist.all_gather_into_tensor(out.view(-1), totals, group=group)
+
+
 def offsets_from_counts(gathered, rank, out=None):
     """Exclusive prefix over ranks: int32 [vertex offset, face offset] for `rank` (on device)."""
     v = gathered[:, 0] - gathered[:, 3]

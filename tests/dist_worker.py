@@ -5,7 +5,7 @@ Launched by ``python -m torch.distributed.run --nproc-per-node N ... tests/dist_
 several ranks share the one GPU of a test box -- and torch.distributed over
 IMPLISOLID_DIST_BACKEND (gloo for the rehearsal, nccl = RCCL on a multi-GPU node).  Each rank runs
 bench.py's multi-GPU step on its Z-slab of config 3's tree (balanced cuts from one interval pass,
-eval, count, the count all-gather in flight while the vertex pass runs, the face pass with the
+eval, count, the vertex pass, the count all-gather on the launch stream, the face pass with the
 gathered counts), then the mesh is gathered to rank 0, which writes it to OUT (.npz).
 
 With the flag "ob02" the scene is config 2 (sphere u rabbit, MC + 3 x [resample, project, QEM]): the
@@ -46,17 +46,20 @@ def main():
     sp = torch.cuda.current_stream(dev).cuda_stream
     cnt = torch.zeros(4, dtype=torch.int32, device=dev)
     gath = torch.zeros(world, 4, dtype=torch.int32, device=dev)
+    totals = D.counts_tensor(slab, dev) if backend == "nccl" else None
     for _ in range(2):   # the second pass runs with outputs sized by the first
         slab.eval(sp)
         slab.count(sp)
         slab.counts(sp)
-        slab.copy_counts(cnt.data_ptr(), sp)
-        torch.cuda.current_stream(dev).synchronize()
-        work = D.gather_counts_async(cnt, gath)
+        # bench.py's step: the vertex pass, then the counts' all-gather on the launch stream (RCCL:
+        # straight from the engine's counters; gloo: a copy, host-synchronised), then the face pass
         slab.emit_verts(sp)
-        if work is not None:
-            work.wait()
-        torch.cuda.current_stream(dev).synchronize()
+        if totals is not None:
+            D.gather_counts_inline(totals, gath)
+        else:
+            slab.copy_counts(cnt.data_ptr(), sp)
+            torch.cuda.current_stream(dev).synchronize()
+            D.gather_counts_inline(cnt, gath)
         slab.emit_faces(0, gath.data_ptr(), rank, sp)
         nv, nf, of = slab.counts(sp)
     assert not of

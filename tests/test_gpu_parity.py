@@ -1313,7 +1313,8 @@ def test_multiprocess_ob02_sharded_gloo(impli, oracle, tmp_path, world, balanced
 @pytest.mark.parametrize("mode", ["slabs", "ob02"])
 def test_rccl_world1_pipeline(impli, oracle, tmp_path, mode):
     """The multi-GPU step over RCCL itself (backend "nccl"), on the one GPU a test box has: world 1
-    under torch.distributed.run -- the counts' all_gather_into_tensor in flight during the vertex pass,
+    under torch.distributed.run -- the counts' all_gather_into_tensor on the launch stream straight
+    from the engine's counters (distributed.counts_tensor / gather_counts_inline),
     the mesh gather to rank 0, and for OB02 the slab meshes' and the owned vertices' padded
     all-gathers -- gives the oracle's mesh byte for byte.  (Point-to-point sends need a second GPU.)"""
     import os
@@ -1432,8 +1433,8 @@ def test_ob02_stream_ordered_shards(impli, oracle, nshard, halo, scene):
 @pytest.mark.parametrize("world,balanced", [(2, True), (3, False)])
 def test_multiprocess_slabs_gloo(impli, oracle, tmp_path, world, balanced):
     """`world` fresh processes (torch.distributed.run, all on this box's GPU, gloo backend) run the
-    bench's multi-GPU step -- balanced or equal Z-slabs, eval, count, the count all-gather overlapped
-    with the vertex pass, the face pass with the gathered counts -- and gather the mesh to rank 0
+    bench's multi-GPU step -- balanced or equal Z-slabs, eval, count, the vertex pass, the count
+    all-gather, the face pass with the gathered counts -- and gather the mesh to rank 0
     (distributed.gather_mesh): byte-identical to the oracle."""
     import os
     import socket
