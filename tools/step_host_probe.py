@@ -121,6 +121,35 @@ def main():
                 torch.cuda.synchronize(dev)
                 row[name] = None
                 row[name + "_error"] = str(exc)[:300]
+        # the bench's N > 1 form: two graphs (eval + count + vertex pass; face pass) with the
+        # all-gather launched between their replays on the same stream
+        try:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream(dev)
+            cs.wait_stream(stream)
+            with torch.cuda.stream(cs):
+                g1.capture_begin()
+                s.eval(cs.cuda_stream); s.count(cs.cuda_stream); s.emit_verts(cs.cuda_stream)
+                g1.capture_end()
+                g2.capture_begin()
+                s.emit_faces(0, gath.data_ptr(), rank, cs.cuda_stream)
+                g2.capture_end()
+            stream.wait_stream(cs)
+
+            def two():
+                g1.replay()
+                dist.all_gather_into_tensor(gath[0:1].view(-1), tot)
+                g2.replay()
+            row["step_two_graphs_ms"] = round(timed(two), 4)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                two()
+            row["step_two_graphs_host_enqueue_ms"] = round((time.perf_counter() - t0) / steps * 1e3, 4)
+            torch.cuda.synchronize(dev)
+            del g1, g2
+        except Exception as exc:
+            torch.cuda.synchronize(dev)
+            row["step_two_graphs_error"] = str(exc)[:300]
         s.close()
         out["ranks"][rank] = row
         print(json.dumps({rank: row}), file=sys.stderr, flush=True)
