@@ -286,6 +286,7 @@ MCBuffers Engine::buffers() const {
     b.scan_blk = scan_blk_.as<uint32_t>();
     b.ulist = ulist_.as<uint4>();
     b.upart = upart_.as<uint32_t>();
+    b.cap_parts = (uint32_t)(n_units(grid_) * kMaxParts + 1);   // ulist_ / upart_ entries
     b.umark = marks_valid_ ? umark_.as<uint32_t>() : nullptr;
     b.mark_id = mark_id_;
     b.counters = counters_.as<uint32_t>();

@@ -177,20 +177,23 @@ __device__ __forceinline__ void mc_count_body(const GridDesc& g, const MCBuffers
         const uint32_t ea = wave_incl_scan<uint32_t>(act, t) - act;
         const uint64_t m = __ballot(ne);
         const uint32_t pos = (uint32_t)__popcll((unsigned long long)(m & ((1ull << t) - 1ull)));
-        // parts: a unit's active cells split into runs of kPartCells for separate waves
+        // parts: a unit's active cells split into runs of kPartCells for separate waves; heavy
+        // units' parts (mc_types.hpp kHeavyCells) and light units' parts counted apart
         const uint32_t parts = ne ? min((uint32_t)kMaxParts, max(1u, (act + kPartCells - 1) / kPartCells)) : 0u;
-        const uint32_t ep = wave_incl_scan<uint32_t>(parts, t) - parts;
+        const bool heavy = act > kHeavyCells;
+        const uint32_t ph = heavy ? parts : 0u, pl = heavy ? 0u : parts;
+        const uint32_t eph = wave_incl_scan<uint32_t>(ph, t) - ph, epl = wave_incl_scan<uint32_t>(pl, t) - pl;
         if (ne) {
             b.unit_cnt[G * kGroupUnits + pos] = make_uint4((uint32_t)t, eo, et, ea);
-            b.unit_part[G * kGroupUnits + pos] = ep | (parts << 16);
+            b.unit_part[G * kGroupUnits + pos] = (heavy ? eph : epl) | (parts << 16) | ((uint32_t)heavy << 20);
             b.unit_cmask[G * kGroupUnits + pos] = s_cm[t];
         }
         const uint32_t sums[kScanParts + 1] = {__shfl(eo + own, 63, 64), __shfl(et + tri, 63, 64),
-                                               __shfl(ea + act, 63, 64), wave_sum(hal), __shfl(ep + parts, 63, 64),
-                                               (uint32_t)__popcll((unsigned long long)m)};
+                                               __shfl(ea + act, 63, 64), wave_sum(hal), __shfl(eph + ph, 63, 64),
+                                               __shfl(epl + pl, 63, 64), (uint32_t)__popcll((unsigned long long)m)};
         if (t <= kScanParts) {
             const uint32_t v = t == 0 ? sums[0] : t == 1 ? sums[1] : t == 2 ? sums[2] : t == 3 ? sums[3]
-                             : t == 4 ? sums[4] : sums[5];
+                             : t == 4 ? sums[4] : t == 5 ? sums[5] : sums[6];
             b.scan_blk[(int64_t)t * gridDim.x + G] = v;
         }
     }
@@ -211,12 +214,12 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
     const int64_t G = blockIdx.x, ng = n_groups(g);
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const bool last = G == ng - 1;
-    const uint32_t nne = b.scan_blk[5 * ng + G];   // non-empty units of the group
+    const uint32_t nne = b.scan_blk[kScanParts * ng + G];   // non-empty units of the group
     if (nne == 0 && !last) return;   // uniform
     const uint4 e = b.unit_cnt[G * kGroupUnits + (t < (int)nne ? t : 0)];
     const uint32_t pp = b.unit_part[G * kGroupUnits + (t < (int)nne ? t : 0)];
     const uint32_t cm = b.unit_cmask[G * kGroupUnits + (t < (int)nne ? t : 0)];
-    uint32_t acc[kScanRows] = {0u, 0u, 0u, 0u, 0u, 0u};
+    uint32_t acc[kScanRows] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll 4
     for (int64_t i = t; i < G; i += kScanBlock)
 #pragma unroll
@@ -236,21 +239,27 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
     __syncthreads();
     if (t < (int)nne) {
         const uint4 ent = make_uint4((uint32_t)(G * kGroupUnits) + e.x, s_base[0] + e.y, s_base[1] + e.z, s_base[2] + e.w);
-        const uint32_t P = pp >> 16, at = s_base[4] + (pp & 0xffffu);
+        const uint32_t P = (pp >> 16) & 15u;
+        const bool heavy = (pp >> 20) & 1u;
+        // heavy parts from the list's front, light parts from its end backwards
+        const uint32_t r = (heavy ? s_base[4] : s_base[5]) + (pp & 0xffffu);
         for (uint32_t q = 0; q < P; ++q) {
-            b.ulist[at + q] = ent;
-            b.upart[at + q] = q | (P << 4) | (cm << 8);
+            const uint32_t at = heavy ? r + q : b.cap_parts - 1u - (r + q);
+            b.ulist[at] = ent;
+            b.upart[at] = q | (P << 4) | (cm << 8);
         }
     }
     if (last && t == 0) {
-        b.counters[0] = s_base[4] + b.scan_blk[4 * ng + G];       // unit parts
+        const uint32_t nh = s_base[4] + b.scan_blk[4 * ng + G];
+        b.counters[7] = nh;                                       // heavy parts (the list's front)
+        b.counters[0] = nh + s_base[5] + b.scan_blk[5 * ng + G];  // unit parts
         b.counters[1] = s_base[3] + b.scan_blk[3 * ng + G];       // halo-owned vertices (ids below the slab's first)
         b.counters[2] = s_base[0] + b.scan_blk[G];                // owned vertices incl. halo
         b.counters[3] = s_base[1] + b.scan_blk[ng + G];           // triangles
         b.counters[4] = s_base[2] + b.scan_blk[2 * ng + G];       // active cells (face records)
         b.counters[5] = s_base[3] + b.scan_blk[3 * ng + G];       // = [1]: [2, 6) is the totals block
                                                                   // copy_counts / read_counts take whole
-        b.counters[6] = s_base[5] + nne;                          // non-empty units (statistics)
+        b.counters[6] = s_base[6] + nne;                          // non-empty units (statistics)
     }
 }
 __global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) { unit_scan_body(g, b); }

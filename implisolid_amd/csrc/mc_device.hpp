@@ -160,6 +160,9 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
     const int64_t rows = n_rows(g);
     const int items = kUnitRows * nch;
     {
+        // the e-th part: heavy parts from the list's front, then the light ones from its end
+        const uint32_t nh = b.counters[7];
+        e = e < nh ? e : b.cap_parts - 1u - (e - nh);
         const uint4 ent = b.ulist[e];   // {unit, vbase, fbase, abase}
         // part | parts << 4 | chunk mask << 8: this wave emits windows w % parts == part; the unit's
         // chunks without a non-trivial cell (k_mc_count) are not loaded

@@ -23,7 +23,12 @@ constexpr int kUnitRows = 4;
 constexpr int kGroupUnits = 64;        // units per group: one count block; the group scan's element
 constexpr int kVertsWaves = 4;         // waves per verts block (grid-stride over the unit list)
 constexpr int kVertsMaxBlocks = 4096;  // cells grid cap (2048: +1 us at 512^3)
-constexpr int kScanParts = 5;          // group sums scanned: own, tri, act, halo own, unit parts
+constexpr int kScanParts = 6;          // group sums scanned: own, tri, act, halo own, heavy / light unit parts
+// A unit with more than kHeavyCells active cells takes several 64-cell windows, so its parts live
+// 2-3x longer than a one-window part: the flat list holds them first (from the front) and the
+// light ones after them (placed from the list's end backwards), so the longest parts start in
+// the vertex pass's first wave generation instead of trailing it.
+constexpr uint32_t kHeavyCells = 64;
 // A non-empty unit with many active cells is handed to several waves ("parts"): part p of P takes
 // the unit's 64-cell windows w with w % P == p (the other windows only advance its bases).
 constexpr int kPartCells = 128;        // active cells per part
@@ -39,10 +44,12 @@ struct MCBuffers {
                              // then the group's non-empty unit count (not scanned)
     uint4* ulist;            // all parts of the non-empty units in order: {unit, vbase, fbase, abase}
     uint32_t* upart;         // ... part index | part count << 4 | the unit's chunk mask << 8 (k_unit_scan)
+    uint32_t cap_parts;      // ulist / upart entries: heavy parts at [0, H), light at [cap - L, cap)
     const uint32_t* umark;   // [unit][chunk]: the 64-cell chunks of a unit whose cells touch an evaluated
     uint32_t mark_id;        // brick hold mark_id (k_brick_fill); null: every chunk is counted (dense eval)
     uint32_t* counters;      // [0] unit parts, [1] halo own (read by the vertex pass), [2..5] totals
-                             // own/tri/act/halo (copied as one block; [5] == [1]), [6] non-empty units
+                             // own/tri/act/halo (copied as one block; [5] == [1]), [6] non-empty units,
+                             // [7] heavy unit parts (the flat list's front)
     uint32_t* vidc;          // 3 * cap_rec: per active cell (record order) the slab-local ids (vid - H, mod
                              // 2^32) of its owned edges 5, 6, 10 (unused slots undefined); faces add Voff
     uint32_t* vid_halo;      // 3 * m^2: the same per cell of the halo layer (cell id L < m^2), written
