@@ -955,8 +955,11 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
 struct implisolid_batch {
     std::vector<std::unique_ptr<Engine>> engines;
     bool merged = false;                 // one launch per stage for all objects (ObjArgs rows)
-    DevBuf objs;                         // merged: ObjArgs[n] on the device
+    DevBuf objs;                         // merged: ObjArgs[n] on the device, shallow objects first
     int depth = 0;
+    // merged: objects of tree depth <= kBatchShallowDepth (rows [0, n_shallow)) run the interval and
+    // eval passes with 9-slot node stacks (three waves per SIMD), the rest with 12 or 16
+    int n_shallow = 0, depth_shallow = 0, depth_deep = 0;
     std::vector<hipGraphExec_t> execs;   // empty when capture is unavailable (direct launches)
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> events;      // fork (0) and one join event per stream
@@ -1016,10 +1019,16 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         }
         if (b->merged) {   // the objects' device state, one row each; every object has the same grid
             std::vector<ObjArgs> rows;
-            for (auto& e : b->engines) {
-                rows.push_back(e->obj_args());
-                b->depth = std::max(b->depth, e->depth());
-            }
+            for (int pass = 0; pass < 2; ++pass)   // shallow objects first (launch_batch_eval's classes)
+                for (auto& e : b->engines) {
+                    const bool shallow = e->depth() <= kBatchShallowDepth;
+                    if (shallow != (pass == 0)) continue;
+                    rows.push_back(e->obj_args());
+                    b->depth = std::max(b->depth, e->depth());
+                    int& d = shallow ? b->depth_shallow : b->depth_deep;
+                    d = std::max(d, e->depth());
+                    b->n_shallow += shallow ? 1 : 0;
+                }
             b->objs.reserve(rows.size() * sizeof(ObjArgs));
             IMPLI_HIP(hipMemcpy(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice));
             IMPLI_HIP(hipStreamSynchronize(s0));
@@ -1068,8 +1077,25 @@ int implisolid_batch_run(implisolid_batch* b, void* stream) {
         if (b->merged) {
             Engine& E0 = *b->engines[0];
             const int n = (int)b->engines.size();
-            launch_batch_eval(b->objs.as<ObjArgs>(), n, b->depth, E0.d_rabbit(), E0.tab_range(), E0.grid(),
-                              Engine::pruning() >= 2 ? 1 : 0, s);
+            const int fill = Engine::pruning() >= 2 ? 1 : 0;
+            // the deep objects' passes (few objects: latency-bound launches) on the batch's side
+            // stream beside the shallow ones', joined before the merged marching cubes
+            const bool both = b->n_shallow > 0 && n > b->n_shallow;
+            hipStream_t q = both ? b->streams[0] : s;
+            if (both) {
+                IMPLI_HIP(hipEventRecord(b->events[0], s));
+                IMPLI_HIP(hipStreamWaitEvent(q, b->events[0], 0));
+            }
+            if (n > b->n_shallow)
+                launch_batch_eval(b->objs.as<ObjArgs>() + b->n_shallow, n - b->n_shallow, b->depth_deep, E0.d_rabbit(),
+                                  E0.tab_range(), E0.grid(), fill, q);
+            if (b->n_shallow > 0)
+                launch_batch_eval(b->objs.as<ObjArgs>(), b->n_shallow, b->depth_shallow, E0.d_rabbit(), E0.tab_range(),
+                                  E0.grid(), fill, s);
+            if (both) {
+                IMPLI_HIP(hipEventRecord(b->events[1], q));
+                IMPLI_HIP(hipStreamWaitEvent(s, b->events[1], 0));
+            }
             launch_batch_mc(b->objs.as<ObjArgs>(), n, E0.d_cases(), E0.grid(), s);
             IMPLI_HIP(hipGetLastError());
             return 0;

@@ -156,7 +156,7 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &vidc_, &vid_halo_, &items_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &claimed_, &vidc_, &vid_halo_, &items_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -219,6 +219,7 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     fill_.reserve((size_t)brick_grid(grid_).n_bricks + 64);
     blist_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));
     lmodes_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint64_t));
+    claimed_.reserve(((size_t)brick_grid(grid_).n_bricks + 16) * sizeof(uint32_t));   // merged eval's second pass
     if (n_chunks(grid_) > kMaxChunks) throw InputError("grid: more than 8189 cells per row");
     const size_t mark_bytes = (size_t)(n_units(grid_) * n_chunks(grid_) + 1) * sizeof(uint32_t);
     umark_.reserve(mark_bytes);
@@ -550,6 +551,7 @@ ObjArgs Engine::obj_args() const {
     o.field = field_.as<float>();
     o.signs = signs_.p;
     o.counters = counters_.as<uint32_t>();
+    o.claimed = claimed_.as<uint32_t>();
     o.mc = buffers();
     o.mc.offsets = offsets_.as<uint32_t>();
     return o;

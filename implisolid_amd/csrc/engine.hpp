@@ -176,7 +176,7 @@ private:
     float key_box_[6] = {};
     HostBuf hcounters_;   // pinned landing zone of read_counts / raw_counters (one small copy)
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, vidc_, vid_halo_, items_, records_, verts_, faces_;
+    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, claimed_, vidc_, vid_halo_, items_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
     hipEvent_t ev_[11] = {};   // 0-8 phase boundaries, 9 after the coarse pass, 10 after refine

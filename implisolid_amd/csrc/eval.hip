@@ -458,9 +458,10 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill_b(const ObjArgs* __re
                     o.counters + kBrickListWord, static_cast<sign_piece_t*>(o.signs), o.counters + kCoarseListWord,
                     o.umark, o.mark_id);
 }
-template <int D, bool Pair>
-__global__ __launch_bounds__(256) void k_eval_field_pruned_b(const ObjArgs* __restrict__ objs, int n,
-                                                             const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
+// W: the occupancy request (three waves per SIMD at stack depth 9, 168 VGPRs without scratch)
+template <int D, bool Pair, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_eval_field_pruned_b(
+    const ObjArgs* __restrict__ objs, int n, const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
     __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
     const uint32_t total = batch_prefix(objs, n, kBrickListWord, 1u, (uint32_t)bg.n_bricks, s_pre);
     const uint32_t stride = gridDim.x * 4;
@@ -470,8 +471,31 @@ __global__ __launch_bounds__(256) void k_eval_field_pruned_b(const ObjArgs* __re
         const uint32_t li = i - s_pre[k];
         // Pair: both layers in one pass of the interpreter (InterpEval2; twice the node stacks in VGPRs)
         const ClaimCtx cc{o.fill, o.ccls, o.modes, o.cmodes, bg.nbx, bg.nbx * bg.nby};
-        eval_listed<InterpEval2<D, ProgC>, Pair>(InterpEval2<D, ProgC>{{prog_const(o.prog), tab}}, g, bg, cc, o.blist[li], o.lmodes[li], o.field,
-                                          static_cast<sign_piece_t*>(o.signs));
+        eval_listed_deferred<InterpEval2<D, ProgC>, Pair>(InterpEval2<D, ProgC>{{prog_const(o.prog), tab}}, g, bg, cc,
+                                                          o.blist[li], o.lmodes[li], o.field,
+                                                          static_cast<sign_piece_t*>(o.signs), o.claimed,
+                                                          o.counters + kClaimedWord, (uint32_t)bg.n_bricks);
+    }
+}
+// the claimed candidates of every object (eval_listed_deferred), one wave per candidate: values
+// only -- their sign pieces are constant and already written -- with the candidate's own modes
+template <int D, bool Pair>
+__global__ __launch_bounds__(256) void k_eval_claimed_b(const ObjArgs* __restrict__ objs, int n,
+                                                        const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
+    __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
+    const uint32_t total = batch_prefix(objs, n, kClaimedWord, 1u, (uint32_t)bg.n_bricks, s_pre);
+    const uint32_t stride = gridDim.x * 4;
+    for (uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); i < total; i += stride) {
+        const int k = __builtin_amdgcn_readfirstlane(batch_object_of(s_pre, n, i));
+        const ObjArgs& o = objs[k];
+        const int cur = (int)__builtin_amdgcn_readfirstlane(o.claimed[i - s_pre[k]]);
+        int cx, cy, cz;
+        brick_of(cur, bg, cx, cy, cz);
+        const int cb = cx + cy * bg.nbx + (cz / kCZ) * bg.nbx * bg.nby;   // the coarse box (same x, y grid)
+        const uint64_t m = o.ccls[cb] == kBrickMixed ? o.modes[cur] : o.cmodes[cb];
+        uint64_t neg[kBZ], valid;
+        eval_one_brick<InterpEval2<D, ProgC>, Pair>(InterpEval2<D, ProgC>{{prog_const(o.prog), tab}}, g, bg, cur, m, o.field,
+                                                    static_cast<sign_piece_t*>(o.signs), false, neg, valid);
     }
 }
 
@@ -647,23 +671,26 @@ void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_r
     const BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0 || n <= 0) return;
     if (n > kMaxBatchObjects) throw std::runtime_error("merged object stream: more than 1024 objects per launch");
-    depth = eval_depth(depth);
     const dim3 gc((unsigned)((cg.n_bricks + 255) / 256), (unsigned)n);
     const dim3 gf(fill_grid(g), (unsigned)n);
-#define IMPLI_BATCH_EVAL(DD)                                                                               \
-    do {                                                                                                   \
-        k_coarse_modes_b<DD><<<gc, 256, 0, s>>>(d_objs, d_rabbit, tab_range, g, cg);                       \
-        k_brick_refine_b<DD><<<kBatchRefineBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, tab_range, g, bg, cg); \
-        k_brick_fill_b<<<gf, kFillBlock, 0, s>>>(d_objs, g, bg, cg, sign_fill);                            \
-        if (interp_pair())                                                                             \
-            k_eval_field_pruned_b<DD, true><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);  \
-        else                                                                                               \
-            k_eval_field_pruned_b<DD, false><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg); \
+#define IMPLI_BATCH_EVAL(DD, WW)                                                                               \
+    do {                                                                                                       \
+        k_coarse_modes_b<DD><<<gc, 256, 0, s>>>(d_objs, d_rabbit, tab_range, g, cg);                           \
+        k_brick_refine_b<DD><<<kBatchRefineBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, tab_range, g, bg, cg);     \
+        k_brick_fill_b<<<gf, kFillBlock, 0, s>>>(d_objs, g, bg, cg, sign_fill);                                \
+        if (interp_pair()) {                                                                                   \
+            k_eval_field_pruned_b<DD, true, WW><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);  \
+            k_eval_claimed_b<DD, true><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);           \
+        } else {                                                                                               \
+            k_eval_field_pruned_b<DD, false, WW><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg); \
+            k_eval_claimed_b<DD, false><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);          \
+        }                                                                                                      \
     } while (0)
-    if (depth <= 4) IMPLI_BATCH_EVAL(4);
-    else if (depth <= 8) IMPLI_BATCH_EVAL(8);
-    else if (depth <= 12) IMPLI_BATCH_EVAL(12);
-    else IMPLI_BATCH_EVAL(16);
+    // stack capacity: kBatchShallowDepth slots for shallow objects (kernels.hpp), else the
+    // interpreter's floor (12: VGPR index mode) or 16
+    if (depth <= kBatchShallowDepth) IMPLI_BATCH_EVAL(kBatchShallowDepth, 3);
+    else if (depth <= 12) IMPLI_BATCH_EVAL(12, 2);
+    else IMPLI_BATCH_EVAL(16, 1);
 #undef IMPLI_BATCH_EVAL
 }
 

@@ -216,6 +216,39 @@ __device__ __forceinline__ void eval_listed(const Eval& ev, const GridDesc& g, c
     }
 }
 
+// The same entry without evaluating the claimed candidates in this wave: they are appended to
+// `claimed` (one atomic per claiming wave) for a second pass (eval.hip k_eval_claimed_b).  The
+// merged object-stream eval runs the interpreter, whose candidate loop kept its state live across a
+// second tree evaluation: 227 -> 196 VGPRs without it at stack depth 12, and at depth 9 168 -- three
+// waves per SIMD instead of two.
+template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
+__device__ __forceinline__ void eval_listed_deferred(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
+                                                     const ClaimCtx& cc, uint32_t entry, uint64_t m64,
+                                                     float* __restrict__ field, sign_piece_t* __restrict__ signs,
+                                                     uint32_t* __restrict__ claimed_list, uint32_t* __restrict__ claimed_count,
+                                                     uint32_t claimed_cap) {
+    const int b = (int)(entry & ~kListCheck);
+    const bool check = (entry & kListCheck) && cc.fill;
+    uint64_t neg[kBZ], valid;
+    eval_one_brick<Eval, Pair>(ev, g, bg, b, m64, field, signs, true, neg, valid);
+    if (!check) return;
+    const uint32_t claimed = claim_neighbours(g, bg, cc, b, neg, valid);
+    if (!claimed) return;   // uniform
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(claimed_count, (uint32_t)__popc(claimed));
+    base = __builtin_amdgcn_readfirstlane(base);
+    // lane d < 6 writes direction d's neighbour if claimed, at its rank among the claimed ones
+    if (lane < 6 && ((claimed >> lane) & 1u)) {
+        int bx, by, bz;
+        brick_of(b, bg, bx, by, bz);
+        const int ax = lane >> 1, up = lane & 1;
+        const int step = ax == 0 ? 1 : ax == 1 ? bg.nbx : bg.nbx * bg.nby;
+        const uint32_t at = base + (uint32_t)__popc(claimed & ((1u << lane) - 1u));
+        if (at < claimed_cap) claimed_list[at] = (uint32_t)(up ? b + step : b - step);
+    }
+}
+
 template <class Eval, bool Pair = IMPLI_EVAL_PAIR != 0>
 __device__ __forceinline__ void eval_bricks_body(const Eval& ev, const GridDesc& g, const BrickGrid& bg,
                                                  const ClaimCtx& cc, const uint64_t* __restrict__ modes,

@@ -44,6 +44,8 @@ static_assert(kBX * kBY == 64 && (kBX == 8 || kBX == 16 || kBX == 32), "a brick 
 // The pruned eval zeroes it without a memset: the coarse pass's first block clears every word but
 // [13], which it appends to; the fill kernel clears [13] once the refine pass has read it.
 constexpr int kBrickListWord = 12, kCoarseListWord = 13, kOverflowWord = 16, kCounterWords = 32;
+// [15]: the merged object-stream eval's claimed candidates (eval_listed_deferred)
+constexpr int kClaimedWord = 15;
 enum BrickClass : uint8_t { kBrickMixed = 0, kBrickPos = 1, kBrickNeg = 2, kBrickNoFill = 4 };
 // fill[b] (written by the pruned eval) = class | fill class << 4 | flags.  Fill class kBrickPos /
 // kBrickNeg: the brick's sign pieces are constant (no cell corner in it needs its exact value unless

@@ -74,12 +74,17 @@ struct ObjArgs {
     float* field;
     void* signs;
     uint32_t* counters;
+    uint32_t* claimed;   // the merged eval's claimed candidates, appended at counters[kClaimedWord]
     MCBuffers mc;
 };
 // eval (interval passes, fill, listed bricks) and MC (count, scan, vertices, faces) of n objects;
 // blocks per object are capped for the grid-stride kernels (small grids: most blocks would idle)
+// Node-stack capacity: 9 slots for objects of depth <= 9 (the smallest capacity the compiler
+// still indexes through VGPR index mode rather than select chains; the eval then fits three waves
+// per SIMD), else the interpreter's 12 or 16
 void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                        int sign_fill, hipStream_t s);
+constexpr int kBatchShallowDepth = 9;
 void launch_batch_mc(const ObjArgs* d_objs, int n, const CaseInfo* d_cases, const GridDesc& g, hipStream_t s);
 
 }  // namespace impli
