@@ -1036,6 +1036,59 @@ def test_batch_stream_matches_oracle(impli, oracle, n_streams):
                 assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), (rep, i)
 
 
+def _depth_class_objects():
+    """Objects of every depth class of the merged batch (abi.hip implisolid_batch: stacks of 9, 12 and
+    16 slots, the deeper classes on the batch's side stream) with rotated and sheared matrices (x and
+    y rows that read z, so the layer pair's samples differ in every coordinate)."""
+    import math
+    import random
+    from implisolid_amd import scenes
+    rng = random.Random(4242)
+
+    def rot(a, b, t):
+        ca, sa, cb, sb = math.cos(a), math.sin(a), math.cos(b), math.sin(b)
+        return [ca, -sa * cb, sa * sb, t[0], sa, ca * cb, -ca * sb, t[1], 0.0, sb, cb, t[2]]
+
+    def chain(n):   # a left-deep chain: tree depth n
+        node = scenes.random_leaf(rng)
+        for k in range(n - 1):
+            op = ("Union", "Difference", "Intersection")[k % 3]
+            leaf = scenes.random_leaf(rng)
+            if op == "Intersection":
+                leaf = {"type": "iellipsoid", "matrix": scenes.st(2.0, 0.0, 0.0, 0.0)}
+            node = {"type": op, "matrix": rot(0.1 * k, 0.05 * k, (0, 0, 0)) if k % 4 == 1 else list(scenes.EYE),
+                    "children": [node, leaf]}
+        return node
+
+    objs = [scenes.random_tree(11, 5), chain(9), chain(12), chain(14), scenes.random_tree(3, 30),
+            {"type": "Union", "matrix": rot(0.7, 0.4, (0.05, -0.03, 0.02)),
+             "children": [scenes.random_tree(5, 6), scenes.random_leaf(rng)]},
+            scenes.random_leaf(rng)]
+    depths = sorted(scenes.tree_stats(o)[2] for o in objs)
+    # stack depth = tree depth + 1: every class present (<= 9, 10..12, 13..16 slots)
+    assert depths[0] <= 8 and any(9 <= d <= 11 for d in depths) and depths[-1] >= 12, depths
+    return objs
+
+
+def test_batch_depth_classes_against_oracle(impli, oracle):
+    """The merged batch over objects of all three interpreter depth classes, with rotated node
+    matrices: each object's mesh is the oracle's, byte for byte, on two replays (the side-stream
+    fork and join of the deeper classes replayed)."""
+    from implisolid_amd import scenes
+    objs = _depth_class_objects()
+    mc = scenes.mc_settings(40, 1.0)
+    with impli.Batch(objs, mc, n_streams=0) as b:
+        assert b.n == len(objs) and b.merged
+        for rep in range(2):
+            b.run()
+            for i, sh in enumerate(objs):
+                v, f = b.download(i)
+                vr, fr = oracle.marching_cubes(oracle.mp5_to_nodes(json.dumps(sh)), 40, [-1, 1] * 3)
+                assert len(fr) > 0, i
+                assert np.array_equal(f, fr), (rep, i)
+                assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), (rep, i)
+
+
 _INTERP_SCRIPT = r"""
 import hashlib, sys
 import numpy as np
