@@ -952,6 +952,16 @@ int64_t implisolid_slab_read_field(implisolid_slab* s, float* out, int64_t capac
 
 // ---- object stream (config 5): one engine per object, each object's eval + count + emit captured
 //      once in a hipGraph and replayed; objects spread over a few streams ----------------------------
+// merged object streams: pipelines the shallow class is split into (IMPLISOLID_BATCH_GROUPS, 1-8)
+static int batch_groups() {
+    static const int k = [] {
+        const char* e = std::getenv("IMPLISOLID_BATCH_GROUPS");
+        const int v = e ? std::atoi(e) : kBatchGroups;
+        return v < 1 ? 1 : v > 8 ? 8 : v;
+    }();
+    return k;
+}
+
 struct implisolid_batch {
     std::vector<std::unique_ptr<Engine>> engines;
     bool merged = false;                 // one launch per stage for all objects (ObjArgs rows)
@@ -960,6 +970,10 @@ struct implisolid_batch {
     // merged: objects of tree depth <= kBatchShallowDepth (rows [0, n_shallow)) run the interval and
     // eval passes with 9-slot node stacks (three waves per SIMD), the rest with 12 or 16
     int n_shallow = 0, depth_shallow = 0, depth_deep = 0;
+    // merged: the groups run as independent pipelines (eval passes + marching cubes), group 0 on the
+    // caller's stream, group k on streams[k - 1]: {first row, rows, stack depth}
+    struct Group { int row0, n, depth; };
+    std::vector<Group> groups;
     std::vector<hipGraphExec_t> execs;   // empty when capture is unavailable (direct launches)
     std::vector<hipStream_t> streams;
     std::vector<hipEvent_t> events;      // fork (0) and one join event per stream
@@ -997,7 +1011,8 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         } held;
         if (Engine::pruning() > 0 && !b->merged) held.s = TreeJit::instance().precompile(progs, 16);
         b->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        const int ns = b->merged ? 1 : std::max(1, std::min(n_streams, 8));
+        // merged: the shallow class in batch_groups() pipelines, the deep class (if any) in one more
+        const int ns = b->merged ? batch_groups() : std::max(1, std::min(n_streams, 8));
         for (int k = 0; k < ns; ++k) {
             hipStream_t q;
             IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
@@ -1029,6 +1044,13 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
                     d = std::max(d, e->depth());
                     b->n_shallow += shallow ? 1 : 0;
                 }
+            // groups: the shallow rows split into batch_groups() consecutive runs, then the deep rows
+            const int K = std::max(1, std::min(batch_groups(), b->n_shallow));
+            for (int k = 0; k < K && b->n_shallow > 0; ++k) {
+                const int r0 = b->n_shallow * k / K, r1 = b->n_shallow * (k + 1) / K;
+                if (r1 > r0) b->groups.push_back({r0, r1 - r0, b->depth_shallow});
+            }
+            if (n > b->n_shallow) b->groups.push_back({b->n_shallow, n - b->n_shallow, b->depth_deep});
             b->objs.reserve(rows.size() * sizeof(ObjArgs));
             IMPLI_HIP(hipMemcpy(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice));
             IMPLI_HIP(hipStreamSynchronize(s0));
@@ -1076,27 +1098,28 @@ int implisolid_batch_run(implisolid_batch* b, void* stream) {
         hipStream_t s = (hipStream_t)stream;
         if (b->merged) {
             Engine& E0 = *b->engines[0];
-            const int n = (int)b->engines.size();
             const int fill = Engine::pruning() >= 2 ? 1 : 0;
-            // the deep objects' passes (few objects: latency-bound launches) on the batch's side
-            // stream beside the shallow ones', joined before the merged marching cubes
-            const bool both = b->n_shallow > 0 && n > b->n_shallow;
-            hipStream_t q = both ? b->streams[0] : s;
-            if (both) {
+            // each group's pipeline -- interval and eval passes, then marching cubes -- on its own
+            // stream: one group's latency-bound launches (the coarse pass, the list fills, the count
+            // and scan of few objects) run beside another's throughput-bound eval; the deep class
+            // (few objects, 12- or 16-slot stacks) is the last group.  Forked from and joined to the
+            // caller's stream.
+            const int ng = (int)b->groups.size();
+            if (ng > 1) {
                 IMPLI_HIP(hipEventRecord(b->events[0], s));
-                IMPLI_HIP(hipStreamWaitEvent(q, b->events[0], 0));
+                for (int k = 1; k < ng; ++k) IMPLI_HIP(hipStreamWaitEvent(b->streams[(size_t)k - 1], b->events[0], 0));
             }
-            if (n > b->n_shallow)
-                launch_batch_eval(b->objs.as<ObjArgs>() + b->n_shallow, n - b->n_shallow, b->depth_deep, E0.d_rabbit(),
-                                  E0.tab_range(), E0.grid(), fill, q);
-            if (b->n_shallow > 0)
-                launch_batch_eval(b->objs.as<ObjArgs>(), b->n_shallow, b->depth_shallow, E0.d_rabbit(), E0.tab_range(),
-                                  E0.grid(), fill, s);
-            if (both) {
-                IMPLI_HIP(hipEventRecord(b->events[1], q));
-                IMPLI_HIP(hipStreamWaitEvent(s, b->events[1], 0));
+            for (int k = ng - 1; k >= 0; --k) {   // the deep class first: its passes are the longest chain
+                const implisolid_batch::Group& gr = b->groups[(size_t)k];
+                hipStream_t q = k == 0 ? s : b->streams[(size_t)k - 1];
+                const ObjArgs* rows = b->objs.as<ObjArgs>() + gr.row0;
+                launch_batch_eval(rows, gr.n, gr.depth, E0.d_rabbit(), E0.tab_range(), E0.grid(), fill, q);
+                launch_batch_mc(rows, gr.n, E0.d_cases(), E0.grid(), q);
             }
-            launch_batch_mc(b->objs.as<ObjArgs>(), n, E0.d_cases(), E0.grid(), s);
+            for (int k = 1; k < ng; ++k) {
+                IMPLI_HIP(hipEventRecord(b->events[(size_t)k], b->streams[(size_t)k - 1]));
+                IMPLI_HIP(hipStreamWaitEvent(s, b->events[(size_t)k], 0));
+            }
             IMPLI_HIP(hipGetLastError());
             return 0;
         }

@@ -85,6 +85,10 @@ struct ObjArgs {
 void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                        int sign_fill, hipStream_t s);
 constexpr int kBatchShallowDepth = 9;
+// merged object streams: the shallow class as this many pipelines on separate streams (abi.hip;
+// the deep class is always one more).  Config 5: 2 / 3 / 4 pipelines 0.58 / 0.64 / 0.85 ms against
+// 0.545 for one (profiles/r04x_*): concurrent merged kernels contend more than they overlap.
+constexpr int kBatchGroups = 1;
 void launch_batch_mc(const ObjArgs* d_objs, int n, const CaseInfo* d_cases, const GridDesc& g, hipStream_t s);
 
 }  // namespace impli

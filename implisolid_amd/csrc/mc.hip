@@ -208,8 +208,10 @@ __global__ __launch_bounds__(512) void k_mc_count(GridDesc g, MCBuffers b) { mc_
 // cross the XCDs' L2s at memory latency, one round trip per 64 groups walked.)
 constexpr int kScanBlock = 256;
 constexpr int kScanRows = kScanParts + 1;   // + the non-empty unit counts (summed for statistics)
+template <int BS = kScanBlock>
 __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffers& b) {
-    __shared__ uint32_t s_part[kScanBlock / 64][kScanRows];
+    static_assert(BS >= kGroupUnits, "a lane per unit of the group");
+    __shared__ uint32_t s_part[BS / 64][kScanRows];
     __shared__ uint32_t s_base[kScanRows];
     const int64_t G = blockIdx.x, ng = n_groups(g);
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -221,7 +223,7 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
     const uint32_t cm = b.unit_cmask[G * kGroupUnits + (t < (int)nne ? t : 0)];
     uint32_t acc[kScanRows] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll 4
-    for (int64_t i = t; i < G; i += kScanBlock)
+    for (int64_t i = t; i < G; i += BS)
 #pragma unroll
         for (int c = 0; c < kScanRows; ++c) acc[c] += b.scan_blk[c * ng + i];
 #pragma unroll
@@ -233,7 +235,7 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
     if (t < kScanRows) {
         uint32_t s = 0;
 #pragma unroll
-        for (int w = 0; w < kScanBlock / 64; ++w) s += s_part[w][t];
+        for (int w = 0; w < BS / 64; ++w) s += s_part[w][t];
         s_base[t] = s;
     }
     __syncthreads();
@@ -262,7 +264,7 @@ __device__ __forceinline__ void unit_scan_body(const GridDesc& g, const MCBuffer
         b.counters[6] = s_base[6] + nne;                          // non-empty units (statistics)
     }
 }
-__global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) { unit_scan_body(g, b); }
+__global__ __launch_bounds__(kScanBlock) void k_unit_scan(GridDesc g, MCBuffers b) { unit_scan_body<>(g, b); }
 
 __global__ __launch_bounds__(64 * kVertsWaves) __attribute__((amdgpu_waves_per_eu(6))) void k_mc_cells(const CaseInfo* __restrict__ cases, GridDesc g, MCBuffers b) {
     mc_cells_body(cases, g, b);
@@ -372,8 +374,9 @@ __global__ __launch_bounds__(256) void k_mc_faces(const CaseInfo* __restrict__ c
 __global__ __launch_bounds__(512) void k_mc_count_b(const ObjArgs* __restrict__ objs, GridDesc g) {
     mc_count_body(g, objs[blockIdx.y].mc);
 }
-__global__ __launch_bounds__(kScanBlock) void k_unit_scan_b(const ObjArgs* __restrict__ objs, GridDesc g) {
-    unit_scan_body(g, objs[blockIdx.y].mc);
+template <int B>
+__global__ __launch_bounds__(B) void k_unit_scan_b(const ObjArgs* __restrict__ objs, GridDesc g) {
+    unit_scan_body<B>(g, objs[blockIdx.y].mc);
 }
 // vertex pass: one flat index over every object's unit parts (batch_device.hpp), a wave per part
 __global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells_b(const CaseInfo* __restrict__ cases,
@@ -444,14 +447,21 @@ namespace impli {
 
 // grids of the flat merged vertex / face kernels
 constexpr unsigned kBatchCellBlocks = 4096, kBatchFaceBlocks = 2048;
+constexpr int kBatchCountLanes = 128;
 
 void launch_batch_mc(const ObjArgs* d_objs, int n, const CaseInfo* d_cases, const GridDesc& g, hipStream_t s) {
     const int64_t ng = n_groups(g), nu = n_units(g);
     if (ng == 0 || n <= 0) return;
+    // An object's grid is small (128^3: 2 chunks per row, 63 groups): most of a group's (unit, chunk)
+    // pairs are unmarked, so its count block loops over few items, and block count x waves is what
+    // costs -- n objects' groups as blocks of kBatchCountLanes lanes (the single-grid path's 512-lane
+    // blocks: 4x the waves of a 512^3 grid's count for the same samples).  The scan of <= 64 groups
+    // reads them with one wave.
     const int items = kGroupUnits * kUnitRows * ((g.m + 63) / 64);
-    const unsigned threads = (unsigned)std::min(512, (items + 63) / 64 * 64);
+    const unsigned threads = (unsigned)std::min(kBatchCountLanes, (items + 63) / 64 * 64);
     k_mc_count_b<<<dim3((unsigned)ng, (unsigned)n), threads, 0, s>>>(d_objs, g);
-    k_unit_scan_b<<<dim3((unsigned)ng, (unsigned)n), kScanBlock, 0, s>>>(d_objs, g);
+    if (ng <= 64) k_unit_scan_b<64><<<dim3((unsigned)ng, (unsigned)n), 64, 0, s>>>(d_objs, g);
+    else k_unit_scan_b<kScanBlock><<<dim3((unsigned)ng, (unsigned)n), kScanBlock, 0, s>>>(d_objs, g);
     (void)nu;
     k_mc_cells_b<<<kBatchCellBlocks, 64 * kVertsWaves, 0, s>>>(d_cases, d_objs, n, g);
     k_mc_faces_b<<<kBatchFaceBlocks, 256, 0, s>>>(d_cases, d_objs, n, g);

@@ -1,18 +1,17 @@
 #!/bin/bash
-# config-5 merged pass: the current library (with and without the depth-class split) against
-# variants (tools/build_variant.sh), three rounds alternating: tools/c5_ab.sh <tag> variant ...
+# config-5 merged pass: the current library against variants (tools/build_variant.sh), three rounds
+# alternating: tools/c5_ab.sh <tag> variant ...
 set -euo pipefail
 tag=${1:?tag}; shift
 out=gpurun_out/$tag
 mkdir -p "$out"
 root=$(pwd)
 for rep in 1 2 3; do
-  for v in main nosplit "$@"; do
-    lib=""; env_split=1
-    [ "$v" = nosplit ] && env_split=0
-    [ "$v" != main ] && [ "$v" != nosplit ] && lib=$root/variants/$v/implisolid_amd/lib/libimplisolid_mi355x.so
+  for v in main "$@"; do
+    lib=""
+    [ "$v" != main ] && lib=$root/variants/$v/implisolid_amd/lib/libimplisolid_mi355x.so
     echo -n "$v $rep " >> "$out/c5_ab.txt"
-    IMPLISOLID_BATCH_SPLIT=$env_split IMPLISOLID_LIB=$lib timeout -k 10 120 python3 tools/config5_merged_probe.py 64 128 20 2>/dev/null | grep merged >> "$out/c5_ab.txt"
+    IMPLISOLID_LIB=$lib timeout -k 10 120 python3 tools/config5_merged_probe.py 64 128 20 2>/dev/null | grep merged >> "$out/c5_ab.txt"
   done
 done
 cat "$out/c5_ab.txt"
