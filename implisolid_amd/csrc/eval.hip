@@ -139,8 +139,9 @@ __device__ __forceinline__ void eval_f2_pruned(ProgP __restrict__ prog, const fl
         }
         if (I.op == OP_XFORM) {
             const float* M = mat_row(prog, I.mat);
-            const V3 q0 = xform(M, px0[sp], py0[sp], pz0[sp]);
-            const V3 q1 = xform(M, px1[sp], py1[sp], pz1[sp]);
+            const bool diag = I.type == XF_DIAG;
+            const V3 q0 = diag ? xform_diag(M, px0[sp], py0[sp], pz0[sp]) : xform(M, px0[sp], py0[sp], pz0[sp]);
+            const V3 q1 = diag ? xform_diag(M, px1[sp], py1[sp], pz1[sp]) : xform(M, px1[sp], py1[sp], pz1[sp]);
             ++sp;
             px0[sp] = q0.x; py0[sp] = q0.y; pz0[sp] = q0.z;
             px1[sp] = q1.x; py1[sp] = q1.y; pz1[sp] = q1.z;

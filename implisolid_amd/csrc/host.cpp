@@ -461,6 +461,22 @@ Program compile_mp5(const Json& shape, bool ignore_root_matrix) {
     Builder b;
     b.node(shape, ignore_root_matrix);
     b.p.max_depth = b.max_depth + 1;
+    for (int i = 0; i < b.p.n_instr; ++i) {   // XFORM patterns (program.hpp XformPattern)
+        Instr& I = b.p.instr[i];
+        if (I.op != OP_XFORM) continue;
+        const float* m = b.p.mats[I.mat];
+        bool diag = true;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) {
+                const float v = m[4 * r + c];
+                uint32_t bits;
+                std::memcpy(&bits, &v, 4);
+                if (!std::isfinite(v)) diag = false;
+                else if (c == 3 && bits == 0x80000000u) diag = false;   // a -0 translation
+                else if (c != 3 && c != r && v != 0.f) diag = false;
+            }
+        I.type = diag ? XF_DIAG : XF_GENERIC;
+    }
     return b.p;
 }
 

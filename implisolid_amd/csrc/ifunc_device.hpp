@@ -47,6 +47,14 @@ __device__ __forceinline__ V3 xform(const float* __restrict__ m, float x, float 
     r.z = m[8] * x + m[9] * y + m[10] * z + m[11];
     return r;
 }
+// an XF_DIAG matrix's rows at a finite point (program.hpp XformPattern): m_dd v + m_d3
+__device__ __forceinline__ V3 xform_diag(const float* __restrict__ m, float x, float y, float z) {
+    V3 r;
+    r.x = m[0] * x + m[3];
+    r.y = m[5] * y + m[7];
+    r.z = m[10] * z + m[11];
+    return r;
+}
 // gradient post-transform inv^T * g (e.g. transformed_union.hpp:76-83)
 __device__ __forceinline__ V3 grad_xform(const float* __restrict__ m, V3 g) {
     V3 r;

@@ -97,6 +97,17 @@ __device__ __forceinline__ Box xform_iv(const float* __restrict__ m, Box p) {
     return r;
 }
 
+// an XF_DIAG matrix (program.hpp XformPattern) over a box of finite points: each row's term of its
+// own coordinate plus the translation -- the dropped +-0 terms change at most the sign of a zero
+// endpoint, which no decision or class reads (jit.cpp xform_iv_row emits the same rows)
+__device__ __forceinline__ Box xform_iv_diag(const float* __restrict__ m, Box p) {
+    Box r;
+    r.x = settle_point(add(mulc(p.x, m[0]), ivc(m[3])));
+    r.y = settle_point(add(mulc(p.y, m[5]), ivc(m[7])));
+    r.z = settle_point(add(mulc(p.z, m[10]), ivc(m[11])));
+    return r;
+}
+
 // ---- primitives (mirroring ifunc_device.hpp operation for operation) ------------------------
 __device__ __forceinline__ Iv egg_iv(Box p) {
     const Iv u = divc(sub(p.x, ivc(0.f)), 0.5f), v = divc(sub(p.y, ivc(0.f)), 0.5f), w = divc(sub(p.z, ivc(0.f)), 0.5f);
@@ -386,7 +397,7 @@ __device__ __forceinline__ Iv eval_iv(ProgP __restrict__ prog, const float* __re
         }
         const Box cur{Iv{xl[sp], xh[sp]}, Iv{yl[sp], yh[sp]}, Iv{zl[sp], zh[sp]}};
         if (I.op == OP_XFORM) {
-            const Box q = xform_iv(mat_row(prog, I.mat), cur);
+            const Box q = I.type == XF_DIAG ? xform_iv_diag(mat_row(prog, I.mat), cur) : xform_iv(mat_row(prog, I.mat), cur);
             ++sp;
             xl[sp] = q.x.lo; xh[sp] = q.x.hi; yl[sp] = q.y.lo; yh[sp] = q.y.hi; zl[sp] = q.z.lo; zh[sp] = q.z.hi;
         } else if (I.op == OP_PRIM) {
@@ -437,7 +448,8 @@ __device__ __forceinline__ float eval_f_pruned(ProgP __restrict__ prog, const fl
             }
         }
         if (I.op == OP_XFORM) {
-            const V3 q = xform(mat_row(prog, I.mat), px[sp], py[sp], pz[sp]);
+            const float* M = mat_row(prog, I.mat);
+            const V3 q = I.type == XF_DIAG ? xform_diag(M, px[sp], py[sp], pz[sp]) : xform(M, px[sp], py[sp], pz[sp]);
             ++sp;
             px[sp] = q.x; py[sp] = q.y; pz[sp] = q.z;
         } else if (I.op == OP_PRIM) {

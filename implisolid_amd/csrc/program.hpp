@@ -52,7 +52,7 @@ enum OpCode : int32_t {
 
 struct Instr {
     int16_t op;          // OpCode
-    int16_t type;        // PRIM/CSG: NodeType
+    int16_t type;        // PRIM/CSG: NodeType; XFORM: XformPattern of its matrix
     int16_t mat;         // index of the node's inverse matrix (XFORM: the one to apply)
     int16_t csg;         // OP_CSG: index of this CSG node (pruning modes), else -1
     int16_t skip_csg;    // XFORM that starts a CSG operand: that CSG node's index, else -1
@@ -61,6 +61,15 @@ struct Instr {
     int16_t prm;         // OP_PRIM: row of mats[] holding the primitive's parameters (raw floats)
 };
 static_assert(sizeof(Instr) == 16, "Instr layout");
+
+// XFORM instructions: the pattern of the node's matrix, set by compile_mp5 (host.cpp).  XF_DIAG:
+// every off-diagonal coefficient of the three rows is +-0, every translation is finite and not -0
+// and every diagonal coefficient finite -- a scale + translate, whose rows the brick interpreters
+// evaluate as m_dd v + m_d3 (xform_diag): at the finite sample points of a brick that is the full
+// row's value (a zero coefficient adds a +-0, which the row's final + m_d3 != -0 absorbs), exactly
+// the row the JIT emits for such a matrix (jit.cpp xform_row).  Points that may be NaN or infinite
+// (OB02 vertices) keep the full rows.
+enum XformPattern : int16_t { XF_GENERIC = 0, XF_DIAG = 1 };
 
 // Per-brick pruning: 2 bits per CSG node (index < kMaxPruned): both operands, left only, right only.
 enum PruneMode : uint32_t { PM_BOTH = 0, PM_LEFT = 1, PM_RIGHT = 2 };
