@@ -40,6 +40,20 @@ def progress(what):
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+
+def jit_wait(I, what="tree-module compiles"):
+    """I.jit_wait() with a progress line every 20 s while it blocks: on a box with an empty JIT cache
+    the headline's modules compile before the first leg starts (the ctypes call releases the GIL)."""
+    import threading
+    t = threading.Thread(target=I.jit_wait, daemon=True)
+    t.start()
+    while True:
+        t.join(20.0)
+        if not t.is_alive():
+            return
+        progress("waiting for %s" % what)
+
+
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # kernel (profile short name) -> the engine's timed phase (Slab.KERNELS; tools/pmc_traffic.py)
 KERNEL_PHASE = {"impli_coarse_modes": "brick_modes", "impli_brick_refine": "brick_modes", "k_brick_fill": "brick_modes",
@@ -326,15 +340,16 @@ def main():
                 slab.emit(0, sp)
             if e: e[3].record(stream)
 
+        progress("headline R=%d: warmup" % R)
         # warmup (first call sizes the output buffers); the tree module compiles in the background
         # meanwhile (async JIT) -- wait for it, so the timed steps run the compiled kernels
         for _ in range(max(1, warmup)):
             step()
-        I.jit_wait()
+        jit_wait(I)
         for _ in range(max(1, warmup)):
             step()
         # a hot object's baked module (bake mode 2) is requested after a few evals: wait for it too
-        I.jit_wait()
+        jit_wait(I)
         for _ in range(max(1, warmup)):
             step()
         # no compilation may run beside the timed steps (host threads compiling next to the launch
@@ -347,7 +362,7 @@ def main():
             done = jit_count()
             for _ in range(max(1, warmup)):
                 step()
-            I.jit_wait()
+            jit_wait(I)
             if jit_count() == done:
                 break
         nv, nf, grew = slab.counts(sp)
@@ -516,7 +531,7 @@ def main():
             for _ in range(3):
                 for _ in range(4):
                     step(main_s)
-                I.jit_wait()
+                jit_wait(I)
             torch.cuda.synchronize(dev)
             if any(sl.counts(0)[2] for sl in slabs):   # the first call sized the outputs
                 step(main_s)
@@ -667,7 +682,7 @@ def main():
             F = torch.from_numpy(f_mc.reshape(-1).copy()).to(dev)
             voff = np.concatenate([[0], np.cumsum(nvs)]).astype(np.int64)
             D.ob02_shards_local(shape, mc, V, F, voff, timing=True)   # warm (point modules, tables)
-            I.jit_wait()
+            jit_wait(I)
             v, f, st8 = D.ob02_shards_local(shape, mc, V, F, voff, timing=True)
             _, _, st1 = D.ob02_shards_local(shape, mc, V, F, [0, len(v_mc)], timing=True)
             crit = sum(max(x["shard_ms"]) for x in st8["steps"])
@@ -728,7 +743,7 @@ def main():
             first["r%d" % Rf] = {"gpu_first_call_ms": round(t_gpu * 1e3, 3), "cpu_oracle_ms": round(t_cpu * 1e3, 3),
                                  "faces_identical": bool(np.array_equal(f, fr)),
                                  "verts_identical": bool(np.array_equal(v.view(np.uint32), vr.view(np.uint32)))}
-        I.jit_wait()
+        jit_wait(I)
         first["jit"] = I.jit_stats()
         legs["first_call"] = round(time.perf_counter() - t_leg, 2)
 
@@ -747,7 +762,7 @@ def main():
             for _ in range(2):
                 for _ in range(5):
                     I.make_geometry(shape, mc)
-                I.jit_wait()
+                jit_wait(I)
             ts = []
             for _ in range(7):
                 t0 = time.perf_counter()
@@ -776,7 +791,7 @@ def main():
             t0 = time.perf_counter()
             I.make_geometry(shape, mc)
             t_first = time.perf_counter() - t0
-            I.jit_wait()
+            jit_wait(I)
             I.make_geometry(shape, mc)
             ts = []
             for _ in range(3):

@@ -24,6 +24,7 @@
 #include <sys/stat.h>
 #include <sys/time.h>
 #include <unistd.h>
+#include <dlfcn.h>
 
 #include "generated/jit_headers.inc"
 
@@ -587,6 +588,15 @@ void TreeJit::build(Slot* slot) {
             }
         };
         if (!from_disk) compile_and_store(slot->src);
+        // the process is exiting (shutdown() joins this worker): load nothing into a runtime that
+        // is being torn down
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            if (stop_) {
+                slot->failed.store(true, std::memory_order_release);
+                return;
+            }
+        }
         int prev = 0;
         (void)hipGetDevice(&prev);
         if (prev != slot->device) IMPLI_HIP_THROW(hipSetDevice(slot->device));
@@ -704,6 +714,9 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake, hipStream
     }
     int dev = 0;
     (void)hipGetDevice(&dev);
+    // the disk-cache key's device architecture, queried here on the caller's thread: a worker then
+    // makes no HIP runtime call before its compile is done (at exit it makes none at all, build())
+    (void)device_arch(dev);
     Slot* slot = nullptr;
     bool fresh = false;
     std::vector<Slot*> evict;
@@ -731,6 +744,16 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake, hipStream
             if (m == kAsync && !stop_) {
                 queue_.push_back(slot);
                 if (workers_.empty()) {   // a small pool, started on first use
+                    // hipRTC loads its compiler (comgr, the builtins) at the first compile; loaded now,
+                    // their static destructors are registered before the exit handler below, so at
+                    // exit shutdown() joins a worker still compiling before the compiler is torn down
+                    // (exiting with a compile in flight otherwise crashed in the compiler)
+                    static const bool preloaded = [] {
+                        (void)dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);
+                        (void)dlopen("libhiprtc-builtins.so.7", RTLD_NOW | RTLD_GLOBAL);
+                        return true;
+                    }();
+                    (void)preloaded;
                     const unsigned hw = std::thread::hardware_concurrency();
                     const int n = (int)std::max(1u, std::min(4u, hw ? hw / 2 : 1u));
                     for (int i = 0; i < n; ++i) workers_.emplace_back([this] { worker(); });
@@ -974,6 +997,12 @@ std::vector<char> TreeJit::compile(const std::string& src) {
     // the static library's floating-point contract: no FMA contraction, IEEE division/sqrt
     const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
     const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+    // hipRTC loads its compiler libraries at the first compile, and their static destructors run at
+    // exit before the handlers registered earlier: shutdown() (which joins a worker still compiling)
+    // is registered once more now, so it runs before those destructors (a process that exited with
+    // a compile in flight crashed in the compiler's torn-down state).  shutdown() is idempotent.
+    static std::once_flag exit_hook;
+    std::call_once(exit_hook, [] { std::atexit([] { TreeJit::instance().shutdown(); }); });
     if (r != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);

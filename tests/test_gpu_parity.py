@@ -1089,6 +1089,32 @@ def test_batch_depth_classes_against_oracle(impli, oracle):
                 assert np.array_equal(v.view(np.uint32), vr.view(np.uint32)), (rep, i)
 
 
+_EXIT_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import torch
+torch.cuda.is_available()
+import implisolid_amd as I
+from implisolid_amd import scenes
+v, f = I.make_geometry(*scenes.config3(24))
+print(len(v), len(f), flush=True)
+"""
+
+
+def test_exit_with_compiles_in_flight(tmp_path):
+    """A process that exits right after its first build -- its tree modules still compiling on the
+    JIT's worker threads (an empty disk cache) -- exits cleanly: the exit handler joins the workers
+    and they load nothing into the runtime being torn down (it crashed or hung before)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IMPLISOLID_JIT_CACHE=str(tmp_path / "jit"))
+    r = subprocess.run([sys.executable, "-c", _EXIT_SCRIPT, root], env=env, capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    assert r.stdout.split() == ["698", "1384"], r.stdout   # config 3 at 24^3 (the oracle's mesh size)
+
+
 _INTERP_SCRIPT = r"""
 import hashlib, sys
 import numpy as np
