@@ -665,7 +665,10 @@ void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_
 }
 
 // flat merged kernels (refine, eval): a fixed grid over all objects' items
-constexpr unsigned kBatchRefineBlocks = 2048, kBatchEvalBlocks = 4096;
+// (eval grid 2048 blocks: 0.531 ms per config-5 pass against 0.546 at 4096, 0.550 at 1536 and 0.537
+// at 3072; the claimed pass 1024: 0.529 against 0.532 at 2048 and 0.537 at 4096 -- profiles/r04ap_*,
+// r04aq_*, r04ar_*)
+constexpr unsigned kBatchRefineBlocks = 2048, kBatchEvalBlocks = 2048, kBatchClaimedBlocks = 1024;
 
 void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                        int sign_fill, hipStream_t s) {
@@ -681,10 +684,10 @@ void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_r
         k_brick_fill_b<<<gf, kFillBlock, 0, s>>>(d_objs, g, bg, cg, sign_fill);                                \
         if (interp_pair()) {                                                                                   \
             k_eval_field_pruned_b<DD, true, WW><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);  \
-            k_eval_claimed_b<DD, true><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);           \
+            k_eval_claimed_b<DD, true><<<kBatchClaimedBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);        \
         } else {                                                                                               \
             k_eval_field_pruned_b<DD, false, WW><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg); \
-            k_eval_claimed_b<DD, false><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);          \
+            k_eval_claimed_b<DD, false><<<kBatchClaimedBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);       \
         }                                                                                                      \
     } while (0)
     // stack capacity: kBatchShallowDepth slots for shallow objects (kernels.hpp), else the
