@@ -968,7 +968,7 @@ struct implisolid_batch {
     DevBuf objs;                         // merged: ObjArgs[n] on the device, shallow objects first
     int depth = 0;
     // merged: objects of tree depth <= kBatchShallowDepth (rows [0, n_shallow)) run the interval and
-    // eval passes with 9-slot node stacks (three waves per SIMD), the rest with 12 or 16
+    // eval passes with 9-slot node stacks (four waves per SIMD), the rest with 12 or 16
     int n_shallow = 0, depth_shallow = 0, depth_deep = 0;
     // merged: the groups run as independent pipelines (eval passes + marching cubes), group 0 on the
     // caller's stream, group k on streams[k - 1]: {first row, rows, stack depth}

@@ -459,7 +459,8 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill_b(const ObjArgs* __re
                     o.counters + kBrickListWord, static_cast<sign_piece_t*>(o.signs), o.counters + kCoarseListWord,
                     o.umark, o.mark_id);
 }
-// W: the occupancy request (three waves per SIMD at stack depth 9, 168 VGPRs without scratch)
+// W: the occupancy request (four waves per SIMD at stack depth 9: 128 VGPRs and 28 B of scratch,
+// 0.531 -> 0.507 ms per config-5 pass against three waves without scratch; five spill far more: 1.0 ms)
 template <int D, bool Pair, int W>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_eval_field_pruned_b(
     const ObjArgs* __restrict__ objs, int n, const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
@@ -692,7 +693,7 @@ void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_r
     } while (0)
     // stack capacity: kBatchShallowDepth slots for shallow objects (kernels.hpp), else the
     // interpreter's floor (12: VGPR index mode) or 16
-    if (depth <= kBatchShallowDepth) IMPLI_BATCH_EVAL(kBatchShallowDepth, 3);
+    if (depth <= kBatchShallowDepth) IMPLI_BATCH_EVAL(kBatchShallowDepth, 4);
     else if (depth <= 12) IMPLI_BATCH_EVAL(12, 2);
     else IMPLI_BATCH_EVAL(16, 1);
 #undef IMPLI_BATCH_EVAL
