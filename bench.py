@@ -109,24 +109,28 @@ def cpu_baseline(shape, target_s=20.0):
                       % (R, dt, f.shape[0]), "host": host_info()}, (R, v, f)
 
 
-def _c5_oracle_object(k):
-    """One config-5 object's eval + MC on the oracle (a worker process of config5_cpu_baseline)."""
-    sys.path.insert(0, ROOT)
-    import oracle
-    from implisolid_amd import scenes
-    shape, _ = scenes.config5_objects(64, 128)[k]
+_C5_WORKER = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+import oracle
+from implisolid_amd import scenes
+objs = scenes.config5_objects(64, 128)
+for k in map(int, sys.argv[2].split(",")):
+    shape, _ = objs[k]
     t0 = time.perf_counter()
     v, f = oracle.marching_cubes(oracle.mp5_to_nodes(json.dumps(shape)), 128, [-1.0, 1.0] * 3)
-    return k, time.perf_counter() - t0, int(v.shape[0]), int(f.shape[0])
+    print(json.dumps([k, time.perf_counter() - t0, int(v.shape[0]), int(f.shape[0])]), flush=True)
+"""
 
 
 def config5_cpu_baseline(n_objects=64):
     """config 5's CPU figure on N = cores processes -- the oracle polygonises the 64
-    objects at 128^3 (the whole stream, not a sample), one object per task, over a pool of as many
-    processes as this process may use (the affinity mask, capped by OMP_NUM_THREADS, which the GPU
-    box sets to its CPU share).  Worker processes are spawned (fresh interpreters, nothing inherited
-    from this process's GPU context)."""
-    import multiprocessing as mp
+    objects at 128^3 (the whole stream, not a sample) on as many worker processes as this process
+    may use (the affinity mask, capped by OMP_NUM_THREADS, which the GPU box sets to its CPU share).
+    Each worker is a plain child interpreter (subprocess, nothing inherited from this process's GPU
+    context, no multiprocessing semaphores or resource tracker) taking every cores-th object; all of
+    them are reaped before this returns."""
+    import subprocess
     import oracle
     oracle.build()
     try:
@@ -137,27 +141,30 @@ def config5_cpu_baseline(n_objects=64):
     if cap and cap.isdigit() and int(cap) > 0:
         cores = min(cores, int(cap))
     cores = max(1, min(cores, n_objects))
-    ctx = mp.get_context("spawn")
+    env = dict(os.environ, OMP_NUM_THREADS="1")
     t0 = time.perf_counter()
-    pool = ctx.Pool(cores)
+    procs = [subprocess.Popen([sys.executable, "-c", _C5_WORKER, ROOT,
+                               ",".join(str(k) for k in range(w, n_objects, cores))],
+                              stdout=subprocess.PIPE, text=True, env=env) for w in range(cores)]
+    rows = []
     try:
-        rows = pool.map(_c5_oracle_object, range(n_objects), chunksize=1)
-        pool.close()
+        for p in procs:
+            out, _ = p.communicate(timeout=600)
+            if p.returncode != 0:
+                raise RuntimeError("config-5 oracle worker exited with %d" % p.returncode)
+            rows += [json.loads(line) for line in out.splitlines() if line.strip()]
     finally:
-        pool.terminate()
-        pool.join()   # every worker reaped before the bench goes on
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
     wall = time.perf_counter() - t0
-    # the spawn context started multiprocessing's resource tracker for the pool's semaphores: stop
-    # it now, so the bench leaves no child process behind (BENCH_r03 recorded one at its end)
-    try:
-        from multiprocessing import resource_tracker
-        resource_tracker._resource_tracker._stop()
-    except Exception:
-        pass
+    if len(rows) != n_objects:
+        raise RuntimeError("config-5 oracle workers returned %d of %d objects" % (len(rows), n_objects))
     one = sum(r[1] for r in rows)
     return {"value": round(n_objects / wall, 2), "unit": "objects/s", "cores": cores, "kind": "port",
-            "sample": "oracle restatement (C): all %d config-5 objects at 128^3, eval+MC, one object per task on "
-                      "%d processes (%.2f s wall incl. process start; %.1f s summed per-object CPU time = %.2f "
+            "sample": "oracle restatement (C): all %d config-5 objects at 128^3, eval+MC, the objects dealt over "
+                      "%d worker processes (%.2f s wall incl. process start; %.1f s summed per-object CPU time = %.2f "
                       "objects/s on one core)" % (n_objects, cores, wall, one, n_objects / one),
             "mvoxels_per_s": round(n_objects * 128 ** 3 / wall / 1e6, 2),
             "faces": sum(r[3] for r in rows)}
@@ -213,7 +220,22 @@ def headline_parity(name, v, f):
     sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
     same = sha(v) == s["sha256_verts"]
     diff = 0.0 if same else None
-    if not same and len(v) == s["n_verts"]:
+    over = "all vertices" if same else "the summary's 4096 sampled rows"
+    full = None
+    if not same and len(v) == s["n_verts"]:   # the oracle's full vertex array, where one is committed
+        try:
+            full = np.load(os.path.join(ROOT, "tests", "golden", "headline_ob02_verts.npz"))[name]
+        except Exception:
+            full = None
+    if full is not None:
+        v = np.asarray(v)
+        fin = np.isfinite(full).all(1)
+        d = np.abs(v[fin].astype(np.float64) - full[fin])
+        diff = float(d.max(initial=0.0))
+        over = "all vertices (the oracle's full array): %.5f of the rows bit-identical" % float((d == 0).all(1).mean())
+        if not np.array_equal(np.isfinite(v).all(1), fin):
+            diff = float("inf")
+    elif not same and len(v) == s["n_verts"]:
         # the oracle's 4096 sampled rows (trees with a twist: the gradient's double cos)
         try:
             smp = np.load(os.path.join(ROOT, "tests", "golden", "headline_samples.npz"))
@@ -224,7 +246,7 @@ def headline_parity(name, v, f):
             diff = None
     return {"checked": True, "against": "oracle summary " + name, "verts": int(len(v)), "faces": int(len(f)),
             "faces_identical": sha(f) == s["sha256_faces"], "verts_identical": same,
-            "max_abs_v_diff": diff, "v_diff_over": "all vertices" if same else "the summary's 4096 sampled rows"}
+            "max_abs_v_diff": diff, "v_diff_over": over}
 
 
 def copy_attainable(dev, nbytes=1 << 30, reps=10):
@@ -269,8 +291,7 @@ def main():
     ap.add_argument("--bake", type=int, default=None,
                     help="tree modules with the matrices baked in: 0 never, 1 every object, 2 hot objects (library default)")
     ap.add_argument("--graph", action="store_true",
-                    help="N = 1: replay the step as a hipGraph (measured no faster than direct launches: "
-                         "0.176 vs 0.172 ms at 512^3)")
+                    help="N = 1: replay the step as a hipGraph (an A/B switch; direct launches are the default)")
     args = ap.parse_args()
 
     import torch
@@ -616,8 +637,8 @@ def main():
     # against the oracle's committed summary
     ob02_sharded = None
     if world > 1 and not args.skip_ob02:
-        def run_ob02_sharded():
-            shape, mc = scenes.config3_shifted(256)
+        def run_ob02_sharded(Re=256):
+            shape, mc = scenes.config3_shifted(Re)
             cuts = D.balanced_cuts(shape, mc, world)
             slab = I.Slab(shape, mc, rank, world, cuts=cuts)
             cnt = torch.zeros(4, dtype=torch.int32, device=dev)
@@ -645,17 +666,22 @@ def main():
                 t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 times.append(float(t.item()))
-            out_ = {"workload": "config 3 on the shifted box (scenes.config3_shifted) at 256^3: MC on %d balanced Z-slabs, "
-                                "then 3 x [resample, project, QEM] sharded by owned vertex ranges" % world,
+            out_ = {"workload": "config %s on the shifted box (scenes.config3_shifted) at %d^3: MC on %d balanced Z-slabs, "
+                                "then 3 x [resample, project, QEM] sharded by owned vertex ranges"
+                                % ("3" if Re == 256 else "4", Re, world),
                     "ob02_ms": round(min(times) * 1e3, 3), "verts": int(V.numel() // 3), "faces": int(F.numel() // 3),
                     "owned_verts": [int(voff[r + 1] - voff[r]) for r in range(world)]}
             if rank == 0:
-                out_["parity"] = headline_parity("config3s_ob02_r256", *res)
+                out_["parity"] = headline_parity("config3s_ob02_r256" if Re == 256 else "config4s_ob02_r512", *res)
             return out_
         try:
             ob02_sharded = leg("ob02_sharded", run_ob02_sharded)
         except Exception as exc:   # reported, never the reason the bench line is lost
             ob02_sharded = {"error": repr(exc)[:300]}
+        try:   # config 4's size
+            ob02_sharded["r512"] = leg("ob02_sharded_r512", lambda: run_ob02_sharded(512))
+        except Exception as exc:
+            ob02_sharded["r512"] = {"error": repr(exc)[:300]}
 
     # N = 1: the sharded OB02 loop's 8-rank critical path, estimated on this GPU: config 3
     # on the shifted box at 256^3, its MC mesh owned by the 8 balanced slabs' vertex ranges, every
@@ -665,9 +691,9 @@ def main():
     # bytes over xGMI); the same loop on one shard is the single-GPU figure beside it.
     ob02_est = None
     if world == 1 and not args.skip_ob02:
-        def run_ob02_estimate(n=8):
+        def run_ob02_estimate(Re=256, n=8):
             from implisolid_amd import distributed as D
-            shape, mc = scenes.config3_shifted(256)
+            shape, mc = scenes.config3_shifted(Re)
             cuts = D.balanced_cuts(shape, mc, n)
             nvs = []
             for r in range(n):
@@ -692,8 +718,8 @@ def main():
             nbytes = st8["exchange_bytes"]
             per_rank = [b / n for b in nbytes]
             ex_ms = sum(0.025 + pb / 50e9 * 1e3 for pb in per_rank)
-            return {"workload": "config 3 on the shifted box (scenes.config3_shifted) at 256^3, 3 x [resample, project, "
-                                "QEM], the MC mesh's vertices owned by the 8 balanced Z-slabs",
+            return {"workload": "config %s on the shifted box (scenes.config3_shifted) at %d^3, 3 x [resample, project, "
+                                "QEM], the MC mesh's vertices owned by the 8 balanced Z-slabs" % ("3" if Re == 256 else "4", Re),
                     "shards": n, "owned_verts": nvs, "steps": [x["step"] + ":" + str(x["exchange"]) for x in st8["steps"]],
                     "loop_compute_ms_8": round(crit, 4), "loop_compute_ms_1": round(one, 4),
                     "step_max_ms": [max(x["shard_ms"]) for x in st8["steps"]],
@@ -704,11 +730,15 @@ def main():
                                       "measured: one GPU here)",
                     "estimate_ms_8": round(crit + ex_ms + max(st8["attach_ms"]), 4),
                     "single_ms": round(one + st1["attach_ms"][0], 4),
-                    "parity": headline_parity("config3s_ob02_r256", v, f)}
+                    "parity": headline_parity("config3s_ob02_r256" if Re == 256 else "config4s_ob02_r512", v, f)}
         try:
             ob02_est = leg("ob02_sharded_estimate", run_ob02_estimate)
         except Exception as exc:   # an estimate, never the reason the bench line is lost
             ob02_est = {"error": repr(exc)[:300]}
+        try:   # config 4's size: the 512^3 mesh
+            ob02_est["r512"] = leg("ob02_sharded_estimate_r512", lambda: run_ob02_estimate(512))
+        except Exception as exc:
+            ob02_est["r512"] = {"error": repr(exc)[:300]}
 
     c5 = None
     if world == 1 and not args.skip_config5:
@@ -782,7 +812,10 @@ def main():
     # NaN normals at a singular sample); on the box shifted by 0.003 the alpha
     # search and bisection run on every face (config3s)
     ob02_legs = (("config2_r128", scenes.config2(128)), ("config3_r256", scenes.config3(256)),
-                 ("config3s_r256", scenes.config3_shifted(256)))
+                 ("config3s_r256", scenes.config3_shifted(256)), ("config4s_r512", scenes.config3_shifted(512)))
+    # the oracle takes ~60 s for the 512^3 loop: that leg is checked against the committed summary
+    # of the same workload (tests/golden/make_headline.py config4s_ob02_r512) instead of a live run
+    ob02_summary = {"config4s_r512": "config4s_ob02_r512"}
     if world == 1 and not args.skip_ob02:
         ob02 = {}
         for key, (shape, mc) in ob02_legs:
@@ -801,6 +834,8 @@ def main():
             ob02[key] = {"build_geometry_ms": round(min(ts) * 1e3, 3), "first_build_ms": round(t_first * 1e3, 3),
                          "verts": int(len(v)), "faces": int(len(f)),
                          "steps": "MC + 3 x [vertex resampling, centroid projection, QEM]"}
+            if key in ob02_summary:
+                ob02[key]["parity"] = headline_parity(ob02_summary[key], v, f)
             # one profiled build (stream drained at every stage boundary): per-stage times, the
             # projection's evaluation count, and SURVEY.md 8d's per-iteration algorithmic bytes over them
             # (resample 60 F + 28 V, project (24 + 12 k) F with k evaluations per face, QEM (12 + 36 deg) V)
@@ -825,6 +860,10 @@ def main():
                 "note": "profiled build: the stream is drained at each stage boundary (edge_fold includes the "
                         "projection's prep pass, which overlaps the host fold in unprofiled builds)"}
         ob02["config3s_r256"]["workload"] = "config 3 with its box shifted by 0.003 (scenes.config3_shifted): finite average edge length, live alpha search + bisection"
+        ob02["config4s_r512"]["workload"] = ("config 4: the same tree at 512^3 on the shifted box, the same loop; parity "
+                                             "against the oracle's committed summary (the oracle ran %.1f s for it "
+                                             "in the build container, one core)" % json.load(open(os.path.join(
+                                                 ROOT, "tests", "golden", "headline_summaries.json")))["config4s_ob02_r512"]["oracle_s"])
         legs["ob02"] = round(time.perf_counter() - t_leg, 2)
         if not args.no_cpu_baseline:
             # the oracle runs every configuration on this host: its time on one core, and max|v - v_ref|
@@ -834,6 +873,8 @@ def main():
             progress("ob02_cpu_oracle ...")
             t_leg = time.perf_counter()
             for key, (shape, mc) in ob02_legs:
+                if key in ob02_summary:
+                    continue
                 v, f = I.make_geometry(shape, mc)
                 t0 = time.perf_counter()
                 v_ref, f_ref = oracle.polygonize(json.dumps(shape), json.dumps(mc))

@@ -201,6 +201,37 @@ def ob02_plan(st):
     return out
 
 
+def shard_transfers(voff, halos, rank, kind="halo"):
+    """The vertex ranges one exchange moves for `rank` (a pure function: every exchange path --
+    ob02_sharded over RCCL and over gloo, and ob02_shards_local's device copies -- takes its ranges
+    from here).  voff: the owned-range offsets (world + 1); halos[q]: (h0, h1), the vertex range
+    rank q's next resampling reads (Ob02Shard.halo()).
+      kind "halo": rank sends q the owned vertices inside q's halo, and receives from q q's owned
+                   vertices inside its own halo;
+      kind "full": rank sends its whole owned range to every q and receives every q's.
+    Returns (sends, recvs): lists of (peer, a, b) vertex ranges [a, b), non-empty, peers ascending.
+    What r sends q is exactly what q receives from r (tests/test_cpu.py::test_shard_transfers_*)."""
+    world = len(voff) - 1
+    v0, v1 = int(voff[rank]), int(voff[rank + 1])
+    sends, recvs = [], []
+    for q in range(world):
+        if q == rank:
+            continue
+        q0, q1 = int(voff[q]), int(voff[q + 1])
+        if kind == "halo":
+            a, b = max(v0, int(halos[q][0])), min(v1, int(halos[q][1]))        # my owned vertices q reads
+            c, d = max(q0, int(halos[rank][0])), min(q1, int(halos[rank][1]))  # q's owned vertices I read
+        elif kind == "full":
+            a, b, c, d = v0, v1, q0, q1
+        else:
+            raise ValueError("kind must be 'halo' or 'full'")
+        if a < b:
+            sends.append((q, a, b))
+        if c < d:
+            recvs.append((q, c, d))
+    return sends, recvs
+
+
 def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_step=None, halo=True):
     """The OB02 loop (ob02_plan) over Z-slab shards: every rank holds the whole mesh and owns its
     slab's vertices [voff[rank], voff[rank + 1]).  Stream-ordered: the loop runs on the shard's HIP
@@ -256,16 +287,7 @@ def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_ste
                 ob.unpack(rows.data_ptr(), m, voff, rank)
 
         def halo_exchange():
-            sends, recvs = [], []
-            for q in range(world):
-                if q == rank:
-                    continue
-                a, b = max(v0, H[q][0]), min(v1, H[q][1])          # my owned vertices q reads
-                if a < b:
-                    sends.append((q, a, b))
-                a, b = max(voff[q], H[rank][0]), min(voff[q + 1], H[rank][1])   # q's that I read
-                if a < b:
-                    recvs.append((q, a, b))
+            sends, recvs = shard_transfers(voff, H, rank, "halo")
             if gloo:
                 s_ob.synchronize()
                 host = W.cpu()
@@ -348,15 +370,9 @@ def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
                 s.synchronize()
             moved = 0
             for r in range(n):
-                for q in range(n):
-                    if q == r:
-                        continue
-                    a, b = voff[q], voff[q + 1]
-                    if kind == "halo":
-                        a, b = max(a, H[r][0]), min(b, H[r][1])
-                    if a < b:
-                        Ws[r][3 * a:3 * b].copy_(Ws[q][3 * a:3 * b])
-                        moved += 12 * (b - a)
+                for q, a, b in shard_transfers(voff, H, r, kind)[1]:
+                    Ws[r][3 * a:3 * b].copy_(Ws[q][3 * a:3 * b])
+                    moved += 12 * (b - a)
             torch.cuda.synchronize(device)
             return moved
 

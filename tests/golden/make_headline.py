@@ -15,6 +15,8 @@ run alone takes ~16 s of CPU):
   config2_ob02_r128 config 2 (sphere u rabbit, R = 128, MC + 3 x [resample, project, QEM])
   config3s_ob02_r256 config 3 with its box shifted by 0.003 (scenes.config3_shifted): no singular
                     sample, every vertex finite, so the alpha search and bisection run on every face
+  config4_ob02_r512 / config4s_ob02_r512   config 4: the same tree at R = 512 through the same
+                    loop, on the dyadic box and on the box shifted by 0.003
   config5_mc_r128   config 5's 64 objects at 128^3, eval + MC: per object V / F and the SHA-256s
 
 Per configuration: V / F counts, SHA-256 of the face array, SHA-256 of the vertex array (for the
@@ -60,6 +62,9 @@ def configs():
         "config3_ob02_r256": scenes.config3(256),
         "config2_ob02_r128": scenes.config2(128),
         "config3s_ob02_r256": scenes.config3_shifted(256),
+        # config 4's tree at 512^3 through the whole OB02 loop (BASELINE config 4 "eval + MC (+ OB02)")
+        "config4_ob02_r512": scenes.config3(512),
+        "config4s_ob02_r512": scenes.config3_shifted(512),
     }
 
 
@@ -112,7 +117,7 @@ def main():
     # 1e-5, the twist's gradient going through the double cos): every row, not only the samples
     path_v = os.path.join(HERE, "headline_ob02_verts.npz")
     full = dict(np.load(path_v)) if (not redo and os.path.exists(path_v)) else {}
-    for name in ("config3_ob02_r256", "config3s_ob02_r256"):
+    for name in ("config3_ob02_r256", "config3s_ob02_r256", "config4s_ob02_r512"):
         if name in full:
             continue
         shape, mc = out[name]["shape"], out[name]["mc"]

@@ -639,3 +639,44 @@ def test_ob02_exchange_plan(impli):
     proj_only = impli.parse_settings(scenes.mc_settings(32, 1.0, projection=1, qem=1, overall_repeats=2))
     assert D.ob02_plan(proj_only) == [("P", "full"), ("P", "full")]
     assert D.ob02_plan(impli.parse_settings(scenes.mc_settings(32, 1.0))) == []
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_transfers_symmetric_and_covering(world):
+    """distributed.shard_transfers (the ranges every exchange path of the sharded OB02 loop moves:
+    RCCL point-to-point / all-gather, gloo, and the one-process device copies): what rank r sends q
+    is what q receives from r, nothing is sent to oneself, and after a halo exchange each rank holds
+    its whole halo (own range plus the received ranges tile it exactly); a full exchange gives every
+    rank every other rank's owned range."""
+    from implisolid_amd import distributed as D
+    rng = np.random.default_rng(world)
+    for trial in range(200):
+        cuts = np.sort(rng.integers(0, 5000, size=world - 1))
+        voff = [0] + [int(c) for c in cuts] + [5000]
+        halos = []
+        for r in range(world):   # a halo reaches a little below and above the owned range
+            lo = max(0, voff[r] - int(rng.integers(0, 400)))
+            hi = min(5000, voff[r + 1] + int(rng.integers(0, 400)))
+            halos.append((lo, hi) if voff[r] < voff[r + 1] else (0, 0))
+        for kind in ("halo", "full"):
+            plans = [D.shard_transfers(voff, halos, r, kind) for r in range(world)]
+            for r, (sends, recvs) in enumerate(plans):
+                assert all(q != r and a < b for q, a, b in sends + recvs)
+                for q, a, b in sends:
+                    assert (r, a, b) in plans[q][1]
+                    assert voff[r] <= a and b <= voff[r + 1]
+                for q, a, b in recvs:
+                    assert (r, a, b) in plans[q][0]
+                    assert voff[q] <= a and b <= voff[q + 1]
+                have = np.zeros(5000, bool)
+                have[voff[r]:voff[r + 1]] = True
+                for q, a, b in recvs:
+                    assert not have[a:b].any()
+                    have[a:b] = True
+                want = np.zeros(5000, bool)
+                if kind == "full":
+                    want[:] = True
+                else:
+                    want[halos[r][0]:halos[r][1]] = True
+                    want[voff[r]:voff[r + 1]] = True
+                assert np.array_equal(have, want)

@@ -1166,7 +1166,7 @@ def _headline():
 
 
 @pytest.mark.parametrize("name", ["config4_mc_r512", "config4_mc_r256", "config3_ob02_r256", "config3s_ob02_r256",
-                                  "config2_ob02_r128"])
+                                  "config2_ob02_r128", "config4_ob02_r512", "config4s_ob02_r512"])
 def test_headline_against_oracle_summary(impli, name):
     """The exact meshes bench.py times (config 4's tree at 512^3 and 256^3, eval + MC) and the OB02
     legs it reports (config 3 at 256^3, config 2 at 128^3, 3 repeats of resample + project + QEM),
@@ -1203,13 +1203,14 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def test_config3_shifted_projection_live(impli):
-    """Config 3 at 256^3 on the shifted box (scenes.config3_shifted): the average edge length stays
-    finite, so the projection runs its alpha search and bisection on the faces (many evaluations
-    per face and repeat, not config 3's one), and the mesh is still the oracle's (faces SHA-256,
-    every vertex finite, sampled rows within 1e-5: the tree holds a twist)."""
+@pytest.mark.parametrize("name", ["config3s_ob02_r256", "config4s_ob02_r512"])
+def test_config3_shifted_projection_live(impli, name):
+    """Config 3 at 256^3 and config 4 at 512^3 on the shifted box (scenes.config3_shifted): the
+    average edge length stays finite, so the projection runs its alpha search and bisection on the
+    faces (many evaluations per face and repeat, not config 3's one), and the mesh is still the
+    oracle's (faces SHA-256, every vertex finite, sampled rows within 1e-5: the tree holds a twist)."""
     summ, samples = _headline()
-    s = summ["config3s_ob02_r256"]
+    s = summ[name]
     impli.ob02_profile(True)
     try:
         v, f = impli.make_geometry(s["shape"], s["mc"])
@@ -1217,7 +1218,7 @@ def test_config3_shifted_projection_live(impli):
     finally:
         impli.ob02_profile(False)
     assert _sha(f) == s["sha256_faces"] and np.isfinite(v).all() and s["nonfinite_rows"] == []
-    idx, vs = samples["config3s_ob02_r256_idx"], samples["config3s_ob02_r256_v"]
+    idx, vs = samples[name + "_idx"], samples[name + "_v"]
     assert np.abs(v[idx].astype(np.float64) - vs).max() < 1e-5
     evals_per_face = st["projection_evals"] / (len(f) * s["mc"]["overall_repeats"])
     assert evals_per_face > 10, evals_per_face
@@ -1539,3 +1540,36 @@ def test_multiprocess_slabs_gloo(impli, oracle, tmp_path, world, balanced):
     assert np.array_equal(g["verts"].view(np.uint32), vr.view(np.uint32))
     if balanced:
         assert len(g["cuts"]) == world + 1
+
+
+def test_config4_ob02_r512_sharded_against_summary(impli):
+    """Config 4's OB02 loop at its own size: the tree at 512^3 on the shifted box (live alpha search
+    and bisection), the MC mesh's vertices owned by the 8 balanced Z-slabs' ranges, every shard
+    stepped on its own stream with the halo / full exchanges (distributed.ob02_shards_local, the
+    bench's 8-rank estimate), against the oracle's summary (tests/golden/make_headline.py
+    config4s_ob02_r512): faces byte-identical, every vertex row within 1e-5 of the oracle's full
+    array (the tree holds a twist), > 99.9 % of them bit-identical."""
+    import torch
+    from implisolid_amd import distributed as D
+    summ, _ = _headline()
+    s = summ["config4s_ob02_r512"]
+    shape, mc = s["shape"], s["mc"]
+    cuts = D.balanced_cuts(shape, mc, 8)
+    nvs = []
+    for r in range(8):
+        sl = impli.Slab(shape, mc, r, 8, cuts=cuts)
+        nvs.append(sl.run()[0])
+        sl.close()
+    mc_only = dict(mc, vresampl={"iters": 0, "c": 1.0}, projection={"enabled": 0}, qem={"enabled": 0},
+                   subdiv={"enabled": 0})
+    v_mc, f_mc = impli.make_geometry(shape, mc_only)
+    assert sum(nvs) == len(v_mc)
+    V = torch.from_numpy(v_mc.reshape(-1).copy()).cuda()
+    F = torch.from_numpy(f_mc.reshape(-1).copy()).cuda()
+    voff = np.concatenate([[0], np.cumsum(nvs)]).astype(np.int64)
+    v, f, _ = D.ob02_shards_local(shape, mc, V, F, voff)
+    assert _sha(f) == s["sha256_faces"] and np.isfinite(v).all()
+    vr = np.load(_golden("headline_ob02_verts.npz"))["config4s_ob02_r512"]
+    d = np.abs(v.astype(np.float64) - vr)
+    assert d.max() < 1e-5, d.max()
+    assert (d == 0).all(1).mean() > 0.999
