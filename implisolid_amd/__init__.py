@@ -342,6 +342,23 @@ def make_geometry(shape, mc_settings):
     return v, f
 
 
+def make_geometry_views(shape, mc_settings):
+    """build_geometry as the reference's front end reads it (implisolid_main.js:227-237): the mesh is
+    left in the library's result buffers (pinned host memory) and returned as numpy views over
+    get_v_ptr / get_f_ptr -- no copy.  The views are valid until the next build_geometry or
+    finish_geometry; copy them to keep them."""
+    L = lib()
+    L.finish_geometry()
+    L.build_geometry(_s(shape), _s(mc_settings))
+    _check()
+    nv, nf = L.get_v_size(), L.get_f_size()
+    v = np.ctypeslib.as_array(ctypes.cast(L.get_v_ptr(), ctypes.POINTER(ctypes.c_float)), shape=(nv, 3)) if nv \
+        else np.zeros((0, 3), np.float32)
+    f = np.ctypeslib.as_array(ctypes.cast(L.get_f_ptr(), ctypes.POINTER(ctypes.c_int32)), shape=(nf, 3)) if nf \
+        else np.zeros((0, 3), np.int32)
+    return v, f
+
+
 def make_geometry_progressive(shape, mc_settings, call_specs=None):
     """build_geometry_u with a progress hook (the reference's worker path, worker_api.js:315-345 and
     send_progress_update :399-416): returns (verts, faces, updates), updates = the intermediate

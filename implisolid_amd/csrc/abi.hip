@@ -125,6 +125,12 @@ hipStream_t abi_stream() {
     return s;
 }
 
+hipStream_t abi_copy_stream() {   // the vertices' device-to-host copy beside the face pass
+    static hipStream_t s = nullptr;
+    if (!s) IMPLI_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+}
+
 // ---- build_geometry over several devices (implisolid_set_devices) -------------------------------
 std::vector<int> g_devices;   // empty: the current device only
 
@@ -247,16 +253,16 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         ob_ptr->load_mesh(dv.as<float>(), nv, df.as<int32_t>(), nf);
     } else {
         E.set_grid(st.resolution, st.box, 0, 1);
-        roctxRangePush("marching cubes");
-        SlabCounts c = E.marching_cubes(s);   // polygonize_step_0
-        roctxRangePop();
-        nv = c.n_verts();
-        nf = c.n_faces();
         const bool refine = st.overall_repeats > 0 && (st.vresampl_iters > 0 || st.projection || st.subdiv);
-        if (!refine) {   // the MC mesh is the result: straight to the host, no refinement state
-            g_state.verts.resize((size_t)nv * 3);
-            g_state.faces.resize((size_t)nf * 3);
-            E.download(g_state.verts.data(), g_state.faces.data(), c, s);
+        if (!refine) {   // the MC mesh is the result: straight into the library's pinned result buffers
+            roctxRangePush("marching cubes");
+            E.marching_cubes_to_host(s, abi_copy_stream(), [](int64_t v, int64_t f, float** hv, int32_t** hf) {
+                g_state.verts.resize((size_t)v * 3);
+                g_state.faces.resize((size_t)f * 3);
+                *hv = g_state.verts.data();
+                *hf = g_state.faces.data();
+            });
+            roctxRangePop();
             g_last_refined = false;
             send_mesh_back_to_client(nullptr, cs);   // mcc2.cpp:351
             // the repeats of an empty loop still report after their (empty) resampling (:372)
@@ -264,6 +270,11 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
             g_state.active = true;
             return;
         }
+        roctxRangePush("marching cubes");
+        SlabCounts c = E.marching_cubes(s);   // polygonize_step_0
+        roctxRangePop();
+        nv = c.n_verts();
+        nf = c.n_faces();
         if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
         ob_ptr->set_profile(g_ob02_profile);
         ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf);
@@ -531,17 +542,20 @@ int implisolid_debug_fold(const float* terms, int64_t n, float* sum_out, int64_t
     try {
         (void)engine();   // the device context
         int tc = 0;
-        static long long st[11];
+        static long long st[14];
         static int tr[256];
         *sum_out = debug_fold(terms, n, &tc, st, tr);
         if (std::getenv("IMPLISOLID_FOLD_TRACE")) {
-            for (int i = 0; i < 256 && i < st[0] + st[1] + st[2] + st[6]; ++i)
+            for (int i = 0; i < 256 && i < st[0] + st[1] + st[2]; ++i)
                 std::fprintf(stderr, "%s k=%d E=%d\n", (tr[i] >> 28) == 1 ? "table" : (tr[i] >> 28) == 3 ? "jump " : (tr[i] >> 28) == 4 ? "fast+" : (tr[i] >> 28) == 5 ? "fast-" : (tr[i] >> 28) == 6 ? "fastX" : "term ",
                              tr[i] & 0xfffff, ((tr[i] >> 20) & 0xff) - 64);
         }
         if (std::getenv("IMPLISOLID_FOLD_STATS"))
-            std::fprintf(stderr, "fold n=%lld steps zero/serial %lld table %lld terms %lld global-term-loads %lld run-jumps %lld cycles stage %lld walk %lld (table %lld terms %lld) term parts: preamble %lld fast %lld\n",
-                         (long long)n, st[0], st[1], st[2], st[3], st[6], st[4], st[5], st[7], st[8], st[9], st[10]);
+            std::fprintf(stderr, "fold n=%lld steps zero/serial %lld table %lld terms %lld global-term-loads %lld fast %lld "
+                         "fast-finished %lld serial-chunks %lld cycles stage %lld walk %lld (table %lld terms %lld) term parts: "
+                         "preamble %lld fast %lld serial %lld\n",
+                         (long long)n, st[0], st[1], st[2], st[3], st[11], st[12], st[13], st[4], st[5], st[7], st[8], st[9],
+                         st[10], st[6]);
         if (table_chunks) *table_chunks = tc;
     } catch (const std::exception& e) {
         report(e.what(), false);

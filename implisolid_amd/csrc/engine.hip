@@ -156,6 +156,8 @@ void Engine::kernel_times(float out[kTimedKernels]) {
 Engine::~Engine() {
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
+    if (ev_counts_) (void)hipEventDestroy(ev_counts_);
+    if (ev_verts_) (void)hipEventDestroy(ev_verts_);
     DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &claimed_, &vidc_, &vid_halo_, &items_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
@@ -531,6 +533,52 @@ SlabCounts Engine::marching_cubes(hipStream_t s) {
         c = read_counts(s, &of);
         if (of) throw HipError("marching cubes: output capacity overflow after resize");
     }
+    return c;
+}
+
+SlabCounts Engine::marching_cubes_to_host(hipStream_t s, hipStream_t cs,
+                                          const std::function<void(int64_t, int64_t, float**, int32_t**)>& host) {
+    if (!ev_counts_) IMPLI_HIP(hipEventCreateWithFlags(&ev_counts_, hipEventDisableTiming));
+    if (!ev_verts_) IMPLI_HIP(hipEventCreateWithFlags(&ev_verts_, hipEventDisableTiming));
+    hcounters_.reserve(kCounterWords * sizeof(uint32_t));
+    uint32_t* h = hcounters_.as<uint32_t>();
+    eval_field(s);
+    count(s);
+    // the totals land in pinned memory while the emission kernels run behind them
+    IMPLI_HIP(hipMemcpyAsync(h, counters_.p, (kOverflowWord + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipEventRecord(ev_counts_, s));
+    emit_verts(s);
+    IMPLI_HIP(hipEventRecord(ev_verts_, s));
+    emit_faces(nullptr, nullptr, 0, s);
+    IMPLI_HIP(hipEventSynchronize(ev_counts_));
+    SlabCounts c{h[2], h[3], h[4], h[5]};
+    if (!fits(c)) {   // the emission wrote past nothing (it checks its capacity): grow, emit again
+        IMPLI_HIP(hipStreamSynchronize(s));
+        ensure_capacity(c);
+        IMPLI_HIP(hipMemsetAsync(counters_.as<uint32_t>() + kOverflowWord, 0, 4 * sizeof(uint32_t), s));
+        emit(nullptr, s);
+        bool of = false;
+        c = read_counts(s, &of);
+        if (of) throw HipError("marching cubes: output capacity overflow after resize");
+        float* hv = nullptr;
+        int32_t* hf = nullptr;
+        host(c.n_verts(), c.n_faces(), &hv, &hf);
+        download(hv, hf, c, s);
+        return c;
+    }
+    float* hv = nullptr;
+    int32_t* hf = nullptr;
+    host(c.n_verts(), c.n_faces(), &hv, &hf);
+    if (c.n_verts()) {
+        IMPLI_HIP(hipStreamWaitEvent(cs, ev_verts_, 0));
+        IMPLI_HIP(hipMemcpyAsync(hv, verts_.p, (size_t)c.n_verts() * 12, hipMemcpyDeviceToHost, cs));
+    }
+    if (c.n_faces()) IMPLI_HIP(hipMemcpyAsync(hf, faces_.p, (size_t)c.n_faces() * 12, hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipMemcpyAsync(h + kOverflowWord, counters_.as<uint32_t>() + kOverflowWord, sizeof(uint32_t),
+                             hipMemcpyDeviceToHost, s));
+    IMPLI_HIP(hipStreamSynchronize(cs));
+    IMPLI_HIP(hipStreamSynchronize(s));
+    if (h[kOverflowWord] != 0) throw HipError("marching cubes: output overflow within capacity");
     return c;
 }
 

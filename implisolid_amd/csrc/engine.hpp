@@ -1,5 +1,6 @@
 // engine.hpp -- device-resident polygoniser state for one GPU (one Z-slab of one object).
 #pragma once
+#include <functional>
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -90,9 +91,19 @@ public:
     SlabCounts read_counts(hipStream_t stream, bool* overflow);
     // make sure the output buffers can hold the counted mesh (re-run emit() after growing)
     bool ensure_capacity(const SlabCounts& c);
+    bool fits(const SlabCounts& c) const {   // the output buffers hold the counted mesh as they are
+        return (int64_t)c.n_verts() + 1 <= cap_v_ && (int64_t)c.n_faces() + 1 <= cap_f_ &&
+               (int64_t)c.act_total + 1 <= cap_rec_;
+    }
 
     // whole single-GPU marching cubes: eval + count + emit (+ retry on overflow); returns counts
     SlabCounts marching_cubes(hipStream_t stream);
+    // the same straight to host memory, with the copies overlapped: the counts are read back while
+    // the emission kernels run, `host(nv, nf, &verts, &faces)` then sizes the host result, the
+    // vertices' copy runs on copy_stream beside the face pass and the faces' copy follows it on
+    // stream (blocking until both have landed)
+    SlabCounts marching_cubes_to_host(hipStream_t stream, hipStream_t copy_stream,
+                                      const std::function<void(int64_t, int64_t, float**, int32_t**)>& host);
 
     // this object's state for the merged launches of an object stream (kernels.hpp ObjArgs); the
     // pruned path after one eval_field (its unit marks), valid until the buffers grow
@@ -175,6 +186,7 @@ private:
     uint64_t obj_gen_ = 0, key_obj_gen_ = ~0ull;   // set_object's generation / the one the grid's buffers hold
     float key_box_[6] = {};
     HostBuf hcounters_;   // pinned landing zone of read_counts / raw_counters (one small copy)
+    hipEvent_t ev_counts_ = nullptr, ev_verts_ = nullptr;   // marching_cubes_to_host
     DevBuf prog_, rabbit_, cases_;
     DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, claimed_, vidc_, vid_halo_, items_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;

@@ -31,9 +31,10 @@
 namespace impli {
 
 constexpr int kFoldChunk = 256;    // terms per table row (one wave, 4 per lane)
-constexpr int kFoldBinades = 6;    // binades per chunk: E in [base, base + 6), base = the binade of a
-                                   // double-precision estimate of the sum before the chunk, minus 3
-                                   // (the float chain drifts from it by well under a factor 2)
+constexpr int kFoldBinades = 4;    // binades per chunk: E in [base, base + 4), base = the binade of a
+                                   // double-precision estimate of the sum before the chunk, minus 1
+                                   // (the float chain drifts from it by well under a factor 2, and the
+                                   // chunk may take it up two binades more)
 constexpr uint8_t kFoldBad = 1, kFoldNaN = 4;   // a term the pair cannot express; a NaN term
 constexpr uint32_t kFoldCap = 1u << 24;
 
@@ -82,7 +83,7 @@ IMPLI_FOLD_HD inline FoldPair fold_pair_term(uint32_t bits, int E, uint8_t& flag
     return p;
 }
 
-// the window base of a chunk from the estimate of the sum before it (frexp exponent minus 3; a
+// the window base of a chunk from the estimate of the sum before it (frexp exponent minus 1; a
 // zero / tiny / non-finite estimate gives a base no chain value uses: the chunk goes term by term)
 IMPLI_FOLD_HD inline int fold_base(double est) {
     if (!(est >= 0x1p-100) || !(est <= 0x1p100)) return -1000;
@@ -90,7 +91,7 @@ IMPLI_FOLD_HD inline int fold_base(double est) {
     double m = est;
     while (m >= 1.0) { m *= 0.5; ++E; }
     while (m < 0.5) { m *= 2.0; --E; }
-    return E - 3;
+    return E - 1;
 }
 
 // one table cell, in term order (host reference; the device kernel splits the chunk over a wave)

@@ -972,8 +972,8 @@ std::string TreeJit::point_source(const Program& p) {
       << "};\n}  // namespace impli\n"
       << "using impli::JitPt;\nusing impli::ob::ProjArgs;\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_centroid_normals(const float* M, const float* tab,\n"
-      << "    const float* v, const int32_t* f, int64_t nf, float* C, float* N) {\n"
-      << "    impli::ob::centroid_normals_body(JitPt{M, tab}, v, f, nf, C, N);\n}\n"
+      << "    const float* v, const int32_t* f, const int64_t* rng, float* C, float* N) {\n"
+      << "    impli::ob::centroid_normals_body(JitPt{M, tab}, v, f, rng, C, N);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_prep(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_prep_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_early(const float* M, const float* tab, ProjArgs a) {\n"
@@ -981,8 +981,8 @@ std::string TreeJit::point_source(const Program& p) {
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_normals_at(const float* M, const float* tab,\n"
-      << "    const float* P, int64_t n, float* G) {\n"
-      << "    impli::ob::normals_at_body(JitPt{M, tab}, P, n, G);\n}\n"
+      << "    const float* P, const int64_t* rng, float* G) {\n"
+      << "    impli::ob::normals_at_body(JitPt{M, tab}, P, rng, G);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_points(const float* M, const float* tab,\n"
       << "    const float* xyz, int64_t n, float* f, float* grad) {\n"
       << "    impli::ob::points_body(JitPt{M, tab}, xyz, n, f, grad);\n}\n";

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <future>
@@ -168,12 +169,26 @@ __global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ in, i
 // the misc words zeroed (a memset and two copies were three host launch costs on the sync's heels)
 __global__ __launch_bounds__(256) void k_load_mesh(float* __restrict__ v, const float* __restrict__ sv, int64_t nv3,
                                                    int32_t* __restrict__ f, const int32_t* __restrict__ sf, int64_t nf3,
-                                                   uint32_t* __restrict__ deg, int64_t ndeg, uint32_t* __restrict__ misc) {
+                                                   uint32_t* __restrict__ deg, int64_t ndeg, uint32_t* __restrict__ misc,
+                                                   int64_t* __restrict__ rng, int64_t nv, int64_t nf) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < nv3) v[i] = sv[i];
     if (i < nf3) f[i] = sf[i];
     if (i < ndeg) deg[i] = 0u;
     if (i < 16) misc[i] = 0u;
+    if (i < kRngFields) rng[i] = (i == kRngHalo + 1 || i == kRngOwn + 1) ? nv : (i & 1) ? nf : 0;   // the whole mesh
+}
+
+// the range block of one shard: every range the whole mesh, or the owned vertices [v0, v1) with
+// the min / max scratch reset for the range passes (k_work_range, k_fof_range, k_face_vertex_range)
+__global__ void k_ranges_set(int64_t* __restrict__ rng, int64_t v0, int64_t v1, int64_t nv, int64_t nf, int sharded) {
+    const int i = threadIdx.x;
+    if (i < kRngFields) rng[i] = (i == kRngHalo + 1 || i == kRngOwn + 1) ? nv : (i & 1) ? nf : 0;
+    __syncthreads();
+    if (!sharded) return;
+    if (i == kRngOwn) rng[i] = v0;
+    if (i == kRngOwn + 1) rng[i] = v1;
+    if (i >= kRngScratch && i < kRngScratch + 6) rng[i] = (i & 1) ? (int64_t)-1 : INT64_MAX;   // (min, max): empty
 }
 
 __global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const uint32_t* __restrict__ off,
@@ -422,8 +437,9 @@ using namespace ob;
 template <int D>
 __global__ __launch_bounds__(256) void k_centroid_normals(const Program* __restrict__ prog, const float* __restrict__ tab,
                                                           const float* __restrict__ v, const int32_t* __restrict__ f,
-                                                          int64_t nf, float* __restrict__ C, float* __restrict__ N) {
-    centroid_normals_body(InterpPt<D>{prog, tab}, v, f, nf, C, N);
+                                                          const int64_t* __restrict__ rng, float* __restrict__ C,
+                                                          float* __restrict__ N) {
+    centroid_normals_body(InterpPt<D>{prog, tab}, v, f, rng, C, N);
 }
 template <int D>
 __global__ __launch_bounds__(256) void k_project_prep(const Program* __restrict__ prog, const float* __restrict__ tab,
@@ -442,8 +458,9 @@ __global__ __launch_bounds__(256) void k_project_late(const Program* __restrict_
 }
 template <int D>
 __global__ __launch_bounds__(256) void k_normals_at(const Program* __restrict__ prog, const float* __restrict__ tab,
-                                                    const float* __restrict__ P, int64_t n, float* __restrict__ G) {
-    normals_at_body(InterpPt<D>{prog, tab}, P, n, G);
+                                                    const float* __restrict__ P, const int64_t* __restrict__ rng,
+                                                    float* __restrict__ G) {
+    normals_at_body(InterpPt<D>{prog, tab}, P, rng, G);
 }
 
 // ---- step 1 ----------------------------------------------------------------------------------
@@ -497,12 +514,13 @@ __device__ __forceinline__ float kij(int64_t i, int64_t j, const float* __restri
 }
 
 __global__ void k_face_weights(const float* __restrict__ C, const float* __restrict__ N, const int32_t* __restrict__ fof,
-                               int64_t i0, int64_t i1, float c, float* __restrict__ W) {   // faces [i0, i1)
-    const int64_t i = i0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= i1) return;
-    float ki = 0;   // wi, vertex_resampling.hpp:79-91
-    for (int j = 0; j < 3; ++j) ki += kij(i, fof[3 * i + j], C, N);
-    W[i] = (float)(1.0 + (double)(c * ki));
+                               const int64_t* __restrict__ rng, float c, float* __restrict__ W) {   // faces [rng[0], rng[1])
+    const int64_t i1 = rng[1];
+    for (int64_t i = rng[0] + grid_lane(); i < i1; i += grid_lanes()) {
+        float ki = 0;   // wi, vertex_resampling.hpp:79-91
+        for (int j = 0; j < 3; ++j) ki += kij(i, fof[3 * i + j], C, N);
+        W[i] = (float)(1.0 + (double)(c * ki));
+    }
 }
 
 __global__ void k_resample(const uint32_t* __restrict__ off, const int32_t* __restrict__ lst, const float* __restrict__ W,
@@ -523,50 +541,96 @@ __global__ void k_resample(const uint32_t* __restrict__ off, const int32_t* __re
     out[3 * v] = x; out[3 * v + 1] = y; out[3 * v + 2] = z;
 }
 
-// the faces [out[0], out[1]] touching a vertex in [v0, v1) (slab sharding): min / max face index
-__global__ void k_touch_range(const int32_t* __restrict__ f, int64_t nf, int64_t v0, int64_t v1,
-                              unsigned long long* __restrict__ out) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= nf) return;
-    bool t = false;
+// A shard's ranges on the device (Ob02::set_owned_vertices; no host round trip), each pass a
+// min / max over the previous pass's range, one atomic pair per wave:
+//   k_work_range         the work faces: faces touching an owned vertex = the first and last face
+//                        of the owned vertices' umbrellas (sorted ascending)
+//   k_fof_range          the faces the work faces' resampling weights read: those and their edge
+//                        neighbours
+//   k_face_vertex_range  the vertices of those faces (the next resampling's one-ring halo)
+//   k_ranges_final       the min / max pairs to half-open ranges (an empty work range: none)
+__device__ __forceinline__ void wave_minmax_atomic(long long lo, long long hi, long long* out) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) t = t || (f[3 * j + q] >= v0 && f[3 * j + q] < v1);
-    if (t) {
-        atomicMin(&out[0], (unsigned long long)j);
-        atomicMax(&out[1], (unsigned long long)j);
+    for (int d = 32; d >= 1; d >>= 1) {
+        const long long a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
     }
-}
-// the lowest and highest vertex of faces [j0, j1) (out[0], out[1])
-__global__ void k_face_vertex_range(const int32_t* __restrict__ f, int64_t j0, int64_t j1, unsigned long long* __restrict__ out) {
-    const int64_t j = j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= j1) return;
-    unsigned long long lo = ~0ull, hi = 0ull;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int32_t v = f[3 * j + q];
-        if (v >= 0) {
-            lo = (unsigned long long)v < lo ? (unsigned long long)v : lo;
-            hi = (unsigned long long)v > hi ? (unsigned long long)v : hi;
+    if ((threadIdx.x & 63) == 0) {
+        if (lo <= hi) {
+            atomicMin(&out[0], lo);
+            atomicMax(&out[1], hi);
         }
     }
-    atomicMin(&out[0], lo);
-    atomicMax(&out[1], hi);
 }
-// ... and the min / max over those faces' edge neighbours (the faces the weights read)
-__global__ void k_fof_range(const int32_t* __restrict__ fof, int64_t j0, int64_t j1, unsigned long long* __restrict__ out) {
-    const int64_t j = j0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= j1) return;
-    unsigned long long lo = (unsigned long long)j, hi = (unsigned long long)j;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int32_t g = fof[3 * j + q];
-        if (g >= 0) {
-            lo = (unsigned long long)g < lo ? (unsigned long long)g : lo;
-            hi = (unsigned long long)g > hi ? (unsigned long long)g : hi;
+constexpr long long kNoMin = 0x7fffffffffffffffll;
+
+__global__ __launch_bounds__(256) void k_work_range(const uint32_t* __restrict__ off, const int32_t* __restrict__ lst,
+                                                    int64_t* __restrict__ rng) {
+    const int64_t v1 = rng[kRngOwn + 1];
+    long long lo = kNoMin, hi = -1;
+    for (int64_t v = rng[kRngOwn] + grid_lane(); v < v1; v += grid_lanes()) {
+        const uint32_t a = off[v], e = off[v + 1];
+        if (a < e) {
+            lo = min(lo, (long long)lst[a]);
+            hi = max(hi, (long long)lst[e - 1]);
         }
     }
-    atomicMin(&out[2], lo);
-    atomicMax(&out[3], hi);
+    wave_minmax_atomic(lo, hi, (long long*)rng + kRngScratch);
+}
+
+__global__ __launch_bounds__(256) void k_fof_range(const int32_t* __restrict__ fof, int64_t* __restrict__ rng) {
+    const long long j0 = rng[kRngScratch], j1 = rng[kRngScratch + 1];   // inclusive (j0 > j1: empty)
+    if (j0 > j1) return;   // uniform
+    long long lo = kNoMin, hi = -1;
+    for (long long j = j0 + grid_lane(); j <= j1; j += grid_lanes()) {
+        lo = min(lo, j);
+        hi = max(hi, j);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int32_t g = fof[3 * j + q];
+            if (g >= 0) {
+                lo = min(lo, (long long)g);
+                hi = max(hi, (long long)g);
+            }
+        }
+    }
+    wave_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 2);
+}
+
+__global__ __launch_bounds__(256) void k_face_vertex_range(const int32_t* __restrict__ f, int64_t* __restrict__ rng) {
+    const long long j0 = rng[kRngScratch + 2], j1 = rng[kRngScratch + 3];   // inclusive (j0 > j1: empty)
+    if (j0 > j1) return;   // uniform
+    long long lo = kNoMin, hi = -1;
+    for (long long j = j0 + grid_lane(); j <= j1; j += grid_lanes()) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int32_t v = f[3 * j + q];
+            if (v >= 0) {
+                lo = min(lo, (long long)v);
+                hi = max(hi, (long long)v);
+            }
+        }
+    }
+    wave_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 4);
+}
+
+__global__ void k_ranges_final(int64_t* __restrict__ rng) {
+    if (threadIdx.x != 0) return;
+    const int64_t v0 = rng[kRngOwn], v1 = rng[kRngOwn + 1];
+    const int64_t* m = rng + kRngScratch;
+    if (m[0] > m[1]) {   // no face touches the owned vertices
+        rng[kRngWork] = rng[kRngWork + 1] = rng[kRngCen] = rng[kRngCen + 1] = 0;
+        rng[kRngHalo] = v0;
+        rng[kRngHalo + 1] = v1;
+        return;
+    }
+    rng[kRngWork] = m[0];
+    rng[kRngWork + 1] = m[1] + 1;
+    rng[kRngCen] = m[2];
+    rng[kRngCen + 1] = m[3] + 1;
+    rng[kRngHalo] = m[4] < v0 ? m[4] : v0;
+    rng[kRngHalo + 1] = m[5] + 1 > v1 ? m[5] + 1 : v1;
 }
 
 // ---- step 2 ----------------------------------------------------------------------------------
@@ -729,7 +793,7 @@ __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e,
             pairs[c * kFoldBinades + b] = all;
             flags[c * kFoldBinades + b] = (uint8_t)f;
         }
-        if (b == 3 || b == 4) fl34 |= f;
+        if (b == 1 || b == 2) fl34 |= f;   // the binades of the estimate and of twice it
     }
     if (lane == 0) {
         const double lo = est_c * (1.0 - 0x1p-7), hi = est_c1 * (1.0 + 0x1p-7);
@@ -785,24 +849,35 @@ __device__ void alpha_list_dev(float avg, FoldOut* o) {
 // One block: its waves stage a window of the table (kWalkWindow chunk rows) and the terms of the
 // window's hinted chunks (kWalkSlots of them) in LDS, then wave 0 walks the window from LDS; terms
 // of an unhinted chunk the walk needs are read from memory.
-constexpr int kWalkThreads = 1024, kWalkWindow = 1536, kWalkSlots = 40, kWalkB0 = 2, kWalkBins = kFoldBinades - kWalkB0;
+constexpr int kWalkThreads = 1024, kWalkWindow = 1536, kWalkSlots = 64, kWalkB0 = 0, kWalkBins = kFoldBinades - kWalkB0;
+// A table step's lane l takes the window's chunks s + 4 l .. s + 4 l + 3: chunk i's LDS position is
+// (i mod 4) (W / 4) + i / 4, so for each of the four the lanes read consecutive words (chunk i at
+// position i put the lanes 4 chunks = 128 bytes of pairs apart: 32-way bank conflicts)
+__device__ __forceinline__ int walk_pos(int i) { return (i & 3) * (kWalkWindow / 4) + (i >> 2); }
 
+// kCycles: the clock64 split of the walk (diagnostics, implisolid_debug_fold with IMPLISOLID_FOLD_STATS):
+// each reading is an s_memtime whose wait also drains the wave's LDS operations, so the production
+// walk is compiled without them
+template <bool kCycles>
+__device__ __forceinline__ long long walk_clock() {
+    if constexpr (kCycles) return clock64();
+    return 0;
+}
+
+template <bool kCycles>
 __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restrict__ e, int64_t n64,
                                                             const int32_t* __restrict__ base, const FoldPair* __restrict__ pairs,
                                                             const uint8_t* __restrict__ flags, const uint8_t* __restrict__ hint,
                                                             int64_t nf, FoldOut* __restrict__ out) {
-    // the table cells of binades base + kWalkB0 .. base + 5 (the chain stays within a factor 2 of
-    // the estimate: binades base + 3 and base + 4 in practice; a cell outside goes term by term)
+    // the table cells of binades base + kWalkB0 .. base + 3 (the chain stays within a factor 2 of
+    // the estimate: binades base + 1 and base + 2 in practice; a cell outside goes term by term),
+    // binade-major, chunks at walk_pos (a table step's lanes read consecutive words)
     __shared__ FoldPair w_pair[kWalkWindow * kWalkBins];
     __shared__ uint8_t w_flag[kWalkWindow * kWalkBins];
     __shared__ int32_t w_base[kWalkWindow];
     __shared__ int16_t w_slot[kWalkWindow];
     __shared__ int16_t w_slot_chunk[kWalkSlots];
-    __shared__ float w_terms[kWalkSlots][kFoldChunk];
-    // per staged chunk: the lanes' inclusive prefix maps in binade base + 3 and suffix maps in base + 4
-    // (4 terms per lane), and the lanes holding a term either binade cannot express
-    __shared__ FoldPair w_pre[kWalkSlots][2][64];
-    __shared__ uint64_t w_prebad[kWalkSlots][2];
+    __shared__ uint4 w_terms[kWalkSlots][64];   // a staged chunk's terms (bits), 4 per lane
     __shared__ int w_nslots;
     __shared__ int w_wcnt[kWalkThreads / 64];
     __shared__ int w_ready[kWalkSlots];
@@ -813,10 +888,10 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
     int k = 0;
     int table_chunks = 0;
     bool done = false;   // wave 0: a NaN or an inf decided the result
-    int st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0, st5 = 0;
-    long long cyc_stage = 0, cyc_walk = 0, cyc_table = 0, cyc_term = 0, cyc_pre = 0, cyc_fast = 0;
+    int st0 = 0, st1 = 0, st2 = 0, st3 = 0, st6 = 0;
+    long long cyc_stage = 0, cyc_walk = 0, cyc_table = 0, cyc_term = 0, cyc_pre = 0, cyc_serial = 0;
     for (int c0 = 0; c0 < nc; c0 += kWalkWindow) {
-        const long long tc0 = clock64();
+        const long long tc0 = walk_clock<kCycles>();
         const int wn = nc - c0 < kWalkWindow ? nc - c0 : kWalkWindow;
         if (t == 0) w_nslots = 0;
         if (t < kWalkSlots) w_ready[t] = 0;
@@ -828,11 +903,12 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             const int64_t c = c0 + i;
             bool h = false;
             if (i < wn) {
-                w_base[i] = base[c];
+                const int q = walk_pos(i);
+                w_base[q] = base[c];
 #pragma unroll
                 for (int b = 0; b < kWalkBins; ++b) {
-                    w_pair[i * kWalkBins + b] = pairs[c * kFoldBinades + kWalkB0 + b];
-                    w_flag[i * kWalkBins + b] = flags[c * kFoldBinades + kWalkB0 + b];
+                    w_pair[b * kWalkWindow + q] = pairs[c * kFoldBinades + kWalkB0 + b];
+                    w_flag[b * kWalkWindow + q] = flags[c * kFoldBinades + kWalkB0 + b];
                 }
                 h = hint[c] != 0;
             }
@@ -851,50 +927,24 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             __syncthreads();
         }
         const int ns = w_nslots < kWalkSlots ? w_nslots : kWalkSlots;
-        cyc_stage += clock64() - tc0;
+        cyc_stage += walk_clock<kCycles>() - tc0;
         if (wid != 0) {
-            // waves 1.. stage the slots while wave 0 walks: a slot's terms, then its lanes' maps --
-            // prefix scan in base + 3, suffix scan in base + 4, what a term step entering the chunk at
-            // its start in base + 3 needs -- then its ready flag (the walk waits for it)
+            // waves 1.. stage the slots' terms while wave 0 walks, each then its ready flag (the walk
+            // waits for it)
             for (int sl = wid - 1; sl < ns; sl += kWalkThreads / 64 - 1) {
                 const int kk0 = (c0 + w_slot_chunk[sl]) * kFoldChunk + 4 * lane;
-                uint32_t tb[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    tb[j] = kk0 + j < n ? __float_as_uint(e[kk0 + j]) : 0u;
-                    w_terms[sl][4 * lane + j] = __uint_as_float(tb[j]);
-                }
-                const int Eb = w_base[w_slot_chunk[sl]] + 3;
-                FoldPair p3{0u, 0u}, p4{0u, 0u};
-                uint32_t f3 = 0, f4 = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint8_t fa, fb;
-                    p3 = fold_compose(p3, fold_pair_term(tb[j], Eb, fa));
-                    p4 = fold_compose(p4, fold_pair_term(tb[j], Eb + 1, fb));
-                    f3 |= fa;
-                    f4 |= fb;
-                }
-                w_pre[sl][0][lane] = wave_scan_pairs(p3);
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {   // suffix: lane l <- its group, then the lanes after it
-                    FoldPair y;
-                    y.c0 = (uint32_t)__shfl_down((int)p4.c0, d, 64);
-                    y.c1 = (uint32_t)__shfl_down((int)p4.c1, d, 64);
-                    if (lane + d < 64) p4 = fold_compose(p4, y);
-                }
-                w_pre[sl][1][lane] = p4;
-                const uint64_t b3 = __ballot(f3 != 0u), b4 = __ballot(f4 != 0u);
-                if (lane == 0) {
-                    w_prebad[sl][0] = b3;
-                    w_prebad[sl][1] = b4;
-                }
+                uint4 tb;
+                tb.x = kk0 + 0 < n ? __float_as_uint(e[kk0 + 0]) : 0u;
+                tb.y = kk0 + 1 < n ? __float_as_uint(e[kk0 + 1]) : 0u;
+                tb.z = kk0 + 2 < n ? __float_as_uint(e[kk0 + 2]) : 0u;
+                tb.w = kk0 + 3 < n ? __float_as_uint(e[kk0 + 3]) : 0u;
+                w_terms[sl][lane] = tb;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0) __hip_atomic_store(&w_ready[sl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             continue;
         }
-        const long long tc1 = clock64();
+        const long long tc1 = walk_clock<kCycles>();
         const int kend_w = (c0 + wn) * kFoldChunk < n ? (c0 + wn) * kFoldChunk : n;
         while (!done && k < kend_w) {   // uniform over wave 0
             // the walk's state is wave-uniform: kept in scalar registers, so its branches are scalar
@@ -935,21 +985,21 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             (void)frexpf(s, &E);   // s in [2^(E-1), 2^E): spacing 2^(E-24)
             E = __builtin_amdgcn_readfirstlane(E);
             uint32_t su = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E));   // in [2^23, 2^24)
-            const long long tA = clock64();
+            const long long tA = walk_clock<kCycles>();
             if ((k & (kFoldChunk - 1)) == 0) {   // whole chunks from the table, 4 per lane: 256 per step
-                if (lane == 0 && st0 + st1 + st2 + st4 < 256) out->trace[st0 + st1 + st2 + st4] = (1 << 28) | k;
+                if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (1 << 28) | k;
                 ++st1;
                 const int i0 = k / kFoldChunk - c0 + 4 * lane;
                 FoldPair tp[4];
                 bool ok[4];
                 int bb[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bb[j] = E - w_base[i0 + j < wn ? i0 + j : wn - 1];
+                for (int j = 0; j < 4; ++j) bb[j] = E - w_base[walk_pos(i0 + j < wn ? i0 + j : wn - 1)];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int i = i0 + j < wn ? i0 + j : wn - 1;
                     const bool inb = i0 + j < wn && bb[j] >= kWalkB0 && bb[j] < kFoldBinades;
-                    const int cell = i * kWalkBins + (inb ? bb[j] - kWalkB0 : 0);
+                    const int cell = (inb ? bb[j] - kWalkB0 : 0) * kWalkWindow + walk_pos(i);
                     tp[j] = w_pair[cell];
                     ok[j] = inb && w_flag[cell] == 0;
                     if (!ok[j]) tp[j] = FoldPair{0u, 0u};
@@ -981,20 +1031,26 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     k += fb * kFoldChunk;
                     if (k >= kend_w) {
                         if (k > n) k = n;
+                        cyc_table += walk_clock<kCycles>() - tA;
                         continue;
                     }
                     k = __builtin_amdgcn_readfirstlane(k);
-                    if (!lm) continue;   // the step's reach ended, not the run: another table step
+                    if (!lm) {   // the step's reach ended, not the run: another table step
+                        cyc_table += walk_clock<kCycles>() - tA;
+                        continue;
+                    }
                     su = tt;   // the chunk that ended the run goes term by term now (same binade)
                 }
             }
-            const long long tB = clock64();
+            const long long tB = walk_clock<kCycles>();
             cyc_table += tB - tA;
-            // the chunk the table could not take: its terms from k, 4 consecutive per lane, in order, as
-            // maps of the current binade (fold.hpp) up to the first event -- an unusable term, or the
-            // one that reaches the binade's end -- which is added as the chain's own float add; then on
-            // from the next term in the binade the sum is in now, within the same step
-            if (lane == 0 && st0 + st1 + st2 + st4 < 256) out->trace[st0 + st1 + st2 + st4] = (2 << 28) | k | (E + 64) << 20;
+            // the chunk the table could not take (the sum crosses a binade in it, or a term is flagged):
+            // its terms from k, 4 consecutive per lane, added serially; a chunk holding a NaN or an
+            // infinity goes in segments -- its terms as maps of the current binade (fold.hpp) up to
+            // the first event, an unusable term or the one that reaches the binade's end, which is
+            // added as the chain's own float add; then on from the next term in the binade the sum
+            // is in now
+            if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (2 << 28) | k | (E + 64) << 20;
             ++st2;
             const int kc = k & ~(kFoldChunk - 1);
             const int kend = kc + kFoldChunk < n ? kc + kFoldChunk : n;
@@ -1005,8 +1061,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             if (sl >= 0) {
                 while (__hip_atomic_load(&w_ready[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
                     __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) xb[j] = __float_as_uint(w_terms[sl][4 * lane + j]);
+                const uint4 tb = w_terms[sl][lane];
+                xb[0] = tb.x; xb[1] = tb.y; xb[2] = tb.z; xb[3] = tb.w;
             } else {
                 ++st3;
 #pragma unroll
@@ -1015,92 +1071,44 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     xb[j] = __float_as_uint(e[kk < n ? kk : kc]);
                 }
             }
-            // Fast path: a staged chunk entered at its start with the sum in binade base + 3.  Its
-            // lanes' prefix maps (staged) give each lane's value before and after its group at once;
-            // the first lane whose group reaches 2^24 or holds an unusable term holds the event, found
-            // term by term inside that group; the event term is the chain's own float add; then the
-            // group's remaining terms and the later lanes' suffix map (staged, binade base + 4) finish
-            // the chunk if the sum is in base + 4 and nothing there saturates or is unusable.  Any
-            // other case continues with the segments below from where this stopped.
-            const long long tF = clock64();
+            // The chunk's terms from k on, one by one, as the chain's own float adds: every lane runs
+            // the same chain over the wave's terms, read lane by lane (v_readlane, eight reads ahead
+            // of their adds; the terms outside [k, kend) masked to -0 in their lanes, which adds
+            // nothing to any value).  A chunk the table could not take crosses a binade or holds a
+            // term the table cannot express; 256 dependent adds (~2.4 k cycles) cost less than
+            // locating the crossing in it (a scan of the lanes' term maps, ~3.3 k cycles with the
+            // maps staged).  Finite terms only: a NaN payload or an infinity goes the segments' way
+            // below.
+            const long long tF = walk_clock<kCycles>();
             cyc_pre += tF - tB;
-            if (sl >= 0 && k == kc && s >= 0x1p-100f && s <= 0x1p100f) {
-                int E1 = 0;
-                (void)frexpf(s, &E1);
-                E1 = __builtin_amdgcn_readfirstlane(E1);
-                const int ic = kc / kFoldChunk - c0;
-                if (E1 == w_base[ic] + 3) {
-                    const uint32_t x0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E1));
-                    // independent of the sum: the lane's term maps in E1 (its group's search) and, in
-                    // E1 + 1, the maps of its group's terms from each position to the group's end
-                    FoldPair t1[4], g2[5];
-                    uint32_t f1[4], b2[5];
-                    g2[4] = FoldPair{0u, 0u};
-                    b2[4] = 0u;
+            {
+                uint32_t m[4];
+                bool special = false;
 #pragma unroll
-                    for (int j = 3; j >= 0; --j) {
-                        uint8_t fa, fb;
-                        t1[j] = fold_pair_term(xb[j], E1, fa);
-                        g2[j] = fold_compose(fold_pair_term(xb[j], E1 + 1, fb), g2[j + 1]);
-                        f1[j] = fa;
-                        b2[j] = b2[j + 1] | fb;
-                    }
-                    const FoldPair incl = w_pre[sl][0][lane];
-                    const FoldPair excl = lane ? w_pre[sl][0][lane - 1] : FoldPair{0u, 0u};
-                    const uint32_t vb = pair_apply(excl, x0), ve = pair_apply(incl, x0);
-                    const uint64_t lm = __ballot(((w_prebad[sl][0] >> lane) & 1ull) != 0ull || ve >= kFoldCap);
-                    if (lm) {
-                        const int L = __ffsll((unsigned long long)lm) - 1;
-                        // the later lanes' suffix map in E1 + 1 (staged), read while the group is searched
-                        const FoldPair sufL = L < 63 ? w_pre[sl][1][L + 1] : FoldPair{0u, 0u};
-                        const bool badL = L < 63 && (w_prebad[sl][1] >> (L + 1)) != 0ull;
-                        uint32_t v = vb, before = vb, xe = 0;
-                        int first = 4;
-                        FoldPair rest = g2[4];   // the group's terms after the event, in E1 + 1
-                        uint32_t rest_bad = 0u;
+                for (int j = 0; j < 4; ++j) {
+                    const int kk = kc + 4 * lane + j;
+                    const bool act = kk >= k && kk < kend;
+                    special = special || (act && (xb[j] & 0x7f800000u) == 0x7f800000u);
+                    m[j] = act ? xb[j] : 0x80000000u;
+                }
+                if (!__ballot(special) && s >= 0x1p-100f && s <= 0x1p100f) {
+                    float sv = s;
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const uint32_t v2 = pair_apply(t1[j], v);
-                            const bool live = first == 4, stop = live && (f1[j] != 0u || v2 >= kFoldCap);
-                            before = stop ? v : before;
-                            xe = stop ? xb[j] : xe;
-                            rest = stop ? g2[j + 1] : rest;
-                            rest_bad = stop ? b2[j + 1] : rest_bad;
-                            first = stop ? j : first;
-                            v = (live && !stop) ? v2 : v;
-                        }
-                        const int jf = (int)lane_value((uint32_t)first, L);   // < 4: lane L holds the event
-                        const FoldPair restL{lane_value(rest.c0, L), lane_value(rest.c1, L)};
-                        const FoldPair tail = fold_compose(restL, sufL);      // the chunk after the event
-                        const bool tail_bad = badL || lane_value(rest_bad, L) != 0u;
-                        s = ldexpf((float)lane_value(before, L), E1 - 24);
-                        const float xv = __uint_as_float(lane_value(xe, L));
-                        k = kc + 4 * L + jf + 1;
-                        if (xv != xv) {
-                            s = quiet_nan_of(xv);
-                            done = true;
-                        } else {
-                            s = s + xv;   // the event term: the chain's own float add
-                            if (k < kend && s >= 0x1p-100f && s <= 0x1p100f) {
-                                int E2 = 0;
-                                (void)frexpf(s, &E2);
-                                E2 = __builtin_amdgcn_readfirstlane(E2);
-                                const uint32_t x2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E2));
-                                const uint32_t x4 = pair_apply(tail, x2);
-                                const bool ok2 = E2 == E1 + 1 && !tail_bad && x4 < kFoldCap;
-                                if (ok2) {
-                                    s = ldexpf((float)x4, E2 - 24);
-                                    k = kend;
-                                }
-                                st5 += ok2 ? 1 : 0;
-                            }
-                        }
-                        ++st4;
+                    for (int l = 0; l < 64; l += 2) {
+                        uint32_t r[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) r[i] = (uint32_t)__builtin_amdgcn_readlane((int)m[i & 3], l + (i >> 2));
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) sv = sv + __uint_as_float(r[i]);
                     }
+                    s = sv;
+                    k = kend;
+                    ++st6;
+                    cyc_serial += walk_clock<kCycles>() - tF;
+                    cyc_term += walk_clock<kCycles>() - tB;
+                    continue;
                 }
             }
-            const long long tG = clock64();
-            cyc_fast += tG - tF;
             for (; !done && k < kend;) {   // segments of the chunk, each ending at an event
                 if (!(s >= 0x1p-100f && s <= 0x1p100f)) break;   // the outer loop's term-by-term paths
                 (void)frexpf(s, &E);
@@ -1144,17 +1152,17 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 s = s + x;   // the event term: the chain's own float add
                 if (k >= kend) break;
             }
-            cyc_term += clock64() - tB;
+            cyc_term += walk_clock<kCycles>() - tB;
         }
-        cyc_walk += clock64() - tc1;
+        cyc_walk += walk_clock<kCycles>() - tc1;
     }
     if (t == 0) {
         out->sum = s;
         out->table_chunks = table_chunks;
         out->steps[0] = st0; out->steps[1] = st1; out->steps[2] = st2; out->steps[3] = st3;
-        out->steps[4] = st4; out->steps[5] = st5;
+        out->steps[4] = 0; out->steps[5] = 0; out->steps[6] = st6;
         out->cycles[0] = cyc_stage; out->cycles[1] = cyc_walk; out->cycles[2] = cyc_table; out->cycles[3] = cyc_term;
-        out->cycles[4] = cyc_pre; out->cycles[5] = cyc_fast;
+        out->cycles[4] = cyc_pre; out->cycles[5] = 0; out->cycles[6] = cyc_serial;
         const float avg = (float)((double)s / (3. * (double)nf));
         out->avg = avg;
         alpha_list_dev(avg, out);
@@ -1375,6 +1383,53 @@ std::shared_ptr<const std::vector<float>> random_pm1_cached(int64_t n) {
 
 }  // namespace
 
+// The perturbation table of a face count on one device, shared by every Ob02 of the process
+// (the shards of one process, the builds of one engine): drawn once on a host thread, copied once
+// into pinned memory and uploaded once, on the stream of the Ob02 that first needs it; `ready`
+// orders every other stream after that upload.  The last few (device, face count) tables are kept.
+struct PertDev {
+    int device = -1;
+    int64_t nf = -1;
+    HostBuf pinned;
+    DevBuf buf;
+    hipEvent_t ready = nullptr;
+    ~PertDev() {
+        if (ready) (void)hipEventSynchronize(ready);
+        if (ready) (void)hipEventDestroy(ready);
+        buf.release();
+        pinned.release();
+    }
+};
+
+namespace {
+std::shared_ptr<PertDev> pert_device_table(int64_t nf, std::future<std::shared_ptr<const std::vector<float>>>& job,
+                                           hipStream_t s, bool& uploaded_here) {
+    static std::mutex mu;
+    static std::deque<std::shared_ptr<PertDev>> cache;
+    int device = 0;
+    IMPLI_HIP(hipGetDevice(&device));
+    std::lock_guard<std::mutex> lock(mu);
+    uploaded_here = false;
+    for (auto& e : cache)
+        if (e->device == device && e->nf == nf) return e;
+    auto host = job.get();
+    auto e = std::make_shared<PertDev>();
+    e->device = device;
+    e->nf = nf;
+    const size_t bytes = host->size() * 4;
+    e->pinned.reserve(bytes + 16);
+    std::memcpy(e->pinned.p, host->data(), bytes);
+    e->buf.reserve(bytes + 16);
+    IMPLI_HIP(hipEventCreateWithFlags(&e->ready, hipEventDisableTiming));
+    IMPLI_HIP(hipMemcpyAsync(e->buf.p, e->pinned.p, bytes, hipMemcpyHostToDevice, s));
+    IMPLI_HIP(hipEventRecord(e->ready, s));
+    uploaded_here = true;
+    cache.emplace_front(e);
+    if (cache.size() > 8) cache.pop_back();   // a table still in use lives on in its Ob02s
+    return e;
+}
+}  // namespace
+
 Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
     misc_.reserve(512);
 }
@@ -1383,7 +1438,7 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     nv = nv_;
     nf = nf_;
     if (d_work) {   // the caller's vertex array is the working one (sharded loop): no copy
-        verts_.attach(d_work, (size_t)(nv + 1) * 12);
+        verts_.attach(d_work, (size_t)nv * 12);   // exactly the caller's 3 nv floats
         d_verts = d_work;
     } else if (verts_.ext) {
         verts_.release();   // a previous attach: own buffer again
@@ -1403,70 +1458,73 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     if (!verts_.ext) verts_.reserve((size_t)(nv + 1) * 12);
     faces_.reserve((size_t)(nf + 1) * 12);
     deg_.reserve((size_t)(nv + 1) * 4);
-    // the mesh copied, the degree counters and misc ((unused), cap hits, evaluations) zeroed
+    rng_.reserve(kRngFields * sizeof(int64_t));
+    // the mesh copied, the degree counters and misc ((unused), cap hits, evaluations) zeroed, the
+    // range block set to the whole mesh
     const int64_t nmax = std::max<int64_t>(std::max<int64_t>(3 * nv, 3 * nf), nv + 1);
     k_load_mesh<<<blocks_for(std::max<int64_t>(nmax, 16)), 256, 0, s>>>(verts_.as<float>(), d_verts,
                                                                        verts_.as<float>() == d_verts ? 0 : 3 * nv, faces_.as<int32_t>(),
                                                                        d_faces, 3 * nf, deg_.as<uint32_t>(), nv + 1,
-                                                                       misc_.as<uint32_t>());
+                                                                       misc_.as<uint32_t>(), rng_.as<int64_t>(), nv, nf);
     start_perturbations();   // host thread, overlaps the topology and resampling kernels
     build_topology(true);
-    own_v0_ = 0; own_v1_ = nv; wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
-    hv0_ = 0; hv1_ = nv;
+    whole_ranges();
+}
+
+void Ob02::whole_ranges() {   // host side of the range block's whole-mesh state
+    own_v0_ = 0;
+    own_v1_ = nv;
+    const int64_t h[8] = {0, nv, 0, nf, 0, nf, 0, nv};
+    std::memcpy(hrng_, h, sizeof h);
+    hrng_valid_ = true;
+    est_work_ = est_cen_ = nf;
     sharded_ = false;
 }
 
+// The shard's ranges are found on the device, in stream order (k_work_range -> k_fof_range ->
+// k_face_vertex_range -> k_ranges_final), and the per-face passes read them there: no host round
+// trip (the three read-backs of round 4 cost 0.3-0.5 ms per shard).  Their grids are sized by an
+// estimate -- a mesh has about two faces per vertex, plus a layer of faces at the slab's boundary --
+// and grid-stride over whatever the range turns out to be.
 void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
     if (v0 < 0 || v1 < v0 || v1 > nv) throw InputError("ob02: owned vertex range outside the mesh");
     if (!topo_valid_) build_topology();
+    rng_.reserve(kRngFields * sizeof(int64_t));
+    const bool sharded = !(v0 == 0 && v1 == nv);
+    k_ranges_set<<<1, 64, 0, s>>>(rng_.as<int64_t>(), v0, v1, nv, nf, sharded ? 1 : 0);
+    if (!sharded) {
+        whole_ranges();
+        IMPLI_HIP(hipGetLastError());
+        return;
+    }
     own_v0_ = v0;
     own_v1_ = v1;
-    sharded_ = !(v0 == 0 && v1 == nv);
-    if (!sharded_) {
-        wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
-        hv0_ = 0; hv1_ = nv;
-        return;
-    }
-    DevBuf& r = scan_tmp_;   // scratch: 4 x u64 (only topology uses it, before this)
-    r.reserve(64);
-    const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
-    IMPLI_HIP(hipMemcpyAsync(r.p, init, sizeof init, hipMemcpyHostToDevice, s));
-    if (nf) k_touch_range<<<blocks_for(nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, v0, v1, r.as<unsigned long long>());
-    unsigned long long h[4];
-    IMPLI_HIP(hipMemcpyAsync(h, r.p, sizeof h, hipMemcpyDeviceToHost, s));
-    IMPLI_HIP(hipStreamSynchronize(s));
-    if (h[0] > h[1]) {   // no face touches the owned vertices
-        wf0_ = wf1_ = cf0_ = cf1_ = 0;
-        hv0_ = v0;
-        hv1_ = v1;
-        return;
-    }
-    wf0_ = (int64_t)h[0];
-    wf1_ = (int64_t)h[1] + 1;
-    IMPLI_HIP(hipMemcpyAsync(r.p, init, sizeof init, hipMemcpyHostToDevice, s));
-    k_fof_range<<<blocks_for(wf1_ - wf0_), 256, 0, s>>>(fof_.as<int32_t>(), wf0_, wf1_, r.as<unsigned long long>());
-    IMPLI_HIP(hipMemcpyAsync(h, r.p, sizeof h, hipMemcpyDeviceToHost, s));
-    IMPLI_HIP(hipStreamSynchronize(s));
-    cf0_ = (int64_t)h[2];
-    cf1_ = (int64_t)h[3] + 1;
-    // the vertices the next resampling reads: those of the centroid faces (its one-ring halo)
-    IMPLI_HIP(hipMemcpyAsync(r.p, init, sizeof init, hipMemcpyHostToDevice, s));
-    k_face_vertex_range<<<blocks_for(cf1_ - cf0_), 256, 0, s>>>(faces_.as<int32_t>(), cf0_, cf1_, r.as<unsigned long long>());
-    IMPLI_HIP(hipMemcpyAsync(h, r.p, sizeof h, hipMemcpyDeviceToHost, s));
-    IMPLI_HIP(hipStreamSynchronize(s));
-    hv0_ = std::min<int64_t>((int64_t)h[0], v0);
-    hv1_ = std::max<int64_t>((int64_t)h[1] + 1, v1);
+    sharded_ = true;
+    hrng_valid_ = false;
+    const int64_t nown = v1 - v0;
+    est_work_ = std::min<int64_t>(nf, 2 * nown + nown / 4 + 4096);
+    est_cen_ = std::min<int64_t>(nf, est_work_ + 4096);
+    int64_t* r = rng_.as<int64_t>();
+    if (nown) k_work_range<<<blocks_for(nown), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), r);
+    if (est_work_) k_fof_range<<<blocks_for(est_work_), 256, 0, s>>>(fof_.as<int32_t>(), r);
+    if (est_cen_) k_face_vertex_range<<<blocks_for(est_cen_), 256, 0, s>>>(faces_.as<int32_t>(), r);
+    k_ranges_final<<<1, 64, 0, s>>>(r);
     IMPLI_HIP(hipGetLastError());
 }
 
 // every rank's owned range, all-gathered into equal padded rows (row r: rank r's 3 (v1 - v0)
-// floats), unpacked into this rank's vertex array except its own range (one kernel on the stream)
-__global__ void k_unpack_ranges(float* __restrict__ v, const float* __restrict__ rows, int64_t row_len,
-                                const int64_t* __restrict__ voff, int world, int self) {
+// floats), unpacked into this rank's vertex array except its own range (one kernel on the stream;
+// the offsets travel as a kernel argument, so nothing is staged in host memory)
+constexpr int kMaxUnpackRanks = 64;
+struct UnpackOffsets {
+    int64_t o[kMaxUnpackRanks + 1];
+};
+__global__ void k_unpack_ranges(float* __restrict__ v, const float* __restrict__ rows, int64_t row_len, UnpackOffsets voff,
+                                int self) {
     const int r = blockIdx.y;
     if (r == self) return;
-    const int64_t n = 3 * (voff[r + 1] - voff[r]);
-    float* dst = v + 3 * voff[r];
+    const int64_t n = 3 * (voff.o[r + 1] - voff.o[r]);
+    float* dst = v + 3 * voff.o[r];
     const float* src = rows + (int64_t)r * row_len;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
 }
@@ -1474,25 +1532,34 @@ __global__ void k_unpack_ranges(float* __restrict__ v, const float* __restrict__
 void Ob02::unpack_ranges(const float* d_rows, int64_t row_len, const std::vector<int64_t>& voff, int self) {
     const int world = (int)voff.size() - 1;
     if (world < 1 || voff.back() != nv || self < 0 || self >= world) throw InputError("ob02: bad owned ranges");
+    if (world > kMaxUnpackRanks) throw InputError("ob02: more than 64 ranks in one unpack");
+    UnpackOffsets o{};
     int64_t longest = 0;
     for (int r = 0; r < world; ++r) {
         if (voff[r + 1] < voff[r] || 3 * (voff[r + 1] - voff[r]) > row_len) throw InputError("ob02: bad owned ranges");
         longest = std::max<int64_t>(longest, voff[r + 1] - voff[r]);
     }
-    voff_dev_.reserve(voff.size() * sizeof(int64_t));
-    // pinned staging, so the upload is stream-ordered without a host synchronisation
-    voff_host_.reserve(voff.size() * sizeof(int64_t));
-    std::memcpy(voff_host_.p, voff.data(), voff.size() * sizeof(int64_t));
-    IMPLI_HIP(hipMemcpyAsync(voff_dev_.p, voff_host_.p, voff.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    for (int r = 0; r <= world; ++r) o.o[r] = voff[r];
     const unsigned bx = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (3 * longest + 255) / 256), 1024);
-    k_unpack_ranges<<<dim3(bx, (unsigned)world), 256, 0, s>>>(verts_.as<float>(), d_rows, row_len, voff_dev_.as<int64_t>(),
-                                                               world, self);
+    k_unpack_ranges<<<dim3(bx, (unsigned)world), 256, 0, s>>>(verts_.as<float>(), d_rows, row_len, o, self);
     IMPLI_HIP(hipGetLastError());
 }
 
-void Ob02::ranges(int64_t out[8]) const {
-    out[0] = own_v0_; out[1] = own_v1_; out[2] = wf0_; out[3] = wf1_; out[4] = cf0_; out[5] = cf1_;
-    out[6] = hv0_; out[7] = hv1_;
+void Ob02::ranges(int64_t out[8]) {
+    if (!hrng_valid_) {   // blocking: read the device's range block back once
+        int64_t h[kRngFields];
+        IMPLI_HIP(hipMemcpyAsync(h, rng_.p, sizeof h, hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+        const int64_t m[8] = {h[kRngOwn], h[kRngOwn + 1], h[kRngWork], h[kRngWork + 1], h[kRngCen], h[kRngCen + 1],
+                              h[kRngHalo], h[kRngHalo + 1]};
+        const bool ok = 0 <= m[0] && m[0] <= m[1] && m[1] <= nv && 0 <= m[2] && m[2] <= m[3] && m[3] <= nf &&
+                        0 <= m[4] && m[4] <= m[5] && m[5] <= nf && (m[2] == m[3] || (m[4] <= m[2] && m[3] <= m[5])) &&
+                        0 <= m[6] && m[6] <= m[0] && m[1] <= m[7] && m[7] <= nv;
+        if (!ok) throw HipError("ob02: the device's shard ranges are inconsistent");
+        std::memcpy(hrng_, m, sizeof m);
+        hrng_valid_ = true;
+    }
+    std::memcpy(out, hrng_, sizeof hrng_);
 }
 
 EdgeTab Ob02::edge_table() {
@@ -1578,7 +1645,7 @@ Ob02::~Ob02() {
     dir_.release();
     evals_buf_.release();
     for (DevBuf* b : {&verts_, &faces_, &vnew_, &cen_, &nrm_, &w_, &fof_, &uoff_, &ulst_, &etab_, &deg_, &proj_, &grad_,
-                      &fn_, &norms_, &pert_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_, &fold_sum_, &fold_out_})
+                      &fn_, &norms_, &pend_, &misc_, &fnew_, &rtab_, &scan_tmp_, &fold_sum_, &fold_out_})
         b->release();
     for (auto& kv : snaps_) kv.second.buf.release();
 }
@@ -1588,26 +1655,26 @@ void Ob02::vertex_resampling(float c) {
     if (!topo_valid_) build_topology();
     Stage st(this, kStageResample);
     store_pointset("pre_resampling_vertices", verts_.as<float>(), nv, true);   // vertex_resampling.hpp:176-180
-    // centroids and normals of faces [cf0, cf1), weights of [wf0, wf1), vertices [v0, v1) (the whole
-    // mesh unless sharded); per-face pointers are offset to the range's first face
-    const int64_t ncf = cf1_ - cf0_;
-    if (ncf > 0) {
+    // centroids and normals of the centroid faces, weights of the work faces, vertices [v0, v1) (the
+    // whole mesh unless sharded); the face ranges are read on the device (the range block)
+    const int64_t* rng = rng_.as<int64_t>();
+    if (est_cen_ > 0) {
         if (const TreeJit::PointKernels* pk = E.point_jit(s)) {
             const float *m = E.d_mats(), *tab = E.d_rabbit(), *v = verts_.as<float>();
-            const int32_t* f = faces_.as<int32_t>() + 3 * cf0_;
-            float *C = cen_.as<float>() + 3 * cf0_, *N = nrm_.as<float>() + 3 * cf0_;
-            int64_t n = ncf;
-            void* args[] = {&m, &tab, &v, &f, &n, &C, &N};
-            TreeJit::launch(pk->cnormals, blocks_for(ncf), args, s, "impli_pt_centroid_normals");
+            const int32_t* f = faces_.as<int32_t>();
+            const int64_t* rc = rng + kRngCen;
+            float *C = cen_.as<float>(), *N = nrm_.as<float>();
+            void* args[] = {&m, &tab, &v, &f, &rc, &C, &N};
+            TreeJit::launch(pk->cnormals, blocks_for(est_cen_), args, s, "impli_pt_centroid_normals");
             ++jit_launches_;
         } else {
-            DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(ncf), 256, s, E.d_program(), E.d_rabbit(), verts_.as<float>(),
-                         faces_.as<int32_t>() + 3 * cf0_, ncf, cen_.as<float>() + 3 * cf0_, nrm_.as<float>() + 3 * cf0_);
+            DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(est_cen_), 256, s, E.d_program(), E.d_rabbit(),
+                         verts_.as<float>(), faces_.as<int32_t>(), rng + kRngCen, cen_.as<float>(), nrm_.as<float>());
         }
     }
-    if (wf1_ > wf0_)
-        k_face_weights<<<blocks_for(wf1_ - wf0_), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(), wf0_,
-                                                                wf1_, c, w_.as<float>());
+    if (est_work_ > 0)
+        k_face_weights<<<blocks_for(est_work_), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(),
+                                                              rng + kRngWork, c, w_.as<float>());
     // in place: the new positions are weighted sums of the centroids alone (vertex_resampling.hpp
     // :93-141), which were computed above, so nothing reads the old positions any more and the
     // vertex buffer stays the same (a sharded caller's exchange writes into it directly)
@@ -1635,7 +1702,7 @@ struct FoldLayout {
 // the table passes on `ts`, then the walk on `ws` after them (ws may be ts); with d_verts the terms
 // are the mesh's edge lengths, computed into d_terms by the first pass
 void launch_fold(float* d_terms, int64_t n, int64_t nf, const float* d_verts, const int32_t* d_faces, char* d_tab,
-                 FoldOut* d_out, hipStream_t ts, hipStream_t ws, hipEvent_t table_done) {
+                 FoldOut* d_out, hipStream_t ts, hipStream_t ws, hipEvent_t table_done, bool cycles = false) {
     if (n >= ((int64_t)1 << 31) - kFoldChunk) throw InputError("edge-length fold: more than 2^31 terms");
     const FoldLayout L(n);
     FoldPair* d_pair = reinterpret_cast<FoldPair*>(d_tab);
@@ -1654,7 +1721,10 @@ void launch_fold(float* d_terms, int64_t n, int64_t nf, const float* d_verts, co
         IMPLI_HIP(hipEventRecord(table_done, ts));
         IMPLI_HIP(hipStreamWaitEvent(ws, table_done, 0));
     }
-    k_fold_walk<<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
+    if (cycles)
+        k_fold_walk<true><<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
+    else
+        k_fold_walk<false><<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
 }
 
 // compute_average_edge_length (cp:70-82) is one serial float chain in face order.  The terms, the
@@ -1694,7 +1764,8 @@ float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* 
     tab.reserve(L.bytes);
     fo.reserve(sizeof(FoldOut));
     if (n) IMPLI_HIP(hipMemcpy(terms.p, h_terms, (size_t)n * 4, hipMemcpyHostToDevice));
-    launch_fold(terms.as<float>(), n, n, nullptr, nullptr, tab.as<char>(), fo.as<FoldOut>(), 0, 0, nullptr);
+    launch_fold(terms.as<float>(), n, n, nullptr, nullptr, tab.as<char>(), fo.as<FoldOut>(), 0, 0, nullptr,
+                stats != nullptr && std::getenv("IMPLISOLID_FOLD_STATS") != nullptr);
     IMPLI_HIP(hipGetLastError());
     FoldOut h;
     IMPLI_HIP(hipMemcpy(&h, fo.p, offsetof(FoldOut, alphas), hipMemcpyDeviceToHost));
@@ -1707,7 +1778,10 @@ float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* 
         for (int i = 0; i < 4; ++i) stats[i] = h.steps[i];
         stats[4] = h.cycles[0];
         stats[5] = h.cycles[1];
-        stats[6] = h.steps[4] * 1000 + h.steps[5];
+        stats[6] = h.cycles[6];
+        stats[11] = h.steps[4];
+        stats[12] = h.steps[5];
+        stats[13] = h.steps[6];
         stats[7] = h.cycles[2];
         stats[8] = h.cycles[3];
         stats[9] = h.cycles[4];
@@ -1737,18 +1811,18 @@ void Ob02::start_perturbations() {
     const int64_t n = nf;
     pert_job_ = std::async(std::launch::async, [n] { return random_pm1_cached(n); });
     pert_nf_ = nf;
-    pert_uploaded_ = false;
+    pert_dev_.reset();
 }
 
 const float* Ob02::perturbations() {
     if (pert_nf_ != nf) start_perturbations();
-    if (!pert_uploaded_) {
-        pert_host_ = pert_job_.get();
-        pert_.reserve(pert_host_->size() * 4 + 16);
-        IMPLI_HIP(hipMemcpyAsync(pert_.p, pert_host_->data(), pert_host_->size() * 4, hipMemcpyHostToDevice, s));
-        pert_uploaded_ = true;
+    if (!pert_dev_) {
+        bool mine = false;
+        pert_dev_ = pert_device_table(nf, pert_job_, s, mine);
+        // another Ob02's upload (on its stream): order this stream after it, once
+        if (!mine) IMPLI_HIP(hipStreamWaitEvent(s, pert_dev_->ready, 0));
     }
-    return pert_.as<float>();
+    return pert_dev_->buf.as<float>();
 }
 
 void Ob02::centroids_projection(bool enable_qem) {
@@ -1762,21 +1836,22 @@ void Ob02::centroids_projection(bool enable_qem) {
     pend_.reserve((size_t)(nf + 2) * 4);
     if (profile_) evals_buf_.reserve((size_t)(nf + 1) * 4);
     DevBuf& fcbuf = w_;   // f(centroid) per face; the resampling weights are dead here
-    // the work faces [wf0, wf1) (every face unless sharded): per-face pointers offset to the first
-    const int64_t j0 = wf0_, nw = wf1_ - wf0_;
+    // the work faces (every face unless sharded; the range block on the device), grids sized by
+    // the estimate
+    const int64_t nw = est_work_;
     ProjArgs a{};
     a.v = verts_.as<float>();
-    a.f = faces_.as<int32_t>() + 3 * j0;
-    a.nf = nw;
-    a.out = proj_.as<float>() + 3 * j0;
-    a.fn = fn_.as<float>() + 3 * j0;
-    a.fc = fcbuf.as<float>() + j0;
-    a.pend = pend_.as<uint32_t>() + j0;
+    a.f = faces_.as<int32_t>();
+    a.rng = rng_.as<int64_t>() + kRngWork;
+    a.out = proj_.as<float>();
+    a.fn = fn_.as<float>();
+    a.fc = fcbuf.as<float>();
+    a.pend = pend_.as<uint32_t>();
     a.pend_count = misc_.as<uint32_t>();
     a.cap_hits = misc_.as<uint32_t>() + 1;
-    a.cen = cen_.as<float>() + 3 * j0;
-    a.dir = dir_.as<float>() + 3 * j0;
-    a.evals = profile_ ? evals_buf_.as<uint32_t>() + j0 : nullptr;
+    a.cen = cen_.as<float>();
+    a.dir = dir_.as<float>();
+    a.evals = profile_ ? evals_buf_.as<uint32_t>() : nullptr;
     const TreeJit::PointKernels* pk = E.point_jit(s);   // one choice for the whole projection
     const float *jm = E.d_mats(), *jtab = E.d_rabbit();
     void* jargs[] = {&jm, &jtab, &a};
@@ -1796,7 +1871,7 @@ void Ob02::centroids_projection(bool enable_qem) {
     const unsigned grid = blocks_for(nw * kProjGroup);
     // centroids left unresolved need the randomised directions (types 2-6): the late pass covers
     // every face and reads the early pass's per-face flags on the device (no host round trip)
-    a.pert = perturbations() + 3 * j0;
+    a.pert = perturbations();
     if (nw > 0) {
         if (pk) TreeJit::launch(pk->early, grid, jargs, s, "impli_pt_project_early");
         else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
@@ -1805,8 +1880,11 @@ void Ob02::centroids_projection(bool enable_qem) {
     }
     IMPLI_HIP(hipGetLastError());
     if (profile_ && nw > 0) {   // the evaluations of this projection, summed on the host
-        std::vector<uint32_t> h((size_t)nw);
-        IMPLI_HIP(hipMemcpyAsync(h.data(), evals_buf_.as<uint32_t>() + j0, (size_t)nw * 4, hipMemcpyDeviceToHost, s));
+        int64_t r[8];
+        ranges(r);
+        std::vector<uint32_t> h((size_t)(r[3] - r[2]));
+        if (!h.empty())
+            IMPLI_HIP(hipMemcpyAsync(h.data(), evals_buf_.as<uint32_t>() + r[2], h.size() * 4, hipMemcpyDeviceToHost, s));
         IMPLI_HIP(hipStreamSynchronize(s));
         for (uint32_t e : h) evals_ += e;
     }
@@ -1817,14 +1895,14 @@ void Ob02::centroids_projection(bool enable_qem) {
         grad_.reserve((size_t)(nf + 1) * 12);
         if (nw <= 0) {
         } else if (pk) {
-            const float* P = proj_.as<float>() + 3 * j0;
-            float* G = grad_.as<float>() + 3 * j0;
-            int64_t n = nw;
-            void* nargs[] = {&jm, &jtab, &P, &n, &G};
+            const float* P = proj_.as<float>();
+            float* G = grad_.as<float>();
+            const int64_t* rw = a.rng;
+            void* nargs[] = {&jm, &jtab, &P, &rw, &G};
             TreeJit::launch(pk->normals, blocks_for(nw), nargs, s, "impli_pt_normals_at");
         } else {
-            DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nw), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>() + 3 * j0,
-                         nw, grad_.as<float>() + 3 * j0);
+            DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nw), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>(),
+                         a.rng, grad_.as<float>());
         }
         // QEM of the owned vertices (all unless sharded), in place
         const int64_t nov = own_v1_ - own_v0_;
@@ -1964,9 +2042,9 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
         etab_valid_ = false;
         // the new vertices and faces are covered by later steps: the ranges become the whole mesh
         // (a sharded caller sets its owned vertices of the subdivided mesh again)
-        own_v0_ = 0; own_v1_ = nv; wf0_ = 0; wf1_ = nf; cf0_ = 0; cf1_ = nf;
-        hv0_ = 0; hv1_ = nv;
-        sharded_ = false;
+        rng_.reserve(kRngFields * sizeof(int64_t));
+        k_ranges_set<<<1, 64, 0, s>>>(rng_.as<int64_t>(), 0, nv, nv, nf, 0);
+        whole_ranges();
     }
     add_rand_noise(amplitude);
 }

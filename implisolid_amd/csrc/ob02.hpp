@@ -12,6 +12,12 @@
 namespace impli {
 
 struct EdgeTab;   // ob02.hip: open-addressed (vmin, vmax) table of the current faces
+struct PertDev;   // ob02.hip: a face count's perturbation table on one device (process-wide cache)
+
+// Ob02's range block (int64 fields of rng_): [kRngWork, +2) work faces, [kRngCen, +2) centroid
+// faces, [kRngHalo, +2) halo vertices, [kRngOwn, +2) owned vertices (half-open), then three
+// (min, max) scratch pairs of the range passes
+constexpr int kRngWork = 0, kRngCen = 2, kRngHalo = 4, kRngOwn = 6, kRngScratch = 8, kRngFields = 14;
 
 class Ob02 {
 public:
@@ -36,8 +42,10 @@ public:
     void set_owned_vertices(int64_t v0, int64_t v1);
     // [v0, v1, work faces f0, f1, centroid faces f0, f1, halo vertices h0, h1]: [h0, h1) are the
     // vertices the next resampling reads (those of the centroid faces), so after a step only they
-    // must be current before another resampling (the edge-length fold reads every vertex)
-    void ranges(int64_t out[8]) const;
+    // must be current before another resampling (the edge-length fold reads every vertex).  The
+    // ranges are found on the device in stream order; this reads them back (blocking) once per
+    // set_owned_vertices.
+    void ranges(int64_t out[8]);
     // the exchange after a vertex-moving step: rows holds every rank's owned range (row r: rank r's
     // 3 (voff[r+1] - voff[r]) floats at r row_len), copied into the vertex array except row `self`,
     // on the stream (no host synchronisation)
@@ -85,6 +93,7 @@ private:
     hipStream_t start_edge_fold();
     void finish_edge_fold();
     void start_perturbations();
+    void whole_ranges();
     const float* perturbations();
     struct Stage {   // profiling scope: stage k from construction to next() / destruction
         Ob02* ob;
@@ -99,15 +108,17 @@ private:
     hipStream_t s;
     int64_t nv = 0, nf = 0;
     DevBuf verts_, faces_, vnew_, cen_, nrm_, w_, fof_, uoff_, ulst_, etab_, deg_, proj_, grad_, fn_, norms_,
-        pert_, pend_, misc_, fnew_, rtab_, scan_tmp_;
+        pend_, misc_, fnew_, rtab_, scan_tmp_;
     bool topo_valid_ = false;
     bool etab_valid_ = false;   // the edge table (subdivision only) matches the current faces
     int64_t own_v0_ = 0, own_v1_ = 0;   // owned vertices
-    int64_t wf0_ = 0, wf1_ = 0;         // work faces: touching an owned vertex
-    int64_t cf0_ = 0, cf1_ = 0;         // faces whose centroid / normal the weights of the work faces read
-    int64_t hv0_ = 0, hv1_ = 0;         // vertices of those faces (the next resampling's input)
-    DevBuf voff_dev_;                   // unpack_ranges: the ranks' vertex offsets
-    HostBuf voff_host_;
+    // the range block in device memory (int64, kRng* below): work faces (touching an owned vertex),
+    // centroid faces (whose centroid / normal the work faces' weights read), halo vertices (those
+    // faces' vertices: the next resampling's input), owned vertices, and the range passes' scratch
+    DevBuf rng_;
+    int64_t hrng_[8] = {};              // host copy (ranges()), valid if hrng_valid_
+    bool hrng_valid_ = false;
+    int64_t est_work_ = 0, est_cen_ = 0;   // grid sizes of the per-face passes (the kernels grid-stride)
     bool sharded_ = false;
     int64_t rand_hi_rows_ = 0;
     float avg_edge_ = 0.f;
@@ -123,9 +134,8 @@ private:
     hipEvent_t mesh_ready_ = nullptr, prep_done_ = nullptr;
     DevBuf dir_, evals_buf_;
     std::future<std::shared_ptr<const std::vector<float>>> pert_job_;
-    std::shared_ptr<const std::vector<float>> pert_host_;
+    std::shared_ptr<PertDev> pert_dev_;   // the device table in use (process-wide cache, ob02.hip)
     int64_t pert_nf_ = -1;
-    bool pert_uploaded_ = false;
     struct Snapshot {
         DevBuf buf;
         int64_t n = 0;

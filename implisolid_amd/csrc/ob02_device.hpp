@@ -37,19 +37,26 @@ __device__ __forceinline__ V3 centroid(const float* __restrict__ v, const int32_
               (v[3 * a + 2] + v[3 * b + 2] + v[3 * c + 2]) / (float)(3.0)};
 }
 
+// Face ranges live in device memory: a pass over faces [rng[0], rng[1]) reads them in stream order
+// (a Z-slab shard's work faces are found on the device, Ob02::set_owned_vertices, with no host
+// round trip), its grid sized by an estimate on the host and grid-striding over the range.
+__device__ __forceinline__ int64_t grid_lane() { return (int64_t)blockIdx.x * 256 + threadIdx.x; }
+__device__ __forceinline__ int64_t grid_lanes() { return (int64_t)gridDim.x * 256; }
+
 // vertex_resampling.hpp:185-188: f and normalize_1111(grad) at the face centroids
 template <class Ev>
 __device__ __forceinline__ void centroid_normals_body(const Ev& ev, const float* __restrict__ v,
-                                                      const int32_t* __restrict__ f, int64_t nf, float* __restrict__ C,
-                                                      float* __restrict__ N) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= nf) return;
-    const V3 c = centroid(v, f, j);
-    V3 g;
-    (void)ev.fg(c.x, c.y, c.z, g);
-    const float nm = norm2f(g.x, g.y, g.z);   // normalize_1111 normalise_inplace.hpp:60-70
-    C[3 * j] = c.x; C[3 * j + 1] = c.y; C[3 * j + 2] = c.z;
-    N[3 * j] = g.x / nm; N[3 * j + 1] = g.y / nm; N[3 * j + 2] = g.z / nm;
+                                                      const int32_t* __restrict__ f, const int64_t* __restrict__ rng,
+                                                      float* __restrict__ C, float* __restrict__ N) {
+    const int64_t j1 = rng[1];
+    for (int64_t j = rng[0] + grid_lane(); j < j1; j += grid_lanes()) {
+        const V3 c = centroid(v, f, j);
+        V3 g;
+        (void)ev.fg(c.x, c.y, c.z, g);
+        const float nm = norm2f(g.x, g.y, g.z);   // normalize_1111 normalise_inplace.hpp:60-70
+        C[3 * j] = c.x; C[3 * j + 1] = c.y; C[3 * j + 2] = c.z;
+        N[3 * j] = g.x / nm; N[3 * j + 1] = g.y / nm; N[3 * j + 2] = g.z / nm;
+    }
 }
 
 __device__ __forceinline__ float get_sign(float v) { return (v > kRootTol) ? 1.f : (v < -kRootTol) ? -1.f : 0.f; }
@@ -96,9 +103,10 @@ struct FoldOut {
     float avg;          // (float)((double)sum / (3. * nf)): max_dist of the searches and QEM's clamp
     int nal;            // alphas in the list
     int table_chunks;   // chunks taken from the chunk table (statistics)
-    int steps[6];       // walk steps (statistics): zero-skip / serial terms, table runs, term runs, global term
-                        // loads, run jumps, (spare)
-    long long cycles[6];   // staging, walking, table steps, term steps, staging parts (clock64)
+    int steps[8];       // walk steps (statistics): zero-skip / serial terms, table runs, term runs, global term
+                        // loads, fast crossings, fast crossings that finished their chunk, serial chunks, (spare)
+    long long cycles[8];   // staging, walking, table steps, term steps, term preamble, fast path, serial chunks
+                           // (clock64)
     int trace[256];        // the walk's first steps (diagnostics): kind << 28 | term index
     float alphas[kMaxAlphas];
 };
@@ -106,7 +114,7 @@ struct FoldOut {
 struct ProjArgs {
     const float* v;
     const int32_t* f;
-    int64_t nf;
+    const int64_t* rng;     // the faces to project: [rng[0], rng[1]) (device memory; per-face arrays absolute)
     const FoldOut* fold;    // alphas, their count and max_dist (the average edge length)
     const float* pert;      // type-2 perturbations (3 per centroid), only for the late pass
     float* out;             // projected centroids
@@ -247,9 +255,7 @@ __device__ __forceinline__ bool try_direction(const Grp& g, const Ev& ev, V3 x, 
 // f(centroid) and the type-0 direction -normalise(grad) s_c; one lane per face.  Nothing here needs
 // the average edge length, so it runs while k_fold_walk folds the edge lengths.
 template <class Ev>
-__device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& a) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= a.nf) return;
+__device__ __forceinline__ void project_prep_face(const Ev& ev, const ProjArgs& a, int64_t j) {
     const V3 x = centroid(a.v, a.f, j);
     const V3 fnv = facet_normal(a.v, a.f, j);
     V3 gr;
@@ -264,12 +270,15 @@ __device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& 
     if (a.evals) a.evals[j] = 1;
 }
 
+template <class Ev>
+__device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& a) {
+    const int64_t j1 = a.rng[1];
+    for (int64_t j = a.rng[0] + grid_lane(); j < j1; j += grid_lanes()) project_prep_face(ev, a, j);
+}
+
 // direction types 0 (gradient) and 1 (mesh normal); kProjGroup lanes per face
 template <class Ev>
-__device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs& a) {
-    const Grp g;
-    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kProjGroup;
-    if (j >= a.nf) return;   // uniform per group
+__device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs& a, const Grp& g, int64_t j) {
     const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const V3 d0{a.dir[3 * j], a.dir[3 * j + 1], a.dir[3 * j + 2]};
@@ -290,13 +299,18 @@ __device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs&
     if (a.evals && g.sub == 0) a.evals[j] += evals;
 }
 
+template <class Ev>
+__device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs& a) {
+    const Grp g;
+    const int64_t j1 = a.rng[1];
+    for (int64_t j = a.rng[0] + grid_lane() / kProjGroup; j < j1; j += grid_lanes() / kProjGroup)   // uniform per group
+        project_early_face(ev, a, g, j);
+}
+
 // types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes); the grid
 // covers every face, groups of faces the early pass resolved exit at once
 template <class Ev>
-__device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& a) {
-    const Grp g;
-    const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kProjGroup;
-    if (j >= a.nf || !a.pend[j]) return;   // uniform per group
+__device__ __forceinline__ void project_late_face(const Ev& ev, const ProjArgs& a, const Grp& g, int64_t j) {
     const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const float fcv = a.fc[j];
@@ -322,15 +336,26 @@ __device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& 
     if (a.evals && g.sub == 0) a.evals[j] += evals;
 }
 
-// normalize_1111(grad) at arbitrary points (the QEM normals at the projected centroids, qem.hpp:256-316)
 template <class Ev>
-__device__ __forceinline__ void normals_at_body(const Ev& ev, const float* __restrict__ P, int64_t n, float* __restrict__ G) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    V3 g;
-    (void)ev.fg(P[3 * j], P[3 * j + 1], P[3 * j + 2], g);
-    const float nm = norm2f(g.x, g.y, g.z);
-    G[3 * j] = g.x / nm; G[3 * j + 1] = g.y / nm; G[3 * j + 2] = g.z / nm;
+__device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& a) {
+    const Grp g;
+    const int64_t j1 = a.rng[1];
+    for (int64_t j = a.rng[0] + grid_lane() / kProjGroup; j < j1; j += grid_lanes() / kProjGroup)
+        if (a.pend[j]) project_late_face(ev, a, g, j);   // uniform per group
+}
+
+// normalize_1111(grad) at arbitrary points (the QEM normals at the projected centroids, qem.hpp:256-316)
+// over the faces [rng[0], rng[1]) (P, G absolute)
+template <class Ev>
+__device__ __forceinline__ void normals_at_body(const Ev& ev, const float* __restrict__ P, const int64_t* __restrict__ rng,
+                                                float* __restrict__ G) {
+    const int64_t j1 = rng[1];
+    for (int64_t j = rng[0] + grid_lane(); j < j1; j += grid_lanes()) {
+        V3 g;
+        (void)ev.fg(P[3 * j], P[3 * j + 1], P[3 * j + 2], g);
+        const float nm = norm2f(g.x, g.y, g.z);
+        G[3 * j] = g.x / nm; G[3 * j + 1] = g.y / nm; G[3 * j + 2] = g.z / nm;
+    }
 }
 
 

@@ -232,6 +232,30 @@ def shard_transfers(voff, halos, rank, kind="halo"):
     return sends, recvs
 
 
+_SHARDS = {}   # (shape, mc settings, slot) -> Ob02Shard, kept across builds
+
+
+def shard_handle(shape, mc_settings, slot=0):
+    """The rank's OB02 shard handle for this object, created once and reused by later builds, as
+    build_geometry keeps its one refinement state (abi.hip g_ob02): a fresh handle allocates every
+    device buffer, its side stream and events on its first attach and projection (0.3-0.8 ms per
+    shard), a reused one only re-attaches the mesh.  release_shards() frees them."""
+    import json
+    import implisolid_amd as I
+    key = (json.dumps(shape, sort_keys=True), json.dumps(mc_settings, sort_keys=True), int(slot))
+    ob = _SHARDS.get(key)
+    if ob is None or not ob.h:
+        ob = _SHARDS[key] = I.Ob02Shard(shape, mc_settings)
+    return ob
+
+
+def release_shards():
+    """Close every kept shard handle (shard_handle)."""
+    for ob in _SHARDS.values():
+        ob.close()
+    _SHARDS.clear()
+
+
 def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_step=None, halo=True):
     """The OB02 loop (ob02_plan) over Z-slab shards: every rank holds the whole mesh and owns its
     slab's vertices [voff[rank], voff[rank + 1]).  Stream-ordered: the loop runs on the shard's HIP
@@ -255,7 +279,7 @@ def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_ste
     voff = [int(x) for x in voff]
     v0, v1 = voff[rank], voff[rank + 1]
     W = V.clone()   # the working array (updated in place)
-    ob = I.Ob02Shard(shape, mc_settings)
+    ob = shard_handle(shape, mc_settings)
     try:
         cur = torch.cuda.current_stream(device) if cuda else None
         ob.attach(W.data_ptr(), nv, F.data_ptr(), nf, v0, v1, cur.cuda_stream if cur is not None else 0)
@@ -330,12 +354,13 @@ def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_ste
             s_ob.synchronize()
         return None
     finally:
-        ob.close()
+        if cuda:
+            torch.cuda.ExternalStream(ob.stream(), device=device).synchronize()   # W lives until the loop is done
 
 
 def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
     """The sharded loop of ob02_sharded with every shard in this process, on one GPU (tests and the
-    bench's 8-rank estimate): shard r owns [voff[r], voff[r + 1]) and steps on its own HIP stream;
+    bench's 8-rank estimate; shard r's handle is shard_handle(..., slot=r), kept across calls): shard r owns [voff[r], voff[r + 1]) and steps on its own HIP stream;
     the exchanges of ob02_plan are device copies between the shards' arrays (full: every owned range
     to every shard; halo: each shard's halo from its owners).  timing=True: every shard's step is
     timed with HIP events on its stream, run one shard at a time (so the shards do not share the
@@ -348,7 +373,7 @@ def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
     voff = [int(x) for x in voff]
     n = len(voff) - 1
     Ws = [V.clone() for _ in range(n)]
-    obs = [I.Ob02Shard(shape, mc_settings) for _ in range(n)]
+    obs = [shard_handle(shape, mc_settings, slot=r) for r in range(n)]
     stats = {"steps": [], "exchange_bytes": []}
     try:
         import time
@@ -396,5 +421,4 @@ def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
         v, f = obs[0].download()
         return v, f, stats
     finally:
-        for ob in obs:
-            ob.close()
+        torch.cuda.synchronize(device)   # the shards' streams are done with Ws

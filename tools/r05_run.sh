@@ -5,6 +5,7 @@
 #   bench       the default bench line (N = 1)
 #   benchob     the bench's OB02 legs only (no config 5, no concurrent builds, no CPU baselines)
 #   ob02prof    kernel stats of tools/ob02_probe.py (config 2 / 3 / 3s builds)
+#   fold        the edge-length fold alone on real meshes' edge lengths (stats + kernel trace)
 # Each GPU step has its own time limit; the first failure ends the script.
 set -euo pipefail
 tag=${1:?tag}
@@ -29,6 +30,10 @@ for what in "$@"; do
     ob02prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/ob02" -o run -- \
           python3 tools/ob02_probe.py 5 > "$out/ob02_probe.log" 2>&1 ;;
+    fold)
+      IMPLISOLID_FOLD_STATS=1 timeout -k 10 200 python3 tools/fold_mesh_probe.py 3 > "$out/fold_stats.log" 2>&1
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/fold" -o run -- \
+          python3 tools/fold_mesh_probe.py 5 > "$out/fold_probe.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
   echo "step $what done"
