@@ -551,11 +551,10 @@ int implisolid_debug_fold(const float* terms, int64_t n, float* sum_out, int64_t
                              tr[i] & 0xfffff, ((tr[i] >> 20) & 0xff) - 64);
         }
         if (std::getenv("IMPLISOLID_FOLD_STATS"))
-            std::fprintf(stderr, "fold n=%lld steps zero/serial %lld table %lld terms %lld global-term-loads %lld fast %lld "
-                         "fast-finished %lld serial-chunks %lld cycles stage %lld walk %lld (table %lld terms %lld) term parts: "
-                         "preamble %lld fast %lld serial %lld\n",
-                         (long long)n, st[0], st[1], st[2], st[3], st[11], st[12], st[13], st[4], st[5], st[7], st[8], st[9],
-                         st[10], st[6]);
+            std::fprintf(stderr, "fold n=%lld steps: zero/single %lld run-lookups %lld scans %lld term-chunks %lld (serial %lld, "
+                         "global term loads %lld); cycles: stage %lld walk %lld (lookups %lld scans %lld serial %lld "
+                         "segments %lld; waiting for staged terms %lld)\n",
+                         (long long)n, st[0], st[1], st[2], st[3], st[10], st[11], st[4], st[5], st[6], st[7], st[8], st[9], st[12]);
         if (table_chunks) *table_chunks = tc;
     } catch (const std::exception& e) {
         report(e.what(), false);

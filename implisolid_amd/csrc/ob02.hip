@@ -745,9 +745,14 @@ __device__ __forceinline__ FoldPair wave_excl_pairs(FoldPair incl) { return dpp_
 __device__ __forceinline__ uint32_t pair_apply(FoldPair p, uint32_t x) { return x + ((x & 1u) ? p.c1 : p.c0); }
 
 // hint[c] = 1: the walk will probably need chunk c's terms (the estimate is 0, the estimated sum
-// crosses a power of two inside the chunk, with a margin of 2^-7 for the float chain's drift from the
-// double estimate, or the chunk is flagged in the binades the estimate puts s in) -- k_fold_walk
-// stages those chunks' terms in LDS beforehand
+// crosses a power of two inside the chunk, with a margin for the float chain's drift from the double
+// estimate, or the chunk is flagged in the binades the estimate puts s in) -- k_fold_walk stages
+// those chunks' terms in LDS beforehand and adds them serially; the other chunks it takes a run at a
+// time.  The margin only trades hinted chunks the sum does not cross in (a serial chunk each, ~2 k
+// cycles) against crossings in unhinted ones (a failed run lookup and a scan of the table); the
+// chain's relative drift is ~sqrt(n) 2^-25, 2^-15.5 for 500 k terms.  2^-7 hinted six chunks per
+// crossing at 256^3, 2^-12 about one.
+constexpr double kFoldHintMargin = 0x1p-12;
 __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e, int64_t n, const double* __restrict__ cs,
                                                     const double* __restrict__ bs, int32_t* __restrict__ base,
                                                     FoldPair* __restrict__ pairs, uint8_t* __restrict__ flags,
@@ -796,7 +801,7 @@ __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e,
         if (b == 1 || b == 2) fl34 |= f;   // the binades of the estimate and of twice it
     }
     if (lane == 0) {
-        const double lo = est_c * (1.0 - 0x1p-7), hi = est_c1 * (1.0 + 0x1p-7);
+        const double lo = est_c * (1.0 - kFoldHintMargin), hi = est_c1 * (1.0 + kFoldHintMargin);
         int elo = 0, ehi = 0;
         (void)frexp(lo, &elo);
         (void)frexp(hi, &ehi);
@@ -849,32 +854,178 @@ __device__ void alpha_list_dev(float avg, FoldOut* o) {
 // One block: its waves stage a window of the table (kWalkWindow chunk rows) and the terms of the
 // window's hinted chunks (kWalkSlots of them) in LDS, then wave 0 walks the window from LDS; terms
 // of an unhinted chunk the walk needs are read from memory.
-constexpr int kWalkThreads = 1024, kWalkWindow = 1536, kWalkSlots = 64, kWalkB0 = 0, kWalkBins = kFoldBinades - kWalkB0;
-// A table step's lane l takes the window's chunks s + 4 l .. s + 4 l + 3: chunk i's LDS position is
-// (i mod 4) (W / 4) + i / 4, so for each of the four the lanes read consecutive words (chunk i at
-// position i put the lanes 4 chunks = 128 bytes of pairs apart: 32-way bank conflicts)
-__device__ __forceinline__ int walk_pos(int i) { return (i & 3) * (kWalkWindow / 4) + (i >> 2); }
+constexpr int kWalkThreads = 1024, kWalkWindow = 4096, kWalkSlots = 32;
+static_assert(kWalkWindow % 256 == 0, "the window is whole run tiles");
 
-// kCycles: the clock64 split of the walk (diagnostics, implisolid_debug_fold with IMPLISOLID_FOLD_STATS):
-// each reading is an s_memtime whose wait also drains the wave's LDS operations, so the production
-// walk is compiled without them
+// Run maps (the walk's staging): for every chunk c that is not hinted, the composed map of chunks
+// [c, e) in binade base + 1 (the binade of the estimate of the sum before c: where no chunk is hinted
+// the estimate stays 2^-12 away from a power of two, 2^3.5 times the chain's drift from it, so the
+// sum is in that binade), e = the first hinted chunk after c, the first chunk of another base, or
+// the end of c's 256-chunk tile; its flags OR-ed; and the run's length.  The walk takes a whole run
+// with one lookup -- exact whenever the run's map keeps the value below 2^24 (every increment is
+// >= 0, so no chunk inside left the binade).  One wave per tile, 4 chunks per lane: in-lane suffixes,
+// then a segmented scan of the lanes' heads across the wave.
+struct FoldRun {
+    int32_t base;
+    uint16_t len;       // 0: a hinted chunk
+    uint8_t flags;      // the run's flags in binade base + 1
+    uint8_t pad;
+    FoldPair run;       // the run's map in binade base + 1
+};
+static_assert(sizeof(FoldRun) == 16, "one 16-byte row");
+constexpr int kRunTile = 256, kRunBinade = 1;
+
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x, int ctrl, uint32_t old = 0u) {
+    switch (ctrl) {
+        case 0x111: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x111, 0xf, 0xf, false);
+        case 0x112: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x112, 0xf, 0xf, false);
+        case 0x114: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x114, 0xf, 0xf, false);
+        case 0x118: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x118, 0xf, 0xf, false);
+        case 0x142: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x142, 0xa, 0xf, false);
+        case 0x143: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x143, 0xc, 0xf, false);
+        default: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    }
+}
+
+// One step of a segmented scan in lane order whose lower lanes hold LATER chunks (the lanes own the
+// tile's chunks in reverse): a lane still open (no run end yet) appends what the lanes below it
+// gathered -- their map after its own, their flags, their openness and their end.  A lane with no
+// source reads the identity: the identity map, no flags, and open (so it stays open).
+template <int Ctrl>
+__device__ __forceinline__ void runs_step(FoldPair& x, uint32_t& f, uint32_t& open) {
+    const FoldPair l = dpp_pair(x, Ctrl, 0);
+    const uint32_t lf = dpp_u32(f, Ctrl), lo = dpp_u32(open, Ctrl, 1u);
+    if (open) {
+        x = fold_compose(x, l);
+        f |= lf;
+        open = lo;
+    }
+}
+template <int Ctrl>
+__device__ __forceinline__ void runs_end_step(uint32_t& end, uint32_t& open) {
+    const uint32_t le = dpp_u32(end, Ctrl), lo = dpp_u32(open, Ctrl, 1u);
+    if (open && !lo) end = le;   // the first run end below: kept once found
+    if (open) open = lo;
+}
+
+// One wave: the run records of one 256-chunk tile (tile * kRunTile < nc), stored through `put(c, rec)`.
+template <class Put>
+__device__ __forceinline__ void fold_runs_tile(const FoldPair* __restrict__ pairs, const uint8_t* __restrict__ flags,
+                                               const int32_t* __restrict__ base, const uint8_t* __restrict__ hint, int nc,
+                                               int tile, const Put& put) {
+    const int lane = threadIdx.x & 63;
+    // lane l owns the tile's chunks 4 (63 - l) .. 4 (63 - l) + 3, so the DPP scans, which move data
+    // up the lanes, carry the later chunks' maps to the earlier ones
+    const int c0 = tile * kRunTile + 4 * (63 - lane);
+    bool in[5], hin[5];
+    int bs[5];
+    // every load first (one round trip): the chunks' pairs and flags in binade base + 1
+    FoldPair pv[4];
+    uint32_t fv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j < nc ? c0 + j : nc - 1;
+        pv[j] = pairs[(int64_t)c * kFoldBinades + kRunBinade];
+        fv[j] = flags[(int64_t)c * kFoldBinades + kRunBinade];
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {   // the lane's chunks and the one after them
+        const int c = c0 + j;
+        in[j] = c < nc && (j < 4 || lane > 0);
+        const int cq = in[j] ? c : 0;
+        hin[j] = in[j] && hint[cq] != 0;
+        bs[j] = in[j] ? base[cq] : 0;
+    }
+    bool bnd[4];   // a run ends after chunk j
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bnd[j] = !in[j] || !in[j + 1] || hin[j] || hin[j + 1] || bs[j + 1] != bs[j];
+    int nextb[4];   // the first run end at or after j in the lane (4: none)
+    nextb[3] = bnd[3] ? 3 : 4;
+#pragma unroll
+    for (int j = 2; j >= 0; --j) nextb[j] = bnd[j] ? j : nextb[j + 1];
+    const uint32_t lane_open = nextb[0] == 4 ? 1u : 0u;
+    // where the run that leaves this lane ends: the first run end in the later lanes
+    uint32_t end = lane_open ? 0u : (uint32_t)(c0 + nextb[0]), eo = lane_open;
+    runs_end_step<0x111>(end, eo);
+    runs_end_step<0x112>(end, eo);
+    runs_end_step<0x114>(end, eo);
+    runs_end_step<0x118>(end, eo);
+    runs_end_step<0x142>(end, eo);
+    runs_end_step<0x143>(end, eo);
+    const int tail_end = (int)dpp_u32(end, 0x138);   // gathered by the lanes holding the later chunks
+    FoldPair v[4];
+    uint32_t f[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool use = in[j] && !hin[j];
+        v[j] = use ? pv[j] : FoldPair{0u, 0u};
+        f[j] = use ? fv[j] : 0u;
+    }
+    FoldPair acc[4];   // in-lane: from chunk j to the first run end at or after it
+    uint32_t fa[4];
+    acc[3] = v[3];
+    fa[3] = f[3];
+#pragma unroll
+    for (int j = 2; j >= 0; --j) {
+        acc[j] = bnd[j] ? v[j] : fold_compose(v[j], acc[j + 1]);
+        fa[j] = bnd[j] ? f[j] : (f[j] | fa[j + 1]);
+    }
+    // the lanes' heads: each lane's map from its first chunk to the end of its run
+    FoldPair x = acc[0];
+    uint32_t xf = fa[0], open = lane_open;
+    runs_step<0x111>(x, xf, open);
+    runs_step<0x112>(x, xf, open);
+    runs_step<0x114>(x, xf, open);
+    runs_step<0x118>(x, xf, open);
+    runs_step<0x142>(x, xf, open);
+    runs_step<0x143>(x, xf, open);
+    const FoldPair tail = dpp_pair(x, 0x138, 0);
+    const uint32_t tailf = dpp_u32(xf, 0x138);
+    FoldRun rec[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool cont = nextb[j] == 4;   // the run goes on past this lane
+        rec[j].base = bs[j];
+        rec[j].len = (uint16_t)((!in[j] || hin[j]) ? 0 : (cont ? tail_end - (c0 + j) + 1 : nextb[j] - j + 1));
+        rec[j].flags = (uint8_t)(cont ? (fa[j] | tailf) : fa[j]);
+        rec[j].pad = 0;
+        rec[j].run = cont ? fold_compose(acc[j], tail) : acc[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (in[j]) put(c0 + j, rec[j]);
+}
+
+// kCycles: the clock64 split of the walk and its step counts (diagnostics, implisolid_debug_fold
+// with IMPLISOLID_FOLD_STATS): each reading is an s_memtime whose wait also drains the wave's LDS
+// operations, and the counters hold scalar registers the walk needs, so the production walk is
+// compiled without them
 template <bool kCycles>
 __device__ __forceinline__ long long walk_clock() {
     if constexpr (kCycles) return clock64();
     return 0;
 }
 
+// One block.  Its waves stage a window of the run maps (kWalkWindow chunks) and the terms of the
+// window's hinted chunks (up to kWalkSlots) in LDS; wave 0 walks the window:
+//   - at a chunk boundary, the run map of the chunk in the binade the sum is in: one lookup takes
+//     the chunks up to the next hinted one;
+//   - a hinted chunk, or one inside a run whose map does not hold (the sum crossed a binade where
+//     the estimate did not), goes term by term: its terms added serially, the chain's own float
+//     adds (256 dependent adds); a run that failed is first re-entered by a scan of the
+//     chunk table (64 lanes x 4 chunks) that finds the chunk where it failed;
+//   - a chunk holding a NaN or an infinity goes in segments (its terms as maps of the current
+//     binade up to each event, the event term as the chain's own add).
+// Every step adds exactly what the chain adds, so the sum is the serial chain's bit for bit
+// (fold_walk's semantics: the first NaN term decides the result, quieted as x86's addss quiets it;
+// after an inf only a NaN changes the sum).  Then the average edge length and make_alpha_list
+// (cp:144-194) for it, into FoldOut.
 template <bool kCycles>
 __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restrict__ e, int64_t n64,
                                                             const int32_t* __restrict__ base, const FoldPair* __restrict__ pairs,
                                                             const uint8_t* __restrict__ flags, const uint8_t* __restrict__ hint,
                                                             int64_t nf, FoldOut* __restrict__ out) {
-    // the table cells of binades base + kWalkB0 .. base + 3 (the chain stays within a factor 2 of
-    // the estimate: binades base + 1 and base + 2 in practice; a cell outside goes term by term),
-    // binade-major, chunks at walk_pos (a table step's lanes read consecutive words)
-    __shared__ FoldPair w_pair[kWalkWindow * kWalkBins];
-    __shared__ uint8_t w_flag[kWalkWindow * kWalkBins];
-    __shared__ int32_t w_base[kWalkWindow];
+    __shared__ uint4 w_rec[kWalkWindow];   // the chunks' FoldRun records
     __shared__ int16_t w_slot[kWalkWindow];
     __shared__ int16_t w_slot_chunk[kWalkSlots];
     __shared__ uint4 w_terms[kWalkSlots][64];   // a staged chunk's terms (bits), 4 per lane
@@ -888,46 +1039,57 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
     int k = 0;
     int table_chunks = 0;
     bool done = false;   // wave 0: a NaN or an inf decided the result
-    int st0 = 0, st1 = 0, st2 = 0, st3 = 0, st6 = 0;
-    long long cyc_stage = 0, cyc_walk = 0, cyc_table = 0, cyc_term = 0, cyc_pre = 0, cyc_serial = 0;
+    int st_zero = 0, st_lookup = 0, st_scan = 0, st_terms = 0, st_serial = 0, st_global = 0;
+    long long cyc_stage = 0, cyc_walk = 0, cyc_lookup = 0, cyc_scan = 0, cyc_serial = 0, cyc_seg = 0, cyc_wait = 0;
     for (int c0 = 0; c0 < nc; c0 += kWalkWindow) {
         const long long tc0 = walk_clock<kCycles>();
         const int wn = nc - c0 < kWalkWindow ? nc - c0 : kWalkWindow;
-        if (t == 0) w_nslots = 0;
         if (t < kWalkSlots) w_ready[t] = 0;
         __syncthreads();   // the previous window's walk is over
-        // the window's table rows, and slots for its hinted chunks in chunk order (the walk meets
-        // them in that order): a ballot per wave and the waves' counts before it
-        for (int i0 = 0; i0 < wn; i0 += kWalkThreads) {
-            const int i = i0 + t;
-            const int64_t c = c0 + i;
-            bool h = false;
-            if (i < wn) {
-                const int q = walk_pos(i);
-                w_base[q] = base[c];
-#pragma unroll
-                for (int b = 0; b < kWalkBins; ++b) {
-                    w_pair[b * kWalkWindow + q] = pairs[c * kFoldBinades + kWalkB0 + b];
-                    w_flag[b * kWalkWindow + q] = flags[c * kFoldBinades + kWalkB0 + b];
-                }
-                h = hint[c] != 0;
-            }
-            const uint64_t hm = __ballot(h);
-            if (lane == 0) w_wcnt[wid] = (int)__popcll((unsigned long long)hm);
-            __syncthreads();
-            int before = w_nslots;
-            for (int w = 0; w < wid; ++w) before += w_wcnt[w];
-            const int sl = before + (int)__popcll((unsigned long long)(hm & ((1ull << lane) - 1ull)));
-            if (i < wn) {
-                w_slot[i] = (int16_t)(h && sl < kWalkSlots ? sl : -1);
-                if (h && sl < kWalkSlots) w_slot_chunk[sl] = (int16_t)i;
-            }
-            __syncthreads();
-            if (t == kWalkThreads - 1) w_nslots = before + (int)__popcll((unsigned long long)hm);
-            __syncthreads();
+        // the window's run records, a wave per 256-chunk tile (the window is whole tiles), and the
+        // tiles' hinted-chunk counts
+        static_assert(kWalkWindow / kRunTile <= kWalkThreads / 64, "a tile per wave");
+        if (wid * kRunTile < wn) {
+            fold_runs_tile(pairs, flags, base, hint, nc, c0 / kRunTile + wid, [&](int c, const FoldRun& r) {
+                w_rec[c - c0] = *reinterpret_cast<const uint4*>(&r);
+            });
         }
+        __syncthreads();
+        // slots for the window's hinted chunks (len 0) in chunk order: a tile's lanes hold its chunks
+        // in reverse (fold_runs_tile), so a chunk's rank counts the hinted chunks of the higher lanes
+        int tile_hinted = 0, before = 0, total = 0;
+        uint64_t hb[4];
+        const int ct = wid * kRunTile + 4 * (63 - lane);   // this lane's first chunk in the window
+        if (wid * kRunTile < wn) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                hb[j] = __ballot(ct + j < wn && (w_rec[ct + j < wn ? ct + j : 0].y & 0xffffu) == 0u);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tile_hinted += (int)__popcll((unsigned long long)hb[j]);
+        }
+        if (lane == 0) w_wcnt[wid] = tile_hinted;
+        __syncthreads();
+        for (int w = 0; w < kWalkThreads / 64; ++w) {
+            before += w < wid ? w_wcnt[w] : 0;
+            total += w_wcnt[w];
+        }
+        if (wid * kRunTile < wn) {
+            const uint64_t above = lane < 63 ? ~0ull << (lane + 1) : 0ull;
+            int rank = before;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rank += (int)__popcll((unsigned long long)(hb[j] & above));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool h = (hb[j] >> lane) & 1ull;
+                if (ct + j < wn) w_slot[ct + j] = (int16_t)(h && rank < kWalkSlots ? rank : -1);
+                if (h && rank < kWalkSlots) w_slot_chunk[rank] = (int16_t)(ct + j);
+                rank += h ? 1 : 0;
+            }
+        }
+        if (t == 0) w_nslots = total;
+        __syncthreads();
         const int ns = w_nslots < kWalkSlots ? w_nslots : kWalkSlots;
-        cyc_stage += walk_clock<kCycles>() - tc0;
+        if constexpr (kCycles) cyc_stage += walk_clock<kCycles>() - tc0;
         if (wid != 0) {
             // waves 1.. stage the slots' terms while wave 0 walks, each then its ready flag (the walk
             // waits for it)
@@ -951,7 +1113,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             k = __builtin_amdgcn_readfirstlane(k);
             s = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s)));
             if (!(s >= 0x1p-100f && s <= 0x1p100f)) {
-                ++st0;
+                if constexpr (kCycles) ++st_zero;
                 if (s == 0.f) {   // 0 + (+-0) = +0: on to the first term of nonzero magnitude (or NaN)
                     const int kk = k + lane;
                     const bool in = kk < kend_w;
@@ -986,30 +1148,61 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             E = __builtin_amdgcn_readfirstlane(E);
             uint32_t su = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E));   // in [2^23, 2^24)
             const long long tA = walk_clock<kCycles>();
-            if ((k & (kFoldChunk - 1)) == 0) {   // whole chunks from the table, 4 per lane: 256 per step
-                if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (1 << 28) | k;
-                ++st1;
-                const int i0 = k / kFoldChunk - c0 + 4 * lane;
+            int ic = k / kFoldChunk - c0;
+            bool failed = false;   // a run map that did not hold: the table scan below re-enters it
+            if ((k & (kFoldChunk - 1)) == 0) {
+                // runs, one lookup each, while their maps keep the value in this binade (E and the
+                // integer su carry the exact value; s is formed once at the end)
+                for (;;) {
+                    const uint4 r0 = w_rec[ic];   // FoldRun: base, len | flags << 16, run map
+                    const int len = (int)(r0.y & 0xffffu);
+                    if (len == 0) break;   // a hinted chunk: its terms
+                    if constexpr (kCycles) ++st_lookup;
+                    const bool fb = E - (int)r0.x != kRunBinade || ((r0.y >> 16) & 0xffu) != 0u;
+                    const uint32_t x2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pair_apply(FoldPair{r0.z, r0.w}, su));
+                    if (fb || x2 >= kFoldCap) {
+                        failed = true;
+                        break;
+                    }
+                    su = x2;   // exact: the run's map kept it in this binade
+                    table_chunks += len;
+                    k += len * kFoldChunk;
+                    ic += len;
+                    if (k >= kend_w) break;
+                }
+                s = ldexpf((float)su, E - 24);
+                if (k >= kend_w) {
+                    if (k > n) k = n;
+                    if constexpr (kCycles) cyc_lookup += walk_clock<kCycles>() - tA;
+                    continue;
+                }
+                if constexpr (kCycles) cyc_lookup += walk_clock<kCycles>() - tA;
+            }
+            if (failed) {
+                // the run does not hold: a scan of the chunk table from here (64 lanes x 4 chunks,
+                // the lanes' maps in the binade s is in, prefix-composed) finds the chunk where the
+                // value first reaches 2^24 or meets a flagged chunk; the chunks before it are exact
+                if constexpr (kCycles) ++st_scan;
+                const int cc = k / kFoldChunk;
                 FoldPair tp[4];
                 bool ok[4];
-                int bb[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) bb[j] = E - w_base[walk_pos(i0 + j < wn ? i0 + j : wn - 1)];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int i = i0 + j < wn ? i0 + j : wn - 1;
-                    const bool inb = i0 + j < wn && bb[j] >= kWalkB0 && bb[j] < kFoldBinades;
-                    const int cell = (inb ? bb[j] - kWalkB0 : 0) * kWalkWindow + walk_pos(i);
-                    tp[j] = w_pair[cell];
-                    ok[j] = inb && w_flag[cell] == 0;
-                    if (!ok[j]) tp[j] = FoldPair{0u, 0u};
+                    const int c = cc + 4 * lane + j;
+                    const int cq = c < nc ? c : nc - 1;
+                    const int bb = E - base[cq];
+                    const bool inb = c < nc && c < c0 + wn && bb >= 0 && bb < kFoldBinades;
+                    const int64_t cell = (int64_t)cq * kFoldBinades + (inb ? bb : 0);
+                    tp[j] = pairs[cell];
+                    ok[j] = inb && flags[cell] == 0;
                 }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (!ok[j]) tp[j] = FoldPair{0u, 0u};
                 FoldPair p{0u, 0u};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) p = fold_compose(p, tp[j]);
                 const FoldPair incl = wave_scan_pairs(p), excl = wave_excl_pairs(incl);
-                // the lanes' values from the exact start: the first chunk that is unusable or takes
-                // the value to 2^24 ends the run (every map before it exact: no clamped value yet)
                 uint32_t v = pair_apply(excl, su), before = v;
                 int first = 4;
 #pragma unroll
@@ -1022,65 +1215,52 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 }
                 const uint64_t lm = __ballot(first < 4);
                 const int L = lm ? __ffsll((unsigned long long)lm) - 1 : 63;
-                const int fb = lm ? 4 * L + (int)lane_value((uint32_t)first, L) : 256;
-                if (fb > 0) {
+                const int fbk = lm ? 4 * L + (int)lane_value((uint32_t)first, L) : 256;
+                if (fbk > 0) {
                     const uint32_t tt = lm ? lane_value(before, L) : pair_apply(FoldPair{lane_value(incl.c0, 63),
-                                                                                          lane_value(incl.c1, 63)}, su);
+                                                                                           lane_value(incl.c1, 63)}, su);
                     s = ldexpf((float)tt, E - 24);   // < 2^24: exact in this binade
-                    table_chunks += fb;
-                    k += fb * kFoldChunk;
-                    if (k >= kend_w) {
+                    table_chunks += fbk;
+                    k += fbk * kFoldChunk;
+                    if (k >= kend_w || !lm) {   // the window's end, or the scan's reach: go on from there
                         if (k > n) k = n;
-                        cyc_table += walk_clock<kCycles>() - tA;
+                        if constexpr (kCycles) cyc_scan += walk_clock<kCycles>() - tA;
                         continue;
                     }
                     k = __builtin_amdgcn_readfirstlane(k);
-                    if (!lm) {   // the step's reach ended, not the run: another table step
-                        cyc_table += walk_clock<kCycles>() - tA;
-                        continue;
-                    }
-                    su = tt;   // the chunk that ended the run goes term by term now (same binade)
+                    ic = k / kFoldChunk - c0;
                 }
+                if constexpr (kCycles) cyc_scan += walk_clock<kCycles>() - tA;
             }
+            // the chunk the runs could not take (hinted, or the sum crosses a binade in it), from k on
             const long long tB = walk_clock<kCycles>();
-            cyc_table += tB - tA;
-            // the chunk the table could not take (the sum crosses a binade in it, or a term is flagged):
-            // its terms from k, 4 consecutive per lane, added serially; a chunk holding a NaN or an
-            // infinity goes in segments -- its terms as maps of the current binade (fold.hpp) up to
-            // the first event, an unusable term or the one that reaches the binade's end, which is
-            // added as the chain's own float add; then on from the next term in the binade the sum
-            // is in now
-            if (lane == 0 && st0 + st1 + st2 < 256) out->trace[st0 + st1 + st2] = (2 << 28) | k | (E + 64) << 20;
-            ++st2;
+            if constexpr (kCycles) ++st_terms;
             const int kc = k & ~(kFoldChunk - 1);
             const int kend = kc + kFoldChunk < n ? kc + kFoldChunk : n;
+            // its terms: from LDS if staged (a hinted chunk; uniform: one chunk), else from memory
             uint32_t xb[4];
-            // the chunk's terms: from LDS if it was staged (uniform: one chunk), else from memory, all
-            // four loads issued before any use
-            const int sl = __builtin_amdgcn_readfirstlane((int)w_slot[k / kFoldChunk - c0]);
+            const int sl = __builtin_amdgcn_readfirstlane((int)w_slot[ic]);
             if (sl >= 0) {
+                const long long tw = walk_clock<kCycles>();
                 while (__hip_atomic_load(&w_ready[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
                     __builtin_amdgcn_s_sleep(1);
+                if constexpr (kCycles) cyc_wait += walk_clock<kCycles>() - tw;
                 const uint4 tb = w_terms[sl][lane];
                 xb[0] = tb.x; xb[1] = tb.y; xb[2] = tb.z; xb[3] = tb.w;
             } else {
-                ++st3;
+                if constexpr (kCycles) ++st_global;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int kk = kc + 4 * lane + j;
                     xb[j] = __float_as_uint(e[kk < n ? kk : kc]);
                 }
             }
-            // The chunk's terms from k on, one by one, as the chain's own float adds: every lane runs
-            // the same chain over the wave's terms, read lane by lane (v_readlane, eight reads ahead
-            // of their adds; the terms outside [k, kend) masked to -0 in their lanes, which adds
-            // nothing to any value).  A chunk the table could not take crosses a binade or holds a
-            // term the table cannot express; 256 dependent adds (~2.4 k cycles) cost less than
-            // locating the crossing in it (a scan of the lanes' term maps, ~3.3 k cycles with the
-            // maps staged).  Finite terms only: a NaN payload or an infinity goes the segments' way
-            // below.
-            const long long tF = walk_clock<kCycles>();
-            cyc_pre += tF - tB;
+            // Added serially, the chain's own float adds: every lane runs the same chain over the
+            // wave's terms read lane by lane (v_readlane, eight reads ahead of their adds; the terms
+            // outside [k, kend) masked to -0 in their lanes, which adds nothing to any value): 256
+            // dependent adds, ~2.2 k cycles, less than locating a crossing in the chunk (a scan of
+            // the lanes' term maps, ~3.3 k cycles with the maps staged).  Unless a NaN or an infinity
+            // is among the terms from k on: then in segments below.
             {
                 uint32_t m[4];
                 bool special = false;
@@ -1091,7 +1271,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     special = special || (act && (xb[j] & 0x7f800000u) == 0x7f800000u);
                     m[j] = act ? xb[j] : 0x80000000u;
                 }
-                if (!__ballot(special) && s >= 0x1p-100f && s <= 0x1p100f) {
+                if (!__ballot(special)) {
+                    if constexpr (kCycles) ++st_serial;
                     float sv = s;
 #pragma unroll
                     for (int l = 0; l < 64; l += 2) {
@@ -1103,9 +1284,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     }
                     s = sv;
                     k = kend;
-                    ++st6;
-                    cyc_serial += walk_clock<kCycles>() - tF;
-                    cyc_term += walk_clock<kCycles>() - tB;
+                    if constexpr (kCycles) cyc_serial += walk_clock<kCycles>() - tB;
                     continue;
                 }
             }
@@ -1152,17 +1331,17 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 s = s + x;   // the event term: the chain's own float add
                 if (k >= kend) break;
             }
-            cyc_term += walk_clock<kCycles>() - tB;
+            if constexpr (kCycles) cyc_seg += walk_clock<kCycles>() - tB;
         }
-        cyc_walk += walk_clock<kCycles>() - tc1;
+        if constexpr (kCycles) cyc_walk += walk_clock<kCycles>() - tc1;
     }
     if (t == 0) {
         out->sum = s;
         out->table_chunks = table_chunks;
-        out->steps[0] = st0; out->steps[1] = st1; out->steps[2] = st2; out->steps[3] = st3;
-        out->steps[4] = 0; out->steps[5] = 0; out->steps[6] = st6;
-        out->cycles[0] = cyc_stage; out->cycles[1] = cyc_walk; out->cycles[2] = cyc_table; out->cycles[3] = cyc_term;
-        out->cycles[4] = cyc_pre; out->cycles[5] = 0; out->cycles[6] = cyc_serial;
+        out->steps[0] = st_zero; out->steps[1] = st_lookup; out->steps[2] = st_scan; out->steps[3] = st_terms;
+        out->steps[4] = st_serial; out->steps[5] = st_global; out->steps[6] = 0;
+        out->cycles[0] = cyc_stage; out->cycles[1] = cyc_walk; out->cycles[2] = cyc_lookup; out->cycles[3] = cyc_scan;
+        out->cycles[4] = cyc_serial; out->cycles[5] = cyc_seg; out->cycles[6] = cyc_wait;
         const float avg = (float)((double)s / (3. * (double)nf));
         out->avg = avg;
         alpha_list_dev(avg, out);
@@ -1698,6 +1877,9 @@ struct FoldLayout {
         bytes = est_off + (size_t)(chunks + 1) * 8;
     }
 };
+// the terms array of a fold: n terms, padded to whole chunks (the walk reads a chunk's terms with
+// scalar loads of the whole chunk)
+inline size_t fold_terms_bytes(int64_t n) { return (size_t)(fold_chunks(n) + 1) * kFoldChunk * sizeof(float); }
 
 // the table passes on `ts`, then the walk on `ws` after them (ws may be ts); with d_verts the terms
 // are the mesh's edge lengths, computed into d_terms by the first pass
@@ -1721,10 +1903,11 @@ void launch_fold(float* d_terms, int64_t n, int64_t nf, const float* d_verts, co
         IMPLI_HIP(hipEventRecord(table_done, ts));
         IMPLI_HIP(hipStreamWaitEvent(ws, table_done, 0));
     }
+    const int64_t nfa = nf > 0 ? nf : 1;
     if (cycles)
-        k_fold_walk<true><<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
+        k_fold_walk<true><<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nfa, d_out);
     else
-        k_fold_walk<false><<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nf > 0 ? nf : 1, d_out);
+        k_fold_walk<false><<<1, kWalkThreads, 0, ws>>>(d_terms, n, d_base, d_pair, d_flags, d_hint, nfa, d_out);
 }
 
 // compute_average_edge_length (cp:70-82) is one serial float chain in face order.  The terms, the
@@ -1735,7 +1918,7 @@ void launch_fold(float* d_terms, int64_t n, int64_t nf, const float* d_verts, co
 // cross-stream signalling per repeat).  No host round trip: the average and the alpha list stay in
 // device memory (FoldOut) for the searches and QEM.
 hipStream_t Ob02::start_edge_fold() {
-    norms_.reserve((size_t)(nf + 1) * 12);
+    norms_.reserve(std::max<size_t>((size_t)(nf + 1) * 12, fold_terms_bytes(3 * nf)));
     const FoldLayout L(3 * nf);
     fold_sum_.reserve(L.bytes);
     fold_out_.reserve(sizeof(FoldOut));
@@ -1760,7 +1943,7 @@ void Ob02::finish_edge_fold() {   // s waits for the prep pass (stream order, no
 float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* stats, int* trace) {
     const FoldLayout L(n);
     DevBuf terms, tab, fo;
-    terms.reserve((size_t)(n + 1) * 4);
+    terms.reserve(fold_terms_bytes(n));
     tab.reserve(L.bytes);
     fo.reserve(sizeof(FoldOut));
     if (n) IMPLI_HIP(hipMemcpy(terms.p, h_terms, (size_t)n * 4, hipMemcpyHostToDevice));
@@ -1774,18 +1957,18 @@ float debug_fold(const float* h_terms, int64_t n, int* table_chunks, long long* 
     tab.release();
     fo.release();
     if (table_chunks) *table_chunks = h.table_chunks;
-    if (stats) {
+    if (stats) {   // steps: zero / single adds, run lookups, scans, term steps, serial chunks, global term loads;
+                   // cycles: staging, walk, lookups, scans, serial chunks, segments
         for (int i = 0; i < 4; ++i) stats[i] = h.steps[i];
         stats[4] = h.cycles[0];
         stats[5] = h.cycles[1];
-        stats[6] = h.cycles[6];
-        stats[11] = h.steps[4];
-        stats[12] = h.steps[5];
-        stats[13] = h.steps[6];
-        stats[7] = h.cycles[2];
-        stats[8] = h.cycles[3];
-        stats[9] = h.cycles[4];
-        stats[10] = h.cycles[5];
+        stats[6] = h.cycles[2];
+        stats[7] = h.cycles[3];
+        stats[8] = h.cycles[4];
+        stats[9] = h.cycles[5];
+        stats[10] = h.steps[4];
+        stats[11] = h.steps[5];
+        stats[12] = h.cycles[6];
     }
     return h.sum;
 }

@@ -34,6 +34,9 @@ for what in "$@"; do
       IMPLISOLID_FOLD_STATS=1 timeout -k 10 200 python3 tools/fold_mesh_probe.py 3 > "$out/fold_stats.log" 2>&1
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/fold" -o run -- \
           python3 tools/fold_mesh_probe.py 5 > "$out/fold_probe.log" 2>&1 ;;
+    shardtrace)   # the 8-shard OB02 loop at 256^3 under a kernel trace (tools/ob02_shard_probe.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$root/$out/shard" -o run -- \
+          python3 tools/ob02_shard_probe.py 8 256 > "$out/shard_probe.json" 2> "$out/shard_probe.err" ;;
     *) echo "unknown step $what"; exit 2 ;;
   esac
   echo "step $what done"
