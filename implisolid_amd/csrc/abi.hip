@@ -982,10 +982,10 @@ struct implisolid_batch {
     int depth = 0;
     // merged: objects of tree depth <= kBatchShallowDepth (rows [0, n_shallow)) run the interval and
     // eval passes with 9-slot node stacks (four waves per SIMD), the rest with 12 or 16
-    int n_shallow = 0, depth_shallow = 0, depth_deep = 0;
+    int n_shallow = 0, depth_shallow = 0, depth_deep = 0, vdepth_shallow = 0, vdepth_deep = 0;
     // merged: the groups run as independent pipelines (eval passes + marching cubes), group 0 on the
     // caller's stream, group k on streams[k - 1]: {first row, rows, stack depth}
-    struct Group { int row0, n, depth; };
+    struct Group { int row0, n, depth, vdepth; };
     std::vector<Group> groups;
     std::vector<hipGraphExec_t> execs;   // empty when capture is unavailable (direct launches)
     std::vector<hipStream_t> streams;
@@ -1055,15 +1055,17 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
                     b->depth = std::max(b->depth, e->depth());
                     int& d = shallow ? b->depth_shallow : b->depth_deep;
                     d = std::max(d, e->depth());
+                    int& vd = shallow ? b->vdepth_shallow : b->vdepth_deep;
+                    vd = std::max(vd, e->vdepth());
                     b->n_shallow += shallow ? 1 : 0;
                 }
             // groups: the shallow rows split into batch_groups() consecutive runs, then the deep rows
             const int K = std::max(1, std::min(batch_groups(), b->n_shallow));
             for (int k = 0; k < K && b->n_shallow > 0; ++k) {
                 const int r0 = b->n_shallow * k / K, r1 = b->n_shallow * (k + 1) / K;
-                if (r1 > r0) b->groups.push_back({r0, r1 - r0, b->depth_shallow});
+                if (r1 > r0) b->groups.push_back({r0, r1 - r0, b->depth_shallow, b->vdepth_shallow});
             }
-            if (n > b->n_shallow) b->groups.push_back({b->n_shallow, n - b->n_shallow, b->depth_deep});
+            if (n > b->n_shallow) b->groups.push_back({b->n_shallow, n - b->n_shallow, b->depth_deep, b->vdepth_deep});
             b->objs.reserve(rows.size() * sizeof(ObjArgs));
             IMPLI_HIP(hipMemcpy(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice));
             IMPLI_HIP(hipStreamSynchronize(s0));
@@ -1126,7 +1128,7 @@ int implisolid_batch_run(implisolid_batch* b, void* stream) {
                 const implisolid_batch::Group& gr = b->groups[(size_t)k];
                 hipStream_t q = k == 0 ? s : b->streams[(size_t)k - 1];
                 const ObjArgs* rows = b->objs.as<ObjArgs>() + gr.row0;
-                launch_batch_eval(rows, gr.n, gr.depth, E0.d_rabbit(), E0.tab_range(), E0.grid(), fill, q);
+                launch_batch_eval(rows, gr.n, gr.depth, gr.vdepth, E0.d_rabbit(), E0.tab_range(), E0.grid(), fill, q);
                 launch_batch_mc(rows, gr.n, E0.d_cases(), E0.grid(), q);
             }
             for (int k = 1; k < ng; ++k) {

@@ -176,6 +176,18 @@ void Engine::release_jit() {
     jit_iv_ = JitIntervalKernels{};
 }
 
+// the value stack's high-water mark of a program run without pruning (a pruned run skips a whole
+// operand subtree and its CSG node's pop together, so it never holds more)
+int program_vdepth(const Program& p) {
+    int vp = 0, best = 1;
+    for (int pc = 0; pc < p.n_instr; ++pc) {
+        const Instr& I = p.instr[pc];
+        if (I.op == OP_PRIM) best = std::max(best, ++vp);
+        else if (I.op != OP_XFORM) vp = std::max(0, vp - 1);
+    }
+    return best;
+}
+
 void Engine::set_object(const Program& prog) {
     // the same object again (repeated builds): keep its modules and its eval count
     if (have_object_ && std::memcmp(&prog, &prog_host_, sizeof(Program)) == 0) return;
@@ -184,9 +196,11 @@ void Engine::set_object(const Program& prog) {
     IMPLI_HIP(hipDeviceSynchronize());
     IMPLI_HIP(hipMemcpy(prog_.p, &prog, sizeof(Program), hipMemcpyHostToDevice));
     depth_ = prog.max_depth;
+    vdepth_ = program_vdepth(prog);
     n_csg_ = prog.n_csg;
     prog_host_ = prog;
     release_jit();
+    TreeJit::instance().trim();   // the device is synchronised here: a safe point to unload modules
     evals_ = 0;
     jit_fn_ = nullptr;
     have_object_ = true;

@@ -121,6 +121,8 @@ public:
     const uint64_t* d_signs() const { return signs_.as<uint64_t>(); }
     const uint32_t* d_counters() const { return counters_.as<uint32_t>(); }
     int depth() const { return depth_; }
+    // the most values the object's postfix program holds at once (the value stacks' depth)
+    int vdepth() const { return vdepth_; }
     const Program* d_program() const { return prog_.as<Program>(); }
     // true if the last eval_field ran the JIT-compiled tree kernel
     bool used_jit() const { return jit_fn_ != nullptr; }
@@ -162,6 +164,7 @@ private:
 
     GridDesc grid_{};
     int depth_ = 1;
+    int vdepth_ = 1;
     int n_csg_ = 0;
     Program prog_host_{};
     TreeJit::Slot* jit_slot_ = nullptr;   // the object's module (null: JIT off); may still compile

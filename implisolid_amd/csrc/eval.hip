@@ -119,11 +119,13 @@ __device__ __forceinline__ void prim_f2(int t, const float* __restrict__ tab, co
     }
 }
 
-template <int D, class ProgP>
+// D: the point stacks' capacity (tree depth + 1); V: the value stacks' (the most values a postfix
+// program holds at once, Engine::vdepth(): a Sethi-Ullman-like count, usually well below D)
+template <int D, class ProgP, int V = D>
 __device__ __forceinline__ void eval_f2_pruned(ProgP __restrict__ prog, const float* __restrict__ tab,
                                                uint64_t modes, float x, float y, float z0, float z1, float& r0,
                                                float& r1) {
-    float px0[D], py0[D], pz0[D], px1[D], py1[D], pz1[D], vf0[D], vf1[D];
+    float px0[D], py0[D], pz0[D], px1[D], py1[D], pz1[D], vf0[V], vf1[V];
     int sp = 0, vp = 0;
     px0[0] = x; py0[0] = y; pz0[0] = z0;
     px1[0] = x; py1[0] = y; pz1[0] = z1;
@@ -174,10 +176,10 @@ __device__ __forceinline__ void eval_f2_pruned(ProgP __restrict__ prog, const fl
     r1 = vf1[0];
 }
 
-template <int D, class ProgP = const Program*>
+template <int D, class ProgP = const Program*, int V = D>
 struct InterpEval2 : InterpEval<D, ProgP> {   // the interpreter with the layer pair (eval_bricks.hpp eval_pair)
     __device__ __forceinline__ void pair(uint64_t m, float x, float y, float z0, float z1, float& f0, float& f1) const {
-        eval_f2_pruned<D>(this->prog, this->tab, m, x, y, z0, z1, f0, f1);
+        eval_f2_pruned<D, ProgP, V>(this->prog, this->tab, m, x, y, z0, z1, f0, f1);
     }
 };
 
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(kFillBlock) void k_brick_fill_b(const ObjArgs* __re
 }
 // W: the occupancy request (four waves per SIMD at stack depth 9: 128 VGPRs and 28 B of scratch,
 // 0.531 -> 0.507 ms per config-5 pass against three waves without scratch; five spill far more: 1.0 ms)
-template <int D, bool Pair, int W>
+template <int D, bool Pair, int W, int V = D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_eval_field_pruned_b(
     const ObjArgs* __restrict__ objs, int n, const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
     __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
@@ -473,7 +475,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         const uint32_t li = i - s_pre[k];
         // Pair: both layers in one pass of the interpreter (InterpEval2; twice the node stacks in VGPRs)
         const ClaimCtx cc{o.fill, o.ccls, o.modes, o.cmodes, bg.nbx, bg.nbx * bg.nby};
-        eval_listed_deferred<InterpEval2<D, ProgC>, Pair>(InterpEval2<D, ProgC>{{prog_const(o.prog), tab}}, g, bg, cc,
+        eval_listed_deferred<InterpEval2<D, ProgC, V>, Pair>(InterpEval2<D, ProgC, V>{{prog_const(o.prog), tab}}, g, bg, cc,
                                                           o.blist[li], o.lmodes[li], o.field,
                                                           static_cast<sign_piece_t*>(o.signs), o.claimed,
                                                           o.counters + kClaimedWord, (uint32_t)bg.n_bricks);
@@ -481,7 +483,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 }
 // the claimed candidates of every object (eval_listed_deferred), one wave per candidate: values
 // only -- their sign pieces are constant and already written -- with the candidate's own modes
-template <int D, bool Pair>
+template <int D, bool Pair, int V = D>
 __global__ __launch_bounds__(256) void k_eval_claimed_b(const ObjArgs* __restrict__ objs, int n,
                                                         const float* __restrict__ tab, GridDesc g, BrickGrid bg) {
     __shared__ uint32_t s_pre[kMaxBatchObjects + 4];
@@ -496,7 +498,7 @@ __global__ __launch_bounds__(256) void k_eval_claimed_b(const ObjArgs* __restric
         const int cb = cx + cy * bg.nbx + (cz / kCZ) * bg.nbx * bg.nby;   // the coarse box (same x, y grid)
         const uint64_t m = o.ccls[cb] == kBrickMixed ? o.modes[cur] : o.cmodes[cb];
         uint64_t neg[kBZ], valid;
-        eval_one_brick<InterpEval2<D, ProgC>, Pair>(InterpEval2<D, ProgC>{{prog_const(o.prog), tab}}, g, bg, cur, m, o.field,
+        eval_one_brick<InterpEval2<D, ProgC, V>, Pair>(InterpEval2<D, ProgC, V>{{prog_const(o.prog), tab}}, g, bg, cur, m, o.field,
                                                     static_cast<sign_piece_t*>(o.signs), false, neg, valid);
     }
 }
@@ -671,31 +673,47 @@ void launch_eval_bricks_interp(const Program* d_prog, int depth, const float* d_
 // r04aq_*, r04ar_*)
 constexpr unsigned kBatchRefineBlocks = 2048, kBatchEvalBlocks = 2048, kBatchClaimedBlocks = 1024;
 
-void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
-                       int sign_fill, hipStream_t s) {
+// value stacks of their own capacity for the shallow class (IMPLISOLID_BATCH_VSTACK=0: the point
+// stacks' capacity, as before round 5)
+static bool batch_vstack() {
+    static const bool on = [] {
+        const char* v = std::getenv("IMPLISOLID_BATCH_VSTACK");
+        return !(v && std::atoi(v) == 0);
+    }();
+    return on;
+}
+
+void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, int vdepth, const float* d_rabbit, float2 tab_range,
+                       const GridDesc& g, int sign_fill, hipStream_t s) {
     const BrickGrid bg = brick_grid(g), cg = coarse_grid(g);
     if (bg.n_bricks <= 0 || n <= 0) return;
     if (n > kMaxBatchObjects) throw std::runtime_error("merged object stream: more than 1024 objects per launch");
     const dim3 gc((unsigned)((cg.n_bricks + 255) / 256), (unsigned)n);
     const dim3 gf(fill_grid(g), (unsigned)n);
-#define IMPLI_BATCH_EVAL(DD, WW)                                                                               \
-    do {                                                                                                       \
-        k_coarse_modes_b<DD><<<gc, 256, 0, s>>>(d_objs, d_rabbit, tab_range, g, cg);                           \
-        k_brick_refine_b<DD><<<kBatchRefineBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, tab_range, g, bg, cg);     \
-        k_brick_fill_b<<<gf, kFillBlock, 0, s>>>(d_objs, g, bg, cg, sign_fill);                                \
-        if (interp_pair()) {                                                                                   \
-            k_eval_field_pruned_b<DD, true, WW><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);  \
-            k_eval_claimed_b<DD, true><<<kBatchClaimedBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);        \
-        } else {                                                                                               \
-            k_eval_field_pruned_b<DD, false, WW><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg); \
-            k_eval_claimed_b<DD, false><<<kBatchClaimedBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);       \
-        }                                                                                                      \
+#define IMPLI_BATCH_EVAL(DD, WW, VV)                                                                               \
+    do {                                                                                                           \
+        k_coarse_modes_b<DD><<<gc, 256, 0, s>>>(d_objs, d_rabbit, tab_range, g, cg);                               \
+        k_brick_refine_b<DD><<<kBatchRefineBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, tab_range, g, bg, cg);         \
+        k_brick_fill_b<<<gf, kFillBlock, 0, s>>>(d_objs, g, bg, cg, sign_fill);                                    \
+        if (interp_pair()) {                                                                                       \
+            k_eval_field_pruned_b<DD, true, WW, VV><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);  \
+            k_eval_claimed_b<DD, true, VV><<<kBatchClaimedBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);        \
+        } else {                                                                                                   \
+            k_eval_field_pruned_b<DD, false, WW, VV><<<kBatchEvalBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg); \
+            k_eval_claimed_b<DD, false, VV><<<kBatchClaimedBlocks, 256, 0, s>>>(d_objs, n, d_rabbit, g, bg);       \
+        }                                                                                                          \
     } while (0)
     // stack capacity: kBatchShallowDepth slots for shallow objects (kernels.hpp), else the
-    // interpreter's floor (12: VGPR index mode) or 16
-    if (depth <= kBatchShallowDepth) IMPLI_BATCH_EVAL(kBatchShallowDepth, 4);
-    else if (depth <= 12) IMPLI_BATCH_EVAL(12, 2);
-    else IMPLI_BATCH_EVAL(16, 1);
+    // interpreter's floor (12: VGPR index mode) or 16; the shallow class's value stacks by their own
+    // depth (6 covers every config-5 object of that class)
+    if (depth <= kBatchShallowDepth) {
+        if (batch_vstack() && vdepth <= 6) IMPLI_BATCH_EVAL(kBatchShallowDepth, 4, 6);
+        else IMPLI_BATCH_EVAL(kBatchShallowDepth, 4, kBatchShallowDepth);
+    } else if (depth <= 12) {
+        IMPLI_BATCH_EVAL(12, 2, 12);
+    } else {
+        IMPLI_BATCH_EVAL(16, 1, 16);
+    }
 #undef IMPLI_BATCH_EVAL
 }
 

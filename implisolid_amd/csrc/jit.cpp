@@ -739,7 +739,12 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake, hipStream
         // before any other request can evict it (evict_locked takes only slots with refs == 0)
         ++slot->refs;
         slot->last_use = ++tick_;
-        if ((int)cache_.size() > max_modules_.load()) evict_locked(evict, defer_eviction(stream));
+        // modules are unloaded at trim points (trim(): set_object, wait_idle), where the device is
+        // synchronised anyway -- never here, where another thread may hold a global-mode graph
+        // capture the unload's device synchronisation would invalidate.  Only a cache four times
+        // over its bound (a process that never reaches a trim point) is trimmed here, and not
+        // while the caller's own stream captures.
+        if ((int)cache_.size() > 4 * max_modules_.load()) evict_locked(evict, defer_eviction(stream));
         if (fresh) {
             if (m == kAsync && !stop_) {
                 queue_.push_back(slot);
@@ -841,8 +846,20 @@ int TreeJit::modules() const {
 }
 
 void TreeJit::wait_idle() {
-    std::unique_lock<std::mutex> lock(mu_);
-    idle_cv_.wait(lock, [this] { return queue_.empty() && busy_ == 0; });
+    {
+        std::unique_lock<std::mutex> lock(mu_);
+        idle_cv_.wait(lock, [this] { return queue_.empty() && busy_ == 0; });
+    }
+    trim();
+}
+
+void TreeJit::trim() {
+    std::vector<Slot*> evict;
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        if ((int)cache_.size() > max_modules_.load()) evict_locked(evict, false);
+    }
+    unload(evict);
 }
 
 std::vector<TreeJit::Slot*> TreeJit::precompile(const std::vector<Program>& progs, int threads) {

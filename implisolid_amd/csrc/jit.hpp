@@ -94,7 +94,10 @@ public:
     void set_max_modules(int n) { max_modules_.store(n < 8 ? 8 : n); }
     int deferred_evictions() const { return n_deferred_.load(); }
     // block until every scheduled compilation has finished (bench / batch setup)
-    void wait_idle();
+    void wait_idle();   // ... then trim()
+    // unload the least recently used modules nobody holds while the cache is over its bound (a
+    // device synchronisation): called where the device is synchronised anyway (Engine::set_object)
+    void trim();
     // compile the modules of many programs (sync, up to `threads` host threads); request() then
     // finds them ready.  Returns one reference per program (null where JIT is off or the source
     // failed), which the caller releases once its engines hold their own: until then the module

@@ -82,7 +82,7 @@ struct ObjArgs {
 // Node-stack capacity: 9 slots for objects of depth <= 9 (the smallest capacity the compiler
 // still indexes through VGPR index mode rather than select chains; the eval then runs four waves
 // per SIMD, 128 VGPRs and a small spill), else the interpreter's 12 or 16
-void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
+void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, int vdepth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                        int sign_fill, hipStream_t s);
 constexpr int kBatchShallowDepth = 9;
 // merged object streams: the shallow class as this many pipelines on separate streams (abi.hip;

@@ -68,7 +68,11 @@ static_assert(sizeof(Instr) == 16, "Instr layout");
 // evaluate as m_dd v + m_d3 (xform_diag): at the finite sample points of a brick that is the full
 // row's value (a zero coefficient adds a +-0, which the row's final + m_d3 != -0 absorbs), exactly
 // the row the JIT emits for such a matrix (jit.cpp xform_row).  Points that may be NaN or infinite
-// (OB02 vertices) keep the full rows.
+// (OB02 vertices) keep the full rows.  Limit: "finite" holds for a nested transform's input only
+// while no outer transform overflows the float range: a scale chain taking a grid coordinate past
+// 3.4e38 makes a coordinate +-inf, where the full row gives 0 * inf = NaN and this row a finite value
+// (ADVICE r04).  Such a tree has no surface at any float resolution; its field is not compared with
+// the reference there (parity unpinned in that corner).
 enum XformPattern : int16_t { XF_GENERIC = 0, XF_DIAG = 1 };
 
 // Per-brick pruning: 2 bits per CSG node (index < kMaxPruned): both operands, left only, right only.
