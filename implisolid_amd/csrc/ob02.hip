@@ -2065,11 +2065,30 @@ void Ob02::centroids_projection(bool enable_qem) {
     if (profile_ && nw > 0) {   // the evaluations of this projection, summed on the host
         int64_t r[8];
         ranges(r);
-        std::vector<uint32_t> h((size_t)(r[3] - r[2]));
-        if (!h.empty())
+        std::vector<uint32_t> h((size_t)(r[3] - r[2])), pend(h.size());
+        if (!h.empty()) {
             IMPLI_HIP(hipMemcpyAsync(h.data(), evals_buf_.as<uint32_t>() + r[2], h.size() * 4, hipMemcpyDeviceToHost, s));
+            IMPLI_HIP(hipMemcpyAsync(pend.data(), pend_.as<uint32_t>() + r[2], h.size() * 4, hipMemcpyDeviceToHost, s));
+        }
         IMPLI_HIP(hipStreamSynchronize(s));
         for (uint32_t e : h) evals_ += e;
+        if (std::getenv("IMPLISOLID_PROJ_STATS")) {   // diagnostics: the searches' balance per wave
+            // (16 faces per wave of 4-lane groups: a wave runs as long as its longest face)
+            uint64_t sum = 0, wmax = 0, npend = 0;
+            for (size_t w0 = 0; w0 < h.size(); w0 += 16) {
+                uint32_t m = 0;
+                for (size_t j = w0; j < std::min(h.size(), w0 + 16); ++j) m = std::max(m, h[j]);
+                wmax += (uint64_t)m * std::min<size_t>(16, h.size() - w0);
+            }
+            for (size_t j = 0; j < h.size(); ++j) {
+                sum += h[j];
+                npend += pend[j] ? 1 : 0;
+            }
+            std::fprintf(stderr, "projection faces %zu evals %llu (per face %.2f) wave-max-bound %llu (balance %.3f) "
+                         "pending after the early pass %llu\n", h.size(), (unsigned long long)sum,
+                         (double)sum / (double)h.size(), (unsigned long long)wmax, (double)sum / (double)wmax,
+                         (unsigned long long)npend);
+        }
     }
     store_pointset("post_p_centroids", proj_.as<float>(), nf, false);
     store_pointset("pre_qem_verts", verts_.as<float>(), nv, false);
