@@ -2008,6 +2008,24 @@ const float* Ob02::perturbations() {
     return pert_dev_->buf.as<float>();
 }
 
+// the late pass's group widths (A/B switches, read once): IMPLISOLID_LATE_WMAX (4..64),
+// IMPLISOLID_LATE_FLAT (0/1)
+static int late_wmax() {
+    static const int w = [] {
+        const char* e = std::getenv("IMPLISOLID_LATE_WMAX");
+        const int v = e ? std::atoi(e) : 64;
+        return v >= 64 ? 64 : v >= 32 ? 32 : v >= 16 ? 16 : v >= 8 ? 8 : 4;
+    }();
+    return w;
+}
+static int late_flat() {
+    static const int f = [] {
+        const char* e = std::getenv("IMPLISOLID_LATE_FLAT");
+        return e ? (std::atoi(e) ? 1 : 0) : 1;
+    }();
+    return f;
+}
+
 void Ob02::centroids_projection(bool enable_qem) {
     if (!nf) return;
     if (!topo_valid_) build_topology();
@@ -2030,7 +2048,8 @@ void Ob02::centroids_projection(bool enable_qem) {
     a.fn = fn_.as<float>();
     a.fc = fcbuf.as<float>();
     a.pend = pend_.as<uint32_t>();
-    a.pend_count = misc_.as<uint32_t>();
+    a.late_wmax = late_wmax();
+    a.late_flat = late_flat();
     a.cap_hits = misc_.as<uint32_t>() + 1;
     a.cen = cen_.as<float>();
     a.dir = dir_.as<float>();

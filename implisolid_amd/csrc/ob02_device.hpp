@@ -121,7 +121,8 @@ struct ProjArgs {
     float* fn;              // facet normals (written by the early pass)
     float* fc;              // f(centroid) (written by the early pass)
     uint32_t* pend;         // early pass: per face, 1 if its centroid is unresolved (the late pass's)
-    uint32_t* pend_count;   // (unused)
+    int late_wmax;          // the late pass's widest group (4..64 lanes, a power of two)
+    int late_flat;          // 1: a round of the late searches may cross directions; 0: one direction per round
     uint32_t* cap_hits;     // bisections that reached kBisectCap (accumulated over the build)
     float* cen;             // centroids (written by the prep pass)
     float* dir;             // the type-0 direction per face (prep pass)
@@ -142,16 +143,33 @@ constexpr int kProjGroup = 4;
 constexpr int kBisLevels = 2;
 static_assert((1 << kBisLevels) - 1 <= kProjGroup && 64 % kProjGroup == 0, "bisection tree fits the group");
 
-struct Grp {   // a centroid's lanes inside the wave (control flow is uniform per group)
+template <int W>
+struct GrpW {   // a centroid's W lanes inside the wave (control flow is uniform per group)
     int sub, base;
-    __device__ Grp() {
+    __device__ GrpW() {
         const int lane = (int)(threadIdx.x & 63);
-        sub = lane & (kProjGroup - 1);
+        sub = lane & (W - 1);
         base = lane - sub;
     }
-    __device__ uint32_t bits(bool p) const {
-        return (uint32_t)((__ballot(p) >> base) & ((1ull << kProjGroup) - 1ull));
+    __device__ uint64_t bits(bool p) const {
+        if constexpr (W == 64) return (uint64_t)__ballot(p);
+        else return (uint64_t)((__ballot(p) >> base) & ((1ull << W) - 1ull));
     }
+    __device__ float from(float v, int k) const { return __shfl(v, base + k, 64); }
+    __device__ V3 from(V3 v, int k) const { return V3{from(v.x, k), from(v.y, k), from(v.z, k)}; }
+};
+using Grp = GrpW<kProjGroup>;
+
+struct GrpR {   // a group of w lanes (w a power of two, 4..64, uniform over the wave), chosen at run time
+    int sub, base, w;
+    uint64_t mask;
+    __device__ explicit GrpR(int width) : w(width) {
+        const int lane = (int)(threadIdx.x & 63);
+        sub = lane & (w - 1);
+        base = lane - sub;
+        mask = w == 64 ? ~0ull : (1ull << w) - 1ull;
+    }
+    __device__ uint64_t bits(bool p) const { return ((uint64_t)__ballot(p) >> base) & mask; }
     __device__ float from(float v, int k) const { return __shfl(v, base + k, 64); }
     __device__ V3 from(V3 v, int k) const { return V3{from(v.x, k), from(v.y, k), from(v.z, k)}; }
 };
@@ -165,11 +183,10 @@ __device__ __forceinline__ V3 bis_mid(V3 a, V3 b) {   // bisection.hpp:225-231: 
 // where f > tol (a NaN moves neither: the serial loop repeats that mid until the cap).  Lane k < 2^L - 1
 // evaluates node k of the next L levels' decision tree (heap order: child 2k+1 after f < -tol, 2k+2
 // after f > tol); the group then walks the path the serial loop takes through those levels.
-template <class Ev>
-__device__ V3 bisect_g(const Grp& g, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_hits,
-                       uint32_t& evals) {
+template <class G, class Ev>
+__device__ V3 bisect_g(const G& g, const int L, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_hits, uint32_t& evals) {
     int it = 0;
-    const int node = g.sub < (1 << kBisLevels) - 1 ? g.sub : 0;
+    const int node = g.sub < (1 << L) - 1 ? g.sub : 0;
     int depth = 0, bits = 0;   // node's path from the root, first decision in the lowest bit (1: x1 <- mid)
     for (int n = node; n > 0; n = (n - 1) >> 1) bits = (bits << 1) | ((n & 1) ? 1 : 0), ++depth;
     for (;;) {
@@ -181,9 +198,9 @@ __device__ V3 bisect_g(const Grp& g, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_h
         }
         const V3 mid = bis_mid(a, b);
         const float vm = ev.f(mid.x, mid.y, mid.z);
-        evals += (1 << kBisLevels) - 1;
+        evals += (1 << L) - 1;
         int cur = 0;
-        for (int lvl = 0; lvl < kBisLevels; ++lvl) {
+        for (int lvl = 0; lvl < L; ++lvl) {
             const float v = g.from(vm, cur);
             ++it;
             if (fabsf(v) <= kRootTol) return g.from(mid, cur);
@@ -192,7 +209,7 @@ __device__ V3 bisect_g(const Grp& g, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_h
                 if (g.sub == 0) atomicAdd(cap_hits, 1u);
                 return g.from(mid, cur);
             }
-            if (lvl + 1 < kBisLevels) {
+            if (lvl + 1 < L) {
                 cur = lo ? 2 * cur + 1 : 2 * cur + 2;
             } else {   // the state after this level: node cur's interval with its outcome applied
                 const V3 na = g.from(a, cur), nb = g.from(b, cur), nm = g.from(mid, cur);
@@ -205,8 +222,8 @@ __device__ V3 bisect_g(const Grp& g, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_h
 
 // f2 = f(best) (cp:904-951) is known: the search evaluated f at the point it returned, and
 // best == x when nothing was found (f(x) = fcv: eval_fg's value is eval_f's)
-template <class Ev>
-__device__ void finalize_g(const Grp& g, const Ev& ev, V3 x, float fcv, bool found, V3 best,
+template <class G, class Ev>
+__device__ void finalize_g(const G& g, const int L, const Ev& ev, V3 x, float fcv, bool found, V3 best,
                            float f2, float* out, const ProjArgs& a, uint32_t& evals) {
     const bool z2 = fabsf(f2) <= kRootTol, z1 = fabsf(fcv) <= kRootTol;
     if (z1) best = x;
@@ -214,7 +231,7 @@ __device__ void finalize_g(const Grp& g, const Ev& ev, V3 x, float fcv, bool fou
     if (found && !(z1 || z2)) {
         V3 x1 = x, x2 = best;
         if (f2 < -kRootTol) { const V3 t = x1; x1 = x2; x2 = t; }
-        r = bisect_g(g, ev, x1, x2, a.cap_hits, evals);
+        r = bisect_g(g, L, ev, x1, x2, a.cap_hits, evals);
     } else if (z1 || z2) {
         r = best;
     } else {
@@ -292,7 +309,7 @@ __device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs&
     float bf = fcv;
     bool found = try_direction(g, ev, x, d0, sc, alphas, nal, max_dist, best, bf, evals);
     if (!found) found = try_direction(g, ev, x, fnv, sc, alphas, nal < 10 ? nal : 10, max_dist, best, bf, evals);
-    if (found) finalize_g(g, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
+    if (found) finalize_g(g, kBisLevels, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
     // unresolved faces are flagged for the late pass (a compacted list cost one same-address atomic
     // per wave: 258 us per pass when every face pends, as with a non-finite average edge length)
     if (g.sub == 0) a.pend[j] = found ? 0u : 1u;
@@ -307,10 +324,12 @@ __device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs&
         project_early_face(ev, a, g, j);
 }
 
-// types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes); the grid
-// covers every face, groups of faces the early pass resolved exit at once
+// types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes), with a
+// group of g.w lanes.  The five searches' (direction, alpha) pairs in serial order (cp:1000-1150) are
+// taken g.w at a time -- a round may cross from one direction to the next -- and the first hit in that
+// order wins, as in the serial loop; the bisection then takes log2(g.w) levels per round.
 template <class Ev>
-__device__ __forceinline__ void project_late_face(const Ev& ev, const ProjArgs& a, const Grp& g, int64_t j) {
+__device__ __forceinline__ void project_late_face(const Ev& ev, const ProjArgs& a, const GrpR& g, int64_t j) {
     const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const float fcv = a.fc[j];
@@ -322,26 +341,76 @@ __device__ __forceinline__ void project_late_face(const Ev& ev, const ProjArgs& 
     V3 z = cross3(fnv, pv);               // cp:250-259, add_inplace is a no-op (F9)
     const float nz = norm2f(z.x, z.y, z.z);
     z = V3{z.x / nz, z.y / nz, z.z / nz};  // normalize_1111
-    V3 z2 = normalise_min(cross3(fnv, z), 0.000001f);   // cp:297-312
+    const V3 z2 = normalise_min(cross3(fnv, z), 0.000001f);   // cp:297-312
     uint32_t evals = 0;
     V3 best = x;
     float bf = fcv;
-    bool found = try_direction(g, ev, x, z, sc, alphas, n10, max_dist, best, bf, evals);
-    if (!found) found = try_direction(g, ev, x, z2, sc, alphas, n10, max_dist, best, bf, evals);
-    for (int ax = 0; ax < 3 && !found; ++ax) {
-        const V3 d{ax == 0 ? 1.f : 0.f, ax == 1 ? 1.f : 0.f, ax == 2 ? 1.f : 0.f};
-        found = try_direction(g, ev, x, d, sc, alphas, n10, max_dist, best, bf, evals);
+    bool found = false;
+    const int n = 5 * n10;
+    for (int c0 = 0; c0 < n;) {
+        const int cend = a.late_flat ? n : (c0 / n10 + 1) * n10;   // this round's last pair + 1
+        const int c = c0 + g.sub;
+        const int di = c / n10, ai = c - di * n10;
+        V3 p = x;
+        float fa = 0.f;
+        bool hit = false;
+        if (c < cend) {
+            const V3 d = di == 0 ? z : di == 1 ? z2 : V3{di == 2 ? 1.f : 0.f, di == 3 ? 1.f : 0.f, di == 4 ? 1.f : 0.f};
+            const float cc = max_dist * alphas[ai];   // try_direction's point
+            p = V3{x.x + cc * d.x, x.y + cc * d.y, x.z + cc * d.z};
+            fa = ev.f(p.x, p.y, p.z);
+            hit = get_sign(fa) * sc <= 0;
+        }
+        const int nxt = cend - c0 < g.w ? cend : c0 + g.w;
+        evals += nxt - c0;
+        c0 = nxt;
+        const uint64_t m = g.bits(hit);
+        if (m) {
+            const int k = __ffsll((unsigned long long)m) - 1;
+            best = g.from(p, k);
+            bf = g.from(fa, k);
+            found = true;
+            break;
+        }
     }
-    finalize_g(g, ev, x, fcv, found, found ? best : x, found ? bf : fcv, a.out + 3 * j, a, evals);
+    finalize_g(g, 31 - __clz(g.w), ev, x, fcv, found, best, bf, a.out + 3 * j, a, evals);
     if (a.evals && g.sub == 0) a.evals[j] += evals;
 }
 
+// The late pass is latency-bound: a few faces in 10^3..10^5 pend, and with 4 lanes each waited on a
+// chain of ~15 search rounds and 2 bisection levels per round.  Each wave takes chunks of 16 faces
+// (the early pass's faces per wave), reads their flags at once and gives each pending face of the
+// chunk 64 / p lanes (p pending, rounded up to a power of two; at least 4): a lone face gets the whole
+// wave (its five searches in one round, 6 bisection levels per round), a chunk where every face pends
+// (as when the average edge length is not finite) 4 lanes per face.  (Chunks of 64 faces, up to 4
+// rounds of 16 faces per wave: a quarter of the waves, 31 -> 55 us on config 2.)
+constexpr int kLateChunk = 64 / kProjGroup;
+
 template <class Ev>
 __device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& a) {
-    const Grp g;
+    const int lane = (int)(threadIdx.x & 63);
     const int64_t j1 = a.rng[1];
-    for (int64_t j = a.rng[0] + grid_lane() / kProjGroup; j < j1; j += grid_lanes() / kProjGroup)
-        if (a.pend[j]) project_late_face(ev, a, g, j);   // uniform per group
+    for (int64_t c0 = a.rng[0] + (grid_lane() >> 6) * kLateChunk; c0 < j1; c0 += (grid_lanes() >> 6) * kLateChunk) {
+        const uint64_t m = (uint64_t)__ballot(lane < kLateChunk && c0 + lane < j1 && a.pend[c0 + lane] != 0u);
+        const int np = __popcll(m);
+        if (!np) continue;
+        int w = np == 1 ? 64 : np == 2 ? 32 : np <= 4 ? 16 : np <= 8 ? 8 : 4;
+        w = w < a.late_wmax ? w : a.late_wmax;
+        // lane r learns the chunk position of the r-th pending face (a scalar walk over the set bits)
+        int pos = 0;
+        uint64_t mm = m;
+        for (int r = 0; r < np; ++r) {
+            const int b = __ffsll((unsigned long long)mm) - 1;
+            mm &= mm - 1;
+            pos = lane == r ? b : pos;
+        }
+        const GrpR g(w);
+        for (int r0 = 0; r0 < np; r0 += 64 / w) {   // one round unless the width is capped
+            const int r = r0 + lane / w;
+            const int at = __shfl(pos, r < np ? r : 0, 64);
+            if (r < np) project_late_face(ev, a, g, c0 + at);   // uniform per group
+        }
+    }
 }
 
 // normalize_1111(grad) at arbitrary points (the QEM normals at the projected centroids, qem.hpp:256-316)

@@ -5,6 +5,7 @@
 #   bench       the default bench line (N = 1)
 #   benchob     the bench's OB02 legs only (no config 5, no concurrent builds, no CPU baselines)
 #   ob02prof    kernel stats of tools/ob02_probe.py (config 2 / 3 / 3s builds)
+#   projstats   the projection's evaluations per face, wave balance and late-pass faces
 #   fold        the edge-length fold alone on real meshes' edge lengths (stats + kernel trace)
 # Each GPU step has its own time limit; the first failure ends the script.
 set -euo pipefail
@@ -34,6 +35,8 @@ for what in "$@"; do
       IMPLISOLID_FOLD_STATS=1 timeout -k 10 200 python3 tools/fold_mesh_probe.py 3 > "$out/fold_stats.log" 2>&1
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/fold" -o run -- \
           python3 tools/fold_mesh_probe.py 5 > "$out/fold_probe.log" 2>&1 ;;
+    projstats)   # the projection's search balance per pass (tools/proj_stats_probe.py)
+      IMPLISOLID_PROJ_STATS=1 timeout -k 10 200 python3 -u tools/proj_stats_probe.py > "$out/proj_stats.log" 2>&1 ;;
     shardtrace)   # the 8-shard OB02 loop at 256^3 under a kernel trace (tools/ob02_shard_probe.py)
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$root/$out/shard" -o run -- \
           python3 tools/ob02_shard_probe.py 8 256 > "$out/shard_probe.json" 2> "$out/shard_probe.err" ;;
