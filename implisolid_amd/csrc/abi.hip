@@ -1259,8 +1259,7 @@ int implisolid_ob02_load(implisolid_ob02* h, const float* d_verts, int64_t nv, c
     OB02_TRY({
         if (nv < 0 || nf < 0 || (nv && !d_verts) || (nf && !d_faces)) throw InputError("implisolid_ob02_load: bad mesh");
         IMPLI_HIP(hipDeviceSynchronize());   // the caller's copies of the mesh are complete
-        h->ob->load_mesh(d_verts, nv, d_faces, nf);
-        h->ob->set_owned_vertices(v0, v1);
+        h->ob->load_shard(d_verts, nv, d_faces, nf, nullptr, v0, v1);
         IMPLI_HIP(hipStreamSynchronize(h->stream));
     })
 }
@@ -1273,8 +1272,7 @@ int implisolid_ob02_attach(implisolid_ob02* h, float* d_verts, int64_t nv, const
         if (!h->ev) IMPLI_HIP(hipEventCreateWithFlags(&h->ev, hipEventDisableTiming));
         IMPLI_HIP(hipEventRecord(h->ev, (hipStream_t)after_stream));
         IMPLI_HIP(hipStreamWaitEvent(h->stream, h->ev, 0));
-        h->ob->load_mesh(d_verts, nv, d_faces, nf, d_verts);
-        h->ob->set_owned_vertices(v0, v1);
+        h->ob->load_shard(d_verts, nv, d_faces, nf, d_verts, v0, v1);
     })
 }
 

@@ -189,6 +189,9 @@ __global__ void k_ranges_set(int64_t* __restrict__ rng, int64_t v0, int64_t v1, 
     if (i == kRngOwn) rng[i] = v0;
     if (i == kRngOwn + 1) rng[i] = v1;
     if (i >= kRngScratch && i < kRngScratch + 6) rng[i] = (i & 1) ? (int64_t)-1 : INT64_MAX;   // (min, max): empty
+    // the umbrella vertices start as the owned ones (an owned vertex in no face has an empty umbrella)
+    if (i == kRngScratch + 6) rng[i] = v1 > v0 ? v0 : INT64_MAX;
+    if (i == kRngScratch + 7) rng[i] = v1 > v0 ? v1 - 1 : (int64_t)-1;
 }
 
 __global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const uint32_t* __restrict__ off,
@@ -204,9 +207,7 @@ __global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const
 // (an umbrella of up to kSortRegs faces is sorted in registers: one load and one store per entry,
 // where the in-memory insertion sort was a chain of dependent global loads)
 constexpr int kSortRegs = 12;
-__global__ void k_sort_umbrella(const uint32_t* __restrict__ off, int32_t* __restrict__ lst, int64_t nv) {
-    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (v >= nv) return;
+__device__ __forceinline__ void sort_umbrella_at(const uint32_t* __restrict__ off, int32_t* __restrict__ lst, int64_t v) {
     const uint32_t a = off[v], e = off[v + 1];
     if (e - a <= (uint32_t)kSortRegs) {
         const int n = (int)(e - a);
@@ -234,6 +235,10 @@ __global__ void k_sort_umbrella(const uint32_t* __restrict__ off, int32_t* __res
         while (j > a && lst[j - 1] > x) { lst[j] = lst[j - 1]; --j; }
         lst[j] = x;
     }
+}
+__global__ void k_sort_umbrella(const uint32_t* __restrict__ off, int32_t* __restrict__ lst, int64_t nv) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v < nv) sort_umbrella_at(off, lst, v);
 }
 
 
@@ -287,11 +292,8 @@ __global__ void k_fof(int64_t nf, EdgeTab t, int32_t* __restrict__ fof) {
 // fof is the same for every mesh, degenerate faces included.  One thread per half-edge walks a's
 // umbrella (~6 faces): 2 dependent L2 loads per face instead of a hash insert with two atomics per
 // half-edge and the table's clear (76 us -> see DESIGN "OB02 on the GPU").
-__global__ __launch_bounds__(256) void k_fof_umbrella(const int32_t* __restrict__ f, int64_t nf,
-                                                      const uint32_t* __restrict__ off, const int32_t* __restrict__ lst,
-                                                      int32_t* __restrict__ fof) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= 3 * nf) return;
+__device__ __forceinline__ int32_t fof_at(const int32_t* __restrict__ f, const uint32_t* __restrict__ off,
+                                          const int32_t* __restrict__ lst, int64_t i) {
     const int64_t fi = i / 3;
     const int k = (int)(i - 3 * fi);
     const int32_t a = f[i], b = f[3 * fi + (k == 2 ? 0 : k + 1)];
@@ -312,7 +314,13 @@ __global__ __launch_bounds__(256) void k_fof_umbrella(const int32_t* __restrict_
             last = max(last, (uint32_t)g);
         }
     }
-    fof[i] = (int32_t)((first != (uint32_t)fi) ? first : (c >= 2 ? last : 0u));
+    return (int32_t)((first != (uint32_t)fi) ? first : (c >= 2 ? last : 0u));
+}
+__global__ __launch_bounds__(256) void k_fof_umbrella(const int32_t* __restrict__ f, int64_t nf,
+                                                      const uint32_t* __restrict__ off, const int32_t* __restrict__ lst,
+                                                      int32_t* __restrict__ fof) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < 3 * nf) fof[i] = fof_at(f, off, lst, i);
 }
 
 // ---- step 3: my_subdiv_ (centroids_projection.cpp:1314-1367) -----------------------------------
@@ -549,19 +557,37 @@ __global__ void k_resample(const uint32_t* __restrict__ off, const int32_t* __re
 //                        neighbours
 //   k_face_vertex_range  the vertices of those faces (the next resampling's one-ring halo)
 //   k_ranges_final       the min / max pairs to half-open ranges (an empty work range: none)
-__device__ __forceinline__ void wave_minmax_atomic(long long lo, long long hi, long long* out) {
+// one atomic pair per workgroup (256 lanes): same-address atomics serialise at ~11 ns each, and one
+// pair per wave cost 10-30 us per range pass at 256^3
+__device__ __forceinline__ void block_minmax_atomic(long long lo, long long hi, long long* out) {
+    __shared__ long long s_lo[4], s_hi[4];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         const long long a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
         lo = a < lo ? a : lo;
         hi = b > hi ? b : hi;
     }
+    const int w = (int)(threadIdx.x >> 6);
     if ((threadIdx.x & 63) == 0) {
+        s_lo[w] = lo;
+        s_hi[w] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            lo = s_lo[k] < lo ? s_lo[k] : lo;
+            hi = s_hi[k] > hi ? s_hi[k] : hi;
+        }
         if (lo <= hi) {
             atomicMin(&out[0], lo);
             atomicMax(&out[1], hi);
         }
     }
+}
+// grid-stride range passes: a bounded grid (each block ends in one atomic pair)
+inline unsigned range_blocks(int64_t n, unsigned cap = 256) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap));
 }
 constexpr long long kNoMin = 0x7fffffffffffffffll;
 
@@ -576,7 +602,7 @@ __global__ __launch_bounds__(256) void k_work_range(const uint32_t* __restrict__
             hi = max(hi, (long long)lst[e - 1]);
         }
     }
-    wave_minmax_atomic(lo, hi, (long long*)rng + kRngScratch);
+    block_minmax_atomic(lo, hi, (long long*)rng + kRngScratch);
 }
 
 __global__ __launch_bounds__(256) void k_fof_range(const int32_t* __restrict__ fof, int64_t* __restrict__ rng) {
@@ -595,7 +621,7 @@ __global__ __launch_bounds__(256) void k_fof_range(const int32_t* __restrict__ f
             }
         }
     }
-    wave_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 2);
+    block_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 2);
 }
 
 __global__ __launch_bounds__(256) void k_face_vertex_range(const int32_t* __restrict__ f, int64_t* __restrict__ rng) {
@@ -612,7 +638,7 @@ __global__ __launch_bounds__(256) void k_face_vertex_range(const int32_t* __rest
             }
         }
     }
-    wave_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 4);
+    block_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 4);
 }
 
 __global__ void k_ranges_final(int64_t* __restrict__ rng) {
@@ -631,6 +657,161 @@ __global__ void k_ranges_final(int64_t* __restrict__ rng) {
     rng[kRngCen + 1] = m[3] + 1;
     rng[kRngHalo] = m[4] < v0 ? m[4] : v0;
     rng[kRngHalo + 1] = m[5] + 1 > v1 ? m[5] + 1 : v1;
+}
+
+// ---- a shard's load and topology (Ob02::load_shard) -------------------------------------------
+// The umbrellas a shard reads are those of its owned vertices (resampling, QEM) and of the vertices
+// of the faces in its work range (their faces of faces): the vertices [u0, u1] (scratch pair 3,
+// inclusive).  Degrees, offsets, fills and sorts cover only those, faces of faces only the work
+// range; the per-vertex / per-face kernels grid-stride over the device ranges.  (The work range is a
+// span: a face inside it need not touch an owned vertex, so its vertices are found from the span.)
+
+// k_load_mesh's copies and zeroing, plus the work range (the first and last face touching an owned
+// vertex), one atomic pair per wave
+__global__ __launch_bounds__(256) void k_load_shard(float* __restrict__ v, const float* __restrict__ sv, int64_t nv3,
+                                                    int32_t* __restrict__ f, const int32_t* __restrict__ sf, int64_t nf,
+                                                    uint32_t* __restrict__ deg, int64_t ndeg, uint32_t* __restrict__ misc,
+                                                    int64_t* __restrict__ rng) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nv3) v[i] = sv[i];
+    if (i < 3 * nf) f[i] = sf[i];
+    if (i < ndeg) deg[i] = 0u;
+    if (i < 16) misc[i] = 0u;
+    const int64_t v0 = rng[kRngOwn], v1 = rng[kRngOwn + 1];
+    long long lo = kNoMin, hi = -1;
+    if (i < nf) {
+        const int32_t a = sf[3 * i], b = sf[3 * i + 1], c = sf[3 * i + 2];
+        if ((a >= v0 && a < v1) || (b >= v0 && b < v1) || (c >= v0 && c < v1)) lo = hi = i;
+    }
+    block_minmax_atomic(lo, hi, (long long*)rng + kRngScratch);
+}
+
+// the vertices of the work range's faces, joined to the owned ones (k_ranges_set's start)
+__global__ __launch_bounds__(256) void k_work_vertices(const int32_t* __restrict__ f, int64_t* __restrict__ rng) {
+    const long long j0 = rng[kRngScratch], j1 = rng[kRngScratch + 1];   // inclusive (j0 > j1: empty)
+    if (j0 > j1) return;   // uniform
+    long long lo = kNoMin, hi = -1;
+    for (long long j = j0 + grid_lane(); j <= j1; j += grid_lanes()) {
+        const int32_t a = f[3 * j], b = f[3 * j + 1], c = f[3 * j + 2];
+        lo = min(lo, (long long)min(min(a, b), c));
+        hi = max(hi, (long long)max(max(a, b), c));
+    }
+    block_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 6);
+}
+
+__global__ __launch_bounds__(256) void k_degree_range(const int32_t* __restrict__ f, int64_t n3, uint32_t* __restrict__ deg,
+                                                      const int64_t* __restrict__ rng) {
+    const int64_t u0 = rng[kRngScratch + 6], u1 = rng[kRngScratch + 7];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n3) {
+        const int32_t x = f[i];
+        if (x >= u0 && x <= u1) atomicAdd(&deg[x], 1u);
+    }
+}
+
+// exclusive scan of in[u0..u1] into out[u0..u1 + 1] (out[u1 + 1] = total), in[] left zeroed (the
+// fill's counters): one workgroup, tiles of 8192 values staged through LDS (coalesced loads, then
+// 8 consecutive values per lane; one word of padding per 32 keeps the lanes' strided reads on
+// distinct banks)
+constexpr int kRangeScanThreads = 1024, kRangeScanPer = 8, kRangeScanTile = kRangeScanThreads * kRangeScanPer;
+__device__ __forceinline__ int scan_pad(int i) { return i + (i >> 5); }
+__global__ __launch_bounds__(kRangeScanThreads) void k_scan_range(uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                                 const int64_t* __restrict__ rng) {
+    __shared__ uint32_t s_v[kRangeScanTile + kRangeScanTile / 32];
+    __shared__ uint32_t s_w[kRangeScanThreads / 64];
+    const int64_t u0 = rng[kRngScratch + 6], u1 = rng[kRngScratch + 7];
+    if (u0 > u1) return;   // uniform
+    const int64_t n = u1 - u0 + 1;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    uint32_t carry = 0;
+    for (int64_t base = 0; base < n; base += kRangeScanTile) {
+        const int64_t m = n - base < kRangeScanTile ? n - base : kRangeScanTile;
+#pragma unroll
+        for (int k = 0; k < kRangeScanPer; ++k) {
+            const int i = k * kRangeScanThreads + t;
+            uint32_t x = 0u;
+            if (i < m) {
+                x = in[u0 + base + i];
+                in[u0 + base + i] = 0u;
+            }
+            s_v[scan_pad(i)] = x;
+        }
+        __syncthreads();
+        uint32_t x[kRangeScanPer], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kRangeScanPer; ++k) {
+            x[k] = s_v[scan_pad(t * kRangeScanPer + k)];
+            sum += x[k];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_w[wid] = incl;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kRangeScanThreads / 64; ++w) {
+            pre += w < wid ? s_w[w] : 0u;
+            tot += s_w[w];
+        }
+        uint32_t run = carry + pre + incl - sum;
+#pragma unroll
+        for (int k = 0; k < kRangeScanPer; ++k) {
+            s_v[scan_pad(t * kRangeScanPer + k)] = run;
+            run += x[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kRangeScanPer; ++k) {
+            const int i = k * kRangeScanThreads + t;
+            if (i < m) out[u0 + base + i] = s_v[scan_pad(i)];
+        }
+        carry += tot;
+        __syncthreads();   // s_v and s_w are rewritten by the next tile
+    }
+    if (t == 0) out[u1 + 1] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_fill_range(const int32_t* __restrict__ f, int64_t n3, const uint32_t* __restrict__ off,
+                                                    uint32_t* __restrict__ fill, int32_t* __restrict__ lst,
+                                                    const int64_t* __restrict__ rng) {
+    const int64_t u0 = rng[kRngScratch + 6], u1 = rng[kRngScratch + 7];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n3) {
+        const int32_t x = f[i];
+        if (x >= u0 && x <= u1) lst[off[x] + atomicAdd(&fill[x], 1u)] = (int32_t)(i / 3);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sort_range(const uint32_t* __restrict__ off, int32_t* __restrict__ lst,
+                                                    const int64_t* __restrict__ rng) {
+    const int64_t u0 = rng[kRngScratch + 6], u1 = rng[kRngScratch + 7];
+    if (u0 > u1) return;   // uniform (an empty range's start is INT64_MAX)
+    for (int64_t v = u0 + grid_lane(); v <= u1; v += grid_lanes()) sort_umbrella_at(off, lst, v);
+}
+
+// faces of faces of the work faces, and (as k_fof_range) the span of those faces and their neighbours
+__global__ __launch_bounds__(256) void k_fof_work(const int32_t* __restrict__ f, const uint32_t* __restrict__ off,
+                                                  const int32_t* __restrict__ lst, int32_t* __restrict__ fof,
+                                                  int64_t* __restrict__ rng) {
+    const long long j0 = rng[kRngScratch], j1 = rng[kRngScratch + 1];   // inclusive (j0 > j1: empty)
+    if (j0 > j1) return;   // uniform
+    long long lo = kNoMin, hi = -1;
+    for (long long i = 3 * j0 + grid_lane(); i < 3 * j1 + 3; i += grid_lanes()) {
+        const int32_t g = fof_at(f, off, lst, i);
+        fof[i] = g;
+        const long long j = i / 3;
+        lo = min(lo, j);
+        hi = max(hi, j);
+        if (g >= 0) {
+            lo = min(lo, (long long)g);
+            hi = max(hi, (long long)g);
+        }
+    }
+    block_minmax_atomic(lo, hi, (long long*)rng + kRngScratch + 2);
 }
 
 // ---- step 2 ----------------------------------------------------------------------------------
@@ -1613,7 +1794,7 @@ Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
     misc_.reserve(512);
 }
 
-void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_, float* d_work) {
+void Ob02::begin_load(const float*& d_verts, int64_t nv_, int64_t nf_, float* d_work) {
     nv = nv_;
     nf = nf_;
     if (d_work) {   // the caller's vertex array is the working one (sharded loop): no copy
@@ -1633,11 +1814,15 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     avg_edge_ = 0.f;
     avg_valid_ = true;
     for (double& t : stage_ms_) t = 0.0;
-    Stage st(this, kStageTopology);
     if (!verts_.ext) verts_.reserve((size_t)(nv + 1) * 12);
     faces_.reserve((size_t)(nf + 1) * 12);
     deg_.reserve((size_t)(nv + 1) * 4);
     rng_.reserve(kRngFields * sizeof(int64_t));
+}
+
+void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_, float* d_work) {
+    begin_load(d_verts, nv_, nf_, d_work);
+    Stage st(this, kStageTopology);
     // the mesh copied, the degree counters and misc ((unused), cap hits, evaluations) zeroed, the
     // range block set to the whole mesh
     const int64_t nmax = std::max<int64_t>(std::max<int64_t>(3 * nv, 3 * nf), nv + 1);
@@ -1648,6 +1833,55 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     start_perturbations();   // host thread, overlaps the topology and resampling kernels
     build_topology(true);
     whole_ranges();
+}
+
+void Ob02::load_shard(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_, float* d_work, int64_t v0,
+                      int64_t v1) {
+    if (v0 < 0 || v1 < v0 || v1 > nv_) throw InputError("ob02: owned vertex range outside the mesh");
+    if (v0 == 0 && v1 == nv_) {
+        load_mesh(d_verts, nv_, d_faces, nf_, d_work);
+        set_owned_vertices(0, nv_);
+        return;
+    }
+    begin_load(d_verts, nv_, nf_, d_work);
+    Stage st(this, kStageTopology);
+    reserve_topology();
+    int64_t* r = rng_.as<int64_t>();
+    k_ranges_set<<<1, 64, 0, s>>>(r, v0, v1, nv, nf, 1);
+    const int64_t nmax = std::max<int64_t>(std::max<int64_t>(3 * nv, 3 * nf), nv + 1);
+    k_load_shard<<<blocks_for(std::max<int64_t>(nmax, 16)), 256, 0, s>>>(verts_.as<float>(), d_verts,
+                                                                        verts_.as<float>() == d_verts ? 0 : 3 * nv,
+                                                                        faces_.as<int32_t>(), d_faces, nf, deg_.as<uint32_t>(),
+                                                                        nv + 1, misc_.as<uint32_t>(), r);
+    start_perturbations();   // host thread, overlaps the kernels below
+    own_v0_ = v0;
+    own_v1_ = v1;
+    sharded_ = true;
+    hrng_valid_ = false;
+    const int64_t nown = v1 - v0;
+    est_work_ = std::min<int64_t>(nf, 2 * nown + nown / 4 + 4096);
+    est_cen_ = std::min<int64_t>(nf, est_work_ + 4096);
+    const int64_t est_umb = std::min<int64_t>(nv, nown + nown / 4 + 4096);
+    uint32_t* deg = deg_.as<uint32_t>();
+    uint32_t* off = uoff_.as<uint32_t>();
+    int32_t* lst = ulst_.as<int32_t>();
+    if (nf) {
+        k_work_vertices<<<range_blocks(est_work_), 256, 0, s>>>(faces_.as<int32_t>(), r);
+        k_degree_range<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg, r);
+        k_scan_range<<<1, kRangeScanThreads, 0, s>>>(deg, off, r);
+        k_fill_range<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, off, deg, lst, r);
+        k_sort_range<<<blocks_for(est_umb), 256, 0, s>>>(off, lst, r);
+        k_fof_work<<<range_blocks(3 * est_work_, 512), 256, 0, s>>>(faces_.as<int32_t>(), off, lst, fof_.as<int32_t>(), r);
+        k_face_vertex_range<<<range_blocks(est_cen_), 256, 0, s>>>(faces_.as<int32_t>(), r);
+    } else {
+        // no faces: every umbrella empty
+        k_scan_range<<<1, kRangeScanThreads, 0, s>>>(deg, off, r);
+    }
+    k_ranges_final<<<1, 64, 0, s>>>(r);
+    IMPLI_HIP(hipGetLastError());
+    etab_valid_ = false;
+    topo_valid_ = true;
+    topo_partial_ = true;
 }
 
 void Ob02::whole_ranges() {   // host side of the range block's whole-mesh state
@@ -1667,7 +1901,7 @@ void Ob02::whole_ranges() {   // host side of the range block's whole-mesh state
 // and grid-stride over whatever the range turns out to be.
 void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
     if (v0 < 0 || v1 < v0 || v1 > nv) throw InputError("ob02: owned vertex range outside the mesh");
-    if (!topo_valid_) build_topology();
+    if (!topo_valid_ || topo_partial_) build_topology();
     rng_.reserve(kRngFields * sizeof(int64_t));
     const bool sharded = !(v0 == 0 && v1 == nv);
     k_ranges_set<<<1, 64, 0, s>>>(rng_.as<int64_t>(), v0, v1, nv, nf, sharded ? 1 : 0);
@@ -1684,9 +1918,9 @@ void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
     est_work_ = std::min<int64_t>(nf, 2 * nown + nown / 4 + 4096);
     est_cen_ = std::min<int64_t>(nf, est_work_ + 4096);
     int64_t* r = rng_.as<int64_t>();
-    if (nown) k_work_range<<<blocks_for(nown), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), r);
-    if (est_work_) k_fof_range<<<blocks_for(est_work_), 256, 0, s>>>(fof_.as<int32_t>(), r);
-    if (est_cen_) k_face_vertex_range<<<blocks_for(est_cen_), 256, 0, s>>>(faces_.as<int32_t>(), r);
+    if (nown) k_work_range<<<range_blocks(nown), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), r);
+    if (est_work_) k_fof_range<<<range_blocks(est_work_), 256, 0, s>>>(fof_.as<int32_t>(), r);
+    if (est_cen_) k_face_vertex_range<<<range_blocks(est_cen_), 256, 0, s>>>(faces_.as<int32_t>(), r);
     k_ranges_final<<<1, 64, 0, s>>>(r);
     IMPLI_HIP(hipGetLastError());
 }
@@ -1752,11 +1986,19 @@ EdgeTab Ob02::edge_table() {
     return t;
 }
 
-void Ob02::build_topology(bool deg_zeroed) {
-    // umbrellas
+void Ob02::reserve_topology() {
     deg_.reserve((size_t)(nv + 1) * 4);
     uoff_.reserve((size_t)(nv + 2) * 4);
     ulst_.reserve((size_t)(3 * nf + 1) * 4);
+    fof_.reserve((size_t)(3 * nf + 1) * 4);
+    cen_.reserve((size_t)(nf + 1) * 12);
+    nrm_.reserve((size_t)(nf + 1) * 12);
+    w_.reserve((size_t)(nf + 1) * 4);
+}
+
+void Ob02::build_topology(bool deg_zeroed) {
+    // umbrellas
+    reserve_topology();
     if (!deg_zeroed) IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
     if (nf) k_degree<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
     scan(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv, true);   // deg_ left zeroed: the fill counters
@@ -1764,16 +2006,13 @@ void Ob02::build_topology(bool deg_zeroed) {
                                                              deg_.as<uint32_t>(), ulst_.as<int32_t>());
     if (nv) k_sort_umbrella<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), nv);
     // faces of faces, from the umbrellas (the edge table is built only for subdivision)
-    fof_.reserve((size_t)(3 * nf + 1) * 4);
     if (nf)
         k_fof_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
                                                           fof_.as<int32_t>());
     etab_valid_ = false;
-    cen_.reserve((size_t)(nf + 1) * 12);
-    nrm_.reserve((size_t)(nf + 1) * 12);
-    w_.reserve((size_t)(nf + 1) * 4);
     IMPLI_HIP(hipGetLastError());
     topo_valid_ = true;
+    topo_partial_ = false;
 }
 
 void Ob02::scan(uint32_t* in, uint32_t* out, int64_t n, bool zero_in) {

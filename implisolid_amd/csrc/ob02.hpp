@@ -15,9 +15,10 @@ struct EdgeTab;   // ob02.hip: open-addressed (vmin, vmax) table of the current 
 struct PertDev;   // ob02.hip: a face count's perturbation table on one device (process-wide cache)
 
 // Ob02's range block (int64 fields of rng_): [kRngWork, +2) work faces, [kRngCen, +2) centroid
-// faces, [kRngHalo, +2) halo vertices, [kRngOwn, +2) owned vertices (half-open), then three
-// (min, max) scratch pairs of the range passes
-constexpr int kRngWork = 0, kRngCen = 2, kRngHalo = 4, kRngOwn = 6, kRngScratch = 8, kRngFields = 14;
+// faces, [kRngHalo, +2) halo vertices, [kRngOwn, +2) owned vertices (half-open), then four
+// (min, max) scratch pairs of the range passes (work faces, centroid faces, halo vertices, and the
+// vertices whose umbrellas a shard's topology holds)
+constexpr int kRngWork = 0, kRngCen = 2, kRngHalo = 4, kRngOwn = 6, kRngScratch = 8, kRngFields = 16;
 
 class Ob02 {
 public:
@@ -40,6 +41,13 @@ public:
     // that moves vertices the caller exchanges the owned ranges (set_verts) before the next step.
     // Call after load_mesh; v0 = 0, v1 = nv restores the whole mesh.
     void set_owned_vertices(int64_t v0, int64_t v1);
+    // load_mesh + set_owned_vertices for a shard in one pass: the ranges are found while the mesh is
+    // copied, and the topology (umbrellas, faces of faces) is built only where the shard's passes
+    // read it -- the umbrellas of the owned vertices and of the work faces' vertices, the faces of
+    // faces of the work faces -- instead of over the whole mesh on every rank.  v0 = 0, v1 = nv is
+    // load_mesh + set_owned_vertices(0, nv).
+    void load_shard(const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, float* d_work, int64_t v0,
+                    int64_t v1);
     // [v0, v1, work faces f0, f1, centroid faces f0, f1, halo vertices h0, h1]: [h0, h1) are the
     // vertices the next resampling reads (those of the centroid faces), so after a step only they
     // must be current before another resampling (the edge-length fold reads every vertex).  The
@@ -86,6 +94,8 @@ public:
 private:
     void store_pointset(const char* key, const float* d, int64_t n, bool keep_first);
     void build_topology(bool deg_zeroed = false);   // deg_zeroed: deg_[0..nv] already 0 (load_mesh)
+    void begin_load(const float*& d_verts, int64_t nv, int64_t nf, float* d_work);   // host state of a load
+    void reserve_topology();
     void scan(uint32_t* in, uint32_t* out, int64_t n, bool zero_in = false);   // exclusive, out[n] = total; zero_in: in[] left 0
     EdgeTab edge_table();
     void rand_tables(int64_t lanes);
@@ -110,6 +120,7 @@ private:
     DevBuf verts_, faces_, vnew_, cen_, nrm_, w_, fof_, uoff_, ulst_, etab_, deg_, proj_, grad_, fn_, norms_,
         pend_, misc_, fnew_, rtab_, scan_tmp_;
     bool topo_valid_ = false;
+    bool topo_partial_ = false;   // the topology covers only a shard's ranges (load_shard)
     bool etab_valid_ = false;   // the edge table (subdivision only) matches the current faces
     int64_t own_v0_ = 0, own_v1_ = 0;   // owned vertices
     // the range block in device memory (int64, kRng* below): work faces (touching an owned vertex),

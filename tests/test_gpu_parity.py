@@ -1423,6 +1423,32 @@ def test_rccl_world1_pipeline(impli, oracle, tmp_path, mode):
     assert np.array_equal(g["verts"].view(np.uint32), vr.view(np.uint32))
 
 
+def test_ob02_shard_owning_nothing(impli):
+    """A shard whose owned range is empty (load_shard with v0 == v1): no work faces, no centroid
+    faces, its halo the empty owned range, and its steps leave every vertex as loaded."""
+    import torch
+    from implisolid_amd import scenes
+    shape, mc = scenes.config2(48)
+    v_mc, f_mc = impli.make_geometry(shape, scenes.mc_settings(48, 1.0))
+    nv, nf = len(v_mc), len(f_mc)
+    V = torch.from_numpy(v_mc.reshape(-1).copy()).cuda()
+    F = torch.from_numpy(f_mc.reshape(-1).copy()).cuda()
+    for at in (0, nv // 2, nv):
+        ob = impli.Ob02Shard(shape, mc)
+        try:
+            ob.load(V.data_ptr(), nv, F.data_ptr(), nf, at, at)
+            assert ob.ranges() == (at, at, 0, 0, 0, 0)
+            assert ob.halo() == (at, at)
+            ob.resample()
+            ob.project()
+            out = torch.empty_like(V)
+            ob.get_verts(out.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), v_mc.reshape(-1).view(np.uint32))
+        finally:
+            ob.close()
+
+
 def test_ob02_shards_in_one_process(impli, oracle):
     """The sharded OB02 loop without processes: config 2 at R = 48 as 3 and 5 vertex-range shards on
     one GPU, stepped together with the owned ranges exchanged on the host after every vertex-moving
