@@ -975,6 +975,13 @@ std::string TreeJit::point_source(const Program& p) {
     PtEmitter eg{nodes, p, true};
     const std::string fg = eg.emit(root, "x0", "y0", "z0", 4);
     std::ostringstream s;
+    // IMPLISOLID_PT_WAVES=n (experiments): an occupancy request of n waves per SIMD on the search
+    // passes (none by default)
+    static const int pt_waves = [] {
+        const char* e = std::getenv("IMPLISOLID_PT_WAVES");
+        return e ? std::atoi(e) : 0;
+    }();
+    const std::string occ = pt_waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(pt_waves) + ")))" : "";
     s << kPrelude << "#include \"ob02_device.hpp\"\n"
       << "namespace impli {\nusing namespace dev;\n"
       << "__device__ __forceinline__ float tree_pf(const float* __restrict__ M, const float* __restrict__ tab,\n"
@@ -993,9 +1000,9 @@ std::string TreeJit::point_source(const Program& p) {
       << "    impli::ob::centroid_normals_body(JitPt{M, tab}, v, f, rng, C, N);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_prep(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_prep_body(JitPt{M, tab}, a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_early(const float* M, const float* tab, ProjArgs a) {\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_early_body(JitPt{M, tab}, a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_normals_at(const float* M, const float* tab,\n"
       << "    const float* P, const int64_t* rng, float* G) {\n"
