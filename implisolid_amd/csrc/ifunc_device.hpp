@@ -113,19 +113,27 @@ __device__ __forceinline__ float cube_f(const float* __restrict__ tab, float X, 
     return -res;
 }
 // cube.hpp:273-315 -- the old six-plane gradient (does not match the rabbit field, F3)
+// The chosen face's normal is carried through the unrolled loop (constant indices only): indexing
+// the table with the winning face made it a private array, which the compiler kept in registers in
+// some processes and in LDS or scratch in others for the same source (18 KB of LDS per workgroup:
+// the f + gradient passes 3-5x slower).
 __device__ __forceinline__ V3 cube_g(float i1, float i2, float i3) {
     const float P[18] = {0.5f, 0, 0, -0.5f, 0, 0, 0, 0.5f, 0, 0, -0.5f, 0, 0, 0, 0.5f, 0, 0, -0.5f};
-    int index = 0;
-    float mn = 0.f;
+    float mn = 0.f, gx = -P[0], gy = -P[1], gz = -P[2];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         const double v = (double)((i1 - 0.f - P[3 * k]) * P[3 * k]) * (-2.) +
                          (double)((i2 - 0.f - P[3 * k + 1]) * P[3 * k + 1]) * (-2.) +
                          (double)((i3 - 0.f - P[3 * k + 2]) * P[3 * k + 2]) * (-2.);
         if (k == 0) mn = (float)v;
-        if (v < (double)mn) { index = k; mn = (float)v; }
+        if (v < (double)mn) {
+            mn = (float)v;
+            gx = -P[3 * k];
+            gy = -P[3 * k + 1];
+            gz = -P[3 * k + 2];
+        }
     }
-    return V3{-P[index * 3], -P[index * 3 + 1], -P[index * 3 + 2]};
+    return V3{gx, gy, gz};
 }
 
 // ---- scylinder, scylinder.hpp:97-166 (radius .5, length 1, centre (0,0,-.5), axis z) ---------
@@ -239,13 +247,15 @@ __device__ __forceinline__ V3 dm_g(float x, float y, float z) {
 // host libm by the oracle's restatement (or_libm.c; sinf and atanf over all 2^32 patterns).
 __device__ __forceinline__ uint32_t abstop12(float f) { return (__float_as_uint(f) >> 20) & 0x7ffu; }
 
-__device__ __forceinline__ uint32_t inv_pio4(int i) {   // __inv_pio4: 32-bit windows of 2/pi
-    const uint32_t T[24] = {0xa2, 0xa2f9, 0xa2f983, 0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
-                            0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd,
-                            0xf534ddc0, 0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43,
-                            0x993c4390, 0x3c439041};
-    return T[i];
-}
+// __inv_pio4: 32-bit windows of 2/pi, in constant memory (a function-local table indexed at run
+// time is a private array whose placement -- registers, LDS, scratch -- the compiler chose
+// differently from process to process)
+static __constant__ uint32_t kInvPio4[24] = {
+    0xa2, 0xa2f9, 0xa2f983, 0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+    0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd,
+    0xf534ddc0, 0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43,
+    0x993c4390, 0x3c439041};
+__device__ __forceinline__ uint32_t inv_pio4(int i) { return kInvPio4[i]; }
 
 // sinf_poly; __sincosf_table[1] (n & 2) is table 0 with the cosine coefficients negated.  The sine
 // (n even) and cosine (n odd) polynomials as one chain of the same operations on selected operands:

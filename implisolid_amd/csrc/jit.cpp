@@ -483,7 +483,7 @@ std::string source_hash(const std::string& src, int device) {
     for (int k = 0; k < kJitNumHeaders; ++k) h = fnv1a(kJitHeaderSources[k], std::strlen(kJitHeaderSources[k]), h);
     int major = 0, minor = 0;
     (void)hiprtcVersion(&major, &minor);
-    const std::string tag = "--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 v4 hiprtc " + std::to_string(major) +
+    const std::string tag = "--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 v5 (points: -disable-promote-alloca-to-lds) hiprtc " + std::to_string(major) +
                             "." + std::to_string(minor) + " " + device_arch(device);
     h = fnv1a(tag.data(), tag.size(), h);
     char buf[32];
@@ -1018,9 +1018,14 @@ std::vector<char> TreeJit::compile(const std::string& src) {
     rtc_check(hiprtcCreateProgram(&prog, src.c_str(), "impli_tree.hip", kJitNumHeaders, kJitHeaderSources,
                                   kJitHeaderNames),
               "hiprtcCreateProgram");
-    // the static library's floating-point contract: no FMA contraction, IEEE division/sqrt
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+    // the static library's floating-point contract: no FMA contraction, IEEE division/sqrt.  Point
+    // modules: no promotion of private arrays to LDS -- whether the compiler promoted them varied
+    // from process to process for the same source (18 KB per workgroup on the rabbit's trees, their
+    // f + gradient passes 3-5x slower: profiles/r05zf_*), so it is ruled out explicitly.
+    const bool points = src.find("impli_pt_project_early") != std::string::npos;
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17", "-mllvm",
+                          "-disable-promote-alloca-to-lds"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, points ? 6 : 4, opts);
     // hipRTC loads its compiler libraries at the first compile, and their static destructors run at
     // exit before the handlers registered earlier: shutdown() (which joins a worker still compiling)
     // is registered once more now, so it runs before those destructors (a process that exited with
