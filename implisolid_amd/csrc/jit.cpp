@@ -965,6 +965,25 @@ std::string TreeJit::kernel_source(const Program& p, bool bake) {
     return s.str();
 }
 
+// the point modules' early pass: the two-loop form (project_early_body); IMPLISOLID_EARLY_SM=1
+// selects the single loop (project_early_sm_body, measured slower: DESIGN "OB02 on the GPU"), its
+// faces per wave chunk IMPLISOLID_EARLY_CHUNK
+bool early_single_loop() {
+    static const bool on = [] {
+        const char* e = std::getenv("IMPLISOLID_EARLY_SM");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    return on;
+}
+int early_chunk() {
+    static const int c = [] {
+        const char* e = std::getenv("IMPLISOLID_EARLY_CHUNK");
+        const int v = e ? std::atoi(e) : 64;
+        return v < 16 ? 16 : v > 4096 ? 4096 : v;
+    }();
+    return c;
+}
+
 std::string TreeJit::point_source(const Program& p) {
     std::vector<Node> nodes;
     int next = 0;
@@ -982,6 +1001,7 @@ std::string TreeJit::point_source(const Program& p) {
         return e ? std::atoi(e) : 0;
     }();
     const std::string occ = pt_waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(pt_waves) + ")))" : "";
+    const char* early = early_single_loop() ? "project_early_sm_body" : "project_early_body";
     s << kPrelude << "#include \"ob02_device.hpp\"\n"
       << "namespace impli {\nusing namespace dev;\n"
       << "__device__ __forceinline__ float tree_pf(const float* __restrict__ M, const float* __restrict__ tab,\n"
@@ -1001,7 +1021,7 @@ std::string TreeJit::point_source(const Program& p) {
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_prep(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_prep_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early(const float* M, const float* tab, ProjArgs a) {\n"
-      << "    impli::ob::project_early_body(JitPt{M, tab}, a);\n}\n"
+      << "    impli::ob::" << early << "(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_normals_at(const float* M, const float* tab,\n"

@@ -149,4 +149,10 @@ private:
     std::string disk_dir_;
 };
 
+// the point modules' early projection pass: the two-loop form by default; IMPLISOLID_EARLY_SM=1
+// selects the single-loop form (ob02_device.hpp project_early_sm_body, an experiment: slower) and
+// IMPLISOLID_EARLY_CHUNK its faces per wave chunk (default 64)
+bool early_single_loop();
+int early_chunk();
+
 }  // namespace impli

@@ -2287,6 +2287,7 @@ void Ob02::centroids_projection(bool enable_qem) {
     a.fn = fn_.as<float>();
     a.fc = fcbuf.as<float>();
     a.pend = pend_.as<uint32_t>();
+    a.early_chunk = early_chunk();
     a.late_wmax = late_wmax();
     a.late_flat = late_flat();
     a.cap_hits = misc_.as<uint32_t>() + 1;
@@ -2314,7 +2315,9 @@ void Ob02::centroids_projection(bool enable_qem) {
     // every face and reads the early pass's per-face flags on the device (no host round trip)
     a.pert = perturbations();
     if (nw > 0) {
-        if (pk) TreeJit::launch(pk->early, grid, jargs, s, "impli_pt_project_early");
+        // the point module's single-loop early pass: a wave per chunk of early_chunk faces
+        const unsigned egrid = early_single_loop() ? blocks_for((nw + a.early_chunk - 1) / a.early_chunk * 64) : grid;
+        if (pk) TreeJit::launch(pk->early, egrid, jargs, s, "impli_pt_project_early");
         else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
         if (pk) TreeJit::launch(pk->late, grid, jargs, s, "impli_pt_project_late");
         else DEPTH_LAUNCH(E.depth(), k_project_late, grid, 256, s, E.d_program(), E.d_rabbit(), a);

@@ -121,6 +121,7 @@ struct ProjArgs {
     float* fn;              // facet normals (written by the early pass)
     float* fc;              // f(centroid) (written by the early pass)
     uint32_t* pend;         // early pass: per face, 1 if its centroid is unresolved (the late pass's)
+    int early_chunk;        // the early pass as one loop (project_early_sm_body): faces per wave chunk
     int late_wmax;          // the late pass's widest group (4..64 lanes, a power of two)
     int late_flat;          // 1: a round of the late searches may cross directions; 0: one direction per round
     uint32_t* cap_hits;     // bisections that reached kBisectCap (accumulated over the build)
@@ -322,6 +323,162 @@ __device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs&
     const int64_t j1 = a.rng[1];
     for (int64_t j = a.rng[0] + grid_lane() / kProjGroup; j < j1; j += grid_lanes() / kProjGroup)   // uniform per group
         project_early_face(ev, a, g, j);
+}
+
+// The early pass as one loop with one tree evaluation per iteration.  project_early_face runs the
+// searches and the bisection as separate loops, each with its own inlined copy of the tree code, and
+// a wave's 16 faces in step: a group whose face is done idles until the wave's longest face ends
+// (0.76-0.84 of the evaluations' bound, IMPLISOLID_PROJ_STATS), and groups in different phases take
+// turns through the two copies.  Here every group is in one of three phases -- searching (4 alphas
+// of the current direction per iteration), bisecting (2 levels per iteration), idle -- and each
+// iteration computes the group's point for its phase, evaluates the tree once for every lane, and
+// then advances each group by the same rules as try_direction / finalize_g / bisect_g (the shuffles
+// they need are taken for every group before the phase-specific update, so none runs in divergent
+// code).  A group that finishes takes the next face of its wave's chunk of early_chunk faces (rank
+// among the finishing groups by ballot: no atomics).  The result of every face is the serial one.
+template <class Ev>
+__device__ __forceinline__ void project_early_sm_body(const Ev& ev, const ProjArgs& a) {
+    constexpr int kSearch = 0, kBisect = 1, kIdle = 2;
+    const Grp g;
+    const int64_t j1 = a.rng[1];
+    const int nal = a.fold->nal;
+    const int n10 = nal < 10 ? nal : 10;
+    const float max_dist = a.fold->avg;
+    const float* alphas = a.fold->alphas;
+    const int chunk = a.early_chunk;
+    // this lane's node of the 2-level bisection tree (bisect_g)
+    const int node = g.sub < (1 << kBisLevels) - 1 ? g.sub : 0;
+    int depth = 0, bits = 0;
+    for (int n = node; n > 0; n = (n - 1) >> 1) bits = (bits << 1) | ((n & 1) ? 1 : 0), ++depth;
+    for (int64_t c0 = a.rng[0] + (grid_lane() >> 6) * chunk; c0 < j1; c0 += (grid_lanes() >> 6) * chunk) {
+        const int cn = (int)(j1 - c0 < chunk ? j1 - c0 : chunk);
+        int next = 0;   // the chunk's next face (wave-uniform)
+        int phase = kIdle;
+        int64_t j = 0;
+        V3 x{0.f, 0.f, 0.f}, fnv = x, d = x, best = x, x1 = x, x2 = x;
+        float fcv = 0.f, sc = 0.f, bf = 0.f;
+        int na = 0, a0 = 0, dir = 0, it = 0;
+        uint32_t evals = 0;
+        auto finish = [&](bool found, V3 r) {
+            if (g.sub == 0) {
+                if (found) { a.out[3 * j] = r.x; a.out[3 * j + 1] = r.y; a.out[3 * j + 2] = r.z; }
+                a.pend[j] = found ? 0u : 1u;
+                if (a.evals) a.evals[j] += evals;
+            }
+            phase = kIdle;
+        };
+        auto settle = [&]() {   // a direction with no alpha left: the next direction, or pending
+            while (phase == kSearch && a0 >= na) {
+                if (dir == 0) {
+                    dir = 1;
+                    d = fnv;
+                    na = n10;
+                    a0 = 0;
+                } else {
+                    finish(false, x);
+                }
+            }
+        };
+        for (;;) {
+            // idle groups take the chunk's next faces in group order
+            const uint64_t idle = __ballot(g.sub == 0 && phase == kIdle);
+            if (phase == kIdle) {
+                const int f = next + __popcll(idle & ((1ull << g.base) - 1ull));   // idle leaders before ours
+                if (f < cn) {
+                    j = c0 + f;
+                    x = V3{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
+                    fnv = V3{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
+                    d = V3{a.dir[3 * j], a.dir[3 * j + 1], a.dir[3 * j + 2]};
+                    fcv = a.fc[j];
+                    sc = get_sign(fcv);
+                    best = x;
+                    bf = fcv;
+                    na = nal;
+                    a0 = 0;
+                    dir = 0;
+                    evals = 0;
+                    phase = kSearch;
+                    settle();
+                }
+            }
+            next += __popcll(idle);
+            if (__ballot(phase != kIdle) == 0) {
+                if (next >= cn) break;
+                continue;   // every new face settled at once (empty alpha lists): hand out more
+            }
+            // this iteration's point: an alpha of the current direction, or this lane's bisection node
+            V3 p = x, ba = x1, bb = x2;
+            bool valid = false;
+            if (phase == kSearch) {
+                const int ai = a0 + g.sub;
+                valid = ai < na;
+                if (valid) {
+                    const float cc = max_dist * alphas[ai];   // (length_factor * alpha) * 4.0 / 4.0 is exact
+                    p = V3{x.x + cc * d.x, x.y + cc * d.y, x.z + cc * d.z};
+                }
+            } else if (phase == kBisect) {
+                for (int k = 0; k < depth; ++k) {
+                    const V3 m = bis_mid(ba, bb);
+                    if ((bits >> k) & 1) ba = m;
+                    else bb = m;
+                }
+                p = bis_mid(ba, bb);
+                valid = true;
+            }
+            float fv = 0.f;
+            if (valid) fv = ev.f(p.x, p.y, p.z);
+            // every group's shuffles, in uniform control flow
+            const bool hit = phase == kSearch && valid && get_sign(fv) * sc <= 0;
+            const uint32_t m = (uint32_t)g.bits(hit);
+            const int k = m ? __ffs(m) - 1 : 0;
+            const V3 pk = g.from(p, k);
+            const float fk = g.from(fv, k);
+            const float v0 = g.from(fv, 0);
+            const int cur1 = v0 < -kRootTol ? 1 : 2;
+            const float v1 = g.from(fv, cur1);
+            const V3 pc0 = g.from(p, 0), pc1 = g.from(p, cur1), a1 = g.from(ba, cur1), b1 = g.from(bb, cur1);
+            if (phase == kSearch) {   // try_direction's round, then finalize_g
+                evals += na - a0 < kProjGroup ? na - a0 : kProjGroup;
+                if (m) {
+                    best = pk;
+                    bf = fk;
+                    const bool z2 = fabsf(bf) <= kRootTol, z1 = fabsf(fcv) <= kRootTol;
+                    if (z1) best = x;
+                    if (!(z1 || z2)) {
+                        x1 = x;
+                        x2 = best;
+                        if (bf < -kRootTol) { const V3 t = x1; x1 = x2; x2 = t; }
+                        it = 0;
+                        phase = kBisect;
+                    } else {
+                        finish(true, best);
+                    }
+                } else {
+                    a0 += kProjGroup;
+                    settle();
+                }
+            } else if (phase == kBisect) {   // bisect_g's two levels
+                evals += (1 << kBisLevels) - 1;
+                const bool lo0 = v0 < -kRootTol, hi0 = v0 > kRootTol;
+                const bool lo1 = v1 < -kRootTol, hi1 = v1 > kRootTol;
+                if (fabsf(v0) <= kRootTol) {
+                    finish(true, pc0);
+                } else if (!(lo0 || hi0) || it + 1 == kBisectCap) {
+                    if (g.sub == 0) atomicAdd(a.cap_hits, 1u);
+                    finish(true, pc0);
+                } else if (fabsf(v1) <= kRootTol) {
+                    finish(true, pc1);
+                } else if (!(lo1 || hi1) || it + 2 == kBisectCap) {
+                    if (g.sub == 0) atomicAdd(a.cap_hits, 1u);
+                    finish(true, pc1);
+                } else {
+                    x1 = lo1 ? pc1 : a1;
+                    x2 = lo1 ? b1 : pc1;
+                    it += 2;
+                }
+            }
+        }
+    }
 }
 
 // types 2 (cross with a perturbation), 3 (cross of that with the mesh normal), 4-6 (axes), with a
