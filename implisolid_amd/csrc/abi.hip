@@ -993,6 +993,8 @@ struct implisolid_batch {
     double jit_seconds = 0;
 };
 
+static void batch_merged_enqueue(implisolid_batch* b, hipStream_t s);
+
 implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, const char* mc_json, int n_streams) {
     g_last_error.clear();
     auto* b = new implisolid_batch();
@@ -1026,9 +1028,21 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         b->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         // merged: the shallow class in batch_groups() pipelines, the deep class (if any) in one more
         const int ns = b->merged ? batch_groups() : std::max(1, std::min(n_streams, 8));
+        // merged: the deep class's pipeline (off the critical path: it ends ~100 us before the
+        // shallow class's) at the lowest stream priority unless IMPLISOLID_BATCH_DEEP_PRIO=0, so the
+        // dispatcher serves the shallow class's waves first when both have work
+        static const bool deep_low = [] {
+            const char* e = std::getenv("IMPLISOLID_BATCH_DEEP_PRIO");
+            return e ? std::atoi(e) != 0 : true;
+        }();
+        int prio_least = 0, prio_greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
         for (int k = 0; k < ns; ++k) {
             hipStream_t q;
-            IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+            if (b->merged && deep_low)
+                IMPLI_HIP(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_least));
+            else
+                IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
             b->streams.push_back(q);
         }
         for (int k = 0; k <= ns; ++k) {
@@ -1069,6 +1083,8 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             b->objs.reserve(rows.size() * sizeof(ObjArgs));
             IMPLI_HIP(hipMemcpy(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice));
             IMPLI_HIP(hipStreamSynchronize(s0));
+            // (the whole pass captured as one graph and replayed: 0.548-0.557 ms against 0.499-0.501
+            // with direct launches, profiles/r05zq_config5_merged_graph_ab.txt)
             return b;
         }
         bool graphs = !std::getenv("IMPLISOLID_NO_GRAPH");
@@ -1108,34 +1124,39 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
     return b;
 }
 
+// one merged pass enqueued on s: the groups' pipelines forked from s and joined back to it
+static void batch_merged_enqueue(implisolid_batch* b, hipStream_t s) {
+    Engine& E0 = *b->engines[0];
+    const int fill = Engine::pruning() >= 2 ? 1 : 0;
+    // each group's pipeline -- interval and eval passes, then marching cubes -- on its own
+    // stream: one group's latency-bound launches (the coarse pass, the list fills, the count
+    // and scan of few objects) run beside another's throughput-bound eval; the deep class
+    // (few objects, 12- or 16-slot stacks) is the last group.  Forked from and joined to the
+    // caller's stream.
+    const int ng = (int)b->groups.size();
+    if (ng > 1) {
+        IMPLI_HIP(hipEventRecord(b->events[0], s));
+        for (int k = 1; k < ng; ++k) IMPLI_HIP(hipStreamWaitEvent(b->streams[(size_t)k - 1], b->events[0], 0));
+    }
+    for (int k = ng - 1; k >= 0; --k) {   // the deep class first: its passes are the longest chain
+        const implisolid_batch::Group& gr = b->groups[(size_t)k];
+        hipStream_t q = k == 0 ? s : b->streams[(size_t)k - 1];
+        const ObjArgs* rows = b->objs.as<ObjArgs>() + gr.row0;
+        launch_batch_eval(rows, gr.n, gr.depth, gr.vdepth, E0.d_rabbit(), E0.tab_range(), E0.grid(), fill, q);
+        launch_batch_mc(rows, gr.n, E0.d_cases(), E0.grid(), q);
+    }
+    for (int k = 1; k < ng; ++k) {
+        IMPLI_HIP(hipEventRecord(b->events[(size_t)k], b->streams[(size_t)k - 1]));
+        IMPLI_HIP(hipStreamWaitEvent(s, b->events[(size_t)k], 0));
+    }
+    IMPLI_HIP(hipGetLastError());
+}
+
 int implisolid_batch_run(implisolid_batch* b, void* stream) {
     try {
         hipStream_t s = (hipStream_t)stream;
         if (b->merged) {
-            Engine& E0 = *b->engines[0];
-            const int fill = Engine::pruning() >= 2 ? 1 : 0;
-            // each group's pipeline -- interval and eval passes, then marching cubes -- on its own
-            // stream: one group's latency-bound launches (the coarse pass, the list fills, the count
-            // and scan of few objects) run beside another's throughput-bound eval; the deep class
-            // (few objects, 12- or 16-slot stacks) is the last group.  Forked from and joined to the
-            // caller's stream.
-            const int ng = (int)b->groups.size();
-            if (ng > 1) {
-                IMPLI_HIP(hipEventRecord(b->events[0], s));
-                for (int k = 1; k < ng; ++k) IMPLI_HIP(hipStreamWaitEvent(b->streams[(size_t)k - 1], b->events[0], 0));
-            }
-            for (int k = ng - 1; k >= 0; --k) {   // the deep class first: its passes are the longest chain
-                const implisolid_batch::Group& gr = b->groups[(size_t)k];
-                hipStream_t q = k == 0 ? s : b->streams[(size_t)k - 1];
-                const ObjArgs* rows = b->objs.as<ObjArgs>() + gr.row0;
-                launch_batch_eval(rows, gr.n, gr.depth, gr.vdepth, E0.d_rabbit(), E0.tab_range(), E0.grid(), fill, q);
-                launch_batch_mc(rows, gr.n, E0.d_cases(), E0.grid(), q);
-            }
-            for (int k = 1; k < ng; ++k) {
-                IMPLI_HIP(hipEventRecord(b->events[(size_t)k], b->streams[(size_t)k - 1]));
-                IMPLI_HIP(hipStreamWaitEvent(s, b->events[(size_t)k], 0));
-            }
-            IMPLI_HIP(hipGetLastError());
+            batch_merged_enqueue(b, s);
             return 0;
         }
         const int ns = (int)b->streams.size();
