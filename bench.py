@@ -682,6 +682,7 @@ def main():
             ob02_sharded["r512"] = leg("ob02_sharded_r512", lambda: run_ob02_sharded(512))
         except Exception as exc:
             ob02_sharded["r512"] = {"error": repr(exc)[:300]}
+        D.release_shards()   # the kept shard handles' streams and buffers are not the later legs'
 
     # N = 1: the sharded OB02 loop's 8-rank critical path, estimated on this GPU: config 3
     # on the shifted box at 256^3, its MC mesh owned by the 8 balanced slabs' vertex ranges, every
@@ -739,6 +740,10 @@ def main():
             ob02_est["r512"] = leg("ob02_sharded_estimate_r512", lambda: run_ob02_estimate(512))
         except Exception as exc:
             ob02_est["r512"] = {"error": repr(exc)[:300]}
+        from implisolid_amd import distributed as D_
+        # the 16 kept shard handles hold 32 HIP streams; left alive, they crowded the process's
+        # hardware queues and the config-5 leg's two pipelines ran 0.85 instead of 0.50 ms per pass
+        D_.release_shards()
 
     c5 = None
     if world == 1 and not args.skip_config5:

@@ -1028,21 +1028,12 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         b->jit_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         // merged: the shallow class in batch_groups() pipelines, the deep class (if any) in one more
         const int ns = b->merged ? batch_groups() : std::max(1, std::min(n_streams, 8));
-        // merged: the deep class's pipeline (off the critical path: it ends ~100 us before the
-        // shallow class's) at the lowest stream priority unless IMPLISOLID_BATCH_DEEP_PRIO=0, so the
-        // dispatcher serves the shallow class's waves first when both have work
-        static const bool deep_low = [] {
-            const char* e = std::getenv("IMPLISOLID_BATCH_DEEP_PRIO");
-            return e ? std::atoi(e) != 0 : true;
-        }();
-        int prio_least = 0, prio_greatest = 0;
-        (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+        // (the deep class's stream at the lowest priority measured 0.5 % faster alone, but with the
+        // bench's earlier legs' streams alive the two pipelines then shared a hardware queue: 0.85 ms
+        // per pass, profiles/r05zr_*; default priority)
         for (int k = 0; k < ns; ++k) {
             hipStream_t q;
-            if (b->merged && deep_low)
-                IMPLI_HIP(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_least));
-            else
-                IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+            IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
             b->streams.push_back(q);
         }
         for (int k = 0; k <= ns; ++k) {
