@@ -170,8 +170,10 @@ void Engine::release_jit() {
     J.release(jit_slot_);
     J.release(bake_slot_);
     J.release(pt_slot_);
-    jit_slot_ = bake_slot_ = pt_slot_ = nullptr;
-    jit_requested_ = bake_requested_ = pt_requested_ = false;
+    J.release(pt_bake_slot_);
+    jit_slot_ = bake_slot_ = pt_slot_ = pt_bake_slot_ = nullptr;
+    jit_requested_ = bake_requested_ = pt_requested_ = pt_bake_requested_ = false;
+    pt_uses_ = 0;
     jit_fn_ = nullptr;
     jit_iv_ = JitIntervalKernels{};
 }
@@ -439,10 +441,20 @@ const float* Engine::d_mats() const {
 }
 
 const TreeJit::PointKernels* Engine::point_jit(hipStream_t s) {
+    TreeJit& J = TreeJit::instance();
     if (!pt_requested_) {
-        pt_slot_ = TreeJit::instance().request(prog_host_, TreeJit::kPoints, false, s);
+        pt_slot_ = J.request(prog_host_, TreeJit::kPoints, J.bake() == TreeJit::kBakeAlways, s);
         pt_requested_ = true;
     }
+    // a hot object gets a point module with its matrices baked in, as its brick module does
+    // (ensure_jit): here after kBakeAfter builds' worth of OB02 steps (a build of 3 repeats asks
+    // twice per repeat: the resampling's normals, the projection)
+    if (++pt_uses_ >= 6 * TreeJit::kBakeAfter && !pt_bake_requested_ && allow_hot_bake_ && J.bake() == TreeJit::kBakeHot &&
+        pt_slot_) {
+        pt_bake_slot_ = J.request(prog_host_, TreeJit::kPoints, true, s);
+        pt_bake_requested_ = true;
+    }
+    if (pt_bake_slot_ && pt_bake_slot_->ready.load(std::memory_order_acquire)) return &pt_bake_slot_->pk;
     return (pt_slot_ && pt_slot_->ready.load(std::memory_order_acquire)) ? &pt_slot_->pk : nullptr;
 }
 

@@ -175,6 +175,9 @@ private:
     bool allow_hot_bake_ = true;
     TreeJit::Slot* pt_slot_ = nullptr;     // the point module
     bool pt_requested_ = false;
+    TreeJit::Slot* pt_bake_slot_ = nullptr;   // a hot object's point module with its matrices baked in
+    bool pt_bake_requested_ = false;
+    int pt_uses_ = 0;                         // point_jit calls since set_object (the hot-object count)
     hipFunction_t jit_fn_ = nullptr;       // what the last eval used (null: interpreter)
     bool counters_fresh_ = false;   // eval_field zeroed the counters; the next count() need not
     uint32_t mark_id_ = 0;          // id of the last pruned eval's unit marks (umark_)

@@ -707,7 +707,7 @@ TreeJit::Slot* TreeJit::request(const Program& p, int kind, bool bake, hipStream
     if (m == kOff) return nullptr;
     std::string src;
     try {
-        src = kind == kPoints ? point_source(p) : kernel_source(p, bake);
+        src = kind == kPoints ? point_source(p, bake) : kernel_source(p, bake);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "implisolid: tree JIT skipped (%s)\n", e.what());
         return nullptr;
@@ -984,7 +984,7 @@ int early_chunk() {
     return c;
 }
 
-std::string TreeJit::point_source(const Program& p) {
+std::string TreeJit::point_source(const Program& p, bool bake) {
     std::vector<Node> nodes;
     int next = 0;
     const int root = parse(p, 0, nodes, next);
@@ -1002,20 +1002,43 @@ std::string TreeJit::point_source(const Program& p) {
     }();
     const std::string occ = pt_waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(pt_waves) + ")))" : "";
     const char* early = early_single_loop() ? "project_early_sm_body" : "project_early_body";
+    // IMPLISOLID_PT_FG_WAVES=n: an occupancy request of n waves per SIMD on the f + gradient passes
+    // at arbitrary points (centroid normals, normals at the projected centroids)
+    static const int fg_waves = [] {
+        const char* e = std::getenv("IMPLISOLID_PT_FG_WAVES");
+        return e ? std::atoi(e) : 0;
+    }();
+    const std::string occ_fg = fg_waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(fg_waves) + ")))" : "";
+    // baked (a hot object's module): the matrices and parameter rows as a constexpr table of exact
+    // literals, so every transform reads immediates -- the same operations on the same values (no
+    // term is dropped: 0 * NaN stays NaN), but no loop-invariant matrix values held in registers
+    // (the early search pass: 189 -> ~130 VGPRs for config 3's tree, two -> three waves per SIMD)
+    std::string table, mparam = "M";
+    if (bake) {
+        std::ostringstream t;
+        const int nm = std::max(1, (int)p.n_mats);
+        t << "__device__ constexpr float kMb[" << 12 * nm << "] = {";
+        for (int i = 0; i < nm; ++i)
+            for (int k = 0; k < 12; ++k) t << (i || k ? ",\n    " : "\n    ") << float_literal(i < p.n_mats ? p.mats[i][k] : 0.f);
+        t << "};\n";
+        table = t.str();
+        mparam = "M_unused";
+    }
+    const std::string mbind = bake ? "    const float* const M = kMb;\n" : "";
     s << kPrelude << "#include \"ob02_device.hpp\"\n"
-      << "namespace impli {\nusing namespace dev;\n"
-      << "__device__ __forceinline__ float tree_pf(const float* __restrict__ M, const float* __restrict__ tab,\n"
+      << "namespace impli {\nusing namespace dev;\n" << table
+      << "__device__ __forceinline__ float tree_pf(const float* __restrict__ " << mparam << ", const float* __restrict__ tab,\n"
       << "                                         float x0, float y0, float z0) {\n"
-      << ef.out.str() << "    return " << f << ";\n}\n"
-      << "__device__ __forceinline__ float tree_pfg(const float* __restrict__ M, const float* __restrict__ tab,\n"
+      << mbind << ef.out.str() << "    return " << f << ";\n}\n"
+      << "__device__ __forceinline__ float tree_pfg(const float* __restrict__ " << mparam << ", const float* __restrict__ tab,\n"
       << "                                          float x0, float y0, float z0, V3& g_out) {\n"
-      << eg.out.str() << "    g_out = g" << fg.substr(1) << ";\n    return " << fg << ";\n}\n"
+      << mbind << eg.out.str() << "    g_out = g" << fg.substr(1) << ";\n    return " << fg << ";\n}\n"
       << "struct JitPt {\n    const float* M;\n    const float* tab;\n"
       << "    __device__ __forceinline__ float f(float x, float y, float z) const { return tree_pf(M, tab, x, y, z); }\n"
       << "    __device__ __forceinline__ float fg(float x, float y, float z, V3& g) const { return tree_pfg(M, tab, x, y, z, g); }\n"
       << "};\n}  // namespace impli\n"
       << "using impli::JitPt;\nusing impli::ob::ProjArgs;\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_centroid_normals(const float* M, const float* tab,\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_centroid_normals(const float* M, const float* tab,\n"
       << "    const float* v, const int32_t* f, const int64_t* rng, float* C, float* N) {\n"
       << "    impli::ob::centroid_normals_body(JitPt{M, tab}, v, f, rng, C, N);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_prep(const float* M, const float* tab, ProjArgs a) {\n"
@@ -1024,7 +1047,7 @@ std::string TreeJit::point_source(const Program& p) {
       << "    impli::ob::" << early << "(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_normals_at(const float* M, const float* tab,\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_normals_at(const float* M, const float* tab,\n"
       << "    const float* P, const int64_t* rng, float* G) {\n"
       << "    impli::ob::normals_at_body(JitPt{M, tab}, P, rng, G);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_points(const float* M, const float* tab,\n"

@@ -34,7 +34,7 @@ public:
     static std::string kernel_source(const Program& p, bool bake = false);
     // C++ source of the point kernels for this shape (OB02 passes and direct evaluation,
     // ob02_device.hpp over straight-line f / (f, grad) code; NaN-exact: no transform specialisation)
-    static std::string point_source(const Program& p);
+    static std::string point_source(const Program& p, bool bake = false);
 
     // hipRTC-compile the source to a gfx950 code object (no GPU needed); throws with the log
     static std::vector<char> compile(const std::string& src);

@@ -705,11 +705,13 @@ def sync_jit(impli):
     impli.set_jit(2)
 
 
+@pytest.mark.parametrize("bake", [False, True])
 @pytest.mark.parametrize("name", ["config2_48", "config3_64", "twist_tbb", "meta_balls"])
-def test_ob02_point_jit_matches_oracle(impli, oracle, sync_jit, name):
+def test_ob02_point_jit_matches_oracle(impli, oracle, sync_jit, name, bake):
     """The OB02 passes over the JIT point module (ob02_device.hpp bodies over straight-line tree
     code) give the oracle's mesh -- config 3 at 64 includes the non-finite rows (NaN centroids
-    through the unspecialised transforms)."""
+    through the unspecialised transforms).  bake: the module with the object's matrices as literals
+    (a hot object's, here from the first build) -- the same operations on the same values."""
     from implisolid_amd import scenes
     if name == "config2_48":
         shape, mc = scenes.config2(48)
@@ -718,14 +720,21 @@ def test_ob02_point_jit_matches_oracle(impli, oracle, sync_jit, name):
     else:
         shape = SCREW_TREES[name]
         mc = scenes.mc_settings(40, 0.7, vresampl_iters=1, vresampl_c=0.4, projection=1, qem=1, overall_repeats=2)
-    _ob02_compare(impli, oracle, shape, mc)
+    if bake:
+        impli.set_jit_bake(1)
+    try:
+        _ob02_compare(impli, oracle, shape, mc)
+    finally:
+        impli.set_jit_bake(2)
     assert impli.last_build_stats()["jit_launches"] > 0
 
 
+@pytest.mark.parametrize("bake", [False, True])
 @pytest.mark.parametrize("name", ["config3_tree", "union_sphere_cube", "twist_tbb", "extrusion_tri", "leaf_cube"])
-def test_eval_points_jit_bit_exact(impli, oracle, sync_jit, name):
+def test_eval_points_jit_bit_exact(impli, oracle, sync_jit, name, bake):
     """Direct evaluation through the JIT point module, including non-finite coordinates (the
-    interpreter's transforms propagate NaN through zero coefficients, and so must the JIT's)."""
+    interpreter's transforms propagate NaN through zero coefficients, and so must the JIT's -- with
+    the matrices baked in as literals too)."""
     shape = TREES[name]
     rng = np.random.default_rng(77)
     pts = rng.uniform(-1.1, 1.1, size=(20000, 3)).astype(np.float32)
@@ -734,8 +743,13 @@ def test_eval_points_jit_bit_exact(impli, oracle, sync_jit, name):
     pts[100:150, 2] = -np.inf
     tree = oracle.mp5_to_nodes(json.dumps(shape))
     f_ref, g_ref = oracle.eval_implicit(tree, pts), oracle.eval_gradient(tree, pts)
-    with impli.ImplicitService(shape) as svc:
-        f, g = svc.eval(pts, gradient=True)
+    if bake:
+        impli.set_jit_bake(1)
+    try:
+        with impli.ImplicitService(shape) as svc:
+            f, g = svc.eval(pts, gradient=True)
+    finally:
+        impli.set_jit_bake(2)
     assert np.array_equal(f.view(np.uint32), f_ref.view(np.uint32)) or np.array_equal(
         np.isnan(f), np.isnan(f_ref)) and np.array_equal(f[~np.isnan(f)], f_ref[~np.isnan(f_ref)])
     ok = np.isfinite(g_ref).all(1)
