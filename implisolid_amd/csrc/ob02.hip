@@ -207,6 +207,7 @@ __global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const
 // (an umbrella of up to kSortRegs faces is sorted in registers: one load and one store per entry,
 // where the in-memory insertion sort was a chain of dependent global loads)
 constexpr int kSortRegs = 12;
+constexpr int kUmbrellaRegs = 8;   // umbrellas up to this size load their faces' data at once (QEM)
 __device__ __forceinline__ void sort_umbrella_at(const uint32_t* __restrict__ off, int32_t* __restrict__ lst, int64_t v) {
     const uint32_t a = off[v], e = off[v + 1];
     if (e - a <= (uint32_t)kSortRegs) {
@@ -537,8 +538,8 @@ __global__ void k_resample(const uint32_t* __restrict__ off, const int32_t* __re
     if (v >= nv) return;
     const uint32_t a = off[v], e = off[v + 1];
     float sw = 0;   // vertex_resampling_VV1 :108-140
-    for (uint32_t k = a; k < e; ++k) sw += W[lst[k]];
     float x = 0, y = 0, z = 0;
+    for (uint32_t k = a; k < e; ++k) sw += W[lst[k]];
     for (uint32_t k = a; k < e; ++k) {
         const int32_t fj = lst[k];
         const float w = W[fj] / sw;
@@ -1647,10 +1648,8 @@ __global__ __launch_bounds__(256) void k_qem(float* __restrict__ verts, int64_t 
     float* v = verts + 3 * vi;
     const float ox = v[0], oy = v[1], oz = v[2];
     float A[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}, b[3] = {0.f, 0.f, 0.f};
-    for (uint32_t k = off[vi]; k < off[vi + 1]; ++k) {
-        const int32_t ni = lst[k];
-        const float nx = N[3 * ni], ny = N[3 * ni + 1], nz = N[3 * ni + 2];
-        const float Px = C[3 * ni] - ox, Py = C[3 * ni + 1] - oy, Pz = C[3 * ni + 2] - oz;
+    auto accum = [&](float nx, float ny, float nz, float cx, float cy, float cz) {
+        const float Px = cx - ox, Py = cy - oy, Pz = cz - oz;
         const float nn00 = nx * nx, nn01 = nx * ny, nn02 = nx * nz, nn11 = ny * ny, nn12 = ny * nz, nn22 = nz * nz;
         A[0][0] += nn00; A[0][1] += nn01; A[0][2] += nn02;
         A[1][0] += nn01; A[1][1] += nn11; A[1][2] += nn12;
@@ -1658,6 +1657,29 @@ __global__ __launch_bounds__(256) void k_qem(float* __restrict__ verts, int64_t 
         b[0] -= nn00 * Px + nn01 * Py + nn02 * Pz;
         b[1] -= nn01 * Px + nn11 * Py + nn12 * Pz;
         b[2] -= nn02 * Px + nn12 * Py + nn22 * Pz;
+    };
+    const uint32_t a0 = off[vi], a1 = off[vi + 1];
+    if (a1 > a0 && a1 - a0 <= (uint32_t)kUmbrellaRegs) {
+        // a small umbrella's loads all in flight at once (indices, then normals and centroids;
+        // past its end the last face is loaded again and not summed), summed in the same order
+        const int n = (int)(a1 - a0);
+        int32_t id[kUmbrellaRegs];
+#pragma unroll
+        for (int k = 0; k < kUmbrellaRegs; ++k) id[k] = lst[a0 + (k < n ? k : n - 1)];
+        float q[kUmbrellaRegs][6];
+#pragma unroll
+        for (int k = 0; k < kUmbrellaRegs; ++k) {
+            q[k][0] = N[3 * id[k]]; q[k][1] = N[3 * id[k] + 1]; q[k][2] = N[3 * id[k] + 2];
+            q[k][3] = C[3 * id[k]]; q[k][4] = C[3 * id[k] + 1]; q[k][5] = C[3 * id[k] + 2];
+        }
+#pragma unroll
+        for (int k = 0; k < kUmbrellaRegs; ++k)
+            if (k < n) accum(q[k][0], q[k][1], q[k][2], q[k][3], q[k][4], q[k][5]);
+    } else {
+        for (uint32_t k = a0; k < a1; ++k) {
+            const int32_t ni = lst[k];
+            accum(N[3 * ni], N[3 * ni + 1], N[3 * ni + 2], C[3 * ni], C[3 * ni + 1], C[3 * ni + 2]);
+        }
     }
     float S[3], U[3][3], V[3][3];
     const int rank = jacobi_svd3(A, (float)(1.0 / 680.0), S, U, V);
