@@ -729,6 +729,20 @@ def test_ob02_point_jit_matches_oracle(impli, oracle, sync_jit, name, bake):
     assert impli.last_build_stats()["jit_launches"] > 0
 
 
+def test_ob02_hot_object_switches_to_baked_point_module(impli, oracle):
+    """The default bake policy: an object built again and again gets its point module rebuilt with
+    its matrices baked in (in the background, after 4 builds' worth of OB02 steps) and switches to
+    it; every build's mesh is the oracle's, before and after the switch."""
+    from implisolid_amd import scenes
+    shape, mc = scenes.config3_shifted(64)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    for k in range(7):
+        v, f = impli.make_geometry(shape, mc)
+        assert np.array_equal(f, fr) and np.array_equal(v.view(np.uint32), vr.view(np.uint32)), k
+        if k == 4:
+            impli.jit_wait()   # the baked modules requested during builds 4-5 are loaded from here on
+
+
 @pytest.mark.parametrize("bake", [False, True])
 @pytest.mark.parametrize("name", ["config3_tree", "union_sphere_cube", "twist_tbb", "extrusion_tri", "leaf_cube"])
 def test_eval_points_jit_bit_exact(impli, oracle, sync_jit, name, bake):
