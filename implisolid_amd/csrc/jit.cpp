@@ -1025,6 +1025,13 @@ std::string TreeJit::point_source(const Program& p, bool bake) {
         mparam = "M_unused";
     }
     const std::string mbind = bake ? "    const float* const M = kMb;\n" : "";
+    // IMPLISOLID_PROJ_GROUP=2 / 8 (experiments): the searches' lanes per face in this module
+    static const int proj_group = [] {
+        const char* e = std::getenv("IMPLISOLID_PROJ_GROUP");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 2 || v == 8 ? v : 0;
+    }();
+    if (proj_group) s << "#define IMPLI_PROJ_GROUP " << proj_group << "\n";
     s << kPrelude << "#include \"ob02_device.hpp\"\n"
       << "namespace impli {\nusing namespace dev;\n" << table
       << "__device__ __forceinline__ float tree_pf(const float* __restrict__ " << mparam << ", const float* __restrict__ tab,\n"

@@ -2332,7 +2332,13 @@ void Ob02::centroids_projection(bool enable_qem) {
     store_pointset("pre_p_centroids", cen_.as<float>(), nf, false);   // cp:1236-1238: the centroids
     a.fold = fold_out_.as<FoldOut>();
     st.next(kStageProject);
-    const unsigned grid = blocks_for(nw * kProjGroup);
+    // lanes per face of the point module's searches (kProjGroup; IMPLISOLID_PROJ_GROUP experiments)
+    static const int pgroup = [] {
+        const char* e = std::getenv("IMPLISOLID_PROJ_GROUP");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 2 || v == 8 ? v : kProjGroup;
+    }();
+    const unsigned grid = blocks_for(nw * (pk ? pgroup : kProjGroup));
     // centroids left unresolved need the randomised directions (types 2-6): the late pass covers
     // every face and reads the early pass's per-face flags on the device (no host round trip)
     a.pert = perturbations();

@@ -140,8 +140,11 @@ struct ProjArgs {
 // 1.51-1.52 ms for config3s against 1.66-1.76 with 8 and 3 (fewer evaluations past the hit, and
 // 3 instead of 7 per two levels), 2 and 1 1.72-1.74, 16 and 4 1.88; configs 2 and 3 within noise.
 // The searches are throughput-bound at this size (90 k faces), not chain-bound.
-constexpr int kProjGroup = 4;
-constexpr int kBisLevels = 2;
+#ifndef IMPLI_PROJ_GROUP   // (experiments: a point module built with IMPLISOLID_PROJ_GROUP=2 / 8)
+#define IMPLI_PROJ_GROUP 4
+#endif
+constexpr int kProjGroup = IMPLI_PROJ_GROUP;
+constexpr int kBisLevels = kProjGroup >= 8 ? 3 : kProjGroup >= 4 ? 2 : 1;
 static_assert((1 << kBisLevels) - 1 <= kProjGroup && 64 % kProjGroup == 0, "bisection tree fits the group");
 
 template <int W>
@@ -339,6 +342,7 @@ __device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs&
 template <class Ev>
 __device__ __forceinline__ void project_early_sm_body(const Ev& ev, const ProjArgs& a) {
     constexpr int kSearch = 0, kBisect = 1, kIdle = 2;
+    static_assert(kBisLevels == 2, "the single-loop form walks two bisection levels per iteration");
     const Grp g;
     const int64_t j1 = a.rng[1];
     const int nal = a.fold->nal;
