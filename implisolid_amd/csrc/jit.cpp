@@ -612,6 +612,7 @@ void TreeJit::build(Slot* slot) {
                 ok = hipModuleGetFunction(&pk.cnormals, slot->mod, "impli_pt_centroid_normals") == hipSuccess &&
                      hipModuleGetFunction(&pk.prep, slot->mod, "impli_pt_project_prep") == hipSuccess &&
                      hipModuleGetFunction(&pk.early, slot->mod, "impli_pt_project_early") == hipSuccess &&
+                     hipModuleGetFunction(&pk.early2, slot->mod, "impli_pt_project_early2") == hipSuccess &&
                      hipModuleGetFunction(&pk.late, slot->mod, "impli_pt_project_late") == hipSuccess &&
                      hipModuleGetFunction(&pk.normals, slot->mod, "impli_pt_normals_at") == hipSuccess &&
                      hipModuleGetFunction(&pk.points, slot->mod, "impli_pt_points") == hipSuccess;
@@ -1052,6 +1053,8 @@ std::string TreeJit::point_source(const Program& p, bool bake) {
       << "    impli::ob::project_prep_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::" << early << "(JitPt{M, tab}, a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early2(const float* M, const float* tab, ProjArgs a) {\n"
+      << "    impli::ob::project_early_body<2>(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_normals_at(const float* M, const float* tab,\n"

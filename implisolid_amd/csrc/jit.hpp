@@ -45,8 +45,8 @@ public:
         hipFunction_t refine = nullptr;   // interval pass, bricks of mixed boxes (brick_refine_body)
     };
     struct PointKernels {                 // the point module (ob02_device.hpp bodies)
-        hipFunction_t cnormals = nullptr, prep = nullptr, early = nullptr, late = nullptr, normals = nullptr,
-                      points = nullptr;
+        hipFunction_t cnormals = nullptr, prep = nullptr, early = nullptr, early2 = nullptr, late = nullptr,
+                      normals = nullptr, points = nullptr;   // early2: the early search with 2 lanes per face
     };
     enum Kind { kBricks = 0, kPoints = 1 };
     // One compiled module (one source on one device).  `ready` is set (release) once `k` holds the

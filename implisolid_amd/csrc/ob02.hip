@@ -2287,6 +2287,9 @@ static int late_flat() {
     return f;
 }
 
+// the work faces from which the point module's early search runs with 2 lanes per face
+constexpr int64_t kEarly2Faces = 400000;
+
 void Ob02::centroids_projection(bool enable_qem) {
     if (!nf) return;
     if (!topo_valid_) build_topology();
@@ -2338,17 +2341,24 @@ void Ob02::centroids_projection(bool enable_qem) {
         const int v = e ? std::atoi(e) : 0;
         return v == 2 || v == 8 ? v : kProjGroup;
     }();
+    // large meshes: the point module's 2-lane early search (project_early_body<2>); the late pass
+    // keeps 4 lanes per face
+    const bool early2 = pk && pgroup == kProjGroup && nw >= kEarly2Faces;
     const unsigned grid = blocks_for(nw * (pk ? pgroup : kProjGroup));
+    const unsigned late_grid = blocks_for(nw * kProjGroup);
     // centroids left unresolved need the randomised directions (types 2-6): the late pass covers
     // every face and reads the early pass's per-face flags on the device (no host round trip)
     a.pert = perturbations();
     if (nw > 0) {
         // the point module's single-loop early pass: a wave per chunk of early_chunk faces
-        const unsigned egrid = early_single_loop() ? blocks_for((nw + a.early_chunk - 1) / a.early_chunk * 64) : grid;
-        if (pk) TreeJit::launch(pk->early, egrid, jargs, s, "impli_pt_project_early");
+        const unsigned egrid = early_single_loop() ? blocks_for((nw + a.early_chunk - 1) / a.early_chunk * 64)
+                               : early2                ? blocks_for(nw * 2)
+                                                       : grid;
+        if (pk && early2) TreeJit::launch(pk->early2, egrid, jargs, s, "impli_pt_project_early2");
+        else if (pk) TreeJit::launch(pk->early, egrid, jargs, s, "impli_pt_project_early");
         else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
-        if (pk) TreeJit::launch(pk->late, grid, jargs, s, "impli_pt_project_late");
-        else DEPTH_LAUNCH(E.depth(), k_project_late, grid, 256, s, E.d_program(), E.d_rabbit(), a);
+        if (pk) TreeJit::launch(pk->late, late_grid, jargs, s, "impli_pt_project_late");
+        else DEPTH_LAUNCH(E.depth(), k_project_late, late_grid, 256, s, E.d_program(), E.d_rabbit(), a);
     }
     IMPLI_HIP(hipGetLastError());
     if (profile_ && nw > 0) {   // the evaluations of this projection, summed on the host

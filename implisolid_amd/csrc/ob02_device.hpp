@@ -149,6 +149,7 @@ static_assert((1 << kBisLevels) - 1 <= kProjGroup && 64 % kProjGroup == 0, "bise
 
 template <int W>
 struct GrpW {   // a centroid's W lanes inside the wave (control flow is uniform per group)
+    static constexpr int kWidth = W;
     int sub, base;
     __device__ GrpW() {
         const int lane = (int)(threadIdx.x & 63);
@@ -246,11 +247,12 @@ __device__ void finalize_g(const G& g, const int L, const Ev& ev, V3 x, float fc
 
 // make_alpha_list's alphas along d, kProjGroup at a time; the first in list order whose sign
 // differs from the centroid's (cp:595-903)
-template <class Ev>
-__device__ __forceinline__ bool try_direction(const Grp& g, const Ev& ev, V3 x, V3 d, float sc,
+template <class G, class Ev>
+__device__ __forceinline__ bool try_direction(const G& g, const Ev& ev, V3 x, V3 d, float sc,
                                               const float* alphas, int na, float max_dist, V3& best,
                                               float& best_f, uint32_t& evals) {
-    for (int a0 = 0; a0 < na; a0 += kProjGroup) {
+    constexpr int kW = G::kWidth;
+    for (int a0 = 0; a0 < na; a0 += kW) {
         const int ai = a0 + g.sub;
         V3 p = x;
         float fa = 0.f;
@@ -261,8 +263,8 @@ __device__ __forceinline__ bool try_direction(const Grp& g, const Ev& ev, V3 x, 
             fa = ev.f(p.x, p.y, p.z);
             hit = get_sign(fa) * sc <= 0;
         }
-        evals += na - a0 < kProjGroup ? na - a0 : kProjGroup;
-        const uint32_t m = g.bits(hit);
+        evals += na - a0 < kW ? na - a0 : kW;
+        const uint32_t m = (uint32_t)g.bits(hit);
         if (m) {
             best = g.from(p, __ffs(m) - 1);
             best_f = g.from(fa, __ffs(m) - 1);
@@ -297,9 +299,11 @@ __device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& 
     for (int64_t j = a.rng[0] + grid_lane(); j < j1; j += grid_lanes()) project_prep_face(ev, a, j);
 }
 
-// direction types 0 (gradient) and 1 (mesh normal); kProjGroup lanes per face
-template <class Ev>
-__device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs& a, const Grp& g, int64_t j) {
+// direction types 0 (gradient) and 1 (mesh normal); W lanes per face (kProjGroup, or 2 on large
+// meshes: see project_early_body)
+template <int W, class Ev>
+__device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs& a, const GrpW<W>& g, int64_t j) {
+    constexpr int kLevels = W >= 8 ? 3 : W >= 4 ? 2 : 1;
     const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const V3 d0{a.dir[3 * j], a.dir[3 * j + 1], a.dir[3 * j + 2]};
@@ -313,19 +317,24 @@ __device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs&
     float bf = fcv;
     bool found = try_direction(g, ev, x, d0, sc, alphas, nal, max_dist, best, bf, evals);
     if (!found) found = try_direction(g, ev, x, fnv, sc, alphas, nal < 10 ? nal : 10, max_dist, best, bf, evals);
-    if (found) finalize_g(g, kBisLevels, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
+    if (found) finalize_g(g, kLevels, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
     // unresolved faces are flagged for the late pass (a compacted list cost one same-address atomic
     // per wave: 258 us per pass when every face pends, as with a non-finite average edge length)
     if (g.sub == 0) a.pend[j] = found ? 0u : 1u;
     if (a.evals && g.sub == 0) a.evals[j] += evals;
 }
 
-template <class Ev>
+// W = kProjGroup (4) everywhere but the point modules' second entry (W = 2), which the host picks
+// for large meshes: there the pass is throughput-bound (tens of thousands of waves) and 2 lanes
+// evaluate fewer alphas past the hit and fewer tree nodes per bisection level (config 4s at 512^3:
+// 184 -> 162 us per call), where on a 180 k-face mesh the longer chains of 2 lanes cost more (69 ->
+// 75 us, profiles/r05zy_*)
+template <int W = kProjGroup, class Ev>
 __device__ __forceinline__ void project_early_body(const Ev& ev, const ProjArgs& a) {
-    const Grp g;
+    const GrpW<W> g;
     const int64_t j1 = a.rng[1];
-    for (int64_t j = a.rng[0] + grid_lane() / kProjGroup; j < j1; j += grid_lanes() / kProjGroup)   // uniform per group
-        project_early_face(ev, a, g, j);
+    for (int64_t j = a.rng[0] + grid_lane() / W; j < j1; j += grid_lanes() / W)   // uniform per group
+        project_early_face<W>(ev, a, g, j);
 }
 
 // The early pass as one loop with one tree evaluation per iteration.  project_early_face runs the
@@ -545,7 +554,7 @@ __device__ __forceinline__ void project_late_face(const Ev& ev, const ProjArgs& 
 // wave (its five searches in one round, 6 bisection levels per round), a chunk where every face pends
 // (as when the average edge length is not finite) 4 lanes per face.  (Chunks of 64 faces, up to 4
 // rounds of 16 faces per wave: a quarter of the waves, 31 -> 55 us on config 2.)
-constexpr int kLateChunk = 64 / kProjGroup;
+constexpr int kLateChunk = 16;   // faces per wave chunk (the late grid: 4 lanes per face)
 
 template <class Ev>
 __device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& a) {
