@@ -1058,8 +1058,8 @@ std::string TreeJit::point_source(const Program& p, bool bake) {
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
       << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_normals_at(const float* M, const float* tab,\n"
-      << "    const float* P, const int64_t* rng, float* G) {\n"
-      << "    impli::ob::normals_at_body(JitPt{M, tab}, P, rng, G);\n}\n"
+      << "    const float* P, const int64_t* rng, float* G, const uint32_t* pend, int mode) {\n"
+      << "    impli::ob::normals_at_body(JitPt{M, tab}, P, rng, G, pend, mode);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_points(const float* M, const float* tab,\n"
       << "    const float* xyz, int64_t n, float* f, float* grad) {\n"
       << "    impli::ob::points_body(JitPt{M, tab}, xyz, n, f, grad);\n}\n";

@@ -468,8 +468,8 @@ __global__ __launch_bounds__(256) void k_project_late(const Program* __restrict_
 template <int D>
 __global__ __launch_bounds__(256) void k_normals_at(const Program* __restrict__ prog, const float* __restrict__ tab,
                                                     const float* __restrict__ P, const int64_t* __restrict__ rng,
-                                                    float* __restrict__ G) {
-    normals_at_body(InterpPt<D>{prog, tab}, P, rng, G);
+                                                    float* __restrict__ G, const uint32_t* __restrict__ pend, int mode) {
+    normals_at_body(InterpPt<D>{prog, tab}, P, rng, G, pend, mode);
 }
 
 // ---- step 1 ----------------------------------------------------------------------------------
@@ -2080,6 +2080,8 @@ const std::map<std::string, std::vector<float>>& Ob02::pointsets() {
 Ob02::~Ob02() {
     if (pert_job_.valid()) pert_job_.wait();
     if (prep_done_) (void)hipEventDestroy(prep_done_);
+    if (early_done_) (void)hipEventDestroy(early_done_);
+    if (normals_done_) (void)hipEventDestroy(normals_done_);
     if (mesh_ready_) (void)hipEventDestroy(mesh_ready_);
     if (side_s_) (void)hipStreamDestroy(side_s_);
     dir_.release();
@@ -2349,6 +2351,23 @@ void Ob02::centroids_projection(bool enable_qem) {
     // centroids left unresolved need the randomised directions (types 2-6): the late pass covers
     // every face and reads the early pass's per-face flags on the device (no host round trip)
     a.pert = perturbations();
+    // the QEM normals of the faces the early pass resolved run on the side stream beside the late
+    // pass (latency-bound: a few pending faces with long chains leave the chip idle), the pending
+    // faces' after it (not while profiling: its stages are drained one by one)
+    const bool split_normals = enable_qem && nw > 0 && !profile_;
+    if (enable_qem) grad_.reserve((size_t)(nf + 1) * 12);
+    auto launch_normals = [&](hipStream_t q, int mode) {
+        const float* P = proj_.as<float>();
+        float* G = grad_.as<float>();
+        const int64_t* rw = a.rng;
+        const uint32_t* pd = pend_.as<uint32_t>();
+        if (pk) {
+            void* nargs[] = {&jm, &jtab, &P, &rw, &G, &pd, &mode};
+            TreeJit::launch(pk->normals, blocks_for(nw), nargs, q, "impli_pt_normals_at");
+        } else {
+            DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nw), 256, q, E.d_program(), E.d_rabbit(), P, rw, G, pd, mode);
+        }
+    };
     if (nw > 0) {
         // the point module's single-loop early pass: a wave per chunk of early_chunk faces
         const unsigned egrid = early_single_loop() ? blocks_for((nw + a.early_chunk - 1) / a.early_chunk * 64)
@@ -2357,6 +2376,14 @@ void Ob02::centroids_projection(bool enable_qem) {
         if (pk && early2) TreeJit::launch(pk->early2, egrid, jargs, s, "impli_pt_project_early2");
         else if (pk) TreeJit::launch(pk->early, egrid, jargs, s, "impli_pt_project_early");
         else DEPTH_LAUNCH(E.depth(), k_project_early, grid, 256, s, E.d_program(), E.d_rabbit(), a);
+        if (split_normals) {
+            if (!early_done_) IMPLI_HIP(hipEventCreateWithFlags(&early_done_, hipEventDisableTiming));
+            if (!normals_done_) IMPLI_HIP(hipEventCreateWithFlags(&normals_done_, hipEventDisableTiming));
+            IMPLI_HIP(hipEventRecord(early_done_, s));
+            IMPLI_HIP(hipStreamWaitEvent(side_s_, early_done_, 0));
+            launch_normals(side_s_, 1);
+            IMPLI_HIP(hipEventRecord(normals_done_, side_s_));
+        }
         if (pk) TreeJit::launch(pk->late, late_grid, jargs, s, "impli_pt_project_late");
         else DEPTH_LAUNCH(E.depth(), k_project_late, late_grid, 256, s, E.d_program(), E.d_rabbit(), a);
     }
@@ -2393,17 +2420,11 @@ void Ob02::centroids_projection(bool enable_qem) {
     store_pointset("pre_qem_verts", verts_.as<float>(), nv, false);
     if (enable_qem) {
         st.next(kStageQem);
-        grad_.reserve((size_t)(nf + 1) * 12);
-        if (nw <= 0) {
-        } else if (pk) {
-            const float* P = proj_.as<float>();
-            float* G = grad_.as<float>();
-            const int64_t* rw = a.rng;
-            void* nargs[] = {&jm, &jtab, &P, &rw, &G};
-            TreeJit::launch(pk->normals, blocks_for(nw), nargs, s, "impli_pt_normals_at");
-        } else {
-            DEPTH_LAUNCH(E.depth(), k_normals_at, blocks_for(nw), 256, s, E.d_program(), E.d_rabbit(), proj_.as<float>(),
-                         a.rng, grad_.as<float>());
+        if (split_normals) {
+            launch_normals(s, 2);   // the faces the late pass resolved
+            IMPLI_HIP(hipStreamWaitEvent(s, normals_done_, 0));
+        } else if (nw > 0) {
+            launch_normals(s, 0);
         }
         // QEM of the owned vertices (all unless sharded), in place
         const int64_t nov = own_v1_ - own_v0_;

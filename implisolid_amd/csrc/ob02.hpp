@@ -143,6 +143,7 @@ private:
     DevBuf fold_out_;                        // FoldOut (ob02_device.hpp): sum, average, alpha list
     hipStream_t side_s_ = nullptr;           // the projection's prep pass, beside the fold's walk on s
     hipEvent_t mesh_ready_ = nullptr, prep_done_ = nullptr;
+    hipEvent_t early_done_ = nullptr, normals_done_ = nullptr;   // the QEM normals beside the late pass
     DevBuf dir_, evals_buf_;
     std::future<std::shared_ptr<const std::vector<float>>> pert_job_;
     std::shared_ptr<PertDev> pert_dev_;   // the device table in use (process-wide cache, ob02.hip)

@@ -584,12 +584,16 @@ __device__ __forceinline__ void project_late_body(const Ev& ev, const ProjArgs& 
 }
 
 // normalize_1111(grad) at arbitrary points (the QEM normals at the projected centroids, qem.hpp:256-316)
-// over the faces [rng[0], rng[1]) (P, G absolute)
+// over the faces [rng[0], rng[1]) (P, G absolute).  pend (the early pass's flags) splits the pass:
+// mode 1 the faces the early pass resolved (run beside the late pass), mode 2 the others (after it),
+// mode 0 every face
 template <class Ev>
 __device__ __forceinline__ void normals_at_body(const Ev& ev, const float* __restrict__ P, const int64_t* __restrict__ rng,
-                                                float* __restrict__ G) {
+                                                float* __restrict__ G, const uint32_t* __restrict__ pend = nullptr,
+                                                int mode = 0) {
     const int64_t j1 = rng[1];
     for (int64_t j = rng[0] + grid_lane(); j < j1; j += grid_lanes()) {
+        if (mode != 0 && (pend[j] != 0u) != (mode == 2)) continue;
         V3 g;
         (void)ev.fg(P[3 * j], P[3 * j + 1], P[3 * j + 2], g);
         const float nm = norm2f(g.x, g.y, g.z);
