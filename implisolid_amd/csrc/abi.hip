@@ -228,6 +228,10 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
     E.set_object(prog);
     int64_t nv = 0, nf = 0;
     std::unique_ptr<Ob02>& ob_ptr = g_ob02;   // one refinement state, its buffers reused by every build
+    // the MC faces' early copy to the host (below); a build that ended in an error left it to finish
+    static hipEvent_t faces_copied = nullptr;
+    bool faces_early = false;
+    if (faces_copied) (void)hipEventSynchronize(faces_copied);
     if (!g_devices.empty()) {
         // polygonize_step_0 over several devices: balanced Z-slabs, concatenated on the host
         multi_device_mc(prog, st, g_state.verts, g_state.faces);
@@ -275,6 +279,22 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         roctxRangePop();
         nv = c.n_verts();
         nf = c.n_faces();
+        // without subdivision the loop never changes the faces: the MC faces go to the host on the
+        // copy stream while the loop runs (8.6 MB at 512^3, ~0.17 ms of PCIe), only the vertices at
+        // the end.  (A progress callback reads intermediate meshes through the same buffers: then
+        // everything is fetched as before.)
+        faces_early = !st.subdiv && !g_progress && nf > 0 && !g_ob02_profile;
+        if (faces_early) {
+            static hipEvent_t mc_done = nullptr;
+            if (!mc_done) IMPLI_HIP(hipEventCreateWithFlags(&mc_done, hipEventDisableTiming));
+            if (!faces_copied) IMPLI_HIP(hipEventCreateWithFlags(&faces_copied, hipEventDisableTiming));
+            g_state.faces.resize((size_t)nf * 3);   // before the copy: the buffer does not move under it
+            IMPLI_HIP(hipEventRecord(mc_done, s));
+            IMPLI_HIP(hipStreamWaitEvent(abi_copy_stream(), mc_done, 0));
+            IMPLI_HIP(hipMemcpyAsync(g_state.faces.data(), E.d_faces(), (size_t)nf * 12, hipMemcpyDeviceToHost,
+                                     abi_copy_stream()));
+            IMPLI_HIP(hipEventRecord(faces_copied, abi_copy_stream()));
+        }
         if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
         ob_ptr->set_profile(g_ob02_profile);
         ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf);
@@ -302,8 +322,14 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
     nv = ob.n_verts();
     nf = ob.n_faces();
     g_state.verts.resize((size_t)nv * 3);
-    g_state.faces.resize((size_t)nf * 3);
-    ob.fetch(g_state.verts.data(), g_state.faces.data());
+    if (faces_early && (int64_t)g_state.faces.size() == 3 * nf) {
+        ob.fetch(g_state.verts.data(), nullptr);
+        IMPLI_HIP(hipEventSynchronize(faces_copied));
+    } else {
+        if (faces_early) IMPLI_HIP(hipEventSynchronize(faces_copied));   // (never: the faces did not change)
+        g_state.faces.resize((size_t)nf * 3);
+        ob.fetch(g_state.verts.data(), g_state.faces.data());
+    }
     ob.capture_replace = true;
     g_pointsets_dirty = true;              // copied to the host when asked for
     g_state.active = true;                 // polygonize_terminate, ob02:163-176

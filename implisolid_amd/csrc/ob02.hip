@@ -2574,7 +2574,7 @@ void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cp
 void Ob02::fetch(float* verts, int32_t* faces) {
     Stage st(this, kStageFetch);
     if (nv) IMPLI_HIP(hipMemcpyAsync(verts, verts_.p, (size_t)nv * 12, hipMemcpyDeviceToHost, s));
-    if (nf) IMPLI_HIP(hipMemcpyAsync(faces, faces_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
+    if (nf && faces) IMPLI_HIP(hipMemcpyAsync(faces, faces_.p, (size_t)nf * 12, hipMemcpyDeviceToHost, s));
     IMPLI_HIP(hipStreamSynchronize(s));
 }
 
