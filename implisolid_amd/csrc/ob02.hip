@@ -1110,13 +1110,22 @@ __device__ __forceinline__ void fold_runs_tile(const FoldPair* __restrict__ pair
         pv[j] = pairs[(int64_t)c * kFoldBinades + kRunBinade];
         fv[j] = flags[(int64_t)c * kFoldBinades + kRunBinade];
     }
+    // the lane's chunks and the one after them: loaded unconditionally (a clamped index), so the
+    // compiler issues the ten loads together instead of one round trip per short-circuited load
+    uint32_t hv[5];
+    int32_t bv[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {   // the lane's chunks and the one after them
+    for (int j = 0; j < 5; ++j) {
         const int c = c0 + j;
         in[j] = c < nc && (j < 4 || lane > 0);
         const int cq = in[j] ? c : 0;
-        hin[j] = in[j] && hint[cq] != 0;
-        bs[j] = in[j] ? base[cq] : 0;
+        hv[j] = hint[cq];
+        bv[j] = base[cq];
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {   // bitwise, no short circuit
+        hin[j] = in[j] & (hv[j] != 0u);
+        bs[j] = bv[j] & -(int32_t)in[j];
     }
     bool bnd[4];   // a run ends after chunk j
 #pragma unroll
@@ -1376,7 +1385,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     const bool inb = c < nc && c < c0 + wn && bb >= 0 && bb < kFoldBinades;
                     const int64_t cell = (int64_t)cq * kFoldBinades + (inb ? bb : 0);
                     tp[j] = pairs[cell];
-                    ok[j] = inb && flags[cell] == 0;
+                    ok[j] = inb & (flags[cell] == 0);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
