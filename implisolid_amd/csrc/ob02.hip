@@ -1335,9 +1335,11 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 continue;
             }
             int E = 0;
-            (void)frexpf(s, &E);   // s in [2^(E-1), 2^E): spacing 2^(E-24)
-            E = __builtin_amdgcn_readfirstlane(E);
-            uint32_t su = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E));   // in [2^23, 2^24)
+            // s in [2^(E-1), 2^E), spacing 2^(E-24), and su = s / 2^(E-24) in [2^23, 2^24): from the
+            // bits (s is normal here), scalar
+            const uint32_t sb = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s));
+            E = (int)((sb >> 23) & 0xffu) - 126;
+            uint32_t su = (sb & 0x7fffffu) | 0x800000u;
             const long long tA = walk_clock<kCycles>();
             int ic = k / kFoldChunk - c0;
             bool failed = false;   // a run map that did not hold: the table scan below re-enters it
@@ -1345,7 +1347,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                 // runs, one lookup each, while their maps keep the value in this binade (E and the
                 // integer su carry the exact value; s is formed once at the end)
                 for (;;) {
-                    const uint4 r0 = w_rec[ic];   // FoldRun: base, len | flags << 16, run map
+                    uint4 r0 = w_rec[ic];   // FoldRun: base, len | flags << 16, run map
+                    // the whole record in one LDS read: without this the compiler reads len first
+                    // and the rest behind the len test, two round trips per lookup
+                    asm volatile("" : "+v"(r0.x), "+v"(r0.y), "+v"(r0.z), "+v"(r0.w));
+                    r0.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0.x);   // uniform: scalar branches
+                    r0.y = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0.y);
+                    r0.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0.z);
+                    r0.w = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0.w);
                     const int len = (int)(r0.y & 0xffffu);
                     if (len == 0) break;   // a hinted chunk: its terms
                     if constexpr (kCycles) ++st_lookup;
@@ -1361,7 +1370,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
                     ic += len;
                     if (k >= kend_w) break;
                 }
-                s = ldexpf((float)su, E - 24);
+                s = __uint_as_float(((uint32_t)(E + 126) << 23) | (su & 0x7fffffu));   // su in [2^23, 2^24)
                 if (k >= kend_w) {
                     if (k > n) k = n;
                     if constexpr (kCycles) cyc_lookup += walk_clock<kCycles>() - tA;
@@ -1481,9 +1490,9 @@ __global__ __launch_bounds__(kWalkThreads) void k_fold_walk(const float* __restr
             }
             for (; !done && k < kend;) {   // segments of the chunk, each ending at an event
                 if (!(s >= 0x1p-100f && s <= 0x1p100f)) break;   // the outer loop's term-by-term paths
-                (void)frexpf(s, &E);
-                E = __builtin_amdgcn_readfirstlane(E);
-                su = (uint32_t)__builtin_amdgcn_readfirstlane((int)ldexpf(s, 24 - E));
+                const uint32_t sb = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s));
+                E = (int)((sb >> 23) & 0xffu) - 126;   // as above
+                su = (sb & 0x7fffffu) | 0x800000u;
                 FoldPair tp[4], p{0u, 0u};
                 bool bad[4];
 #pragma unroll
