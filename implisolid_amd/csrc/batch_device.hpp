@@ -16,11 +16,16 @@ __device__ __forceinline__ uint32_t batch_prefix(const ObjArgs* __restrict__ obj
                                                  uint32_t cap, uint32_t* s_pre, uint32_t align = 1u) {
     __shared__ uint32_t s_part[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;   // 256 threads, up to 4 objects each
-    uint32_t v[4], sum = 0;
+    uint32_t v[4], c[4] = {0u, 0u, 0u, 0u}, sum = 0;
+    if (n > 0) {   // uniform; the four loads unconditional (a clamped index), so they issue together
+                   // instead of one round trip per guarded load
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = objs[4 * t + k < n ? 4 * t + k : n - 1].counters[word];
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int o = 4 * t + k;
-        v[k] = o < n ? (min(objs[o].counters[word], cap) * mult + align - 1u) / align * align : 0u;
+        v[k] = o < n ? (min(c[k], cap) * mult + align - 1u) / align * align : 0u;
         sum += v[k];
     }
     uint32_t inc = sum;
