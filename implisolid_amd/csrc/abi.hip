@@ -679,7 +679,8 @@ int get_pointset_size(char* id) {
 }
 
 void about(void) {
-    std::fprintf(stderr, "Build Info: \n%s %s\n", __DATE__, __TIME__);
+    // no __DATE__ / __TIME__: the library is built reproducibly (the round's profiles name its hash)
+    std::fprintf(stderr, "Build Info: \nreproducible build\n");
     std::fprintf(stderr, "implisolid-mi355x: HIP gfx950 polygoniser (eval + marching cubes + OB02)\n");
     std::fprintf(stderr, "CONFIG: ROOT_TOLERANCE=%g \n", (double)(float)(0.001 / 10.0));
 }
