@@ -39,7 +39,7 @@ ABI_SYMBOLS = [
     "implisolid_slab_copy_mesh", "implisolid_set_jit_bake", "implisolid_jit_wait", "implisolid_jit_stats",
     "implisolid_set_jit_max_modules", "implisolid_jit_modules",
     "implisolid_set_progress_callback", "implisolid_ob02_profile", "implisolid_last_build_stats",
-    "implisolid_jit_compile_points", "implisolid_debug_libm", "implisolid_slab_stats_n",
+    "implisolid_jit_compile_points", "implisolid_debug_libm", "implisolid_debug_cos", "implisolid_slab_stats_n",
     "implisolid_slab_kernel_times_each", "implisolid_debug_fold",
     "implisolid_ob02_create", "implisolid_ob02_destroy", "implisolid_ob02_load", "implisolid_ob02_resample",
     "implisolid_ob02_project", "implisolid_ob02_subdivide", "implisolid_ob02_counts", "implisolid_ob02_ranges",
@@ -93,6 +93,7 @@ def lib():
         "implisolid_last_error": ([], c_char_p), "implisolid_set_error_mode": ([c_int], None),
         "implisolid_eval_points": ([fp, ctypes.c_int64, fp, fp], c_int),
         "implisolid_debug_libm": ([c_int, fp, fp, ctypes.c_int64, fp], c_int),
+        "implisolid_debug_cos": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.POINTER(ctypes.c_double)], c_int),
         "implisolid_debug_fold": ([fp, ctypes.c_int64, fp, ctypes.POINTER(ctypes.c_int64)], c_int),
         "implisolid_ob02_create": ([c_char_p, c_char_p], c_void_p),
         "implisolid_ob02_destroy": ([c_void_p], None),
@@ -494,6 +495,17 @@ def debug_libm(which, a, b=None):
     fp = ctypes.POINTER(ctypes.c_float)
     rc = lib().implisolid_debug_libm(int(which), a.ctypes.data_as(fp), bb.ctypes.data_as(fp) if bb is not None else None,
                                      a.size, out.ctypes.data_as(fp))
+    if rc != 0:
+        raise ImplisolidError(last_error())
+    return out
+
+
+def debug_cos(a):
+    """Diagnostics: the device restatement of glibc's double cos (the screw gradient's) on a float64 array."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    out = np.empty_like(a)
+    dp = ctypes.POINTER(ctypes.c_double)
+    rc = lib().implisolid_debug_cos(a.ctypes.data_as(dp), a.size, out.ctypes.data_as(dp))
     if rc != 0:
         raise ImplisolidError(last_error())
     return out

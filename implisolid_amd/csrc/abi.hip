@@ -617,6 +617,31 @@ int implisolid_debug_libm(int which, const float* a, const float* b, int64_t n, 
     return 0;
 }
 
+int implisolid_debug_cos(const double* a, int64_t n, double* out) {
+    if (n < 0 || (n && (!a || !out))) {
+        report("implisolid_debug_cos: bad arguments", false);
+        return -1;
+    }
+    if (n == 0) return 0;
+    try {
+        Engine& E = engine();
+        hipStream_t s = abi_stream();
+        DevBuf& da = E.scratch(0);
+        DevBuf& dout = E.scratch(2);
+        da.reserve((size_t)n * 8);
+        dout.reserve((size_t)n * 8);
+        IMPLI_HIP(hipMemcpyAsync(da.p, a, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        launch_cos_probe(da.as<double>(), n, dout.as<double>(), s);
+        IMPLI_HIP(hipGetLastError());
+        IMPLI_HIP(hipMemcpyAsync(out, dout.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+        IMPLI_HIP(hipStreamSynchronize(s));
+    } catch (const std::exception& e) {
+        report(e.what(), false);
+        return -1;
+    }
+    return 0;
+}
+
 void calculate_implicit_values(void) {
     if (!g_eval.has_x || !g_eval.has_object) {
         report("Error: You need to set_x() and set_object() first.", false);

@@ -742,4 +742,15 @@ void launch_libm_probe(int which, const float* d_a, const float* d_b, int64_t n,
     k_libm_probe<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(which, d_a, d_b, n, d_out);
 }
 
+// diagnostics: the restated glibc double cos (the screw gradient's) on n arguments
+__global__ __launch_bounds__(256) void k_cos_probe(const double* __restrict__ a, int64_t n, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = dev::glibc_cos(a[i]);
+}
+
+void launch_cos_probe(const double* d_a, int64_t n, double* d_out, hipStream_t s) {
+    if (n <= 0) return;
+    k_cos_probe<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(d_a, n, d_out);
+}
+
 }  // namespace impli

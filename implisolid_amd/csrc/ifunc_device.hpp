@@ -16,6 +16,7 @@
 #endif
 
 #include "generated/tables.h"
+#include "generated/sincostab.h"
 #include "program.hpp"
 
 namespace impli {
@@ -368,6 +369,71 @@ __device__ __forceinline__ float glibc_atan2f(float y, float x) {
     return res;
 }
 
+// ---- glibc 2.35 double cos (sysdeps/ieee754/dbl-64/s_sin.c __cos), the x86_64 FMA variant
+// (s_sin-fma.c, selected on every FMA- and AVX2-capable host), with the contractions that libm's
+// __cos_fma holds: the screw gradient's cos(M_PI * (...)) (screw.hpp:178-180).  oracle/or_libm.c
+// or_cos is the same restatement, checked against the host cos (0 mismatches over 2 G seeded
+// arguments); the GPU test compares this one with it.  __sincostab (i/128: sin hi, lo, cos hi, lo)
+// from the host libm (tools/extract_sincostab.py), in constant memory.  |x| >= 105414350 (glibc's
+// __branred) is not restated: the device libm's cos.
+static __constant__ uint64_t kSinCosTab[440] = {IMPLI_SINCOSTAB_BITS};
+__device__ __forceinline__ double sct(int i) { return __longlong_as_double((long long)kSinCosTab[i]); }
+__device__ __forceinline__ double bits2d(uint64_t u) { return __longlong_as_double((long long)u); }
+// do_cos / do_sin of (x, dx) (TAYLOR_SIN for do_sin of |x| < 0.126)
+__device__ __forceinline__ double glibc_sincos_red(bool is_cos, double x, double dx) {
+    const double xx0 = x * x;
+    if (!is_cos && fabs(x) < 0.126) {
+        const double p = __fma_rn(xx0, __fma_rn(xx0, __fma_rn(xx0, __fma_rn(xx0, bits2d(0xbe5addffc2fcdf59ull),
+                                  bits2d(0x3ec71de27b9a7ed9ull)), bits2d(0xbf2a01a019db08b8ull)),
+                                  bits2d(0x3f81111111110eceull)), bits2d(0xbfc5555555555555ull));
+        return x + __fma_rn(xx0, __fma_rn(p, x, -(dx * 0.5)), dx);
+    }
+    if (is_cos ? x < 0 : x <= 0) dx = -dx;
+    const double big = 0x1.8p45, ax = fabs(x), u = ax + big;
+    const int k = (int)((uint32_t)__double_as_longlong(u) << 2);
+    const double xr = is_cos ? (ax - (u - big)) + dx : ax - (u - big), xx = xr * xr;
+    const double ps = __fma_rn(xx, bits2d(0x3f811110e829872full), bits2d(0xbfc5555555555515ull));
+    const double pc = xx * __fma_rn(xx, __fma_rn(xx, bits2d(0x3f56c16bedd9e239ull), bits2d(0xbfa5555555555535ull)), 0.5);
+    const double sn = sct(k), ssn = sct(k + 1), cs = sct(k + 2), ccs = sct(k + 3);
+    if (is_cos) {
+        const double s = __fma_rn(xr * xx, ps, xr);
+        double cor = __fma_rn(-s, ssn, ccs);
+        cor = __fma_rn(-pc, cs, cor);
+        cor = __fma_rn(-s, sn, cor);
+        return cs + cor;
+    }
+    const double s = xr + __fma_rn(xr * xx, ps, dx);
+    const double c = __fma_rn(xr, dx, pc);
+    double cor = __fma_rn(s, ccs, ssn);
+    cor = __fma_rn(-c, sn, cor);
+    cor = __fma_rn(s, cs, cor);
+    return copysign(sn + cor, x);
+}
+__device__ __forceinline__ double glibc_cos(double x) {
+    const uint32_t k = (uint32_t)((uint64_t)__double_as_longlong(x) >> 32) & 0x7fffffffu;
+    if (k < 0x3e400000u) return 1.0;                                   // |x| < 2^-27
+    if (k < 0x3feb6000u) return glibc_sincos_red(true, x, 0.0);        // |x| < 0.855469
+    if (k < 0x400368fdu) {                                             // |x| < 2.426265
+        const double y = bits2d(0x3ff921fb54442d18ull) - fabs(x);
+        const double a = y + bits2d(0x3c91a62633145c07ull);
+        return glibc_sincos_red(false, a, (y - a) + bits2d(0x3c91a62633145c07ull));
+    }
+    if (k < 0x419921fbu) {                                             // reduce_sincos
+        const double t = __fma_rn(x, bits2d(0x3fe45f306dc9c883ull), 0x1.8p52);
+        const double xn = t - 0x1.8p52;
+        const int n = (int)((uint64_t)__double_as_longlong(t) & 3u) + 1;
+        const double y = __fma_rn(-xn, bits2d(0xbe4dde973c000000ull), __fma_rn(-xn, bits2d(0x3ff921fb58000000ull), x));
+        const double pp3 = bits2d(0xbc8cb3b398000000ull), pp4 = bits2d(0xbacd747f23e32ed7ull);
+        const double t2 = __fma_rn(-xn, pp3, y);
+        const double b = __fma_rn(-xn, pp4, t2);
+        const double db = __fma_rn(-pp3, xn, y - t2) + __fma_rn(-xn, pp4, t2 - b);
+        const double r = glibc_sincos_red((n & 1) != 0, b, db);
+        return (n & 2) ? -r : r;
+    }
+    if (k < 0x7ff00000u) return cos(x);                                // __branred: not restated
+    return x / x;
+}
+
 // ---- screw, screw.hpp:98-150 at its constructor's constants (u, v, w = the axes, A = (0,0,-0.5),
 //      UVW = I; the factory forces the identity transformation_matrix, object_factory.hpp:304-351).
 //      prm = {twist_rate, r0, delta}.  Eigen orders: GEMV t = (x - A) w into a zeroed result; outer
@@ -415,7 +481,7 @@ __device__ __forceinline__ void screw_f2(const float* __restrict__ prm, float xa
 }
 // screw.hpp:152-160 (sympy gradient) at the same constants, with the C++ type of every
 // sub-expression: std::pow(float, 2) -> exact double square, atan2(float, float) -> atanf path,
-// cos(double) -> double cos (device libm; the only call not restated bit for bit), M_PI double.
+// cos(double) -> glibc's double cos (glibc_cos above), M_PI double.
 __device__ __forceinline__ V3 screw_g(const float* __restrict__ prm, float x, float y, float z) {
     const double kPi = 3.14159265358979323846;
     const float tw = prm[0], delta = prm[2];
@@ -429,7 +495,7 @@ __device__ __forceinline__ V3 screw_g(const float* __restrict__ prm, float x, fl
     const double G = sq_exact(U0) + sq_exact(U1);
     const double sq = sqrt((sq_exact(X1) + sq_exact(Y1)) + sq_exact(Z1));
     const float th = glibc_atan2f(U1, U0);
-    const double cv = cos(kPi * (((double)(2 * phi0) - (double)th / kPi) + (double)((2 * s) / tw)));
+    const double cv = glibc_cos(kPi * (((double)(2 * phi0) - (double)th / kPi) + (double)((2 * s) / tw)));
     const double wx2 = sq_exact(wx), wy2 = sq_exact(wy), wz2 = sq_exact(wz);
     const double pd = kPi * (double)delta;
     const double cAx = ((double)u00 * (-wx2 + 1) - (double)(u01 * wx * wy)) - (double)(u02 * wx * wz);

@@ -47,6 +47,7 @@ void launch_eval_points(const Program* d_prog, int depth, const float* d_rabbit,
                         float* d_f, float* d_grad /* nullable: values only */, hipStream_t s);
 // diagnostics: glibc sinf (0) / atanf (1) / atan2f (2) restatements on device operands
 void launch_libm_probe(int which, const float* d_a, const float* d_b, int64_t n, float* d_out, hipStream_t s);
+void launch_cos_probe(const double* d_a, int64_t n, double* d_out, hipStream_t s);
 
 // K2 (count per group) and K2b (group bases + flat list of non-empty units)
 void launch_mc_count(const CaseInfo* d_cases, const GridDesc& g, const MCBuffers& b, hipStream_t s);

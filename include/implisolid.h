@@ -144,6 +144,9 @@ int implisolid_eval_points(const float* xyz, int64_t n, float* f_out, float* gra
    atanf (1) and atan2f (2: out = atan2f(a, b)) that the screw family calls (screw.hpp:20-36,
    std::sin / std::atan2 on floats), on n host operands; 0 or -1 with implisolid_last_error() */
 int implisolid_debug_libm(int which, const float* a, const float* b, int64_t n, float* out);
+/* Additive, diagnostics: the device restatement of glibc 2.35's double cos (x86_64 FMA variant) that
+   the screw gradient calls (screw.hpp:178-180, cos(M_PI * (...))), on n host doubles; 0 or -1 */
+int implisolid_debug_cos(const double* a, int64_t n, double* out);
 /* Additive, diagnostics: the edge-length fold of the projection (compute_average_edge_length,
    centroids_projection.cpp:70-82: s = 0; s += e[k] in order, float) on n host terms, computed as
    build_geometry computes it -- the chunk table and the device walk; *sum_out = s, *table_chunks

@@ -87,6 +87,13 @@ def lib():
         L.or_libm_check.restype = ctypes.c_int64
         L.or_libm_apply.argtypes = [ctypes.c_int, fp, fp, ctypes.c_int64, fp]
         L.or_libm_apply.restype = None
+        L.or_cos.argtypes = [ctypes.c_double]
+        L.or_cos.restype = ctypes.c_double
+        L.or_cos_check.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double]
+        L.or_cos_check.restype = ctypes.c_int64
+        L.or_cos_apply.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.c_int]
+        L.or_cos_apply.restype = None
         L.or_marching_cubes.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, ctypes.POINTER(OrMesh)]
         L.or_mesh_free.argtypes = [ctypes.POINTER(OrMesh)]
         L.or_mc_field.argtypes = [npp, ctypes.c_int, ctypes.c_int, fp, fp]
@@ -450,6 +457,21 @@ def libm_apply(which, a, b=None):
     out = np.empty_like(a)
     fpp = ctypes.POINTER(ctypes.c_float)
     lib().or_libm_apply(int(which), a.ctypes.data_as(fpp), b.ctypes.data_as(fpp), a.size, out.ctypes.data_as(fpp))
+    return out
+
+
+def cos_check(seed, count, lim=64.0):
+    """Mismatches of the restated glibc double cos (x86_64 FMA variant) against this host's cos over
+    `count` seeded arguments (or_libm.c or_cos_check)."""
+    return int(lib().or_cos_check(int(seed), int(count), float(lim)))
+
+
+def cos_apply(a, glibc=False):
+    """The restated glibc double cos (glibc=False) or the host's own cos (True) on a float64 array."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    out = np.empty_like(a)
+    dpp = ctypes.POINTER(ctypes.c_double)
+    lib().or_cos_apply(a.ctypes.data_as(dpp), a.size, out.ctypes.data_as(dpp), int(bool(glibc)))
     return out
 
 

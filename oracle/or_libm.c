@@ -171,6 +171,107 @@ float or_atan2f(float y, float x) {
     }
 }
 
+/* ---- cos (double) ----
+   sysdeps/ieee754/dbl-64/s_sin.c __cos, the x86_64 FMA variant (s_sin-fma.c, selected on every
+   FMA- and AVX2-capable host): the branches and contractions as this image's libm compiles them
+   (read from its __cos_fma).  screw.hpp:178-180 cos(M_PI * (...)): the screw gradient.  The
+   __branred branch (|x| >= 105414350) is not restated: it calls the host cos. */
+#include "../implisolid_amd/csrc/generated/sincostab.h"
+static const uint64_t SINCOSTAB[440] = {IMPLI_SINCOSTAB_BITS};
+static inline double bitsd(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+static inline uint64_t dbits(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+#define CS_BIG 0x1.8p45
+#define CS_T(i) bitsd(SINCOSTAB[(i)])
+
+static double cs_taylor_sin(double a, double da) {   /* TAYLOR_SIN (s_sin.c) */
+    const double xx = a * a;
+    const double p = fma(xx, fma(xx, fma(xx, fma(xx, bitsd(0xbe5addffc2fcdf59ull), bitsd(0x3ec71de27b9a7ed9ull)),
+                                         bitsd(0xbf2a01a019db08b8ull)), bitsd(0x3f81111111110eceull)),
+                         bitsd(0xbfc5555555555555ull));
+    const double t = fma(xx, fma(p, a, -(da * 0.5)), da);
+    return a + t;
+}
+static double cs_do_cos(double x, double dx) {       /* do_cos */
+    if (x < 0) dx = -dx;
+    const double ax = fabs(x), u = ax + CS_BIG;
+    const int k = (int)((uint32_t)dbits(u) << 2);
+    const double xr = (ax - (u - CS_BIG)) + dx, xx = xr * xr;
+    const double s = fma(xr * xx, fma(xx, bitsd(0x3f811110e829872full), bitsd(0xbfc5555555555515ull)), xr);
+    const double c = xx * fma(xx, fma(xx, bitsd(0x3f56c16bedd9e239ull), bitsd(0xbfa5555555555535ull)), 0.5);
+    double cor = fma(-s, CS_T(k + 1), CS_T(k + 3));
+    cor = fma(-c, CS_T(k + 2), cor);
+    cor = fma(-s, CS_T(k), cor);
+    return CS_T(k + 2) + cor;
+}
+static double cs_do_sin(double x, double dx) {       /* do_sin */
+    if (fabs(x) < 0.126) return cs_taylor_sin(x, dx);
+    if (x <= 0) dx = -dx;
+    const double ax = fabs(x), u = ax + CS_BIG;
+    const int k = (int)((uint32_t)dbits(u) << 2);
+    const double xr = ax - (u - CS_BIG), xx = xr * xr;
+    const double s = xr + fma(xr * xx, fma(xx, bitsd(0x3f811110e829872full), bitsd(0xbfc5555555555515ull)), dx);
+    const double c = fma(xr, dx, xx * fma(xx, fma(xx, bitsd(0x3f56c16bedd9e239ull), bitsd(0xbfa5555555555535ull)), 0.5));
+    double cor = fma(s, CS_T(k + 3), CS_T(k + 1));
+    cor = fma(-c, CS_T(k), cor);
+    cor = fma(s, CS_T(k + 2), cor);
+    return copysign(CS_T(k) + cor, x);
+}
+double or_cos(double x) {
+    const uint32_t k = (uint32_t)(dbits(x) >> 32) & 0x7fffffffu;
+    if (k < 0x3e400000u) return 1.0;                           /* |x| < 2^-27 */
+    if (k < 0x3feb6000u) return cs_do_cos(x, 0.0);             /* |x| < 0.855469 */
+    if (k < 0x400368fdu) {                                     /* |x| < 2.426265 */
+        const double y = bitsd(0x3ff921fb54442d18ull) - fabs(x);
+        const double a = y + bitsd(0x3c91a62633145c07ull);
+        const double da = (y - a) + bitsd(0x3c91a62633145c07ull);
+        return cs_do_sin(a, da);
+    }
+    if (k < 0x419921fbu) {                                     /* |x| < 105414350: reduce_sincos */
+        const double t = fma(x, bitsd(0x3fe45f306dc9c883ull), 0x1.8p52);
+        const double xn = t - 0x1.8p52;
+        const int n = (int)(dbits(t) & 3u);
+        const double y = fma(-xn, bitsd(0xbe4dde973c000000ull), fma(-xn, bitsd(0x3ff921fb58000000ull), x));
+        const double pp3 = bitsd(0xbc8cb3b398000000ull), pp4 = bitsd(0xbacd747f23e32ed7ull);
+        const double t2 = fma(-xn, pp3, y);
+        double db = fma(-pp3, xn, y - t2);
+        const double b = fma(-xn, pp4, t2);
+        db = db + fma(-xn, pp4, t2 - b);
+        const double r = ((n + 1) & 1) ? cs_do_cos(b, db) : cs_do_sin(b, db);
+        return ((n + 1) & 2) ? -r : r;
+    }
+    if (k < 0x7ff00000u) return cos(x);                        /* __branred: not restated */
+    return x / x;
+}
+
+/* or_cos against the host cos: `count` seeded arguments (start = seed) from four distributions --
+   uniform in [-lim, lim], uniform bit patterns of |x| < 2^27, and around the branch boundaries and
+   multiples of pi/2; returns the mismatches */
+int64_t or_cos_check(uint64_t start, uint64_t count, double lim) {
+    int64_t bad = 0;
+    uint64_t s = 0x9E3779B97F4A7C15ull * (start + 1);
+    static const double edges[] = {0x1p-27, 0.85546875, 2.426265, 1.5707963267948966, 3.141592653589793,
+                                   4.71238898038469, 6.283185307179586, 105414350.0};
+    for (uint64_t i = 0; i < count; i++) {
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        double x;
+        switch (i & 3) {
+            case 0: x = ((double)(s >> 11) * 0x1p-53 * 2.0 - 1.0) * lim; break;
+            case 1: x = bitsd((s & 0x800fffffffffffffull) | ((uint64_t)(0x3c0 + (s >> 52) % 0x5a) << 52)); break;
+            case 2: { const double e = edges[(s >> 40) % 8]; x = bitsd(dbits(e) + (int64_t)((s & 0xfffff) - 0x80000)); break; }
+            default: x = (double)((int64_t)(s >> 40) - (1ll << 23)) * 1.5707963267948966 + ((double)(s & 0xffff) - 32768.0) * 0x1p-40;
+        }
+        const double a = or_cos(x), b = cos(x);
+        if (!(dbits(a) == dbits(b) || (a != a && b != b))) bad++;
+    }
+    return bad;
+}
+
+/* the restated (glibc = 0) or host (glibc = 1) cos on an array: the GPU test's checker for the
+   device restatement (implisolid_debug_cos) */
+void or_cos_apply(const double* a, int64_t n, double* out, int glibc) {
+    for (int64_t i = 0; i < n; i++) out[i] = glibc ? cos(a[i]) : or_cos(a[i]);
+}
+
 /* mismatching results vs the host libm.  which: 0 sinf, 1 atanf over start + k*stride (count
    patterns); 2 atan2f over `count` seeded pairs (start = seed) drawn from four distributions */
 int64_t or_libm_check(int which, uint32_t start, uint32_t stride, uint64_t count) {

@@ -71,6 +71,10 @@ float or_sinf(float x);
 float or_atanf(float x);
 float or_atan2f(float y, float x);
 int64_t or_libm_check(int which, uint32_t start, uint32_t stride, uint64_t count);
+/* glibc-2.35 double cos (x86_64 FMA variant, s_sin.c __cos) restated (or_libm.c): the screw gradient */
+double or_cos(double x);
+int64_t or_cos_check(uint64_t start, uint64_t count, double lim);
+void or_cos_apply(const double* a, int64_t n, double* out, int glibc);
 
 /* glibc-2.35 acosf restatement (vertex_resampling.hpp:75 calls std::acos(float)) */
 float or_acosf(float x);

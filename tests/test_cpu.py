@@ -204,6 +204,31 @@ def test_libm_restatements_match_glibc_exhaustive(oracle):
     assert oracle.libm_check(2, 2, 1, 100_000_000) == 0
 
 
+def test_cos_restatement_matches_glibc(oracle):
+    """The screw gradient's double cos (screw.hpp:178-180): glibc 2.35's __cos, x86_64 FMA variant,
+    restated from the host libm's __cos_fma (or_libm.c or_cos; its table from libm by
+    tools/extract_sincostab.py) -- bit for bit against the host cos on seeded arguments spanning
+    every branch (|x| < 2^-27, do_cos, do_sin near pi/2, the reduced range with its TAYLOR_SIN
+    path) and the screw's own range (pi x a phase of a few units).  2 G arguments gave 0 mismatches
+    (DESIGN.md section 4)."""
+    for seed, lim in ((1, 4.0), (2, 64.0), (3, 1e4), (4, 1e8)):
+        assert oracle.cos_check(seed, 2_000_000, lim) == 0, (seed, lim)
+    x = np.array([0.0, -0.0, 1e-300, 2.0 ** -27, -(2.0 ** -27), 0.85546875, -0.85546875, 2.426265, np.pi / 2,
+                  -np.pi, 105414349.0, 1e300, np.inf, -np.inf, np.nan])
+    a, b = oracle.cos_apply(x), oracle.cos_apply(x, glibc=True)
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64)) or np.array_equal(np.isnan(a), np.isnan(b))
+
+
+def test_sincostab_header_matches_libm():
+    """csrc/generated/sincostab.h is glibc's __sincostab as this image's libm holds it."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "extract_sincostab.py")], capture_output=True,
+                         text=True, check=True).stdout
+    assert open(os.path.join(root, "implisolid_amd", "csrc", "generated", "sincostab.h")).read() == out
+
+
 def _screw_family():
     from implisolid_amd import scenes
     tw = scenes.twist(1, 0, 0, 0)

@@ -58,11 +58,10 @@ def _screw_trees():
     }
 
 
-# the screw gradient (screw.hpp:152-160) calls the double cos, which is the device libm's here and
-# glibc's in the oracle (both within an ulp of cos): gradients of trees holding a twist are compared
-# to a tolerance, everything else (values, meshes) bit for bit
+# the screw gradient (screw.hpp:152-160) calls the double cos: glibc's in the oracle, its restatement
+# on the device (ifunc_device.hpp glibc_cos, test_device_cos_bit_exact) -- every value, gradient and
+# mesh is compared bit for bit
 SCREW_TREES = _screw_trees()
-GRAD_TOL = 2e-6
 TREES = _trees()
 
 
@@ -79,14 +78,9 @@ def test_eval_points_bit_exact(impli, oracle, name):
         f2 = svc.eval(pts)
     assert np.array_equal(f.view(np.uint32), f_ref.view(np.uint32)), np.flatnonzero(f != f_ref)[:10]
     assert np.array_equal(f2.view(np.uint32), f_ref.view(np.uint32))
-    if _has_twist(shape):
-        ok = np.isfinite(g_ref).all(1)
-        scale = np.maximum(np.abs(g_ref[ok]), 1.0)
-        assert (np.abs(g[ok] - g_ref[ok]) <= GRAD_TOL * scale).all()
-        assert np.array_equal(np.isfinite(g).all(1), ok)
-        assert (g == g_ref).all(1).mean() > 0.999          # bit-identical except where cos rounds apart
-    else:
-        assert np.array_equal(g.view(np.uint32), g_ref.view(np.uint32)), np.flatnonzero((g != g_ref).any(1))[:10]
+    # every gradient bit for bit, twists included (the screw gradient's double cos is glibc's,
+    # restated: test_device_cos_bit_exact)
+    assert np.array_equal(g.view(np.uint32), g_ref.view(np.uint32)), np.flatnonzero((g != g_ref).any(1))[:10]
 
 
 def _same_bits(a, b):
@@ -129,6 +123,28 @@ def test_device_libm_bit_exact(impli, oracle):
     got, ref = impli.debug_libm(2, Y, X), oracle.libm_apply(2, Y, X)
     bad = ~_same_bits(got, ref)
     assert not bad.any(), (Y[bad][:4], X[bad][:4], got[bad][:4], ref[bad][:4])
+
+
+def test_device_cos_bit_exact(impli, oracle):
+    """The screw gradient's double cos on the device (ifunc_device.hpp glibc_cos: glibc 2.35's __cos,
+    x86_64 FMA variant, restated) against the oracle's restatement (pinned to the host cos by
+    test_cpu.test_cos_restatement_matches_glibc) and the host cos itself: every branch, dense bit
+    windows around the branch boundaries and the multiples of pi/2, the screw's own arguments
+    (pi x phase), signed zeros, infinities and NaN.  |x| >= 105414350 (__branred) is not restated."""
+    rng = np.random.default_rng(2026)
+    n = 1 << 21
+    edges = np.array([2.0 ** -27, 0.85546875, 2.426265, np.pi / 4, np.pi / 2, np.pi, 3 * np.pi / 2, 2 * np.pi,
+                      0.126, 1e3, 105414349.0])
+    win = (edges.view(np.int64)[:, None] + np.arange(-4096, 4096)[None, :]).ravel().view(np.float64)
+    x = np.concatenate([rng.uniform(-8, 8, n), rng.uniform(-200, 200, n), rng.uniform(-1e8, 1e8, n // 4),
+                        np.pi * rng.uniform(-6, 6, n), (rng.uniform(-1, 1, n) * 2.0 ** rng.integers(-40, 2, n)),
+                        win, -win, np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-300, -1e-300])])
+    x = np.where(np.isfinite(x) & (np.abs(x) >= 105414350.0), 0.5, x)   # inf and NaN stay
+    got, ref, host = impli.debug_cos(x), oracle.cos_apply(x), oracle.cos_apply(x, glibc=True)
+    same = lambda a, b: (a.view(np.uint64) == b.view(np.uint64)) | (np.isnan(a) & np.isnan(b))
+    assert same(ref, host).all()
+    bad = ~same(got, ref)
+    assert not bad.any(), (bad.sum(), x[bad][:6], got[bad][:3], ref[bad][:3])
 
 
 def _has_twist(shape):
@@ -596,12 +612,12 @@ def test_zslab_gathered_counts_identical(impli, oracle, nranks):
 
 
 def _ob02_compare(impli, oracle, shape, mc, exact=None):
-    """Faces bit-exact; vertices bit-exact, or (trees with a twist, whose gradient goes through the
-    double cos) within 1e-5 -- the north-star vertex tolerance.  Non-finite reference vertices (a
+    """Faces bit-exact; vertices bit-exact (exact=False: within 1e-5, the north-star vertex
+    tolerance).  Non-finite reference vertices (a
     zero gradient at a singular point that lands on a grid sample: normalize_1111 divides by its
     norm, normalise_inplace.hpp:60-70) must be non-finite in the same rows."""
     if exact is None:
-        exact = not _has_twist(shape)
+        exact = True   # twists too: the screw gradient's double cos is glibc's, restated
     v, f = impli.make_geometry(shape, mc)
     vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
     assert np.array_equal(f, fr)
@@ -768,11 +784,7 @@ def test_eval_points_jit_bit_exact(impli, oracle, sync_jit, name, bake):
         np.isnan(f), np.isnan(f_ref)) and np.array_equal(f[~np.isnan(f)], f_ref[~np.isnan(f_ref)])
     ok = np.isfinite(g_ref).all(1)
     assert np.array_equal(np.isfinite(g).all(1), ok)
-    if _has_twist(shape):
-        scale = np.maximum(np.abs(g_ref[ok]), 1.0)
-        assert (np.abs(g[ok] - g_ref[ok]) <= GRAD_TOL * scale).all()
-    else:
-        assert np.array_equal(g[ok], g_ref[ok])
+    assert np.array_equal(g[ok].view(np.uint32), g_ref[ok].view(np.uint32))
 
 
 def _field(impli, shape, mc, level, signs=False):
@@ -876,12 +888,7 @@ def test_golden_points_gpu(impli):
         with impli.ImplicitService(sh) as svc:
             f, gr = svc.eval(g["points"], gradient=True)
         assert np.array_equal(f.view(np.uint32), g["f_" + name].view(np.uint32)), name
-        if _has_twist(sh):
-            ref = g["g_" + name]
-            ok = np.isfinite(ref).all(1)
-            assert (np.abs(gr[ok] - ref[ok]) <= GRAD_TOL * np.maximum(np.abs(ref[ok]), 1.0)).all(), name
-        else:
-            assert np.array_equal(gr.view(np.uint32), g["g_" + name].view(np.uint32)), name
+        assert np.array_equal(gr.view(np.uint32), g["g_" + name].view(np.uint32)), name
 
 
 def test_golden_config2_ob02_gpu(impli):
@@ -1198,10 +1205,10 @@ def _headline():
 def test_headline_against_oracle_summary(impli, name):
     """The exact meshes bench.py times (config 4's tree at 512^3 and 256^3, eval + MC) and the OB02
     legs it reports (config 3 at 256^3, config 2 at 128^3, 3 repeats of resample + project + QEM),
-    against the oracle's summaries: faces byte-identical (SHA-256); vertices bit-identical where the
-    tree has no twist, else every vertex row within the north star's 1e-5 (the oracle's full arrays,
-    headline_ob02_verts.npz) and the finite-vertex sum within 1e-5 per vertex; the reference's
-    non-finite rows at the same rows."""
+    against the oracle's summaries: faces and vertices byte-identical (SHA-256; twist trees included:
+    the screw gradient's double cos is glibc's, restated), the twist tree's OB02 meshes also row by
+    row against the oracle's full arrays (headline_ob02_verts.npz); the reference's non-finite rows
+     at the same rows."""
     import hashlib
     summ, samples = _headline()
     s = summ[name]
@@ -1211,8 +1218,7 @@ def test_headline_against_oracle_summary(impli, name):
     fin = np.isfinite(v).all(1)
     assert np.flatnonzero(~fin).tolist() == s["nonfinite_rows"]
     idx, vs = samples[name + "_idx"], samples[name + "_v"]
-    if not _has_twist(s["shape"]) or "_mc_" in name:   # MC vertices are bit-exact for every tree
-        assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"]
+    assert hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest() == s["sha256_verts"]
     ok = np.isfinite(vs).all(1)
     assert np.abs(v[idx][ok].astype(np.float64) - vs[ok]).max(initial=0.0) < 1e-5
     full = np.load(_golden("headline_ob02_verts.npz"))
@@ -1220,8 +1226,7 @@ def test_headline_against_oracle_summary(impli, name):
         vr = full[name]
         assert np.array_equal(np.isfinite(vr).all(1), fin)
         d = np.abs(v[fin].astype(np.float64) - vr[fin])
-        assert d.max(initial=0.0) < 1e-5, d.max()
-        assert (d == 0).all(1).mean() > 0.999   # bit-identical but where the device cos rounds apart
+        assert d.max(initial=0.0) == 0.0, (d.max(), np.flatnonzero(d.max(1) > 0)[:10])
     tot = v[fin].astype(np.float64).sum(0)
     assert np.abs(tot - np.array(s["finite_sum"])).max() < 1e-5 * max(1, fin.sum())
 
@@ -1236,7 +1241,7 @@ def test_config3_shifted_projection_live(impli, name):
     """Config 3 at 256^3 and config 4 at 512^3 on the shifted box (scenes.config3_shifted): the
     average edge length stays finite, so the projection runs its alpha search and bisection on the
     faces (many evaluations per face and repeat, not config 3's one), and the mesh is still the
-    oracle's (faces SHA-256, every vertex finite, sampled rows within 1e-5: the tree holds a twist)."""
+    oracle's (faces and vertices SHA-256, every vertex finite)."""
     summ, samples = _headline()
     s = summ[name]
     impli.ob02_profile(True)
@@ -1246,8 +1251,9 @@ def test_config3_shifted_projection_live(impli, name):
     finally:
         impli.ob02_profile(False)
     assert _sha(f) == s["sha256_faces"] and np.isfinite(v).all() and s["nonfinite_rows"] == []
+    assert _sha(v) == s["sha256_verts"]
     idx, vs = samples[name + "_idx"], samples[name + "_v"]
-    assert np.abs(v[idx].astype(np.float64) - vs).max() < 1e-5
+    assert np.array_equal(v[idx].astype(np.float64), vs)
     evals_per_face = st["projection_evals"] / (len(f) * s["mc"]["overall_repeats"])
     # config 3's dyadic box: one evaluation per face (every centroid kept); live: 20 at 256^3, 9 at
     # 512^3 (the finer mesh's centroids sit closer to the surface: earlier hits, shorter bisections)
@@ -1576,10 +1582,7 @@ def test_ob02_stream_ordered_shards(impli, oracle, nshard, halo, scene):
     assert np.array_equal(f, fr)
     fin = np.isfinite(vr).all(1)
     assert np.array_equal(np.isfinite(v).all(1), fin)
-    if _has_twist(shape):   # the twist's gradient goes through the double cos (GRAD_TOL)
-        assert np.abs(v[fin] - vr[fin]).max(initial=0.0) < 1e-5
-    else:
-        assert np.array_equal(v[fin].view(np.uint32), vr[fin].view(np.uint32)), (nshard, halo, scene)
+    assert np.array_equal(v[fin].view(np.uint32), vr[fin].view(np.uint32)), (nshard, halo, scene)
     if halo and any(ex == "halo" for _, ex in plan):
         full = 12 * nv * (nshard - 1) / nshard * nshard   # bytes a full exchange moves
         assert min(stats["exchange_bytes"]) < full / 4    # the halo exchanges move a fraction
@@ -1622,8 +1625,7 @@ def test_config4_ob02_r512_sharded_against_summary(impli):
     and bisection), the MC mesh's vertices owned by the 8 balanced Z-slabs' ranges, every shard
     stepped on its own stream with the halo / full exchanges (distributed.ob02_shards_local, the
     bench's 8-rank estimate), against the oracle's summary (tests/golden/make_headline.py
-    config4s_ob02_r512): faces byte-identical, every vertex row within 1e-5 of the oracle's full
-    array (the tree holds a twist), > 99.9 % of them bit-identical."""
+    config4s_ob02_r512): faces and vertices byte-identical (SHA-256)."""
     import torch
     from implisolid_amd import distributed as D
     summ, _ = _headline()
@@ -1644,7 +1646,4 @@ def test_config4_ob02_r512_sharded_against_summary(impli):
     voff = np.concatenate([[0], np.cumsum(nvs)]).astype(np.int64)
     v, f, _ = D.ob02_shards_local(shape, mc, V, F, voff)
     assert _sha(f) == s["sha256_faces"] and np.isfinite(v).all()
-    vr = np.load(_golden("headline_ob02_verts.npz"))["config4s_ob02_r512"]
-    d = np.abs(v.astype(np.float64) - vr)
-    assert d.max() < 1e-5, d.max()
-    assert (d == 0).all(1).mean() > 0.999
+    assert _sha(v) == s["sha256_verts"]
