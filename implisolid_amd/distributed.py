@@ -232,26 +232,42 @@ def shard_transfers(voff, halos, rank, kind="halo"):
     return sends, recvs
 
 
-_SHARDS = {}   # (shape, mc settings, slot) -> Ob02Shard, kept across builds
+_SHARDS = {}   # (device, slot) -> (object key, Ob02Shard): one kept handle per slot and device
 
 
-def shard_handle(shape, mc_settings, slot=0):
+def shard_handle(shape, mc_settings, slot=0, device=None):
     """The rank's OB02 shard handle for this object, created once and reused by later builds, as
     build_geometry keeps its one refinement state (abi.hip g_ob02): a fresh handle allocates every
     device buffer, its side stream and events on its first attach and projection (0.3-0.8 ms per
-    shard), a reused one only re-attaches the mesh.  release_shards() frees them."""
+    shard), a reused one only re-attaches the mesh.  At most one handle is kept per (device, slot):
+    a build of another object (shape or settings) closes the slot's previous handle, so a caller
+    that builds many shapes holds no more buffers and streams than one object's.  release_shards()
+    frees them all; a loop that raises drops its handle (ob02_sharded, ob02_shards_local)."""
     import json
     import implisolid_amd as I
-    key = (json.dumps(shape, sort_keys=True), json.dumps(mc_settings, sort_keys=True), int(slot))
-    ob = _SHARDS.get(key)
-    if ob is None or not ob.h:
-        ob = _SHARDS[key] = I.Ob02Shard(shape, mc_settings)
+    dev = (torch.cuda.current_device() if torch.cuda.is_available() else -1) if device is None else int(device)
+    okey = (json.dumps(shape, sort_keys=True), json.dumps(mc_settings, sort_keys=True))
+    kept = _SHARDS.get((dev, int(slot)))
+    if kept is not None and kept[0] == okey and kept[1].h:
+        return kept[1]
+    if kept is not None:
+        kept[1].close()
+    ob = I.Ob02Shard(shape, mc_settings)
+    _SHARDS[(dev, int(slot))] = (okey, ob)
     return ob
+
+
+def drop_shard(ob):
+    """Close a kept handle and forget it (a loop that failed part-way: its state is not reused)."""
+    for k, (_, kept) in list(_SHARDS.items()):
+        if kept is ob:
+            del _SHARDS[k]
+    ob.close()
 
 
 def release_shards():
     """Close every kept shard handle (shard_handle)."""
-    for ob in _SHARDS.values():
+    for _, ob in _SHARDS.values():
         ob.close()
     _SHARDS.clear()
 
@@ -279,7 +295,8 @@ def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_ste
     voff = [int(x) for x in voff]
     v0, v1 = voff[rank], voff[rank + 1]
     W = V.clone()   # the working array (updated in place)
-    ob = shard_handle(shape, mc_settings)
+    ob = shard_handle(shape, mc_settings, device=device.index if cuda else None)
+    ok = False
     try:
         cur = torch.cuda.current_stream(device) if cuda else None
         ob.attach(W.data_ptr(), nv, F.data_ptr(), nf, v0, v1, cur.cuda_stream if cur is not None else 0)
@@ -348,14 +365,16 @@ def ob02_sharded(shape, mc_settings, V, F, voff, rank, world, group=None, on_ste
                 on_step({"R": "resample", "P": "project"}[step], k // per_rep)
         if st["subdiv"] and st["overall_repeats"] >= 1 and rank == 0:   # polygonize_step_3, last repeat: noise x 10
             ob.subdivide(float(st["post_subdiv_noise"]) * 10.0)
-        if rank == 0:
-            return ob.download()
+        res = ob.download() if rank == 0 else None
         if cuda:
             s_ob.synchronize()
-        return None
+        ok = True
+        return res
     finally:
-        if cuda:
+        if cuda and ob.h:
             torch.cuda.ExternalStream(ob.stream(), device=device).synchronize()   # W lives until the loop is done
+        if not ok:
+            drop_shard(ob)   # a half-attached handle is not reused
 
 
 def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
@@ -373,8 +392,9 @@ def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
     voff = [int(x) for x in voff]
     n = len(voff) - 1
     Ws = [V.clone() for _ in range(n)]
-    obs = [shard_handle(shape, mc_settings, slot=r) for r in range(n)]
+    obs = [shard_handle(shape, mc_settings, slot=r, device=device.index) for r in range(n)]
     stats = {"steps": [], "exchange_bytes": []}
+    ok = False
     try:
         import time
         cur = torch.cuda.current_stream(device)
@@ -419,6 +439,10 @@ def ob02_shards_local(shape, mc_settings, V, F, voff, halo=True, timing=False):
         if st["subdiv"] and st["overall_repeats"] >= 1:
             obs[0].subdivide(float(st["post_subdiv_noise"]) * 10.0)
         v, f = obs[0].download()
+        ok = True
         return v, f, stats
     finally:
         torch.cuda.synchronize(device)   # the shards' streams are done with Ws
+        if not ok:
+            for ob in obs:
+                drop_shard(ob)

@@ -1620,6 +1620,23 @@ def test_multiprocess_slabs_gloo(impli, oracle, tmp_path, world, balanced):
         assert len(g["cuts"]) == world + 1
 
 
+def test_shard_handles_bounded(impli):
+    """distributed.shard_handle keeps one handle per (device, slot): the same object reuses it, another
+    object closes it (its buffers and streams freed), release_shards() closes the rest."""
+    from implisolid_amd import distributed as D, scenes
+    D.release_shards()
+    a = D.shard_handle(scenes.config1()[0], scenes.config1()[1], slot=0)
+    assert D.shard_handle(scenes.config1()[0], scenes.config1()[1], slot=0) is a
+    b = D.shard_handle(scenes.config3_tree(), scenes.config1()[1], slot=0)
+    assert b is not a and a.h is None and b.h
+    c = D.shard_handle(scenes.config3_tree(), scenes.config1()[1], slot=1)
+    assert len(D._SHARDS) == 2
+    D.drop_shard(c)
+    assert c.h is None and len(D._SHARDS) == 1
+    D.release_shards()
+    assert b.h is None and not D._SHARDS
+
+
 def test_config4_ob02_r512_sharded_against_summary(impli):
     """Config 4's OB02 loop at its own size: the tree at 512^3 on the shifted box (live alpha search
     and bisection), the MC mesh's vertices owned by the 8 balanced Z-slabs' ranges, every shard
