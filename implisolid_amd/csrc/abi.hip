@@ -1,4 +1,5 @@
 // abi.hip -- the extern "C" drop-in boundary (mcc2.cpp:88-134) over the MI355X engine.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1094,14 +1095,31 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             b->events.push_back(e);
         }
         hipStream_t s0 = b->streams[0];
+        // IMPLISOLID_BATCH_TIMING=1 (diagnostics): the setup's phases summed over the objects, on stderr
+        static const bool timing = std::getenv("IMPLISOLID_BATCH_TIMING") != nullptr;
+        double ph[4] = {0, 0, 0, 0};
+        auto tick = [](std::chrono::steady_clock::time_point& t) {
+            const auto now = std::chrono::steady_clock::now();
+            const double d = std::chrono::duration<double>(now - t).count();
+            t = now;
+            return d;
+        };
+        auto tp = std::chrono::steady_clock::now();
         for (int i = 0; i < n; ++i) {   // warm run: JIT lookup, output capacities from the real counts
             b->engines.emplace_back(new Engine());
             Engine& E = *b->engines.back();
+            if (timing) ph[0] += tick(tp);
             E.set_hot_bake(false);   // graphs capture the modules found now
             E.set_object(progs[(size_t)i]);
+            if (timing) ph[1] += tick(tp);
             E.set_grid(st.resolution, st.box, 0, 1);
+            if (timing) ph[2] += tick(tp);
             E.marching_cubes(s0);
+            if (timing) ph[3] += tick(tp);
         }
+        if (timing)
+            std::fprintf(stderr, "implisolid_batch_create: %d objects: engines %.2f ms, set_object %.2f ms, set_grid %.2f ms, "
+                                 "warm runs %.2f ms\n", n, ph[0] * 1e3, ph[1] * 1e3, ph[2] * 1e3, ph[3] * 1e3);
         if (b->merged) {   // the objects' device state, one row each; every object has the same grid
             std::vector<ObjArgs> rows;
             for (int pass = 0; pass < 2; ++pass)   // shallow objects first (launch_batch_eval's classes)

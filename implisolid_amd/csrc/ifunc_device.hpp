@@ -374,8 +374,8 @@ __device__ __forceinline__ float glibc_atan2f(float y, float x) {
 // __cos_fma holds: the screw gradient's cos(M_PI * (...)) (screw.hpp:178-180).  oracle/or_libm.c
 // or_cos is the same restatement, checked against the host cos (0 mismatches over 2 G seeded
 // arguments); the GPU test compares this one with it.  __sincostab (i/128: sin hi, lo, cos hi, lo)
-// from the host libm (tools/extract_sincostab.py), in constant memory.  |x| >= 105414350 (glibc's
-// __branred) is not restated: the device libm's cos.
+// from the host libm (tools/extract_sincostab.py), in constant memory.  |x| >= 105414336 (glibc's
+// __branred: high word >= 0x419921fb) is not restated: the device libm's cos.
 static __constant__ uint64_t kSinCosTab[440] = {IMPLI_SINCOSTAB_BITS};
 __device__ __forceinline__ double sct(int i) { return __longlong_as_double((long long)kSinCosTab[i]); }
 __device__ __forceinline__ double bits2d(uint64_t u) { return __longlong_as_double((long long)u); }

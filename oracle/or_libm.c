@@ -175,7 +175,7 @@ float or_atan2f(float y, float x) {
    sysdeps/ieee754/dbl-64/s_sin.c __cos, the x86_64 FMA variant (s_sin-fma.c, selected on every
    FMA- and AVX2-capable host): the branches and contractions as this image's libm compiles them
    (read from its __cos_fma).  screw.hpp:178-180 cos(M_PI * (...)): the screw gradient.  The
-   __branred branch (|x| >= 105414350) is not restated: it calls the host cos. */
+   __branred branch (high word >= 0x419921fb: |x| >= 105414336) is not restated: it calls the host cos. */
 #include "../implisolid_amd/csrc/generated/sincostab.h"
 static const uint64_t SINCOSTAB[440] = {IMPLI_SINCOSTAB_BITS};
 static inline double bitsd(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
@@ -226,7 +226,7 @@ double or_cos(double x) {
         const double da = (y - a) + bitsd(0x3c91a62633145c07ull);
         return cs_do_sin(a, da);
     }
-    if (k < 0x419921fbu) {                                     /* |x| < 105414350: reduce_sincos */
+    if (k < 0x419921fbu) {                                     /* |x| < 105414336: reduce_sincos */
         const double t = fma(x, bitsd(0x3fe45f306dc9c883ull), 0x1.8p52);
         const double xn = t - 0x1.8p52;
         const int n = (int)(dbits(t) & 3u);

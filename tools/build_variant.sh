@@ -3,12 +3,18 @@
 #   tools/build_variant.sh NAME 'sed-expr' [file=csrc/grid.hpp]  (more pairs: 'expr' file ...)
 # -> variants/NAME/implisolid_amd/lib/libimplisolid_mi355x.so (IMPLISOLID_LIB=... selects it).
 # Edits go into the headers themselves, so the JIT's embedded copies see them too.
+# VARIANTS=ab puts the build under ab/ (git-ignored, but not gpurun-ignored: it travels to the box).
+# GIT_REF=<rev> takes csrc/ from that commit instead of the working tree (an A/B base).
 set -euo pipefail
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
-d=$root/variants/$name
+d=$root/${VARIANTS:-variants}/$name
 rm -rf "$d"; mkdir -p "$d/implisolid_amd" "$d/tools"
 cp -r "$root/implisolid_amd/csrc" "$root/implisolid_amd/Makefile" "$d/implisolid_amd/"
+if [ -n "${GIT_REF:-}" ]; then
+    rm -rf "$d/implisolid_amd/csrc"; mkdir -p "$d/implisolid_amd/csrc"
+    (cd "$root" && git archive "$GIT_REF" implisolid_amd/csrc) | tar -x -C "$d" 
+fi
 rm -f "$d/implisolid_amd/csrc/generated/jit_headers.inc"
 cp "$root/tools/embed_headers.py" "$d/tools/"
 cp -r "$root/include" "$d/"
