@@ -602,10 +602,21 @@ def main():
     # into an objects/s over one pass that includes it.
     def run_batch(objs, jit_mode, n_streams):
         I.set_jit(jit_mode)
+        setup_cold = None
         try:
             t0 = time.perf_counter()
             batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=n_streams)
             setup_s = time.perf_counter() - t0
+            if n_streams == 0:
+                # merged launches: the stream's next batch of objects in this process -- created again,
+                # every object parsed, set up and run once -- with the device-memory pool holding the
+                # previous batch's buffers (the serving steady state); the first creation is reported
+                # beside it (its buffers come from hipMalloc)
+                batch.close()
+                setup_cold = setup_s
+                t0 = time.perf_counter()
+                batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=n_streams)
+                setup_s = time.perf_counter() - t0
         finally:
             I.set_jit(2)
         for _ in range(max(1, args.warmup)):
@@ -626,8 +637,15 @@ def main():
         res = {"objects_per_s": round(batch.n / (ms5 * 1e-3), 1), "value": round(batch.n * 128 ** 3 / (ms5 * 1e-3) / 1e6, 2),
                "unit": "Mvoxels/s", "ms_per_stream": round(ms5, 4), "graphs": batch.graphs, "merged": batch.merged,
                "verts": tv, "faces": tf,
-               "setup_s": round(setup_s, 2), "jit_compile_s": round(batch.jit_seconds, 2),
+               "setup_s": round(setup_s, 4), "jit_compile_s": round(batch.jit_seconds, 2),
                "objects_per_s_incl_setup": round(batch.n / (ms5 * 1e-3 + setup_s), 1)}
+        if setup_cold is not None:
+            res["setup_s_first_batch"] = round(setup_cold, 4)
+            res["objects_per_s_incl_setup_first_batch"] = round(batch.n / (ms5 * 1e-3 + setup_cold), 1)
+            res["setup_note"] = ("setup_s: implisolid_batch_create of the 64 objects as the stream's next batch in this "
+                                 "process (programs parsed, engines set up, one merged pass sizing the outputs; the "
+                                 "device-memory pool serves the previous batch's buffers); setup_s_first_batch: the "
+                                 "process's first batch (buffers from hipMalloc)")
         n_streams = batch.n_streams
         batch.close()
         return res, n_streams

@@ -8,6 +8,9 @@
 #include <memory>
 #include <string>
 #include <vector>
+#include <thread>
+#include <mutex>
+#include <algorithm>
 
 #include "../../include/implisolid.h"
 #include "engine.hpp"
@@ -1029,6 +1032,8 @@ static int batch_groups() {
 }
 
 struct implisolid_batch {
+    DevBuf progs;                        // merged: every object's Program, one upload (the engines read them)
+    DevBuf counts;                       // merged: every row's counter block, gathered for one read-back
     std::vector<std::unique_ptr<Engine>> engines;
     bool merged = false;                 // one launch per stage for all objects (ObjArgs rows)
     DevBuf objs;                         // merged: ObjArgs[n] on the device, shallow objects first
@@ -1048,14 +1053,72 @@ struct implisolid_batch {
 
 static void batch_merged_enqueue(implisolid_batch* b, hipStream_t s);
 
+// object streams' HIP streams and events, cached per device for the process's later batches
+static std::mutex g_batch_cache_mu;
+static std::map<int, std::vector<hipStream_t>> g_batch_streams;
+static std::map<int, std::vector<hipEvent_t>> g_batch_events;
+static int current_device() {
+    int d = 0;
+    IMPLI_HIP(hipGetDevice(&d));
+    return d;
+}
+static hipStream_t batch_take_stream() {
+    const int d = current_device();
+    {
+        std::lock_guard<std::mutex> lk(g_batch_cache_mu);
+        auto& v = g_batch_streams[d];
+        if (!v.empty()) {
+            hipStream_t q = v.back();
+            v.pop_back();
+            return q;
+        }
+    }
+    hipStream_t q;
+    IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+    return q;
+}
+static hipEvent_t batch_take_event() {
+    const int d = current_device();
+    {
+        std::lock_guard<std::mutex> lk(g_batch_cache_mu);
+        auto& v = g_batch_events[d];
+        if (!v.empty()) {
+            hipEvent_t e = v.back();
+            v.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e;
+    IMPLI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+}
+
 implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, const char* mc_json, int n_streams) {
     g_last_error.clear();
     auto* b = new implisolid_batch();
     try {
         if (n <= 0) throw InputError("implisolid_batch_create: no objects");
         const MCSettings st = parse_mc_settings(mc_json);
-        std::vector<Program> progs;
-        for (int i = 0; i < n; ++i) progs.push_back(compile_mp5(shapes[i], st.ignore_root_matrix));
+        static const bool timing = std::getenv("IMPLISOLID_BATCH_TIMING") != nullptr;   // diagnostics
+        auto t_start = std::chrono::steady_clock::now();
+        // the MP5 programs, parsed and compiled on host threads (a few tens of us each)
+        std::vector<Program> progs((size_t)n);
+        {
+            const int nt = std::max(1, std::min({n / 8, 8, (int)std::thread::hardware_concurrency()}));
+            std::vector<std::string> errs((size_t)nt);
+            std::vector<std::thread> ths;
+            for (int t = 0; t < nt; ++t)
+                ths.emplace_back([&, t] {
+                    try {
+                        for (int i = t; i < n; i += nt) progs[(size_t)i] = compile_mp5(shapes[i], st.ignore_root_matrix);
+                    } catch (const std::exception& e) {
+                        errs[(size_t)t] = e.what();
+                    }
+                });
+            for (auto& th : ths) th.join();
+            for (auto& e : errs)
+                if (!e.empty()) throw InputError(e);
+        }
         // n_streams <= 0: merged launches (the interpreter kernels, every stage once for all
         // objects); otherwise one hipGraph per object (JIT tree kernels when enabled) over streams
         b->merged = n_streams <= 0 && Engine::pruning() > 0;
@@ -1083,21 +1146,14 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         const int ns = b->merged ? batch_groups() : std::max(1, std::min(n_streams, 8));
         // (the deep class's stream at the lowest priority measured 0.5 % faster alone, but with the
         // bench's earlier legs' streams alive the two pipelines then shared a hardware queue: 0.85 ms
-        // per pass, profiles/r05zr_*; default priority)
-        for (int k = 0; k < ns; ++k) {
-            hipStream_t q;
-            IMPLI_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-            b->streams.push_back(q);
-        }
-        for (int k = 0; k <= ns; ++k) {
-            hipEvent_t e;
-            IMPLI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            b->events.push_back(e);
-        }
+        // per pass, profiles/r05zr_*; default priority).  Streams and events come from a process-wide
+        // cache (batch_take_stream): an object stream creates batch after batch.
+        for (int k = 0; k < ns; ++k) b->streams.push_back(batch_take_stream());
+        for (int k = 0; k <= ns; ++k) b->events.push_back(batch_take_event());
         hipStream_t s0 = b->streams[0];
         // IMPLISOLID_BATCH_TIMING=1 (diagnostics): the setup's phases summed over the objects, on stderr
-        static const bool timing = std::getenv("IMPLISOLID_BATCH_TIMING") != nullptr;
         double ph[4] = {0, 0, 0, 0};
+        const double t_compile = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
         auto tick = [](std::chrono::steady_clock::time_point& t) {
             const auto now = std::chrono::steady_clock::now();
             const double d = std::chrono::duration<double>(now - t).count();
@@ -1105,28 +1161,51 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             return d;
         };
         auto tp = std::chrono::steady_clock::now();
-        for (int i = 0; i < n; ++i) {   // warm run: JIT lookup, output capacities from the real counts
-            b->engines.emplace_back(new Engine());
-            Engine& E = *b->engines.back();
-            if (timing) ph[0] += tick(tp);
-            E.set_hot_bake(false);   // graphs capture the modules found now
-            E.set_object(progs[(size_t)i]);
-            if (timing) ph[1] += tick(tp);
-            E.set_grid(st.resolution, st.box, 0, 1);
-            if (timing) ph[2] += tick(tp);
-            E.marching_cubes(s0);
-            if (timing) ph[3] += tick(tp);
+        if (b->merged) {
+            // merged launches: the programs in one upload, every engine's buffers set up on s0 without
+            // device synchronisations (fresh engines; the pool serves them without hipMalloc from the
+            // second batch of a process on), no warm run per object -- the merged fill writes the unit
+            // marks from the first pass -- and one merged pass below sizes the outputs of all
+            b->progs.reserve((size_t)n * sizeof(Program));
+            IMPLI_HIP(hipMemcpyAsync(b->progs.p, progs.data(), (size_t)n * sizeof(Program), hipMemcpyHostToDevice, s0));
+            const SlabRange whole = slab_partition(st.resolution, 0, 1);
+            for (int i = 0; i < n; ++i) {
+                b->engines.emplace_back(new Engine(s0));
+                Engine& E = *b->engines.back();
+                if (timing) ph[0] += tick(tp);
+                E.set_hot_bake(false);
+                E.set_object(progs[(size_t)i], b->progs.as<Program>() + i);
+                if (timing) ph[1] += tick(tp);
+                E.set_slab(st.resolution, st.box, whole, false, s0);
+                E.arm_merged();
+                if (timing) ph[2] += tick(tp);
+            }
+        } else {
+            for (int i = 0; i < n; ++i) {   // warm run: JIT lookup, output capacities from the real counts
+                b->engines.emplace_back(new Engine());
+                Engine& E = *b->engines.back();
+                if (timing) ph[0] += tick(tp);
+                E.set_hot_bake(false);   // graphs capture the modules found now
+                E.set_object(progs[(size_t)i]);
+                if (timing) ph[1] += tick(tp);
+                E.set_grid(st.resolution, st.box, 0, 1);
+                if (timing) ph[2] += tick(tp);
+                E.marching_cubes(s0);
+                if (timing) ph[3] += tick(tp);
+            }
         }
         if (timing)
             std::fprintf(stderr, "implisolid_batch_create: %d objects: engines %.2f ms, set_object %.2f ms, set_grid %.2f ms, "
                                  "warm runs %.2f ms\n", n, ph[0] * 1e3, ph[1] * 1e3, ph[2] * 1e3, ph[3] * 1e3);
         if (b->merged) {   // the objects' device state, one row each; every object has the same grid
             std::vector<ObjArgs> rows;
+            std::vector<Engine*> order;   // the engine of each row
             for (int pass = 0; pass < 2; ++pass)   // shallow objects first (launch_batch_eval's classes)
                 for (auto& e : b->engines) {
                     const bool shallow = e->depth() <= kBatchShallowDepth;
                     if (shallow != (pass == 0)) continue;
                     rows.push_back(e->obj_args());
+                    order.push_back(e.get());
                     b->depth = std::max(b->depth, e->depth());
                     int& d = shallow ? b->depth_shallow : b->depth_deep;
                     d = std::max(d, e->depth());
@@ -1142,8 +1221,41 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             }
             if (n > b->n_shallow) b->groups.push_back({b->n_shallow, n - b->n_shallow, b->depth_deep, b->vdepth_deep});
             b->objs.reserve(rows.size() * sizeof(ObjArgs));
-            IMPLI_HIP(hipMemcpy(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice));
-            IMPLI_HIP(hipStreamSynchronize(s0));
+            IMPLI_HIP(hipMemcpyAsync(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice, s0));
+            // the first merged pass: every object's counts in one read-back; an object whose mesh
+            // outgrew the set_slab capacities grows its buffers and the pass runs again
+            static std::mutex hc_mu;
+            static HostBuf hc;   // pinned, process-wide (a hipHostMalloc per batch cost more than the pass)
+            std::lock_guard<std::mutex> hc_lock(hc_mu);
+            hc.reserve((size_t)n * kCounterWords * sizeof(uint32_t));
+            DevBuf& dc = b->counts;
+            dc.reserve((size_t)n * kCounterWords * sizeof(uint32_t));
+            for (int pass = 0;; ++pass) {
+                batch_merged_enqueue(b, s0);
+                launch_gather_counters(b->objs.as<ObjArgs>(), n, dc.as<uint32_t>(), s0);   // every row's block
+                IMPLI_HIP(hipMemcpyAsync(hc.p, dc.p, (size_t)n * kCounterWords * sizeof(uint32_t), hipMemcpyDeviceToHost, s0));
+                IMPLI_HIP(hipStreamSynchronize(s0));
+                bool grew = false;
+                for (int r = 0; r < n; ++r) {
+                    const uint32_t* h = hc.as<uint32_t>() + (size_t)r * kCounterWords;
+                    const SlabCounts c{h[2], h[3], h[4], h[5]};
+                    if (h[kOverflowWord] || !order[(size_t)r]->fits(c)) {
+                        if (pass) throw HipError("object stream: output capacity overflow after resize");
+                        order[(size_t)r]->ensure_capacity(c);
+                        rows[(size_t)r] = order[(size_t)r]->obj_args();
+                        IMPLI_HIP(hipMemsetAsync(const_cast<uint32_t*>(order[(size_t)r]->d_counters()) + kOverflowWord, 0,
+                                                 4 * sizeof(uint32_t), s0));
+                        grew = true;
+                    }
+                }
+                if (!grew) break;
+                IMPLI_HIP(hipMemcpyAsync(b->objs.p, rows.data(), rows.size() * sizeof(ObjArgs), hipMemcpyHostToDevice, s0));
+            }
+            if (timing) {
+                ph[3] += tick(tp);
+                std::fprintf(stderr, "implisolid_batch_create (merged): compile + streams %.2f ms, first pass + counts %.2f ms\n",
+                             t_compile * 1e3, ph[3] * 1e3);
+            }
             // (the whole pass captured as one graph and replayed: 0.548-0.557 ms against 0.499-0.501
             // with direct launches, profiles/r05zq_config5_merged_graph_ab.txt)
             return b;
@@ -1438,8 +1550,13 @@ void implisolid_batch_destroy(implisolid_batch* b) {
     if (!b) return;
     for (auto q : b->streams) (void)hipStreamSynchronize(q);
     for (auto x : b->execs) (void)hipGraphExecDestroy(x);
-    for (auto e : b->events) (void)hipEventDestroy(e);
-    for (auto q : b->streams) (void)hipStreamDestroy(q);
+    {   // the streams and events go back to the cache (the streams are idle: synchronised above)
+        int d = 0;
+        (void)hipGetDevice(&d);
+        std::lock_guard<std::mutex> lk(g_batch_cache_mu);
+        for (auto e : b->events) g_batch_events[d].push_back(e);
+        for (auto q : b->streams) g_batch_streams[d].push_back(q);
+    }
     b->objs.release();
     delete b;
 }

@@ -5,6 +5,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include <cstddef>
 
@@ -17,18 +19,106 @@ void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// ---- the device-memory pool behind DevBuf ----------------------------------------------------------
+// Size classes of four steps per octave (at most 25 % over the request), 256 B and up; blocks above
+// kPoolMaxBlock (the field of a large grid) and any block past kPoolMaxCached cached bytes go back
+// to hipFree as before.  A released block waits in `pending` until the next allocation that would
+// reuse it synchronises the device once (hipFree used to synchronise on every call): a kernel still
+// reading it on some stream is done by then.
+namespace {
+constexpr size_t kPoolMaxBlock = size_t(256) << 20, kPoolMaxCached = size_t(4) << 30;
+struct DevicePool {
+    std::map<size_t, std::vector<void*>> ready, pending;
+    size_t ready_bytes = 0, pending_bytes = 0;
+};
+std::mutex g_pool_mu;
+std::map<int, DevicePool> g_pools;
+size_t pool_class(size_t n) {
+    size_t c = 256;
+    while (c < n) c <<= 1;                      // the octave's top
+    const size_t q = c >> 3;                    // c / 2 + k c / 8, k = 1..4
+    for (size_t k = 5; k <= 8; ++k)
+        if (n <= q * k && q * k >= 256) return q * k;
+    return c;
+}
+}  // namespace
+
 void DevBuf::reserve(size_t n) {
     if (n <= bytes && p) return;
     release();
-    size_t want = n < 256 ? 256 : n;
+    int d = 0;
+    IMPLI_HIP(hipGetDevice(&d));
+    const size_t want = pool_class(n < 256 ? 256 : n);
+    if (want <= kPoolMaxBlock) {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        DevicePool& P = g_pools[d];
+        auto take = [&](std::map<size_t, std::vector<void*>>& m, size_t& counted) -> void* {
+            auto it = m.find(want);
+            if (it == m.end() || it->second.empty()) return nullptr;
+            void* q = it->second.back();
+            it->second.pop_back();
+            counted -= want;
+            return q;
+        };
+        void* q = take(P.ready, P.ready_bytes);
+        if (!q && P.pending.count(want) && !P.pending[want].empty()) {
+            IMPLI_HIP(hipDeviceSynchronize());   // every pending block's last user is done
+            for (auto& kv : P.pending)
+                for (void* b : kv.second) P.ready[kv.first].push_back(b);
+            P.ready_bytes += P.pending_bytes;
+            P.pending.clear();
+            P.pending_bytes = 0;
+            q = take(P.ready, P.ready_bytes);
+        }
+        if (q) {
+            p = q;
+            bytes = want;
+            dev = d;
+            return;
+        }
+    }
     IMPLI_HIP(hipMalloc(&p, want));
     bytes = want;
+    dev = d;
 }
 void DevBuf::release() {
-    if (p && !ext) (void)hipFree(p);
+    if (p && !ext) {
+        bool cached = false;
+        if (bytes <= kPoolMaxBlock && dev >= 0 && pool_class(bytes) == bytes) {
+            std::lock_guard<std::mutex> lk(g_pool_mu);
+            DevicePool& P = g_pools[dev];
+            if (P.ready_bytes + P.pending_bytes + bytes <= kPoolMaxCached) {
+                P.pending[bytes].push_back(p);
+                P.pending_bytes += bytes;
+                cached = true;
+            }
+        }
+        if (!cached) (void)hipFree(p);
+    }
     p = nullptr;
     bytes = 0;
     ext = false;
+    dev = -1;
+}
+void DevBuf::pool_stats(size_t out[2]) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    out[0] = out[1] = 0;
+    for (auto& kv : g_pools) {
+        out[0] += kv.second.ready_bytes;
+        out[1] += kv.second.pending_bytes;
+    }
+}
+void DevBuf::pool_trim() {
+    int d = 0;
+    IMPLI_HIP(hipGetDevice(&d));
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pools.find(d);
+    if (it == g_pools.end()) return;
+    IMPLI_HIP(hipDeviceSynchronize());
+    for (auto* m : {&it->second.ready, &it->second.pending})
+        for (auto& kv : *m)
+            for (void* b : kv.second) (void)hipFree(b);
+    g_pools.erase(it);
 }
 
 void HostBuf::reserve(size_t n) {
@@ -73,44 +163,86 @@ void Engine::brick_stats(int64_t out[3], hipStream_t s) {
     out[2] = filled;
 }
 
-Engine::Engine() {
+// The rabbit table (+ block min / max) and the marching-cubes case table are the same for every
+// engine: built once per device and shared (an object stream creates one engine per object: each used
+// to rebuild both on the host and upload them with blocking copies).  They live as long as the process.
+namespace {
+struct SharedTables {
+    void* rabbit = nullptr;
+    size_t rabbit_bytes = 0;
+    void* cases = nullptr;
+};
+std::mutex g_tables_mu;
+std::map<int, SharedTables> g_tables;   // per device
+float2 g_tab_range{0.f, 0.f};
 
-    // rabbit table + the object's trailing members (F8d: out-of-table reads) + zero padding
-    std::vector<float> tab(dev::kRabbitPadded, 0.f);
-    for (int i = 0; i < dev::kRabbitN; ++i) std::memcpy(&tab[i], &IMPLI_RABBIT_BITS[i], 4);
-    const uint32_t tail[4] = {IMPLI_RABBIT_GRID_SIZE_BITS, IMPLI_RABBIT_ORIGIN_X_BITS, IMPLI_RABBIT_ORIGIN_Y_BITS,
-                              IMPLI_RABBIT_ORIGIN_Z_BITS};
-    std::memcpy(&tab[dev::kRabbitN], tail, sizeof tail);
-    tab_range_ = float2{tab[0], tab[0]};
-    for (float v : tab) {
-        tab_range_.x = v < tab_range_.x ? v : tab_range_.x;
-        tab_range_.y = v > tab_range_.y ? v : tab_range_.y;
-    }
-    // block min / max of the eight reads at every flat index (ifunc_device.hpp kRabbitBlockMinMax)
-    const int sx = IMPLI_RABBIT_NX, sxy = IMPLI_RABBIT_NX * IMPLI_RABBIT_NY;
-    std::vector<float> all(tab);
-    all.resize((size_t)dev::kRabbitPadded * 3, 0.f);
-    for (int b = 0; b < dev::kRabbitPadded; ++b) {
-        float lo = INFINITY, hi = -INFINITY;
-        for (int d : {0, 1, sx, sx + 1, sxy, sxy + 1, sxy + sx, sxy + sx + 1}) {
-            const float v = b + d < dev::kRabbitPadded ? tab[b + d] : 0.f;
-            lo = v < lo ? v : lo;
-            hi = v > hi ? v : hi;
+const std::vector<float>& rabbit_host_table() {
+    static const std::vector<float> all = [] {
+        // rabbit table + the object's trailing members (F8d: out-of-table reads) + zero padding
+        std::vector<float> tab(dev::kRabbitPadded, 0.f);
+        for (int i = 0; i < dev::kRabbitN; ++i) std::memcpy(&tab[i], &IMPLI_RABBIT_BITS[i], 4);
+        const uint32_t tail[4] = {IMPLI_RABBIT_GRID_SIZE_BITS, IMPLI_RABBIT_ORIGIN_X_BITS, IMPLI_RABBIT_ORIGIN_Y_BITS,
+                                  IMPLI_RABBIT_ORIGIN_Z_BITS};
+        std::memcpy(&tab[dev::kRabbitN], tail, sizeof tail);
+        g_tab_range = float2{tab[0], tab[0]};
+        for (float v : tab) {
+            g_tab_range.x = v < g_tab_range.x ? v : g_tab_range.x;
+            g_tab_range.y = v > g_tab_range.y ? v : g_tab_range.y;
         }
-        all[dev::kRabbitPadded + 2 * b] = lo;
-        all[dev::kRabbitPadded + 2 * b + 1] = hi;
+        // block min / max of the eight reads at every flat index (ifunc_device.hpp kRabbitBlockMinMax)
+        const int sx = IMPLI_RABBIT_NX, sxy = IMPLI_RABBIT_NX * IMPLI_RABBIT_NY;
+        std::vector<float> a(tab);
+        a.resize((size_t)dev::kRabbitPadded * 3, 0.f);
+        for (int b = 0; b < dev::kRabbitPadded; ++b) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int d : {0, 1, sx, sx + 1, sxy, sxy + 1, sxy + sx, sxy + sx + 1}) {
+                const float v = b + d < dev::kRabbitPadded ? tab[b + d] : 0.f;
+                lo = v < lo ? v : lo;
+                hi = v > hi ? v : hi;
+            }
+            a[dev::kRabbitPadded + 2 * b] = lo;
+            a[dev::kRabbitPadded + 2 * b + 1] = hi;
+        }
+        return a;
+    }();
+    return all;
+}
+}  // namespace
+
+Engine::Engine(hipStream_t setup) {
+    int dev = 0;
+    IMPLI_HIP(hipGetDevice(&dev));
+    {
+        std::lock_guard<std::mutex> lk(g_tables_mu);
+        SharedTables& t = g_tables[dev];
+        if (!t.rabbit) {
+            const std::vector<float>& all = rabbit_host_table();
+            CaseInfo cases[256];
+            build_case_table(cases);
+            void* r = nullptr;
+            void* c = nullptr;
+            IMPLI_HIP(hipMalloc(&r, all.size() * sizeof(float)));
+            IMPLI_HIP(hipMalloc(&c, sizeof cases));
+            IMPLI_HIP(hipMemcpy(r, all.data(), all.size() * sizeof(float), hipMemcpyHostToDevice));
+            IMPLI_HIP(hipMemcpy(c, cases, sizeof cases, hipMemcpyHostToDevice));
+            t.rabbit = r;
+            t.rabbit_bytes = all.size() * sizeof(float);
+            t.cases = c;
+        }
+        rabbit_.attach(t.rabbit, t.rabbit_bytes);
+        cases_.attach(t.cases, sizeof(CaseInfo) * 256);
+        tab_range_ = g_tab_range;
     }
-    rabbit_.reserve(all.size() * sizeof(float));
-    IMPLI_HIP(hipMemcpy(rabbit_.p, all.data(), all.size() * sizeof(float), hipMemcpyHostToDevice));
-    CaseInfo cases[256];
-    build_case_table(cases);
-    cases_.reserve(sizeof cases);
-    IMPLI_HIP(hipMemcpy(cases_.p, cases, sizeof cases, hipMemcpyHostToDevice));
     prog_.reserve(sizeof(Program));
     counters_.reserve(kCounterWords * sizeof(uint32_t));
-    IMPLI_HIP(hipMemset(counters_.p, 0, kCounterWords * sizeof(uint32_t)));   // [13] starts at 0 (grid.hpp)
     offsets_.reserve(16);
-    IMPLI_HIP(hipMemset(offsets_.p, 0, 16));
+    if (setup) {
+        IMPLI_HIP(hipMemsetAsync(counters_.p, 0, kCounterWords * sizeof(uint32_t), setup));   // [13] starts at 0 (grid.hpp)
+        IMPLI_HIP(hipMemsetAsync(offsets_.p, 0, 16, setup));
+    } else {
+        IMPLI_HIP(hipMemset(counters_.p, 0, kCounterWords * sizeof(uint32_t)));
+        IMPLI_HIP(hipMemset(offsets_.p, 0, 16));
+    }
 }
 
 void Engine::set_offsets(uint32_t voff, uint32_t foff) {
@@ -162,7 +294,10 @@ Engine::~Engine() {
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
-    release_jit();   // (hipFree above waited for the device: the modules' last launches are done)
+    // the buffers went to the pool (no hipFree and its implicit synchronisation): the modules'
+    // last launches must be done before release_jit may unload them
+    if (jit_slot_ || bake_slot_ || pt_slot_ || pt_bake_slot_) (void)hipDeviceSynchronize();
+    release_jit();
 }
 
 void Engine::release_jit() {
@@ -190,13 +325,19 @@ int program_vdepth(const Program& p) {
     return best;
 }
 
-void Engine::set_object(const Program& prog) {
+void Engine::set_object(const Program& prog, const Program* d_prog) {
     // the same object again (repeated builds): keep its modules and its eval count
-    if (have_object_ && std::memcmp(&prog, &prog_host_, sizeof(Program)) == 0) return;
+    if (have_object_ && !d_prog && std::memcmp(&prog, &prog_host_, sizeof(Program)) == 0) return;
     // the engine's kernels run on caller streams (often non-blocking): nothing in flight may still
-    // read the program being replaced
-    IMPLI_HIP(hipDeviceSynchronize());
-    IMPLI_HIP(hipMemcpy(prog_.p, &prog, sizeof(Program), hipMemcpyHostToDevice));
+    // read the program being replaced (a fresh engine has launched nothing)
+    if (have_object_ || have_grid_) IMPLI_HIP(hipDeviceSynchronize());
+    if (d_prog) {
+        prog_.attach(const_cast<Program*>(d_prog), sizeof(Program));
+    } else {
+        if (prog_.ext) prog_.release();
+        prog_.reserve(sizeof(Program));
+        IMPLI_HIP(hipMemcpy(prog_.p, &prog, sizeof(Program), hipMemcpyHostToDevice));
+    }
     depth_ = prog.max_depth;
     vdepth_ = program_vdepth(prog);
     n_csg_ = prog.n_csg;
@@ -213,7 +354,13 @@ void Engine::set_grid(int R, const float box[6], int rank, int nranks) {
     set_slab(R, box, slab_partition(R, rank, nranks));   // one halo layer below (owner rule)
 }
 
-void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool probe_only) {
+void Engine::arm_merged() {
+    if (!have_grid_ || !have_object_ || probe_only_) throw InputError("engine: arm_merged needs an object and a grid");
+    if (mark_id_ == 0) mark_id_ = 1;   // the unit marks were reset to 0 with the grid
+    marks_valid_ = true;
+}
+
+void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool probe_only, hipStream_t setup) {
     const SlabRange sr = slab_range(R, sr_in.z0, sr_in.z1);   // validated, 32-bit limits checked
     // the same grid and object again (repeated builds of build_geometry): every buffer keeps its size
     // and its invariants (umark ids only grow, the sign pieces past a row's last brick stay 0,
@@ -225,8 +372,14 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
         return;
     key_R_ = -1;   // set again once the buffers below are valid
     // the buffers below are reset on the null stream, which a non-blocking caller stream does not
-    // order against: no earlier kernel may still run, and the resets finish before the next launch
-    IMPLI_HIP(hipDeviceSynchronize());
+    // order against: no earlier kernel may still run (a fresh engine has launched none), and the
+    // resets finish before the next launch
+    const bool fresh_async = setup && !have_grid_;   // an object stream's fresh engine (see engine.hpp)
+    if (have_grid_) IMPLI_HIP(hipDeviceSynchronize());
+    auto zero = [&](void* p, size_t n) {
+        if (fresh_async) IMPLI_HIP(hipMemsetAsync(p, 0, n, setup));
+        else IMPLI_HIP(hipMemset(p, 0, n));
+    };
     grid_ = make_grid(R, box, sr.z0 - sr.halo, sr.z1, sr.z0);
     probe_only_ = probe_only;
     modes_.reserve((size_t)(brick_grid(grid_).n_bricks + 1) * sizeof(uint64_t));
@@ -241,12 +394,13 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     if (n_chunks(grid_) > kMaxChunks) throw InputError("grid: more than 8189 cells per row");
     const size_t mark_bytes = (size_t)(n_units(grid_) * n_chunks(grid_) + 1) * sizeof(uint32_t);
     umark_.reserve(mark_bytes);
-    IMPLI_HIP(hipMemset(umark_.p, 0, mark_bytes));   // ids start at 1
+    zero(umark_.p, mark_bytes);   // ids start at 1
     marks_valid_ = false;
+    mark_id_ = 0;
     const size_t sign_bytes = (size_t)grid_.n * (grid_.fz1 - grid_.fz0) * sign_row_words(grid_) * sizeof(uint64_t);
     signs_.reserve(sign_bytes + 64);
     // the pieces past the last brick of a row are never written by the pruned path: keep them 0
-    IMPLI_HIP(hipMemset(signs_.p, 0, sign_bytes + 64));
+    zero(signs_.p, sign_bytes + 64);
     if (probe_only) {   // interval_pass / listed_per_layer only
         IMPLI_HIP(hipDeviceSynchronize());
         have_grid_ = true;
@@ -255,8 +409,9 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     const size_t field_bytes = (size_t)field_samples(grid_) * sizeof(float);   // brick-major (grid.hpp)
     field_.reserve(field_bytes);
     // the pruned eval writes only the listed bricks: the rest of the field reads as 0, not as
-    // whatever the allocation held (deterministic read_field; nothing on the path reads it)
-    IMPLI_HIP(hipMemset(field_.p, 0, field_bytes));
+    // whatever the allocation held (deterministic read_field; nothing on the path reads it, so an
+    // object stream's engines skip it)
+    if (!fresh_async) IMPLI_HIP(hipMemset(field_.p, 0, field_bytes));
     unit_cnt_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint4));
     unit_part_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint32_t));
     unit_cmask_.reserve((size_t)(n_groups(grid_) * kGroupUnits + 1) * sizeof(uint32_t));
@@ -268,7 +423,7 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     if (grid_.cz_emit > grid_.cz0) vid_halo_.reserve((size_t)m2 * 3 * sizeof(uint32_t));   // the halo layer's cells
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
                                (uint32_t)std::min<int64_t>(6 * m2, 1u << 31), 0});
-    IMPLI_HIP(hipDeviceSynchronize());
+    if (!fresh_async) IMPLI_HIP(hipDeviceSynchronize());
     have_grid_ = true;
     key_R_ = R;
     key_z0_ = sr.z0;

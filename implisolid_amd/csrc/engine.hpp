@@ -18,11 +18,15 @@ struct HipError : std::runtime_error {
 void hip_check(hipError_t e, const char* what);
 #define IMPLI_HIP(x) ::impli::hip_check((x), #x)
 
-// grow-only device buffer
+// grow-only device buffer.  Its memory comes from a per-device caching pool (engine.hip): a released
+// block is reused for a later reserve of its size class only after a device synchronisation (the
+// guarantee hipFree's implicit synchronisation gave), so an object stream's engines, created and
+// destroyed batch after batch, allocate nothing after the first batch.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
     bool ext = false;   // caller-owned memory (attach): never freed; a reserve past it allocates anew
+    int dev = -1;       // the device the block was allocated on (its pool)
     void reserve(size_t n);
     void release();
     void attach(void* q, size_t n) {
@@ -31,6 +35,10 @@ struct DevBuf {
         bytes = n;
         ext = true;
     }
+    // the pool's cached bytes on every device: [0] reusable, [1] awaiting a device synchronisation
+    static void pool_stats(size_t out[2]);
+    // free every cached block of the current device (synchronises it)
+    static void pool_trim();
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -62,15 +70,24 @@ std::vector<int> cuts_from_layer_work(const std::vector<int64_t>& listed_per_lay
 
 class Engine {
 public:
-    Engine();
+    // setup: the counter block's reset goes on this stream (an object stream's fresh engines, set up
+    // back to back on it without device synchronisations), else on the null stream
+    explicit Engine(hipStream_t setup = nullptr);
     ~Engine();
 
     // object + grid.  rank/nranks select a Z-slab of cell layers (rank 0 of 1 = whole grid), or
     // set_slab takes the slab's layer range itself (balanced cuts, balance_cuts below).
     // probe_only: allocate only what the interval pass needs (interval_pass, listed_per_layer).
-    void set_object(const Program& prog);
+    // d_prog: the program already on the device (an object stream uploads all its programs at once;
+    // the engine reads it there, it must outlive the engine's use)
+    void set_object(const Program& prog, const Program* d_prog = nullptr);
     void set_grid(int R, const float box[6], int rank, int nranks);
-    void set_slab(int R, const float box[6], const SlabRange& sr, bool probe_only = false);
+    // setup: a fresh engine's buffer resets go on this stream, without device synchronisations
+    // (an object stream sets up its engines back to back; every later launch of theirs is on it)
+    void set_slab(int R, const float box[6], const SlabRange& sr, bool probe_only = false, hipStream_t setup = nullptr);
+    // an object stream's merged launches without a warm eval of this engine: the merged fill writes
+    // its unit marks (id 1) from the first pass on
+    void arm_merged();
     // the pruned eval's interval and fill passes alone (no field values), then per stored sample
     // layer of the slab: the number of bricks listed for evaluation (blocking)
     void interval_pass(hipStream_t stream);

@@ -83,6 +83,8 @@ struct ObjArgs {
 // Node-stack capacity: 9 slots for objects of depth <= 9 (the smallest capacity the compiler
 // still indexes through VGPR index mode rather than select chains; the eval then runs four waves
 // per SIMD, 128 VGPRs and a small spill), else the interpreter's 12 or 16
+// every object's counter block (kCounterWords words) into d_out[n][kCounterWords]
+void launch_gather_counters(const ObjArgs* d_objs, int n, uint32_t* d_out, hipStream_t s);
 void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, int vdepth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                        int sign_fill, hipStream_t s);
 constexpr int kBatchShallowDepth = 9;

@@ -393,6 +393,11 @@ __global__ __launch_bounds__(64 * kVertsWaves) void k_mc_cells_b(const CaseInfo*
         mc_cells_part(s_cw, g, objs[k].mc, e - s_pre[k], s_bits[wid], s_excl[wid]);
     }
 }
+// every object's counter block into one array (config 5's setup reads all of them with one copy)
+__global__ __launch_bounds__(256) void k_gather_counters(const ObjArgs* __restrict__ objs, int n, uint32_t* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n * kCounterWords) out[i] = objs[i / kCounterWords].counters[i % kCounterWords];
+}
 // face pass: one flat index over every object's records, a lane per record
 __global__ __launch_bounds__(256) void k_mc_faces_b(const CaseInfo* __restrict__ cases, const ObjArgs* __restrict__ objs,
                                                     int n, GridDesc g) {
@@ -448,6 +453,10 @@ namespace impli {
 // grids of the flat merged vertex / face kernels
 constexpr unsigned kBatchCellBlocks = 4096, kBatchFaceBlocks = 2048;
 constexpr int kBatchCountLanes = 128;
+
+void launch_gather_counters(const ObjArgs* d_objs, int n, uint32_t* d_out, hipStream_t s) {
+    if (n > 0) k_gather_counters<<<(unsigned)((n * kCounterWords + 255) / 256), 256, 0, s>>>(d_objs, n, d_out);
+}
 
 void launch_batch_mc(const ObjArgs* d_objs, int n, const CaseInfo* d_cases, const GridDesc& g, hipStream_t s) {
     const int64_t ng = n_groups(g), nu = n_units(g);
