@@ -330,6 +330,7 @@ def make_geometry(shape, mc_settings):
     """Polygonise an MP5 shape; returns (verts float32 [V,3], faces int32 [F,3]) host copies."""
     L = lib()
     L.finish_geometry()             # implisolid_main.js:214-217
+    _VIEW_GEN[0] += 1   # earlier make_geometry_views arrays are stale from here on
     L.build_geometry(_s(shape), _s(mc_settings))
     _check()
     nv, nf = L.get_v_size(), L.get_f_size()
@@ -343,12 +344,18 @@ def make_geometry(shape, mc_settings):
     return v, f
 
 
+_VIEW_GEN = [0]   # build_geometry calls through make_geometry_views: the generation of its views
+
+
 def make_geometry_views(shape, mc_settings):
     """build_geometry as the reference's front end reads it (implisolid_main.js:227-237): the mesh is
-    left in the library's result buffers (pinned host memory) and returned as numpy views over
-    get_v_ptr / get_f_ptr -- no copy.  The views are valid until the next build_geometry or
-    finish_geometry; copy them to keep them."""
+    left in the library's result buffers (pinned host memory) and returned as read-only numpy views
+    over get_v_ptr / get_f_ptr -- no copy.  The views are valid until the next build_geometry or
+    finish_geometry (a larger next build frees the pinned buffers they point into): keep them with
+    copy_geometry_views(v, f), which refuses stale views; views_current(v) tells whether a view
+    still holds the last build's mesh."""
     L = lib()
+    _VIEW_GEN[0] += 1
     L.finish_geometry()
     L.build_geometry(_s(shape), _s(mc_settings))
     _check()
@@ -357,7 +364,32 @@ def make_geometry_views(shape, mc_settings):
         else np.zeros((0, 3), np.float32)
     f = np.ctypeslib.as_array(ctypes.cast(L.get_f_ptr(), ctypes.POINTER(ctypes.c_int32)), shape=(nf, 3)) if nf \
         else np.zeros((0, 3), np.int32)
+    v, f = v.view(_GeometryView), f.view(_GeometryView)
+    for a in (v, f):
+        a.flags.writeable = False
+        a._gen = _VIEW_GEN[0]
     return v, f
+
+
+class _GeometryView(np.ndarray):
+    """A read-only numpy view into the library's result buffers (make_geometry_views), tagged with the
+    build generation that made it."""
+    _gen = -1
+
+    def __array_finalize__(self, obj):
+        self._gen = getattr(obj, "_gen", -1)
+
+
+def views_current(a):
+    """True while a make_geometry_views array still holds the last build's mesh."""
+    return getattr(a, "_gen", -1) == _VIEW_GEN[0]
+
+
+def copy_geometry_views(v, f):
+    """Owned copies of make_geometry_views' arrays; raises if another build has replaced them."""
+    if not (views_current(v) and views_current(f)):
+        raise ImplisolidError("geometry views are stale: a later build_geometry replaced the mesh they point into")
+    return np.array(v, dtype=np.float32, copy=True), np.array(f, dtype=np.int32, copy=True)
 
 
 def make_geometry_progressive(shape, mc_settings, call_specs=None):
@@ -377,6 +409,7 @@ def make_geometry_progressive(shape, mc_settings, call_specs=None):
     L.finish_geometry()
     L.implisolid_set_progress_callback(cb, None)
     try:
+        _VIEW_GEN[0] += 1
         L.build_geometry_u(_s(shape), _s(mc_settings), _s(call_specs if call_specs is not None else {}))
     finally:
         L.implisolid_set_progress_callback(PROGRESS_CALLBACK(), None)

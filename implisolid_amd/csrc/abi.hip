@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <map>
 #include <memory>
 #include <string>
@@ -708,8 +709,21 @@ int get_pointset_size(char* id) {
 }
 
 void about(void) {
-    // no __DATE__ / __TIME__: the library is built reproducibly (the round's profiles name its hash)
+    // mcc2.cpp:574-576 prints __DATE__ __TIME__ on its second line.  The library is built
+    // reproducibly (the round's profiles name its hash): the Makefile passes SOURCE_DATE_EPOCH (the
+    // reproducible-builds convention) when it is set, formatted as __DATE__ __TIME__ are (UTC)
+#ifdef IMPLI_SOURCE_DATE_EPOCH
+    {
+        const time_t t = (time_t)IMPLI_SOURCE_DATE_EPOCH;
+        struct tm u;
+        gmtime_r(&t, &u);
+        char buf[64];
+        std::strftime(buf, sizeof buf, "%b %e %Y %H:%M:%S", &u);
+        std::fprintf(stderr, "Build Info: \n%s\n", buf);
+    }
+#else
     std::fprintf(stderr, "Build Info: \nreproducible build\n");
+#endif
     std::fprintf(stderr, "implisolid-mi355x: HIP gfx950 polygoniser (eval + marching cubes + OB02)\n");
     std::fprintf(stderr, "CONFIG: ROOT_TOLERANCE=%g \n", (double)(float)(0.001 / 10.0));
 }

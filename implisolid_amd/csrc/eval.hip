@@ -706,12 +706,23 @@ void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, int vdepth, cons
     // stack capacity: kBatchShallowDepth slots for shallow objects (kernels.hpp), else the
     // interpreter's floor (12: VGPR index mode) or 16; the shallow class's value stacks by their own
     // depth (6 covers every config-5 object of that class)
+    // the value stacks (private arrays of V slots) must hold the deepest program's values: vdepth is
+    // the unpruned run's high-water mark (Engine::vdepth, program_vdepth), and a pruned run skips an
+    // operand subtree together with its CSG node's pop, so it never holds more (checked
+    // here rather than assumed -- a future n-ary node would otherwise overflow them silently)
+    auto need = [&](int V, int D) {
+        if (vdepth > V || depth > D)
+            throw std::runtime_error("merged eval: a program's stacks exceed the kernel's (" + std::to_string(vdepth) + " values, depth " +
+                                     std::to_string(depth) + ")");
+    };
     if (depth <= kBatchShallowDepth) {
-        if (batch_vstack() && vdepth <= 6) IMPLI_BATCH_EVAL(kBatchShallowDepth, 4, 6);
-        else IMPLI_BATCH_EVAL(kBatchShallowDepth, 4, kBatchShallowDepth);
+        if (batch_vstack() && vdepth <= 6) { need(6, kBatchShallowDepth); IMPLI_BATCH_EVAL(kBatchShallowDepth, 4, 6); }
+        else { need(kBatchShallowDepth, kBatchShallowDepth); IMPLI_BATCH_EVAL(kBatchShallowDepth, 4, kBatchShallowDepth); }
     } else if (depth <= 12) {
+        need(12, 12);
         IMPLI_BATCH_EVAL(12, 2, 12);
     } else {
+        need(16, 16);
         IMPLI_BATCH_EVAL(16, 1, 16);
     }
 #undef IMPLI_BATCH_EVAL

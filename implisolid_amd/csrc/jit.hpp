@@ -54,6 +54,8 @@ public:
     // release() drops it; the cache holds at most max_modules() slots and, past that, unloads the
     // least recently requested finished slots nobody references (IMPLISOLID_JIT_MAX_MODULES,
     // default 1024; a long-lived service polygonising ever-new objects keeps bounded device memory).
+    // Unloads run at trim() (set_object, wait_idle: device already synchronised); request() itself
+    // evicts only when the cache is 4x over the bound, which is therefore the hard bound in between.
     struct Slot {
         std::atomic<bool> ready{false}, failed{false};
         Kernels k;

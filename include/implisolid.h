@@ -239,7 +239,10 @@ void implisolid_jit_wait(void);
 void implisolid_jit_stats(int32_t out[4], double* compile_seconds);
 /* bound on the loaded tree modules (IMPLISOLID_JIT_MAX_MODULES, default 1024, at least 8): past it
  * the least recently requested modules no engine holds are unloaded (a later request recompiles or
- * reads the disk cache).  Replaces nothing in mcc2.cpp: the reference interprets its trees. */
+ * reads the disk cache).  Unloads happen at trim points -- set_object and implisolid_jit_wait, where
+ * the device is synchronised anyway -- so between them the loaded modules may exceed the bound; a
+ * request evicts on its own only once the cache is 4x over it (4 n modules is the hard bound).
+ * Replaces nothing in mcc2.cpp: the reference interprets its trees. */
 void implisolid_set_jit_max_modules(int n);
 /* [modules resident, bound, modules unloaded so far] */
 void implisolid_jit_modules(int32_t out[3]);

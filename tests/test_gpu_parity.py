@@ -1623,6 +1623,21 @@ def test_multiprocess_slabs_gloo(impli, oracle, tmp_path, world, balanced):
         assert len(g["cuts"]) == world + 1
 
 
+def test_geometry_views_generation(impli):
+    """make_geometry_views' arrays are read-only views into the library's result buffers, valid until
+    the next build: copy_geometry_views copies current ones and refuses stale ones."""
+    from implisolid_amd import scenes
+    v, f = impli.make_geometry_views(*scenes.config1())
+    assert not v.flags.writeable and impli.views_current(v) and impli.views_current(f[1:])
+    vc, fc = impli.copy_geometry_views(v, f)
+    v2, f2 = impli.make_geometry(*scenes.config1())
+    assert np.array_equal(vc, v2) and np.array_equal(fc, f2)
+    impli.make_geometry_views(*scenes.config2(48))
+    assert not impli.views_current(v)
+    with pytest.raises(impli.ImplisolidError):
+        impli.copy_geometry_views(v, f)
+
+
 def test_shard_handles_bounded(impli):
     """distributed.shard_handle keeps one handle per (device, slot): the same object reuses it, another
     object closes it (its buffers and streams freed), release_shards() closes the rest."""
