@@ -603,9 +603,12 @@ def main():
     def run_batch(objs, jit_mode, n_streams):
         I.set_jit(jit_mode)
         setup_cold = None
+        # the objects arrive as JSON text, the form the reference's polygonize entry takes them in
+        # (the generator's dicts serialised before the clock starts)
+        texts = [json.dumps(o[0]) for o in objs]
         try:
             t0 = time.perf_counter()
-            batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=n_streams)
+            batch = I.Batch(texts, objs[0][1], n_streams=n_streams)
             setup_s = time.perf_counter() - t0
             if n_streams == 0:
                 # merged launches: the stream's next batch of objects in this process -- created again,
@@ -615,7 +618,7 @@ def main():
                 batch.close()
                 setup_cold = setup_s
                 t0 = time.perf_counter()
-                batch = I.Batch([o[0] for o in objs], objs[0][1], n_streams=n_streams)
+                batch = I.Batch(texts, objs[0][1], n_streams=n_streams)
                 setup_s = time.perf_counter() - t0
         finally:
             I.set_jit(2)
@@ -642,8 +645,8 @@ def main():
         if setup_cold is not None:
             res["setup_s_first_batch"] = round(setup_cold, 4)
             res["objects_per_s_incl_setup_first_batch"] = round(batch.n / (ms5 * 1e-3 + setup_cold), 1)
-            res["setup_note"] = ("setup_s: implisolid_batch_create of the 64 objects as the stream's next batch in this "
-                                 "process (programs parsed, engines set up, one merged pass sizing the outputs; the "
+            res["setup_note"] = ("setup_s: implisolid_batch_create of the 64 objects (JSON text) as the stream's next "
+                                 "batch in this process (programs parsed, engines set up, one merged pass sizing the outputs; the "
                                  "device-memory pool serves the previous batch's buffers); setup_s_first_batch: the "
                                  "process's first batch (buffers from hipMalloc)")
         n_streams = batch.n_streams
@@ -1161,7 +1164,33 @@ def main():
         legs["config5_cpu_baseline"] = round(time.perf_counter() - t0, 2)
     out["roofline"]["copy_attainable"] = copy_attainable(dev)
     out["legs_wall_s"] = dict(legs, total=round(time.perf_counter() - T_START, 2))
+    # child processes still alive at the end (the config-5 CPU workers are reaped; the driver has
+    # reported one process left behind after the bench): named here, if any
+    try:
+        import psutil
+        out["children_at_exit"] = [" ".join(c.cmdline()[:3]) for c in psutil.Process().children(recursive=True)]
+    except Exception as exc:   # psutil missing or a child gone mid-listing
+        out["children_at_exit"] = "unavailable: %s" % exc
+    # the compact summary last, so a log's tail always holds it (the driver keeps the last 8 KB)
+    summ = {"value": out["value"], "unit": out["unit"], "ms_per_step": out["ms_per_step"], "n_gpus": world,
+            "scaling": out["scaling"], "dominant_kernel_frac": out["roofline"].get("frac")}
+    for k in ("strong", "weak"):
+        if k in out:
+            summ[k] = {"value": out[k]["value"], "ms_per_step": out[k]["ms_per_step"]}
+    if "config5" in out:
+        c = out["config5"]
+        summ["config5"] = {k: c.get(k) for k in ("objects_per_s", "objects_per_s_incl_setup",
+                                                 "objects_per_s_incl_setup_first_batch", "ms_per_stream")}
+    if "ob02" in out:
+        summ["ob02_build_ms"] = {k: v.get("build_geometry_ms") for k, v in out["ob02"].items() if isinstance(v, dict)}
+        summ["ob02_first_build_ms"] = {k: v.get("first_build_ms") for k, v in out["ob02"].items() if isinstance(v, dict)}
+    if "ob02_sharded_estimate" in out:
+        e = out["ob02_sharded_estimate"]
+        summ["ob02_8shard_estimate_ms"] = {"r256": [e.get("estimate_ms_8"), e.get("single_ms")],
+                                           "r512": [e.get("r512", {}).get("estimate_ms_8"), e.get("r512", {}).get("single_ms")]}
+    out["summary"] = summ
     print(json.dumps(out), flush=True)
+    print("bench summary: " + json.dumps(summ), file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

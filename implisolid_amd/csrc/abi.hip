@@ -1048,6 +1048,7 @@ static int batch_groups() {
 struct implisolid_batch {
     DevBuf progs;                        // merged: every object's Program, one upload (the engines read them)
     DevBuf counts;                       // merged: every row's counter block, gathered for one read-back
+    DevBuf resets;                       // merged: the fresh engines' buffer resets (ZeroPiece list)
     std::vector<std::unique_ptr<Engine>> engines;
     bool merged = false;                 // one launch per stage for all objects (ObjArgs rows)
     DevBuf objs;                         // merged: ObjArgs[n] on the device, shallow objects first
@@ -1175,6 +1176,7 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             return d;
         };
         auto tp = std::chrono::steady_clock::now();
+        std::vector<ZeroPiece> pieces;   // merged: uploaded below, read until the first pass's sync
         if (b->merged) {
             // merged launches: the programs in one upload, every engine's buffers set up on s0 without
             // device synchronisations (fresh engines; the pool serves them without hipMalloc from the
@@ -1183,8 +1185,9 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             b->progs.reserve((size_t)n * sizeof(Program));
             IMPLI_HIP(hipMemcpyAsync(b->progs.p, progs.data(), (size_t)n * sizeof(Program), hipMemcpyHostToDevice, s0));
             const SlabRange whole = slab_partition(st.resolution, 0, 1);
+            std::vector<ZeroRange> resets;   // every engine's buffer resets, cleared by one launch below
             for (int i = 0; i < n; ++i) {
-                b->engines.emplace_back(new Engine(s0));
+                b->engines.emplace_back(new Engine(s0, &resets));
                 Engine& E = *b->engines.back();
                 if (timing) ph[0] += tick(tp);
                 E.set_hot_bake(false);
@@ -1192,8 +1195,21 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
                 if (timing) ph[1] += tick(tp);
                 E.set_slab(st.resolution, st.box, whole, false, s0);
                 E.arm_merged();
+                E.detach_resets();
                 if (timing) ph[2] += tick(tp);
             }
+            for (const ZeroRange& r : resets) {
+                if ((uintptr_t)r.p % 16 != 0) {   // (pool blocks are hipMalloc'd: never taken)
+                    IMPLI_HIP(hipMemsetAsync(r.p, 0, r.n, s0));
+                    continue;
+                }
+                for (size_t o = 0; o < r.n; o += kZeroPieceBytes)
+                    pieces.push_back({(uint64_t)(uintptr_t)r.p + o, (uint32_t)std::min<size_t>(kZeroPieceBytes, r.n - o), 0});
+            }
+            b->resets.reserve(std::max<size_t>(pieces.size(), 1) * sizeof(ZeroPiece));
+            IMPLI_HIP(hipMemcpyAsync(b->resets.p, pieces.data(), pieces.size() * sizeof(ZeroPiece), hipMemcpyHostToDevice, s0));
+            launch_zero_pieces(b->resets.as<ZeroPiece>(), (int)pieces.size(), s0);
+            if (timing) ph[2] += tick(tp);
         } else {
             for (int i = 0; i < n; ++i) {   // warm run: JIT lookup, output capacities from the real counts
                 b->engines.emplace_back(new Engine());

@@ -209,7 +209,7 @@ const std::vector<float>& rabbit_host_table() {
 }
 }  // namespace
 
-Engine::Engine(hipStream_t setup) {
+Engine::Engine(hipStream_t setup, std::vector<ZeroRange>* resets) : resets_(resets) {
     int dev = 0;
     IMPLI_HIP(hipGetDevice(&dev));
     {
@@ -236,7 +236,10 @@ Engine::Engine(hipStream_t setup) {
     prog_.reserve(sizeof(Program));
     counters_.reserve(kCounterWords * sizeof(uint32_t));
     offsets_.reserve(16);
-    if (setup) {
+    if (resets_) {
+        resets_->push_back({counters_.p, kCounterWords * sizeof(uint32_t)});
+        resets_->push_back({offsets_.p, 16});
+    } else if (setup) {
         IMPLI_HIP(hipMemsetAsync(counters_.p, 0, kCounterWords * sizeof(uint32_t), setup));   // [13] starts at 0 (grid.hpp)
         IMPLI_HIP(hipMemsetAsync(offsets_.p, 0, 16, setup));
     } else {
@@ -290,7 +293,7 @@ Engine::~Engine() {
         if (e) (void)hipEventDestroy(e);
     if (ev_counts_) (void)hipEventDestroy(ev_counts_);
     if (ev_verts_) (void)hipEventDestroy(ev_verts_);
-    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &claimed_, &vidc_, &vid_halo_, &items_,
+    DevBuf* all[] = {&offsets_, &cmodes_, &ccls_, &clist_, &modes_, &cls_, &fill_, &blist_, &prog_, &rabbit_, &cases_, &field_, &signs_, &scan_blk_, &unit_cnt_, &unit_part_, &unit_cmask_, &ulist_, &upart_, &umark_, &counters_, &lmodes_, &claimed_, &vid_,
                      &records_, &verts_, &faces_};
     for (auto* b : all) b->release();
     for (auto& b : scratch_) b.release();
@@ -377,7 +380,8 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     const bool fresh_async = setup && !have_grid_;   // an object stream's fresh engine (see engine.hpp)
     if (have_grid_) IMPLI_HIP(hipDeviceSynchronize());
     auto zero = [&](void* p, size_t n) {
-        if (fresh_async) IMPLI_HIP(hipMemsetAsync(p, 0, n, setup));
+        if (fresh_async && resets_) resets_->push_back({p, n});
+        else if (fresh_async) IMPLI_HIP(hipMemsetAsync(p, 0, n, setup));
         else IMPLI_HIP(hipMemset(p, 0, n));
     };
     grid_ = make_grid(R, box, sr.z0 - sr.halo, sr.z1, sr.z0);
@@ -419,8 +423,9 @@ void Engine::set_slab(int R, const float box[6], const SlabRange& sr_in, bool pr
     ulist_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint4));
     upart_.reserve((size_t)(n_units(grid_) * kMaxParts + 1) * sizeof(uint32_t));
     const int64_t m2 = (int64_t)grid_.m * grid_.m;
-    items_.reserve((size_t)(n_rows(grid_) * n_chunks(grid_) + 1) * sizeof(uint4));
-    if (grid_.cz_emit > grid_.cz0) vid_halo_.reserve((size_t)m2 * 3 * sizeof(uint32_t));   // the halo layer's cells
+    // owned-id triples by cell id (mc_types.hpp vid): 12 B per cell of the slab (1.6 GB at 512^3),
+    // written only for the ~0.3 % of cells owning a crossing edge
+    vid_.reserve((size_t)(grid_.n_cells + 1) * 3 * sizeof(uint32_t));
     ensure_capacity(SlabCounts{(uint32_t)std::min<int64_t>(6 * m2, 1u << 31), (uint32_t)std::min<int64_t>(12 * m2, 1u << 31),
                                (uint32_t)std::min<int64_t>(6 * m2, 1u << 31), 0});
     if (!fresh_async) IMPLI_HIP(hipDeviceSynchronize());
@@ -445,7 +450,6 @@ bool Engine::ensure_capacity(const SlabCounts& c) {
     grow(verts_, cap_v_, (int64_t)c.n_verts() + 1, 3 * sizeof(float));
     grow(faces_, cap_f_, (int64_t)c.n_faces() + 1, 3 * sizeof(int32_t));
     grow(records_, cap_rec_, (int64_t)c.act_total + 1, sizeof(uint4));
-    vidc_.reserve((size_t)cap_rec_ * 3 * sizeof(uint32_t));   // one owned-id triple per record
     return grew;
 }
 
@@ -464,9 +468,7 @@ MCBuffers Engine::buffers() const {
     b.umark = marks_valid_ ? umark_.as<uint32_t>() : nullptr;
     b.mark_id = mark_id_;
     b.counters = counters_.as<uint32_t>();
-    b.vidc = vidc_.as<uint32_t>();
-    b.vid_halo = grid_.cz_emit > grid_.cz0 ? vid_halo_.as<uint32_t>() : nullptr;
-    b.items = items_.as<uint4>();
+    b.vid = vid_.as<uint32_t>();
     b.records = records_.as<uint4>();
     b.verts = verts_.as<float>();
     b.faces = faces_.as<int32_t>();

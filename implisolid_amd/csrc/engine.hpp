@@ -68,11 +68,16 @@ std::vector<int> balance_cuts(const Program& prog, int R, const float box[6], in
 std::vector<int> cuts_from_layer_work(const std::vector<int64_t>& listed_per_layer, int64_t bricks_per_layer, int R,
                                       int nranks);
 
+struct ZeroRange { void* p; size_t n; };
+
 class Engine {
 public:
     // setup: the counter block's reset goes on this stream (an object stream's fresh engines, set up
-    // back to back on it without device synchronisations), else on the null stream
-    explicit Engine(hipStream_t setup = nullptr);
+    // back to back on it without device synchronisations), else on the null stream.  resets: the
+    // fresh engine's buffer resets (here and in set_slab) are appended to it instead, for the caller
+    // to clear on `setup` before any launch of the engine (launch_zero_pieces); detach_resets()
+    // once the engine is set up
+    explicit Engine(hipStream_t setup = nullptr, std::vector<ZeroRange>* resets = nullptr);
     ~Engine();
 
     // object + grid.  rank/nranks select a Z-slab of cell layers (rank 0 of 1 = whole grid), or
@@ -88,6 +93,7 @@ public:
     // an object stream's merged launches without a warm eval of this engine: the merged fill writes
     // its unit marks (id 1) from the first pass on
     void arm_merged();
+    void detach_resets() { resets_ = nullptr; }
     // the pruned eval's interval and fill passes alone (no field values), then per stored sample
     // layer of the slab: the number of bricks listed for evaluation (blocking)
     void interval_pass(hipStream_t stream);
@@ -204,6 +210,7 @@ private:
     void release_jit();   // drop the module references (after the device has synchronised)
     float2 tab_range_{0.f, 0.f};
     bool have_grid_ = false, have_object_ = false, probe_only_ = false;
+    std::vector<ZeroRange>* resets_ = nullptr;   // a fresh engine's deferred resets (constructor)
     // the grid set_slab last built its buffers for: setting the same one again keeps them
     int key_R_ = -1, key_z0_ = 0, key_z1_ = 0;
     uint64_t obj_gen_ = 0, key_obj_gen_ = ~0ull;   // set_object's generation / the one the grid's buffers hold
@@ -211,7 +218,7 @@ private:
     HostBuf hcounters_;   // pinned landing zone of read_counts / raw_counters (one small copy)
     hipEvent_t ev_counts_ = nullptr, ev_verts_ = nullptr;   // marching_cubes_to_host
     DevBuf prog_, rabbit_, cases_;
-    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, claimed_, vidc_, vid_halo_, items_, records_, verts_, faces_;
+    DevBuf offsets_, cmodes_, ccls_, clist_, modes_, cls_, fill_, blist_, field_, signs_, scan_blk_, unit_cnt_, unit_part_, unit_cmask_, ulist_, upart_, umark_, counters_, lmodes_, claimed_, vid_, records_, verts_, faces_;
     int64_t cap_v_ = 0, cap_f_ = 0, cap_rec_ = 0;
     bool timing_ = false;
     hipEvent_t ev_[11] = {};   // 0-8 phase boundaries, 9 after the coarse pass, 10 after refine

@@ -85,6 +85,11 @@ struct ObjArgs {
 // per SIMD, 128 VGPRs and a small spill), else the interpreter's 12 or 16
 // every object's counter block (kCounterWords words) into d_out[n][kCounterWords]
 void launch_gather_counters(const ObjArgs* d_objs, int n, uint32_t* d_out, hipStream_t s);
+// device byte ranges to clear, one block each (an object stream's fresh engines' resets in one
+// launch instead of a memset call per buffer); p 16-byte aligned, n <= kZeroPieceBytes
+struct ZeroPiece { uint64_t p; uint32_t n, pad; };
+constexpr uint32_t kZeroPieceBytes = 1u << 16;
+void launch_zero_pieces(const ZeroPiece* d_pieces, int n, hipStream_t s);
 void launch_batch_eval(const ObjArgs* d_objs, int n, int depth, int vdepth, const float* d_rabbit, float2 tab_range, const GridDesc& g,
                        int sign_fill, hipStream_t s);
 constexpr int kBatchShallowDepth = 9;

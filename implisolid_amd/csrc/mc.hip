@@ -281,59 +281,32 @@ __constant__ uint8_t c_edge_slot[12] = {1, 0, 1, 0, 1, 0, 1, 0, 2, 2, 2, 2};
 
 // K4: one lane per active cell, XCD-aware (the dispatcher puts block b on XCD b % 8, so XCD x takes
 // the x-th eighth of the records in cell order and the owner cells it gathers from stay in its L2).
-// A lane needs the owned-id triples of the owner cells its case uses (at most 7).  They are stored
-// densely in record order (vidc), so an owner is found by its record index:
-//   - the cell itself: its own record i;
-//   - the -x neighbour: record i - 1 (the cell just before it in cell order is non-trivial: it owns
-//     a crossing edge);
-//   - the others (rows -1, -m, -m-1): the owner's item (row, 64-cell chunk) holds the record index of
-//     its first non-trivial cell and their mask, so the index is that base plus the popcount of the
-//     mask below the owner's bit;
-//   - an owner in the halo layer (the slab's recomputed layer below its first emitted one) has no
-//     record: its triple is read by cell id from vid_halo.
-// Every address is formed before any load is used (a load under a divergent branch waits alone);
-// an owner the case does not use reads the cell's own triple.  The 12 edges' ids go to LDS, and each
-// triangle is one 12-byte store.
+// A lane needs the owned-id triples of the owner cells its case uses (at most 7): the vertex pass
+// wrote every owning cell's triple at its cell id (vid), so an owner's triple is one load at the
+// cell id L minus the owner's offset (-x: 1, -y: m, -z: m^2; an owner in the halo layer below the
+// slab's first emitted one is a cell of the slab like any other).  Round 6: this replaced the
+// record-ordered triples and the (row, 64-cell chunk) item table that found an owner's record --
+// one dependent round trip (record -> items -> triples) fewer.  Every address is formed before any
+// load is used (a load under a divergent branch waits alone); an owner the case does not use reads
+// the cell's own triple.  The 12 edges' ids go to LDS, and each triangle is one 12-byte store.
 // one active-cell record i of a slab: its triangles with the vertex ids of their corners
 __device__ __forceinline__ void face_record(const CaseInfo* s_case, uint32_t (*s_w)[256], const GridDesc& g,
                                             const MCBuffers& b, uint32_t Voff, uint32_t i) {
     const int t = threadIdx.x;
     const uint4 r = b.records[i];
-    const uint32_t L = r.x, ci = r.y, fbase = r.z, row = r.w;
+    const uint32_t L = r.x, ci = r.y, fbase = r.z;
     const CaseInfo& C = s_case[ci];
     const int ntri = C.ntri;
     if (fbase + ntri > (uint64_t)b.cap_f) { *b.overflow = 1u; return; }
     const uint32_t need = C.owners;
-    const uint32_t m = (uint32_t)g.m, nch = (uint32_t)n_chunks(g);
-    const uint32_t xs = L - row * m;   // x - 1 of the cell
-    const bool halo = g.cz_emit > g.cz0 && b.vid_halo;   // rows [0, m) are the halo layer
-    // owners 2..6: (row offset, x offset) = -y, -x-y, -z, -y-z, -x-z
-    const uint32_t drow[5] = {1u, 1u, m, m + 1u, m};
-    const uint32_t dx[5] = {0u, 1u, 0u, 0u, 1u};
-    uint4 it[5];
-    uint32_t ro[5], xo[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        const bool use = (need >> (q + 2)) & 1u;
-        ro[q] = use ? row - drow[q] : row;
-        xo[q] = use ? xs - dx[q] : xs;
-        it[q] = b.items[(size_t)ro[q] * nch + (xo[q] >> 6)];
-    }
-    const IdTriple* vidc = reinterpret_cast<const IdTriple*>(b.vidc);
+    const uint32_t m = (uint32_t)g.m, m2 = m * m;
+    // owners 1..6: -x, -y, -x-y, -z, -y-z, -x-z
+    const uint32_t d[6] = {1u, m, m + 1u, m2, m2 + m, m2 + 1u};
+    const IdTriple* vid = reinterpret_cast<const IdTriple*>(b.vid);
     IdTriple w[7];
-    w[0] = vidc[i];
-    w[1] = vidc[((need >> 1) & 1u) ? i - 1u : i];
+    w[0] = vid[L];
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        const bool use = (need >> (q + 2)) & 1u;
-        const uint64_t nt = (uint64_t)it[q].x | ((uint64_t)it[q].y << 32);
-        const uint32_t j = xo[q] & 63u;
-        const uint32_t idx = it[q].z + (uint32_t)__popcll((unsigned long long)(nt & ((1ull << j) - 1ull)));
-        const bool in_halo = use && halo && ro[q] < m;
-        const IdTriple* p = in_halo ? reinterpret_cast<const IdTriple*>(b.vid_halo) + (ro[q] * m + xo[q])
-                                    : vidc + (use && idx < (uint64_t)b.cap_rec ? idx : i);
-        w[q + 2] = *p;
-    }
+    for (int q = 0; q < 6; ++q) w[q + 1] = vid[((need >> (q + 1)) & 1u) ? L - d[q] : L];
 #pragma unroll
     for (int e = 0; e < 12; ++e) {
         const IdTriple& q = w[c_edge_owner_idx[e]];
@@ -398,6 +371,13 @@ __global__ __launch_bounds__(256) void k_gather_counters(const ObjArgs* __restri
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n * kCounterWords) out[i] = objs[i / kCounterWords].counters[i % kCounterWords];
 }
+__global__ __launch_bounds__(256) void k_zero_pieces(const ZeroPiece* __restrict__ pieces) {
+    const ZeroPiece z = pieces[blockIdx.x];
+    uint8_t* p = reinterpret_cast<uint8_t*>(z.p);
+    const uint32_t n16 = z.n / 16;
+    for (uint32_t i = threadIdx.x; i < n16; i += 256) reinterpret_cast<uint4*>(p)[i] = uint4{0, 0, 0, 0};
+    for (uint32_t i = n16 * 16 + threadIdx.x; i < z.n; i += 256) p[i] = 0;
+}
 // face pass: one flat index over every object's records, a lane per record
 __global__ __launch_bounds__(256) void k_mc_faces_b(const CaseInfo* __restrict__ cases, const ObjArgs* __restrict__ objs,
                                                     int n, GridDesc g) {
@@ -456,6 +436,10 @@ constexpr int kBatchCountLanes = 128;
 
 void launch_gather_counters(const ObjArgs* d_objs, int n, uint32_t* d_out, hipStream_t s) {
     if (n > 0) k_gather_counters<<<(unsigned)((n * kCounterWords + 255) / 256), 256, 0, s>>>(d_objs, n, d_out);
+}
+
+void launch_zero_pieces(const ZeroPiece* d_pieces, int n, hipStream_t s) {
+    if (n > 0) k_zero_pieces<<<(unsigned)n, 256, 0, s>>>(d_pieces);
 }
 
 void launch_batch_mc(const ObjArgs* d_objs, int n, const CaseInfo* d_cases, const GridDesc& g, hipStream_t s) {

@@ -113,7 +113,9 @@ __device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
 // gives every cell its vertex / face / record base; owned vertices are
 // placed from the owner cell's fx/fy/fz (the reference's first emission), their ids go beside the records (vidc)
 // (halo cells, below the slab's first emitted layer: ids only), active cells get a record
-// {L, ci, face base}.  (A separate one-lane-per-active-cell position pass measured 2 us slower.)
+// {L, ci, face base}; the ids of a cell owning a crossing edge go to the dense per-cell table (vid),
+// where the face pass reads its owners' ids by cell id.  (A separate one-lane-per-active-cell
+// position pass measured 2 us slower.)
 // a window's (owned edges <= 3, triangles <= 5, active <= 1) per cell, packed for one 32-bit scan:
 // over 64 cells the sums stay below 2^8 (192), 2^10 (320) and 2^7 (64)
 constexpr int kPackShift[3] = {0, 8, 18};
@@ -185,16 +187,6 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
             const uint32_t cnt = (uint32_t)__popcll((unsigned long long)k.nt);
             const uint32_t incl = wave_incl_scan<uint32_t>(cnt, lane);
             const uint32_t total = __shfl(incl, 63, 64);
-            // the item table (faces find an owner cell's record through it): an emitted item's
-            // non-trivial cells and the record index of its first one (every emitted non-trivial cell
-            // is active); written once, by the unit's first part
-            {
-                const bool emit_item = k.nt != 0 && k.z >= g.cz_emit;
-                const uint32_t acnt = emit_item ? cnt : 0u;
-                const uint32_t aincl = wave_incl_scan<uint32_t>(acnt, lane);
-                if (part == 0 && emit_item)
-                    b.items[(size_t)irow * nch + ic] = make_uint4((uint32_t)k.nt, (uint32_t)(k.nt >> 32), arun0 + aincl - acnt, 0u);
-            }
             __builtin_amdgcn_wave_barrier();   // the previous batch's LDS reads are done
             bits[0][lane] = k.s00; bits[1][lane] = k.t00; bits[2][lane] = k.s10; bits[3][lane] = k.t10;
             bits[4][lane] = k.s01; bits[5][lane] = k.t01; bits[6][lane] = k.s11; bits[7][lane] = k.t11;
@@ -272,18 +264,14 @@ __device__ __forceinline__ void mc_cells_part(const uint32_t* s_cw, const GridDe
                             else { const float mu = (0.f - f3) / (f7 - f3); px = fx2; py = fy2; pz = fz + mu * g.w[2]; }
                             b.verts[3 * (size_t)out] = px; b.verts[3 * (size_t)out + 1] = py; b.verts[3 * (size_t)out + 2] = pz;
                         }
-                        // a halo cell's ids (the layer below the slab's first emitted one), by cell id
-                        if (!emit && b.vid_halo)
-                            *reinterpret_cast<IdTriple*>(b.vid_halo + (size_t)L * 3) = IdTriple{ids[0], ids[1], ids[2]};
+                        // the cell's owned ids by cell id (halo cells too: the slab's layer below its
+                        // first emitted one), where the face pass looks its owners up
+                        *reinterpret_cast<IdTriple*>(b.vid + (size_t)L * 3) = IdTriple{ids[0], ids[1], ids[2]};
                     }
-                    if (act) {   // an active cell: its record and its ids, at its record index
+                    if (act) {   // an active cell: its record, at its record index
                         const uint32_t arun = arun0 + fld(pre, 2);
-                        if (arun < (uint64_t)b.cap_rec) {
-                            b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), (uint32_t)erow);
-                            *reinterpret_cast<IdTriple*>(b.vidc + (size_t)arun * 3) = IdTriple{ids[0], ids[1], ids[2]};
-                        } else {
-                            *b.overflow = 1u;
-                        }
+                        if (arun < (uint64_t)b.cap_rec) b.records[arun] = make_uint4(L, ci, frun0 + fld(pre, 1), (uint32_t)erow);
+                        else *b.overflow = 1u;
                     }
                 }
                 vrun0 += fld(tot, 0);

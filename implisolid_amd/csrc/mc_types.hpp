@@ -50,12 +50,10 @@ struct MCBuffers {
     uint32_t* counters;      // [0] unit parts, [1] halo own (read by the vertex pass), [2..5] totals
                              // own/tri/act/halo (copied as one block; [5] == [1]), [6] non-empty units,
                              // [7] heavy unit parts (the flat list's front)
-    uint32_t* vidc;          // 3 * cap_rec: per active cell (record order) the slab-local ids (vid - H, mod
-                             // 2^32) of its owned edges 5, 6, 10 (unused slots undefined); faces add Voff
-    uint32_t* vid_halo;      // 3 * m^2: the same per cell of the halo layer (cell id L < m^2), written
-                             // only where the cell owns a vertex (null: the slab has no halo layer)
-    uint4* items;            // [row][chunk]: {non-trivial cell mask lo, hi, record index of the item's first
-                             // non-trivial cell, 0}, written for the emitted items holding non-trivial cells
+    uint32_t* vid;           // 3 * n_cells: per cell id L, the slab-local ids (vid - H, mod 2^32) of its
+                             // owned edges 5, 6, 10, written for the cells owning a crossing edge (halo
+                             // layer included; unused slots undefined) -- the face pass reads an owner's
+                             // triple straight from its cell id
     uint4* records;          // active cells: {L, ci, fbase, cell row}
     float* verts;            // 3 * cap_v
     int32_t* faces;          // 3 * cap_f

@@ -1724,61 +1724,81 @@ __global__ __launch_bounds__(256) void k_qem(float* __restrict__ verts, int64_t 
 // ---- host helpers ------------------------------------------------------------------------------
 // boost::random::mt11213b (seed 12) + uniform_01<float>: make_random_pm1(n, 3, 1e-6)
 // (make_random_pm1.hpp:15-29): the twist in three runs (no index wrap inside), tempering of a
-// whole block at once, then uniform_01's rejection of draws that round to 1.0f
-std::vector<float> make_random_pm1(int64_t n, float amplitude) {
+// whole block at once, then uniform_01's rejection of draws that round to 1.0f (pert_prefix)
+// make_random_pm1(n, 3, 1e-6) draws its 3 n values in order from a generator seeded afresh (12) on
+// every call: the table of n faces is the first 3 n values of one sequence, whatever n.  One
+// process-wide prefix of that sequence is kept and grown on demand (the generator's state carries
+// over; a grown table is a new immutable snapshot, so readers of an older one are undisturbed), and
+// the first Ob02 of a process starts drawing kPertAhead faces' worth on a host thread, so a later
+// build of a new face count finds its table drawn.  (Round 5 drew each face count's table afresh.)
+constexpr int64_t kPertAhead = int64_t(1) << 20;
+struct PertSeq {
+    std::mutex mu;
+    uint32_t x[351], t[351];
+    int next = 351;   // the next tempered word of t (351: twist first)
+    bool seeded = false;
+    std::shared_ptr<const std::vector<float>> vals;
+};
+PertSeq& pert_seq() {
+    static PertSeq S;
+    return S;
+}
+std::shared_ptr<const std::vector<float>> pert_prefix(int64_t n, bool only_if_ready = false) {
     constexpr int N = 351, M = 175;
     constexpr uint32_t UM = 0xffffffffu << 19, LM = ~UM, A = 0xccab8ee7u;
-    uint32_t x[N], t[N];
-    x[0] = 12u;
-    for (int i = 1; i < N; ++i) x[i] = 1812433253u * (x[i - 1] ^ (x[i - 1] >> 30)) + (uint32_t)i;
+    PertSeq& S = pert_seq();
+    std::lock_guard<std::mutex> lock(S.mu);
+    const size_t want = (size_t)(3 * n);
+    if (S.vals && S.vals->size() >= want) return S.vals;
+    if (only_if_ready) return nullptr;
+    if (!S.seeded) {
+        S.x[0] = 12u;
+        for (int i = 1; i < N; ++i) S.x[i] = 1812433253u * (S.x[i - 1] ^ (S.x[i - 1] >> 30)) + (uint32_t)i;
+        S.seeded = true;
+    }
+    auto v = std::make_shared<std::vector<float>>();
+    const size_t have = S.vals ? S.vals->size() : 0;
+    const size_t target = std::max(want, 2 * have);
+    v->reserve(target);
+    if (S.vals) v->assign(S.vals->begin(), S.vals->end());
     const float factor = 1.0f / ((float)4294967295u + 1.0f);
-    const double amp = (double)amplitude;
-    std::vector<float> out((size_t)(3 * n));
-    size_t o = 0;
-    while (o < out.size()) {
-        int k = 0;
-        for (; k < N - M; ++k) {
-            const uint32_t y = (x[k] & UM) | (x[k + 1] & LM);
-            x[k] = x[k + M] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+    const double amp = (double)0.000001f;
+    uint32_t* x = S.x;
+    while (v->size() < target) {
+        if (S.next == N) {   // the twist in three runs (no index wrap inside), then a block's tempering
+            int k = 0;
+            for (; k < N - M; ++k) {
+                const uint32_t y = (x[k] & UM) | (x[k + 1] & LM);
+                x[k] = x[k + M] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+            }
+            for (; k < N - 1; ++k) {
+                const uint32_t y = (x[k] & UM) | (x[k + 1] & LM);
+                x[k] = x[k + M - N] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+            }
+            const uint32_t y = (x[N - 1] & UM) | (x[0] & LM);
+            x[N - 1] = x[M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+            for (int i = 0; i < N; ++i) {
+                uint32_t z = x[i];
+                z ^= (z >> 11);
+                z ^= (z << 7) & 0x31b6ab00u;
+                z ^= (z << 15) & 0xffe50000u;
+                z ^= (z >> 17);
+                S.t[i] = z;
+            }
+            S.next = 0;
         }
-        for (; k < N - 1; ++k) {
-            const uint32_t y = (x[k] & UM) | (x[k + 1] & LM);
-            x[k] = x[k + M - N] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
-        }
-        const uint32_t y = (x[N - 1] & UM) | (x[0] & LM);
-        x[N - 1] = x[M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
-        for (int i = 0; i < N; ++i) {
-            uint32_t z = x[i];
-            z ^= (z >> 11);
-            z ^= (z << 7) & 0x31b6ab00u;
-            z ^= (z << 15) & 0xffe50000u;
-            z ^= (z >> 17);
-            t[i] = z;
-        }
-        for (int i = 0; i < N && o < out.size(); ++i) {
-            const float r = (float)t[i] * factor;
-            if (!(r < 1.0f)) continue;
-            out[o++] = (float)(((double)r * 2.0 - 1.0) * amp);
-        }
+        const float r = (float)S.t[S.next++] * factor;
+        if (!(r < 1.0f)) continue;   // uniform_01's rejection of draws that round to 1.0f
+        v->push_back((float)(((double)r * 2.0 - 1.0) * amp));
     }
-    return out;
+    S.vals = v;
+    return S.vals;
 }
-
-// the perturbations depend on the face count alone (seeded afresh on every call): the last few
-// face counts' tables are kept, so rebuilding a mesh of the same size does not redraw them
-std::shared_ptr<const std::vector<float>> random_pm1_cached(int64_t n) {
-    static std::mutex mu;
-    static std::deque<std::pair<int64_t, std::shared_ptr<const std::vector<float>>>> cache;
-    {
-        std::lock_guard<std::mutex> lock(mu);
-        for (auto& e : cache)
-            if (e.first == n) return e.second;
-    }
-    auto v = std::make_shared<const std::vector<float>>(make_random_pm1(n, 0.000001f));
-    std::lock_guard<std::mutex> lock(mu);
-    cache.emplace_front(n, v);
-    if (cache.size() > 4) cache.pop_back();
-    return v;
+// the draw ahead, started once per process (its future waits at exit: no HIP call inside)
+void pert_draw_ahead() {
+    static std::once_flag once;
+    static std::future<std::shared_ptr<const std::vector<float>>> ahead;
+    std::call_once(once, [] { ahead = std::async(std::launch::async, [] { return pert_prefix(kPertAhead); }); });
 }
 
 }  // namespace
@@ -1810,13 +1830,17 @@ std::shared_ptr<PertDev> pert_device_table(int64_t nf, std::future<std::shared_p
     IMPLI_HIP(hipGetDevice(&device));
     std::lock_guard<std::mutex> lock(mu);
     uploaded_here = false;
-    for (auto& e : cache)
-        if (e->device == device && e->nf == nf) return e;
+    for (auto& e : cache)   // any table of this device at least nf faces long: its prefix is nf's
+        if (e->device == device && e->nf >= nf) return e;
     auto host = job.get();
     auto e = std::make_shared<PertDev>();
     e->device = device;
-    e->nf = nf;
-    const size_t bytes = host->size() * 4;
+    // the upload: the next power of two of faces the drawn prefix holds (a later, larger mesh
+    // uploads a longer table; a smaller one reads this one's prefix)
+    int64_t up = 1;
+    while (up < nf) up <<= 1;
+    e->nf = std::min<int64_t>(up, (int64_t)(host->size() / 3));
+    const size_t bytes = (size_t)e->nf * 3 * 4;
     e->pinned.reserve(bytes + 16);
     std::memcpy(e->pinned.p, host->data(), bytes);
     e->buf.reserve(bytes + 16);
@@ -2266,14 +2290,26 @@ float Ob02::last_average_edge() {   // blocking: the last fold's average, read b
 }
 
 // make_random_pm1(nf, 3, 1e-6) (centroids_projection.cpp:239-262) is seeded afresh (seed 12) on
-// every call, so it depends on nf alone: it is generated once per face count on a host thread,
-// started when the mesh is loaded, and uploaded once -- the projection never waits for it unless
-// a centroid needs the type-2 directions before the thread is done
+// every call, so its table is a prefix of one sequence (pert_prefix): drawn on a host thread when the
+// loaded mesh needs more of it than is drawn, and uploaded once per device and length -- the
+// projection never waits for it unless a centroid needs the type-2 directions before the thread is
+// done
 void Ob02::start_perturbations() {
     if (pert_nf_ == nf || nf == 0) return;
     if (pert_job_.valid()) pert_job_.wait();
     const int64_t n = nf;
-    pert_job_ = std::async(std::launch::async, [n] { return random_pm1_cached(n); });
+    if (auto ready = pert_prefix(n, true)) {   // drawn already: no thread
+        std::promise<std::shared_ptr<const std::vector<float>>> p;
+        p.set_value(ready);
+        pert_job_ = p.get_future();
+        pert_draw_ahead();
+    } else {   // this mesh's table first, then the draw ahead behind it
+        pert_job_ = std::async(std::launch::async, [n] {
+            auto v = pert_prefix(n);
+            pert_draw_ahead();
+            return v;
+        });
+    }
     pert_nf_ = nf;
     pert_dev_.reset();
 }

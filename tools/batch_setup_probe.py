@@ -15,12 +15,13 @@ def main():
     import implisolid_amd as I
     from implisolid_amd import scenes
     objs = scenes.config5_objects(64, 128)
+    texts = [json.dumps(o[0]) for o in objs]   # JSON text, as bench.py hands them over
     I.set_jit(0)
     sp = torch.cuda.current_stream().cuda_stream
     out = []
     for k in range(3):
         t0 = time.perf_counter()
-        b = I.Batch([o[0] for o in objs], objs[0][1], n_streams=0)
+        b = I.Batch(texts, objs[0][1], n_streams=0)
         setup = time.perf_counter() - t0
         b.run(sp)
         torch.cuda.synchronize()
