@@ -1116,6 +1116,8 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
         const MCSettings st = parse_mc_settings(mc_json);
         static const bool timing = std::getenv("IMPLISOLID_BATCH_TIMING") != nullptr;   // diagnostics
         auto t_start = std::chrono::steady_clock::now();
+        size_t pool0[4] = {0, 0, 0, 0};
+        if (timing) DevBuf::pool_stats(pool0);
         // the MP5 programs, parsed and compiled on host threads (a few tens of us each)
         std::vector<Program> progs((size_t)n);
         {
@@ -1283,8 +1285,13 @@ implisolid_batch* implisolid_batch_create(const char* const* shapes, int n, cons
             }
             if (timing) {
                 ph[3] += tick(tp);
-                std::fprintf(stderr, "implisolid_batch_create (merged): compile + streams %.2f ms, first pass + counts %.2f ms\n",
-                             t_compile * 1e3, ph[3] * 1e3);
+                size_t pool1[4];
+                DevBuf::pool_stats(pool1);
+                std::fprintf(stderr, "implisolid_batch_create (merged): compile + streams %.2f ms, first pass + counts %.2f ms; "
+                                     "pool: %zu hipMalloc, %zu hipFree during the setup, %.1f MB cached before (%.1f MB "
+                                     "awaiting a sync)\n",
+                             t_compile * 1e3, ph[3] * 1e3, pool1[2] - pool0[2], pool1[3] - pool0[3],
+                             (pool0[0] + pool0[1]) / 1e6, pool0[1] / 1e6);
             }
             // (the whole pass captured as one graph and replayed: 0.548-0.557 ms against 0.499-0.501
             // with direct launches, profiles/r05zq_config5_merged_graph_ab.txt)

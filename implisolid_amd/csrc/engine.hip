@@ -21,18 +21,28 @@ void hip_check(hipError_t e, const char* what) {
 
 // ---- the device-memory pool behind DevBuf ----------------------------------------------------------
 // Size classes of four steps per octave (at most 25 % over the request), 256 B and up; blocks above
-// kPoolMaxBlock (the field of a large grid) and any block past kPoolMaxCached cached bytes go back
+// kPoolMaxBlock (the field of a large grid) and any block past the cached-bytes cap go back
 // to hipFree as before.  A released block waits in `pending` until the next allocation that would
 // reuse it synchronises the device once (hipFree used to synchronise on every call): a kernel still
 // reading it on some stream is done by then.
 namespace {
-constexpr size_t kPoolMaxBlock = size_t(256) << 20, kPoolMaxCached = size_t(4) << 30;
+constexpr size_t kPoolMaxBlock = size_t(256) << 20, kPoolMinCached = size_t(4) << 30;
 struct DevicePool {
     std::map<size_t, std::vector<void*>> ready, pending;
     size_t ready_bytes = 0, pending_bytes = 0;
+    size_t cap = 0;   // cached bytes at most: 1/16 of the device's memory, at least kPoolMinCached
 };
+size_t pool_cap(DevicePool& P, int d) {
+    if (!P.cap) {
+        size_t total = 0;
+        if (hipDeviceTotalMem(&total, d) != hipSuccess) total = 0;
+        P.cap = std::max(kPoolMinCached, total / 16);   // 18 GB of an MI355X's 288
+    }
+    return P.cap;
+}
 std::mutex g_pool_mu;
 std::map<int, DevicePool> g_pools;
+std::atomic<size_t> g_pool_mallocs{0}, g_pool_frees{0};
 size_t pool_class(size_t n) {
     size_t c = 256;
     while (c < n) c <<= 1;                      // the octave's top
@@ -78,6 +88,7 @@ void DevBuf::reserve(size_t n) {
         }
     }
     IMPLI_HIP(hipMalloc(&p, want));
+    g_pool_mallocs.fetch_add(1, std::memory_order_relaxed);
     bytes = want;
     dev = d;
 }
@@ -87,22 +98,27 @@ void DevBuf::release() {
         if (bytes <= kPoolMaxBlock && dev >= 0 && pool_class(bytes) == bytes) {
             std::lock_guard<std::mutex> lk(g_pool_mu);
             DevicePool& P = g_pools[dev];
-            if (P.ready_bytes + P.pending_bytes + bytes <= kPoolMaxCached) {
+            if (P.ready_bytes + P.pending_bytes + bytes <= pool_cap(P, dev)) {
                 P.pending[bytes].push_back(p);
                 P.pending_bytes += bytes;
                 cached = true;
             }
         }
-        if (!cached) (void)hipFree(p);
+        if (!cached) {
+            (void)hipFree(p);
+            g_pool_frees.fetch_add(1, std::memory_order_relaxed);
+        }
     }
     p = nullptr;
     bytes = 0;
     ext = false;
     dev = -1;
 }
-void DevBuf::pool_stats(size_t out[2]) {
+void DevBuf::pool_stats(size_t out[4]) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     out[0] = out[1] = 0;
+    out[2] = g_pool_mallocs.load(std::memory_order_relaxed);
+    out[3] = g_pool_frees.load(std::memory_order_relaxed);
     for (auto& kv : g_pools) {
         out[0] += kv.second.ready_bytes;
         out[1] += kv.second.pending_bytes;

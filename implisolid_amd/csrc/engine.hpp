@@ -35,8 +35,9 @@ struct DevBuf {
         bytes = n;
         ext = true;
     }
-    // the pool's cached bytes on every device: [0] reusable, [1] awaiting a device synchronisation
-    static void pool_stats(size_t out[2]);
+    // the pool's cached bytes on every device: [0] reusable, [1] awaiting a device synchronisation,
+    // [2] hipMalloc calls so far (reserves the pool could not serve), [3] hipFree calls
+    static void pool_stats(size_t out[4]);
     // free every cached block of the current device (synchronises it)
     static void pool_trim();
     template <class T> T* as() const { return static_cast<T*>(p); }
