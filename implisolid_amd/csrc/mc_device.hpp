@@ -111,10 +111,10 @@ __device__ __forceinline__ unsigned chunk_ci(const ChunkBits& k, int j) {
 // K3: one wave per unit.  Lanes find the non-trivial cells of their (row, chunk) items; the cells
 // are then taken in cell order, 64 at a time: a wave scan of (owned edges, triangles, active)
 // gives every cell its vertex / face / record base; owned vertices are
-// placed from the owner cell's fx/fy/fz (the reference's first emission), their ids go beside the records (vidc)
-// (halo cells, below the slab's first emitted layer: ids only), active cells get a record
-// {L, ci, face base}; the ids of a cell owning a crossing edge go to the dense per-cell table (vid),
-// where the face pass reads its owners' ids by cell id.  (A separate one-lane-per-active-cell
+// placed from the owner cell's fx/fy/fz (the reference's first emission) (halo cells, below the
+// slab's first emitted layer: ids only), active cells get a record {L, ci, face base}; the ids of a
+// cell owning a crossing edge go to the dense per-cell table (vid), where the face pass reads its
+// owners' ids by cell id.  (A separate one-lane-per-active-cell
 // position pass measured 2 us slower.)
 // a window's (owned edges <= 3, triangles <= 5, active <= 1) per cell, packed for one 32-bit scan:
 // over 64 cells the sums stay below 2^8 (192), 2^10 (320) and 2^7 (64)
