@@ -382,6 +382,42 @@ const char* prim_g_call(int t) {
     }
 }
 
+// The point modules' transforms (xform / grad_xform, ifunc_device.hpp) written out per matrix.  A
+// coefficient that is exactly 1 multiplies as the identity (1 * v == v: what constant folding makes
+// of a baked module), exact zeros are literals (0 * v is kept: its sign and NaN cases), every other
+// entry is read from M; the rows keep xform's operation order ((m0 x + m1 y) + m2 z) + m3.  Points
+// may be non-finite here, so no term is dropped (unlike xform_row's finite sample rows).
+std::string pt_coef(const float* m, int base, int k, const std::string& v) {
+    uint32_t u;
+    std::memcpy(&u, &m[k], 4);
+    if (u == 0x3f800000u) return v;
+    if (u == 0u) return "0.f * " + v;
+    if (u == 0x80000000u) return "-0.f * " + v;
+    return "M[" + std::to_string(base + k) + "] * " + v;
+}
+std::string pt_const(const float* m, int base, int k) {
+    uint32_t u;
+    std::memcpy(&u, &m[k], 4);
+    if (u == 0u) return "0.f";
+    if (u == 0x80000000u) return "-0.f";
+    return "M[" + std::to_string(base + k) + "]";
+}
+std::string pt_xform(const float* m, int base, const std::string& x, const std::string& y, const std::string& z) {
+    std::string r[3];
+    for (int i = 0; i < 3; ++i)
+        r[i] = "((" + pt_coef(m, base, 4 * i, x) + " + " + pt_coef(m, base, 4 * i + 1, y) + ") + " +
+               pt_coef(m, base, 4 * i + 2, z) + ") + " + pt_const(m, base, 4 * i + 3);
+    return "V3{" + r[0] + ", " + r[1] + ", " + r[2] + "}";
+}
+// grad_xform: inv^T g, row i = (m_i g.x + m_{4+i} g.y) + m_{8+i} g.z (g a V3 variable)
+std::string pt_grad_xform(const float* m, int base, const std::string& g) {
+    std::string r[3];
+    for (int i = 0; i < 3; ++i)
+        r[i] = "(" + pt_coef(m, base, i, g + ".x") + " + " + pt_coef(m, base, 4 + i, g + ".y") + ") + " +
+               pt_coef(m, base, 8 + i, g + ".z");
+    return "V3{" + r[0] + ", " + r[1] + ", " + r[2] + "}";
+}
+
 struct PtEmitter {
     const std::vector<Node>& nodes;
     const Program& prog;
@@ -395,8 +431,9 @@ struct PtEmitter {
         const int id = counter++;
         const std::string pad(ind, ' ');
         const std::string q = "q" + std::to_string(id), f = "f" + std::to_string(id), g = "g" + std::to_string(id);
-        const std::string M = "M + " + std::to_string(12 * n.mat);
-        out << pad << "const V3 " << q << " = xform(" << M << ", " << x << ", " << y << ", " << z << ");\n";
+        const float* mm = prog.mats[n.mat];
+        const int mb = 12 * n.mat;
+        out << pad << "const V3 " << q << " = " << pt_xform(mm, mb, x, y, z) << ";\n";
         if (n.leaf) {
             const std::string call = n.type == NT_LID         ? "lid_f(" + q + ".z)"
                                      : n.type == NT_EXTRUSION ? with_params("extr_f(P, ", n.prm) + q + ".x, " + q + ".y)"
@@ -406,7 +443,8 @@ struct PtEmitter {
                 const std::string gc = n.type == NT_LID         ? std::string("V3{0.f, 0.f, 1.f}")
                                        : n.type == NT_EXTRUSION ? with_params("extr_g(P, ", n.prm) + q + ".x, " + q + ".y)"
                                                                 : with_params(prim_g_call(n.type), n.prm) + q + ".x, " + q + ".y, " + q + ".z)";
-                out << pad << "const V3 " << g << " = grad_xform(" << M << ", " << gc << ");\n";
+                out << pad << "const V3 t" << g << " = " << gc << ";\n";
+                out << pad << "const V3 " << g << " = " << pt_grad_xform(mm, mb, "t" + g) << ";\n";
             }
             return f;
         }
@@ -420,8 +458,9 @@ struct PtEmitter {
         if (grad) {
             const std::string ga = "g" + fa.substr(1), gb = "g" + fb.substr(1);
             const std::string gbs = n.type == NT_DIFFERENCE ? "V3{-" + gb + ".x, -" + gb + ".y, -" + gb + ".z}" : gb;
-            out << pad << "const V3 " << g << " = grad_xform(" << M << ", csg_first(" << n.type << ", " << fa << ", " << fb
-                << ") ? " << ga << " : " << gbs << ");\n";
+            out << pad << "const V3 t" << g << " = csg_first(" << n.type << ", " << fa << ", " << fb << ") ? " << ga << " : "
+                << gbs << ";\n";
+            out << pad << "const V3 " << g << " = " << pt_grad_xform(mm, mb, "t" + g) << ";\n";
         }
         return f;
     }
@@ -1046,21 +1085,21 @@ std::string TreeJit::point_source(const Program& p, bool bake) {
       << "    __device__ __forceinline__ float fg(float x, float y, float z, V3& g) const { return tree_pfg(M, tab, x, y, z, g); }\n"
       << "};\n}  // namespace impli\n"
       << "using impli::JitPt;\nusing impli::ob::ProjArgs;\n"
-      << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_centroid_normals(const float* M, const float* tab,\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_centroid_normals(const float* __restrict__ M, const float* __restrict__ tab,\n"
       << "    const float* v, const int32_t* f, const int64_t* rng, float* C, float* N) {\n"
       << "    impli::ob::centroid_normals_body(JitPt{M, tab}, v, f, rng, C, N);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_prep(const float* M, const float* tab, ProjArgs a) {\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_project_prep(const float* __restrict__ M, const float* __restrict__ tab, ProjArgs a) {\n"
       << "    impli::ob::project_prep_body(JitPt{M, tab}, a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early(const float* M, const float* tab, ProjArgs a) {\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early(const float* __restrict__ M, const float* __restrict__ tab, ProjArgs a) {\n"
       << "    impli::ob::" << early << "(JitPt{M, tab}, a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early2(const float* M, const float* tab, ProjArgs a) {\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_early2(const float* __restrict__ M, const float* __restrict__ tab, ProjArgs a) {\n"
       << "    impli::ob::project_early_body<2>(JitPt{M, tab}, a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_late(const float* M, const float* tab, ProjArgs a) {\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ << " void impli_pt_project_late(const float* __restrict__ M, const float* __restrict__ tab, ProjArgs a) {\n"
       << "    impli::ob::project_late_body(JitPt{M, tab}, a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_normals_at(const float* M, const float* tab,\n"
+      << "extern \"C\" __global__ __launch_bounds__(256)" << occ_fg << " void impli_pt_normals_at(const float* __restrict__ M, const float* __restrict__ tab,\n"
       << "    const float* P, const int64_t* rng, float* G, const uint32_t* pend, int mode) {\n"
       << "    impli::ob::normals_at_body(JitPt{M, tab}, P, rng, G, pend, mode);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_points(const float* M, const float* tab,\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void impli_pt_points(const float* __restrict__ M, const float* __restrict__ tab,\n"
       << "    const float* xyz, int64_t n, float* f, float* grad) {\n"
       << "    impli::ob::points_body(JitPt{M, tab}, xyz, n, f, grad);\n}\n";
     return s.str();

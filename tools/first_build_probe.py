@@ -1,9 +1,8 @@
 #!/usr/bin/env python3
-"""A never-seen object's first build_geometry against its steady state: config 4s (config 3's
-tree on the shifted box) at 512^3, fresh process.  Prints the first build's wall time, then one
-profiled first-kind build (stages drained; a second fresh shape: the same tree with one matrix
-entry nudged, so no module of it is compiled yet), then the steady state after the JIT and bake.
-usage: python tools/first_build_probe.py [R]"""
+"""Config 4s (config 3's tree on the shifted box) at 512^3 in a fresh process: a never-seen
+object's first build_geometry, then edits (the same tree with a root translation nudged: the tree
+structure's unbaked modules, compiled by then), one profiled edit (stages drained), and the steady
+state of a hot object after the JIT and bake.   usage: python tools/first_build_probe.py [R]"""
 import copy
 import json
 import os
@@ -38,6 +37,14 @@ def main():
     I.make_geometry(shape, mc)
     out["second_build_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
     print(json.dumps(out), flush=True)
+    # edits: the same tree with other matrix values (the structure's unbaked modules, compiled now)
+    I.jit_wait()
+    ts = []
+    for k in (2, 3, 4):
+        t0 = time.perf_counter()
+        I.make_geometry(nudged(shape, k), mc)
+        ts.append(time.perf_counter() - t0)
+    out["edit_build_ms"] = round(min(ts) * 1e3, 3)
     # a never-seen shape again, profiled (stage boundaries drained)
     I.ob02_profile(True)
     t0 = time.perf_counter()
