@@ -302,7 +302,8 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         }
         if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
         ob_ptr->set_profile(g_ob02_profile);
-        ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf);
+        // the loop starts with a resampling: its centroid normals go beside the topology passes
+        ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf, nullptr, st.overall_repeats > 0 && st.vresampl_iters > 0);
     }
     Ob02& ob = *ob_ptr;
     g_last_refined = true;

@@ -71,9 +71,61 @@ inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 
 // ---- topology --------------------------------------------------------------------------------
-__global__ void k_degree(const int32_t* __restrict__ f, int64_t n3, uint32_t* __restrict__ deg) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n3) atomicAdd(&deg[f[i]], 1u);
+// Degrees and umbrella slots with the atomics in LDS.  A marching-cubes mesh numbers its faces and
+// vertices in cell order, and a face's corners are owned by its cell or the cells one row / one layer
+// below, so a block's kWinCorners consecutive corners name vertices inside a window of a few
+// thousand ids: the block counts them in LDS and adds each vertex's count to global memory once
+// (about a third of the global atomics of one per corner).  A block whose ids spread wider (an
+// uploaded or subdivided mesh) takes one global atomic per corner.  The counts are the
+// same either way; the slots k_sort_umbrella then orders are the same set.
+constexpr int kWinCorners = 4096, kWinPerLane = kWinCorners / 256, kWinSlots = 8192;
+struct WinRange { int32_t lo, hi; };
+__device__ __forceinline__ WinRange win_range(const int32_t (&v)[kWinPerLane], int32_t* s_red) {
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < kWinPerLane; ++k)
+        if (v[k] >= 0) { lo = min(lo, v[k]); hi = max(hi, v[k]); }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o, 64));
+        hi = max(hi, __shfl_xor(hi, o, 64));
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s_red[w] = lo; s_red[4 + w] = hi; }
+    __syncthreads();
+    WinRange r{min(min(s_red[0], s_red[1]), min(s_red[2], s_red[3])), max(max(s_red[4], s_red[5]), max(s_red[6], s_red[7]))};
+    return r;
+}
+// the block's corners, lane-strided (corner c0 + k 256 + lane); -1 past the end
+__device__ __forceinline__ void win_load(const int32_t* __restrict__ f, int64_t n3, int64_t c0, int32_t (&v)[kWinPerLane]) {
+#pragma unroll
+    for (int k = 0; k < kWinPerLane; ++k) {
+        const int64_t i = c0 + k * 256 + threadIdx.x;
+        v[k] = i < n3 ? f[i] : -1;
+    }
+}
+__global__ __launch_bounds__(256) void k_degree_win(const int32_t* __restrict__ f, int64_t n3, uint32_t* __restrict__ deg) {
+    __shared__ uint32_t cnt[kWinSlots];
+    __shared__ int32_t s_red[8];
+    const int64_t c0 = (int64_t)blockIdx.x * kWinCorners;
+    int32_t v[kWinPerLane];
+    win_load(f, n3, c0, v);
+    const WinRange r = win_range(v, s_red);
+    if (r.hi < r.lo) return;   // (no corner: never, the grid covers n3)
+    const int span = r.hi - r.lo + 1;
+    if (r.hi - r.lo >= kWinSlots) {
+#pragma unroll
+        for (int k = 0; k < kWinPerLane; ++k)
+            if (v[k] >= 0) atomicAdd(&deg[v[k]], 1u);
+        return;
+    }
+    for (int k = threadIdx.x; k < span; k += 256) cnt[k] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kWinPerLane; ++k)
+        if (v[k] >= 0) atomicAdd(&cnt[v[k] - r.lo], 1u);
+    __syncthreads();
+    for (int k = threadIdx.x; k < span; k += 256)
+        if (cnt[k]) atomicAdd(&deg[r.lo + k], cnt[k]);
 }
 
 // exclusive scan of n uint32 into out[0..n] (one workgroup of 1024 lanes); zero_in: in[] is left
@@ -194,13 +246,41 @@ __global__ void k_ranges_set(int64_t* __restrict__ rng, int64_t v0, int64_t v1, 
     if (i == kRngScratch + 7) rng[i] = v1 > v0 ? v1 - 1 : (int64_t)-1;
 }
 
-__global__ void k_fill_umbrella(const int32_t* __restrict__ f, int64_t nf, const uint32_t* __restrict__ off,
-                                uint32_t* __restrict__ fill, int32_t* __restrict__ lst) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= 3 * nf) return;
-    const int32_t v = f[i];
-    const uint32_t p = atomicAdd(&fill[v], 1u);
-    lst[off[v] + p] = (int32_t)(i / 3);
+// The umbrellas' face lists, the block's slot claims in LDS (see k_degree_win): each corner's rank among
+// the block's corners of its vertex from an LDS atomic, one global atomic per vertex for the block's
+// base in that umbrella
+__global__ __launch_bounds__(256) void k_fill_umbrella_win(const int32_t* __restrict__ f, int64_t n3,
+                                                           const uint32_t* __restrict__ off, uint32_t* __restrict__ fill,
+                                                           int32_t* __restrict__ lst) {
+    __shared__ uint32_t cnt[kWinSlots];
+    __shared__ int32_t s_red[8];
+    const int64_t c0 = (int64_t)blockIdx.x * kWinCorners;
+    int32_t v[kWinPerLane];
+    win_load(f, n3, c0, v);
+    const WinRange r = win_range(v, s_red);
+    if (r.hi < r.lo) return;
+    const int span = r.hi - r.lo + 1;
+    if (r.hi - r.lo >= kWinSlots) {
+#pragma unroll
+        for (int k = 0; k < kWinPerLane; ++k)
+            if (v[k] >= 0) {
+                const uint32_t p = atomicAdd(&fill[v[k]], 1u);
+                lst[off[v[k]] + p] = (int32_t)((c0 + k * 256 + threadIdx.x) / 3);
+            }
+        return;
+    }
+    for (int k = threadIdx.x; k < span; k += 256) cnt[k] = 0u;
+    __syncthreads();
+    uint32_t rank[kWinPerLane];
+#pragma unroll
+    for (int k = 0; k < kWinPerLane; ++k) rank[k] = v[k] >= 0 ? atomicAdd(&cnt[v[k] - r.lo], 1u) : 0u;
+    __syncthreads();
+    for (int k = threadIdx.x; k < span; k += 256)   // counts -> the block's base in each umbrella
+        if (cnt[k]) cnt[k] = atomicAdd(&fill[r.lo + k], cnt[k]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kWinPerLane; ++k)
+        if (v[k] >= 0) lst[off[v[k]] + cnt[v[k] - r.lo] + rank[k]] = (int32_t)((c0 + k * 256 + threadIdx.x) / 3);
 }
 
 // make_neighbour_faces_of_vertex lists faces in ascending order: sort each small umbrella
@@ -317,11 +397,60 @@ __device__ __forceinline__ int32_t fof_at(const int32_t* __restrict__ f, const u
     }
     return (int32_t)((first != (uint32_t)fi) ? first : (c >= 2 ? last : 0u));
 }
-__global__ __launch_bounds__(256) void k_fof_umbrella(const int32_t* __restrict__ f, int64_t nf,
-                                                      const uint32_t* __restrict__ off, const int32_t* __restrict__ lst,
-                                                      int32_t* __restrict__ fof) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < 3 * nf) fof[i] = fof_at(f, off, lst, i);
+// fof_at per vertex: vertex a's lane loads its umbrella's faces once (up to kFofRegs, in
+// registers; the loads issue together) and answers fof_at for every half-edge leaving a, where the
+// per-half-edge lanes each reloaded the whole umbrella (~6 faces, 18 corner loads, per half-edge).
+// A larger umbrella takes fof_at per half-edge.
+constexpr int kFofRegs = 12;
+__global__ __launch_bounds__(256) void k_fof_vertex(const int32_t* __restrict__ f, int64_t nv,
+                                                    const uint32_t* __restrict__ off, const int32_t* __restrict__ lst,
+                                                    int32_t* __restrict__ fof) {
+    const int64_t a64 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a64 >= nv) return;
+    const int32_t a = (int32_t)a64;
+    const uint32_t p0 = off[a], p1 = off[a + 1];
+    const int n = (int)(p1 - p0);
+    if (n <= 0) return;
+    if (n > kFofRegs) {
+        for (uint32_t p = p0; p < p1; ++p) {
+            const int32_t g = lst[p];
+            if (p > p0 && lst[p - 1] == g) continue;
+            for (int k = 0; k < 3; ++k)
+                if (f[3 * (int64_t)g + k] == a) fof[3 * (int64_t)g + k] = fof_at(f, off, lst, 3 * (int64_t)g + k);
+        }
+        return;
+    }
+    int32_t G[kFofRegs], V[kFofRegs][3];
+#pragma unroll
+    for (int j = 0; j < kFofRegs; ++j) G[j] = lst[p0 + (uint32_t)min(j, n - 1)];
+#pragma unroll
+    for (int j = 0; j < kFofRegs; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) V[j][k] = f[3 * (int64_t)G[j] + k];
+#pragma unroll
+    for (int j = 0; j < kFofRegs; ++j) {
+        if (j >= n || (j > 0 && G[j] == G[j - 1])) continue;   // (a degenerate face lists a twice)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (V[j][k] != a) continue;
+            const int32_t b = V[j][k == 2 ? 0 : k + 1];
+            uint32_t first = 0xffffffffu, last = 0u, c = 0u;
+#pragma unroll
+            for (int m = 0; m < kFofRegs; ++m) {
+                if (m >= n || (m > 0 && G[m] == G[m - 1])) continue;
+                const int32_t x = V[m][0], y = V[m][1], z = V[m][2];
+                const uint32_t h = (uint32_t)((x == a && y == b) || (x == b && y == a)) +
+                                   (uint32_t)((y == a && z == b) || (y == b && z == a)) +
+                                   (uint32_t)((z == a && x == b) || (z == b && x == a));
+                if (h) {
+                    c += h;
+                    first = min(first, (uint32_t)G[m]);
+                    last = max(last, (uint32_t)G[m]);
+                }
+            }
+            fof[3 * (int64_t)G[j] + k] = (int32_t)((first != (uint32_t)G[j]) ? first : (c >= 2 ? last : 0u));
+        }
+    }
 }
 
 // ---- step 3: my_subdiv_ (centroids_projection.cpp:1314-1367) -----------------------------------
@@ -1859,6 +1988,7 @@ Ob02::Ob02(Engine& e, hipStream_t st) : E(e), s(st) {
 }
 
 void Ob02::begin_load(const float*& d_verts, int64_t nv_, int64_t nf_, float* d_work) {
+    normals_ahead_ = false;
     nv = nv_;
     nf = nf_;
     if (d_work) {   // the caller's vertex array is the working one (sharded loop): no copy
@@ -1884,7 +2014,8 @@ void Ob02::begin_load(const float*& d_verts, int64_t nv_, int64_t nf_, float* d_
     rng_.reserve(kRngFields * sizeof(int64_t));
 }
 
-void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_, float* d_work) {
+void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_, float* d_work,
+                     bool normals_ahead) {
     begin_load(d_verts, nv_, nf_, d_work);
     Stage st(this, kStageTopology);
     // the mesh copied, the degree counters and misc ((unused), cap hits, evaluations) zeroed, the
@@ -1895,6 +2026,21 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
                                                                        d_faces, 3 * nf, deg_.as<uint32_t>(), nv + 1,
                                                                        misc_.as<uint32_t>(), rng_.as<int64_t>(), nv, nf);
     start_perturbations();   // host thread, overlaps the topology and resampling kernels
+    // the first resampling's centroid normals need no topology: with the caller's word that a
+    // resampling comes next, they run on the side stream beside the topology passes (not while
+    // profiling, whose stages are drained one by one)
+    if (normals_ahead && nf > 0 && !profile_) {
+        reserve_topology();   // cen_ / nrm_ sized before the side stream writes them
+        est_cen_ = nf;        // the whole mesh (whole_ranges below)
+        if (!side_s_) IMPLI_HIP(hipStreamCreateWithFlags(&side_s_, hipStreamNonBlocking));
+        if (!mesh_ready_) IMPLI_HIP(hipEventCreateWithFlags(&mesh_ready_, hipEventDisableTiming));
+        if (!cnormals_done_) IMPLI_HIP(hipEventCreateWithFlags(&cnormals_done_, hipEventDisableTiming));
+        IMPLI_HIP(hipEventRecord(mesh_ready_, s));
+        IMPLI_HIP(hipStreamWaitEvent(side_s_, mesh_ready_, 0));
+        launch_centroid_normals(side_s_);
+        IMPLI_HIP(hipEventRecord(cnormals_done_, side_s_));
+        normals_ahead_ = true;
+    }
     build_topology(true);
     whole_ranges();
 }
@@ -1964,6 +2110,7 @@ void Ob02::whole_ranges() {   // host side of the range block's whole-mesh state
 // estimate -- a mesh has about two faces per vertex, plus a layer of faces at the slab's boundary --
 // and grid-stride over whatever the range turns out to be.
 void Ob02::set_owned_vertices(int64_t v0, int64_t v1) {
+    normals_ahead_ = false;
     if (v0 < 0 || v1 < v0 || v1 > nv) throw InputError("ob02: owned vertex range outside the mesh");
     if (!topo_valid_ || topo_partial_) build_topology();
     rng_.reserve(kRngFields * sizeof(int64_t));
@@ -2007,6 +2154,7 @@ __global__ void k_unpack_ranges(float* __restrict__ v, const float* __restrict__
 }
 
 void Ob02::unpack_ranges(const float* d_rows, int64_t row_len, const std::vector<int64_t>& voff, int self) {
+    normals_ahead_ = false;
     const int world = (int)voff.size() - 1;
     if (world < 1 || voff.back() != nv || self < 0 || self >= world) throw InputError("ob02: bad owned ranges");
     if (world > kMaxUnpackRanks) throw InputError("ob02: more than 64 ranks in one unpack");
@@ -2064,15 +2212,16 @@ void Ob02::build_topology(bool deg_zeroed) {
     // umbrellas
     reserve_topology();
     if (!deg_zeroed) IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
-    if (nf) k_degree<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
+    const unsigned wblocks = (unsigned)((3 * nf + kWinCorners - 1) / kWinCorners);
+    if (nf) k_degree_win<<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
     scan(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv, true);   // deg_ left zeroed: the fill counters
-    if (nf) k_fill_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(),
-                                                             deg_.as<uint32_t>(), ulst_.as<int32_t>());
+    if (nf) k_fill_umbrella_win<<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, uoff_.as<uint32_t>(),
+                                                        deg_.as<uint32_t>(), ulst_.as<int32_t>());
     if (nv) k_sort_umbrella<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), nv);
     // faces of faces, from the umbrellas (the edge table is built only for subdivision)
-    if (nf)
-        k_fof_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
-                                                          fof_.as<int32_t>());
+    if (nf && nv)
+        k_fof_vertex<<<blocks_for(nv), 256, 0, s>>>(faces_.as<int32_t>(), nv, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
+                                                    fof_.as<int32_t>());
     etab_valid_ = false;
     IMPLI_HIP(hipGetLastError());
     topo_valid_ = true;
@@ -2125,6 +2274,7 @@ Ob02::~Ob02() {
     if (early_done_) (void)hipEventDestroy(early_done_);
     if (normals_done_) (void)hipEventDestroy(normals_done_);
     if (mesh_ready_) (void)hipEventDestroy(mesh_ready_);
+    if (cnormals_done_) (void)hipEventDestroy(cnormals_done_);
     if (side_s_) (void)hipStreamDestroy(side_s_);
     dir_.release();
     evals_buf_.release();
@@ -2134,28 +2284,35 @@ Ob02::~Ob02() {
     for (auto& kv : snaps_) kv.second.buf.release();
 }
 
+// f and normalised grad f at the centroids of the centroid faces (the range block's kRngCen) on q
+void Ob02::launch_centroid_normals(hipStream_t q) {
+    const int64_t* rng = rng_.as<int64_t>();
+    if (const TreeJit::PointKernels* pk = E.point_jit(s)) {
+        const float *m = E.d_mats(), *tab = E.d_rabbit(), *v = verts_.as<float>();
+        const int32_t* f = faces_.as<int32_t>();
+        const int64_t* rc = rng + kRngCen;
+        float *C = cen_.as<float>(), *N = nrm_.as<float>();
+        void* args[] = {&m, &tab, &v, &f, &rc, &C, &N};
+        TreeJit::launch(pk->cnormals, blocks_for(est_cen_), args, q, "impli_pt_centroid_normals");
+        ++jit_launches_;
+    } else {
+        DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(est_cen_), 256, q, E.d_program(), E.d_rabbit(),
+                     verts_.as<float>(), faces_.as<int32_t>(), rng + kRngCen, cen_.as<float>(), nrm_.as<float>());
+    }
+}
+
 void Ob02::vertex_resampling(float c) {
     if (!nf) return;
+    const bool ahead = normals_ahead_;   // this mesh's centroid normals, computed beside its topology
+    normals_ahead_ = false;
     if (!topo_valid_) build_topology();
     Stage st(this, kStageResample);
     store_pointset("pre_resampling_vertices", verts_.as<float>(), nv, true);   // vertex_resampling.hpp:176-180
     // centroids and normals of the centroid faces, weights of the work faces, vertices [v0, v1) (the
     // whole mesh unless sharded); the face ranges are read on the device (the range block)
     const int64_t* rng = rng_.as<int64_t>();
-    if (est_cen_ > 0) {
-        if (const TreeJit::PointKernels* pk = E.point_jit(s)) {
-            const float *m = E.d_mats(), *tab = E.d_rabbit(), *v = verts_.as<float>();
-            const int32_t* f = faces_.as<int32_t>();
-            const int64_t* rc = rng + kRngCen;
-            float *C = cen_.as<float>(), *N = nrm_.as<float>();
-            void* args[] = {&m, &tab, &v, &f, &rc, &C, &N};
-            TreeJit::launch(pk->cnormals, blocks_for(est_cen_), args, s, "impli_pt_centroid_normals");
-            ++jit_launches_;
-        } else {
-            DEPTH_LAUNCH(E.depth(), k_centroid_normals, blocks_for(est_cen_), 256, s, E.d_program(), E.d_rabbit(),
-                         verts_.as<float>(), faces_.as<int32_t>(), rng + kRngCen, cen_.as<float>(), nrm_.as<float>());
-        }
-    }
+    if (ahead) IMPLI_HIP(hipStreamWaitEvent(s, cnormals_done_, 0));
+    else if (est_cen_ > 0) launch_centroid_normals(s);
     if (est_work_ > 0)
         k_face_weights<<<blocks_for(est_work_), 256, 0, s>>>(cen_.as<float>(), nrm_.as<float>(), fof_.as<int32_t>(),
                                                               rng + kRngWork, c, w_.as<float>());
@@ -2347,6 +2504,7 @@ static int late_flat() {
 constexpr int64_t kEarly2Faces = 400000;
 
 void Ob02::centroids_projection(bool enable_qem) {
+    normals_ahead_ = false;   // (vertex_resampling: the first step after load_mesh only)
     if (!nf) return;
     if (!topo_valid_) build_topology();
     Stage st(this, kStageEdgeFold);
@@ -2563,6 +2721,7 @@ void Ob02::rand_tables(int64_t lanes) {
 }
 
 void Ob02::add_rand_noise(float amplitude) {
+    normals_ahead_ = false;
     const int64_t n = 3 * nv;
     if (!n) return;
     GlibcRand& g = process_rand();
@@ -2580,6 +2739,7 @@ void Ob02::add_rand_noise(float amplitude) {
 }
 
 void Ob02::subdivide(float amplitude) {   // my_subdiv_ (centroids_projection.cpp:1314-1367)
+    normals_ahead_ = false;
     if (!topo_valid_) build_topology();
     Stage st(this, kStageSubdiv);
     int64_t added = 0;

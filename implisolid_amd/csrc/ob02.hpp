@@ -31,7 +31,10 @@ public:
     // d_work (optional): the caller's vertex array (3 nv floats, kept alive by the caller until the
     // next load) becomes the working one in place -- the steps update it and a sharded caller's
     // exchange writes into it directly; d_verts is then ignored
-    void load_mesh(const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, float* d_work = nullptr);
+    // normals_ahead: the caller's next step is vertex_resampling (build_geometry's loop), whose
+    // centroid normals then run beside the topology passes
+    void load_mesh(const float* d_verts, int64_t nv, const int32_t* d_faces, int64_t nf, float* d_work = nullptr,
+                   bool normals_ahead = false);
     // Z-slab sharding of the loop (one Ob02 per rank, each holding the whole mesh): this rank owns
     // vertices [v0, v1) (its slab's).  Resampling and QEM then update only those; the per-face
     // passes run over the faces touching them (the work faces, a contiguous range: faces are in
@@ -96,6 +99,7 @@ private:
     void build_topology(bool deg_zeroed = false);   // deg_zeroed: deg_[0..nv] already 0 (load_mesh)
     void begin_load(const float*& d_verts, int64_t nv, int64_t nf, float* d_work);   // host state of a load
     void reserve_topology();
+    void launch_centroid_normals(hipStream_t q);
     void scan(uint32_t* in, uint32_t* out, int64_t n, bool zero_in = false);   // exclusive, out[n] = total; zero_in: in[] left 0
     EdgeTab edge_table();
     void rand_tables(int64_t lanes);
@@ -142,6 +146,8 @@ private:
     DevBuf fold_sum_;                        // the fold's chunk table (fold.hpp), built on the device
     DevBuf fold_out_;                        // FoldOut (ob02_device.hpp): sum, average, alpha list
     hipStream_t side_s_ = nullptr;           // the projection's prep pass, beside the fold's walk on s
+    hipEvent_t cnormals_done_ = nullptr;     // a new mesh's centroid normals, beside its topology passes
+    bool normals_ahead_ = false;             // cen_ / nrm_ of the loaded mesh are on their way (load_mesh)
     hipEvent_t mesh_ready_ = nullptr, prep_done_ = nullptr;
     hipEvent_t early_done_ = nullptr, normals_done_ = nullptr;   // the QEM normals beside the late pass
     DevBuf dir_, evals_buf_;

@@ -683,6 +683,34 @@ def test_ob02_projection_no_qem(impli, oracle):
     assert p is not None and p.shape[1] == 3
 
 
+@pytest.mark.parametrize("repeats", [1, 2])
+def test_ob02_pointsets_taken_in_order(impli, oracle, repeats):
+    """The reference's STORE_POINTSET records (configs.hpp:106, centroids_projection.cpp:1238-1285)
+    are copied on a stream of their own in build_geometry: each must still hold the array as it was
+    at its point of the loop.  Checked against what they must equal: the final vertices
+    (post_qem_verts), the mesh after the last resampling (pre_qem_verts: the projection moves no
+    vertex; with one repeat, the result of the same loop without projection), the centroids of that
+    mesh (pre_p_centroids, f32 in compute_centroids' order).  (The resampling records keep the
+    process's first build, vertex_resampling.hpp:176-211, so they are not this build's.)"""
+    from implisolid_amd import scenes
+    shape, mc = scenes.config2(40)
+    mc = dict(mc, overall_repeats=repeats)
+    v, f = impli.make_geometry(shape, mc)
+    vr, fr = oracle.polygonize(json.dumps(shape), json.dumps(mc))
+    bits = lambda a: np.ascontiguousarray(a, np.float32).view(np.uint32)
+    assert np.array_equal(f, fr) and np.array_equal(bits(v), bits(vr))
+    ps = {k: impli.get_pointset(k) for k in ("pre_p_centroids", "post_p_centroids", "pre_qem_verts", "post_qem_verts")}
+    assert np.array_equal(bits(ps["post_qem_verts"]), bits(v))
+    pre = ps["pre_qem_verts"]
+    c = pre[f]
+    cen = ((c[:, 0] + c[:, 1]) + c[:, 2]) / np.float32(3.0)
+    assert np.array_equal(bits(ps["pre_p_centroids"]), bits(cen))
+    assert ps["post_p_centroids"].shape == (len(f), 3)
+    if repeats == 1:
+        v_res, _ = impli.make_geometry(shape, dict(mc, projection={"enabled": 0}, qem={"enabled": 0}))
+        assert np.array_equal(bits(pre), bits(v_res))
+
+
 @pytest.mark.parametrize("R", [32, 48])
 def test_ob02_full_config2_shape(impli, oracle, R):
     from implisolid_amd import scenes
