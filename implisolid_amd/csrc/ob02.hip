@@ -194,7 +194,9 @@ __global__ __launch_bounds__(256) void k_scan_tile_sums(const uint32_t* __restri
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ in, int64_t n, const uint32_t* __restrict__ offs,
+// each tile's offset is the sum of the tile sums before it, summed by the tile's own block (a few
+// hundred values at most for the meshes here: no separate scan launch over the sums)
+__global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ in, int64_t n, const uint32_t* __restrict__ sums,
                                                     uint32_t* __restrict__ out, int zero_in) {
     __shared__ uint32_t s_w[4];
     const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
@@ -204,8 +206,11 @@ __global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ in, i
         v[k] = (base + k < n) ? in[base + k] : 0u;
         a += v[k];
     }
+    uint32_t before = 0, off = 0;
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += 256) before += sums[k];
+    (void)block_excl_scan256(before, s_w, off);
     uint32_t total;
-    uint32_t run = offs[blockIdx.x] + block_excl_scan256(a, s_w, total);
+    uint32_t run = off + block_excl_scan256(a, s_w, total);
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
         if (base + k < n) {
@@ -214,7 +219,7 @@ __global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ in, i
         }
         run += v[k];
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = offs[blockIdx.x] + total;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = off + total;
 }
 
 // load_mesh in one launch: the mesh into the refinement state's buffers, the degree counters and
@@ -2234,12 +2239,10 @@ void Ob02::scan(uint32_t* in, uint32_t* out, int64_t n, bool zero_in) {
         k_scan_u32<<<1, 1024, 0, s>>>(in, out, n, zero_in ? 1 : 0);
         return;
     }
-    scan_tmp_.reserve((size_t)(2 * tiles + 2) * 4);
+    scan_tmp_.reserve((size_t)(tiles + 1) * 4);
     uint32_t* sums = scan_tmp_.as<uint32_t>();
-    uint32_t* offs = sums + tiles + 1;
     k_scan_tile_sums<<<(unsigned)tiles, 256, 0, s>>>(in, n, sums);
-    k_scan_u32<<<1, 1024, 0, s>>>(sums, offs, tiles, 0);
-    k_scan_tiles<<<(unsigned)tiles, 256, 0, s>>>(in, n, offs, out, zero_in ? 1 : 0);
+    k_scan_tiles<<<(unsigned)tiles, 256, 0, s>>>(in, n, sums, out, zero_in ? 1 : 0);
 }
 
 // STORE_POINTSET: a device snapshot now (stream-ordered, no host sync), copied to the host only

@@ -188,10 +188,15 @@ __device__ __forceinline__ V3 bis_mid(V3 a, V3 b) {   // bisection.hpp:225-231: 
 // where f > tol (a NaN moves neither: the serial loop repeats that mid until the cap).  Lane k < 2^L - 1
 // evaluates node k of the next L levels' decision tree (heap order: child 2k+1 after f < -tol, 2k+2
 // after f > tol); the group then walks the path the serial loop takes through those levels.
+// nodes < 2^L - 1: only the first `nodes` heap nodes are evaluated (a group too narrow for the
+// whole tree, e.g. 2 lanes over 2 levels: the mid and the child after f < -tol); the walk stops
+// early where its next node was not evaluated.  The mids are the serial loop's either way.
 template <class G, class Ev>
-__device__ V3 bisect_g(const G& g, const int L, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_hits, uint32_t& evals) {
+__device__ V3 bisect_g(const G& g, const int L, const Ev& ev, V3 x1, V3 x2, uint32_t* cap_hits, uint32_t& evals,
+                       int nodes = 0) {
     int it = 0;
-    const int node = g.sub < (1 << L) - 1 ? g.sub : 0;
+    if (nodes <= 0 || nodes > (1 << L) - 1) nodes = (1 << L) - 1;
+    const int node = g.sub < nodes ? g.sub : 0;
     int depth = 0, bits = 0;   // node's path from the root, first decision in the lowest bit (1: x1 <- mid)
     for (int n = node; n > 0; n = (n - 1) >> 1) bits = (bits << 1) | ((n & 1) ? 1 : 0), ++depth;
     for (;;) {
@@ -203,7 +208,7 @@ __device__ V3 bisect_g(const G& g, const int L, const Ev& ev, V3 x1, V3 x2, uint
         }
         const V3 mid = bis_mid(a, b);
         const float vm = ev.f(mid.x, mid.y, mid.z);
-        evals += (1 << L) - 1;
+        evals += nodes;
         int cur = 0;
         for (int lvl = 0; lvl < L; ++lvl) {
             const float v = g.from(vm, cur);
@@ -214,12 +219,14 @@ __device__ V3 bisect_g(const G& g, const int L, const Ev& ev, V3 x1, V3 x2, uint
                 if (g.sub == 0) atomicAdd(cap_hits, 1u);
                 return g.from(mid, cur);
             }
-            if (lvl + 1 < L) {
-                cur = lo ? 2 * cur + 1 : 2 * cur + 2;
+            const int next = lo ? 2 * cur + 1 : 2 * cur + 2;
+            if (lvl + 1 < L && next < nodes) {
+                cur = next;
             } else {   // the state after this level: node cur's interval with its outcome applied
                 const V3 na = g.from(a, cur), nb = g.from(b, cur), nm = g.from(mid, cur);
                 x1 = lo ? nm : na;
                 x2 = lo ? nb : nm;
+                break;
             }
         }
     }
@@ -229,14 +236,14 @@ __device__ V3 bisect_g(const G& g, const int L, const Ev& ev, V3 x1, V3 x2, uint
 // best == x when nothing was found (f(x) = fcv: eval_fg's value is eval_f's)
 template <class G, class Ev>
 __device__ void finalize_g(const G& g, const int L, const Ev& ev, V3 x, float fcv, bool found, V3 best,
-                           float f2, float* out, const ProjArgs& a, uint32_t& evals) {
+                           float f2, float* out, const ProjArgs& a, uint32_t& evals, int nodes = 0) {
     const bool z2 = fabsf(f2) <= kRootTol, z1 = fabsf(fcv) <= kRootTol;
     if (z1) best = x;
     V3 r;
     if (found && !(z1 || z2)) {
         V3 x1 = x, x2 = best;
         if (f2 < -kRootTol) { const V3 t = x1; x1 = x2; x2 = t; }
-        r = bisect_g(g, L, ev, x1, x2, a.cap_hits, evals);
+        r = bisect_g(g, L, ev, x1, x2, a.cap_hits, evals, nodes);
     } else if (z1 || z2) {
         r = best;
     } else {
@@ -303,7 +310,11 @@ __device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& 
 // meshes: see project_early_body)
 template <int W, class Ev>
 __device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs& a, const GrpW<W>& g, int64_t j) {
-    constexpr int kLevels = W >= 8 ? 3 : W >= 4 ? 2 : 1;
+    // bisection levels per evaluation round and the nodes evaluated: the whole tree of 3 / 2 levels
+    // for 8 / 4 lanes; 2 lanes evaluate the mid and its child after f < -tol (2 levels when the walk
+    // goes that way, 1 otherwise)
+    constexpr int kLevels = W >= 8 ? 3 : 2;
+    constexpr int kNodes = W >= 8 ? 7 : W >= 4 ? 3 : 2;
     const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const V3 d0{a.dir[3 * j], a.dir[3 * j + 1], a.dir[3 * j + 2]};
@@ -317,7 +328,7 @@ __device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs&
     float bf = fcv;
     bool found = try_direction(g, ev, x, d0, sc, alphas, nal, max_dist, best, bf, evals);
     if (!found) found = try_direction(g, ev, x, fnv, sc, alphas, nal < 10 ? nal : 10, max_dist, best, bf, evals);
-    if (found) finalize_g(g, kLevels, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals);
+    if (found) finalize_g(g, kLevels, ev, x, fcv, true, best, bf, a.out + 3 * j, a, evals, kNodes);
     // unresolved faces are flagged for the late pass (a compacted list cost one same-address atomic
     // per wave: 258 us per pass when every face pends, as with a non-finite average edge length)
     if (g.sub == 0) a.pend[j] = found ? 0u : 1u;

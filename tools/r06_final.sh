@@ -14,7 +14,10 @@ root=$(pwd)
 if [ "$part" = all ] || [ "$part" = a ]; then
   bash tools/r06_run.sh "$tag" tests
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$out/smoke.log" 2>&1
+  ps -u "$(id -u)" -o pid,ppid,stat,etime,args > "$out/ps_before_profile.txt" || true
   bash tools/profile_round.sh "$tag"
+  sleep 2
+  ps -u "$(id -u)" -o pid,ppid,stat,etime,args > "$out/ps_after_bench.txt" || true
 fi
 if [ "$part" = all ] || [ "$part" = b ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/ob02" -o run -- \
