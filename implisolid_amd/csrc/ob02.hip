@@ -1076,9 +1076,23 @@ __global__ __launch_bounds__(256) void k_fold_table(const float* __restrict__ e,
     __shared__ double s_part[4];
     const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // the sum of the terms before this block's chunks: the block sums before it
+    // the sum of the terms before this block's chunks: the block sums before it, 8 per lane per step
+    // with clamped indices so that the loads issue together (one L2 round trip per 2048 blocks, where
+    // a load per iteration behind the loop's bound was one round trip each).  The estimate only picks
+    // runs and hints (the walk checks every step), so its summation order is free
     double p = 0.0;
-    for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += 256) p += bs[b];
+    const int64_t nb = blockIdx.x;
+    for (int64_t b0 = 0; b0 < nb; b0 += 256 * 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t b = b0 + u * 256 + threadIdx.x;
+            const double x = bs[b < nb ? b : nb - 1];
+            v[u] = b < nb ? x : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p += v[u];
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
     if (lane == 0) s_part[w] = p;
