@@ -94,6 +94,15 @@ void send_mesh_back_to_client(Ob02* ob, const CallSpecs& cs) {
 
 std::map<std::string, std::vector<float>> g_pointsets;   // pointset_set.hpp:8
 std::unique_ptr<Ob02> g_ob02;   // the refinement state of the last build
+// At exit the refinement state is left to the process (released, not destroyed): its destructor
+// waits for its perturbation thread and frees HIP streams, events and memory, which a namespace-scope
+// static would do after the runtime's own teardown.  Registered at the first Ob02, so it runs before
+// g_ob02's destructor.
+static Ob02* new_ob02(Engine& E, hipStream_t s) {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit([] { (void)g_ob02.release(); }); });
+    return new Ob02(E, s);
+}
 // The point sets (get_pointset_*) live on the device in g_ob02's snapshots; they are copied to
 // g_pointsets only when asked for after a build (a D2H copy of every set per build cost ~0.25 ms)
 bool g_pointsets_dirty = false;
@@ -257,7 +266,7 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
         df.reserve((size_t)nf * 12 + 16);
         IMPLI_HIP(hipMemcpyAsync(dv.p, g_state.verts.data(), (size_t)nv * 12, hipMemcpyHostToDevice, s));
         IMPLI_HIP(hipMemcpyAsync(df.p, g_state.faces.data(), (size_t)nf * 12, hipMemcpyHostToDevice, s));
-        if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+        if (!ob_ptr) ob_ptr.reset(new_ob02(E, s));
         ob_ptr->set_profile(g_ob02_profile);
         ob_ptr->load_mesh(dv.as<float>(), nv, df.as<int32_t>(), nf);
     } else {
@@ -300,7 +309,7 @@ void grand_algorithm(const char* shape_json, const MCSettings& st, const CallSpe
                                      abi_copy_stream()));
             IMPLI_HIP(hipEventRecord(faces_copied, abi_copy_stream()));
         }
-        if (!ob_ptr) ob_ptr.reset(new Ob02(E, s));
+        if (!ob_ptr) ob_ptr.reset(new_ob02(E, s));
         ob_ptr->set_profile(g_ob02_profile);
         // the loop starts with a resampling: its centroid normals go beside the topology passes
         ob_ptr->load_mesh(E.d_verts(), nv, E.d_faces(), nf, nullptr, st.overall_repeats > 0 && st.vresampl_iters > 0);

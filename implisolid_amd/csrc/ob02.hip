@@ -22,6 +22,7 @@
 #include <limits>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ifunc_device.hpp"
@@ -1887,9 +1888,9 @@ struct PertSeq {
     bool seeded = false;
     std::shared_ptr<const std::vector<float>> vals;
 };
-PertSeq& pert_seq() {
-    static PertSeq S;
-    return S;
+PertSeq& pert_seq() {   // never destroyed: a draw-ahead thread may still use it while the process exits
+    static PertSeq* S = new PertSeq();
+    return *S;
 }
 std::shared_ptr<const std::vector<float>> pert_prefix(int64_t n, bool only_if_ready = false) {
     constexpr int N = 351, M = 175;
@@ -1942,11 +1943,12 @@ std::shared_ptr<const std::vector<float>> pert_prefix(int64_t n, bool only_if_re
     S.vals = v;
     return S.vals;
 }
-// the draw ahead, started once per process (its future waits at exit: no HIP call inside)
+// the draw ahead, started once per process on a thread of its own, never joined: it touches only
+// the never-destroyed sequence (no HIP call, nothing a static destructor frees), so a process that
+// exits while it draws needs no wait for it (a static future's destructor would have blocked exit)
 void pert_draw_ahead() {
     static std::once_flag once;
-    static std::future<std::shared_ptr<const std::vector<float>>> ahead;
-    std::call_once(once, [] { ahead = std::async(std::launch::async, [] { return pert_prefix(kPertAhead); }); });
+    std::call_once(once, [] { std::thread([] { (void)pert_prefix(kPertAhead); }).detach(); });
 }
 
 }  // namespace
@@ -1972,8 +1974,10 @@ struct PertDev {
 namespace {
 std::shared_ptr<PertDev> pert_device_table(int64_t nf, std::future<std::shared_ptr<const std::vector<float>>>& job,
                                            hipStream_t s, bool& uploaded_here) {
+    // never destroyed: the tables' HIP resources are left to the process's exit (a static
+    // destructor's hipEventSynchronize / hipHostFree would run while the runtime shuts down)
     static std::mutex mu;
-    static std::deque<std::shared_ptr<PertDev>> cache;
+    static auto& cache = *new std::deque<std::shared_ptr<PertDev>>();
     int device = 0;
     IMPLI_HIP(hipGetDevice(&device));
     std::lock_guard<std::mutex> lock(mu);
