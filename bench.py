@@ -880,9 +880,19 @@ def main():
                 t0 = time.perf_counter()
                 v, f = I.make_geometry(shape, mc)
                 ts.append(time.perf_counter() - t0)
-            ob02[key] = {"build_geometry_ms": round(min(ts) * 1e3, 3), "first_build_ms": round(t_first * 1e3, 3),
+            # the same build with the mesh read in place (get_v_ptr / get_f_ptr, the reference front
+            # end's reads, implisolid_main.js:227-237) instead of copied into fresh arrays
+            tv = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                I.make_geometry_views(shape, mc)
+                tv.append(time.perf_counter() - t0)
+            ob02[key] = {"build_geometry_ms": round(min(ts) * 1e3, 3), "build_geometry_views_ms": round(min(tv) * 1e3, 3),
+                         "first_build_ms": round(t_first * 1e3, 3),
                          "verts": int(len(v)), "faces": int(len(f)),
-                         "steps": "MC + 3 x [vertex resampling, centroid projection, QEM]"}
+                         "steps": "MC + 3 x [vertex resampling, centroid projection, QEM]",
+                         "note": "build_geometry_ms: the mesh copied into fresh arrays (get_v / get_f); "
+                                 "build_geometry_views_ms: read in place (get_v_ptr / get_f_ptr)"}
             if key in ob02_summary:
                 ob02[key]["parity"] = headline_parity(ob02_summary[key], v, f)
             # one profiled build (stream drained at every stage boundary): per-stage times, the
@@ -1184,6 +1194,7 @@ def main():
     if "ob02" in out:
         summ["ob02_build_ms"] = {k: v.get("build_geometry_ms") for k, v in out["ob02"].items() if isinstance(v, dict)}
         summ["ob02_first_build_ms"] = {k: v.get("first_build_ms") for k, v in out["ob02"].items() if isinstance(v, dict)}
+        summ["ob02_build_views_ms"] = {k: v.get("build_geometry_views_ms") for k, v in out["ob02"].items() if isinstance(v, dict)}
     if "ob02_sharded_estimate" in out:
         e = out["ob02_sharded_estimate"]
         summ["ob02_8shard_estimate_ms"] = {"r256": [e.get("estimate_ms_8"), e.get("single_ms")],
