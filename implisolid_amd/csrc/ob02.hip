@@ -2037,6 +2037,9 @@ void Ob02::begin_load(const float*& d_verts, int64_t nv_, int64_t nf_, float* d_
     rng_.reserve(kRngFields * sizeof(int64_t));
 }
 
+// the meshes whose first centroid normals run beside their topology (load_mesh)
+constexpr int64_t kNormalsAheadFaces = 400000;
+
 void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, int64_t nf_, float* d_work,
                      bool normals_ahead) {
     begin_load(d_verts, nv_, nf_, d_work);
@@ -2052,7 +2055,9 @@ void Ob02::load_mesh(const float* d_verts, int64_t nv_, const int32_t* d_faces, 
     // the first resampling's centroid normals need no topology: with the caller's word that a
     // resampling comes next, they run on the side stream beside the topology passes (not while
     // profiling, whose stages are drained one by one)
-    if (normals_ahead && nf > 0 && !profile_) {
+    // (large meshes only: on a small one the side stream's event costs more latency than the
+    // overlap saves, 0.70 -> 0.72 ms at 128^3, profiles/r06t_normals_ahead_ab.txt)
+    if (normals_ahead && nf >= kNormalsAheadFaces && !profile_) {
         reserve_topology();   // cen_ / nrm_ sized before the side stream writes them
         est_cen_ = nf;        // the whole mesh (whole_ranges below)
         if (!side_s_) IMPLI_HIP(hipStreamCreateWithFlags(&side_s_, hipStreamNonBlocking));

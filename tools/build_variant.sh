@@ -11,13 +11,14 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 d=$root/${VARIANTS:-variants}/$name
 rm -rf "$d"; mkdir -p "$d/implisolid_amd" "$d/tools"
 cp -r "$root/implisolid_amd/csrc" "$root/implisolid_amd/Makefile" "$d/implisolid_amd/"
-if [ -n "${GIT_REF:-}" ]; then
-    rm -rf "$d/implisolid_amd/csrc"; mkdir -p "$d/implisolid_amd/csrc"
-    (cd "$root" && git archive "$GIT_REF" implisolid_amd/csrc) | tar -x -C "$d" 
-fi
 rm -f "$d/implisolid_amd/csrc/generated/jit_headers.inc"
 cp "$root/tools/embed_headers.py" "$d/tools/"
 cp -r "$root/include" "$d/"
+if [ -n "${GIT_REF:-}" ]; then   # the sources, Makefile, header embedder and ABI header of that commit
+    rm -rf "$d/implisolid_amd/csrc" "$d/include"; mkdir -p "$d/implisolid_amd/csrc"
+    (cd "$root" && git archive "$GIT_REF" implisolid_amd/csrc implisolid_amd/Makefile tools/embed_headers.py include) | tar -x -C "$d"
+    rm -f "$d/implisolid_amd/csrc/generated/jit_headers.inc"
+fi
 while [ $# -gt 0 ]; do
     expr=$1; file=${2:-csrc/grid.hpp}; shift; [ $# -gt 0 ] && shift
     sed -i "$expr" "$d/implisolid_amd/$file"
