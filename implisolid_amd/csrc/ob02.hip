@@ -79,12 +79,15 @@ inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 // (about a third of the global atomics of one per corner).  A block whose ids spread wider (an
 // uploaded or subdivided mesh) takes one global atomic per corner.  The counts are the
 // same either way; the slots k_sort_umbrella then orders are the same set.
-constexpr int kWinCorners = 4096, kWinPerLane = kWinCorners / 256, kWinSlots = 8192;
+// PER corners per lane (256 PER per block): 16 on large meshes, 4 on small ones, whose few blocks
+// would otherwise leave most of the chip idle
+constexpr int kWinSlots = 8192;
 struct WinRange { int32_t lo, hi; };
-__device__ __forceinline__ WinRange win_range(const int32_t (&v)[kWinPerLane], int32_t* s_red) {
+template <int PER>
+__device__ __forceinline__ WinRange win_range(const int32_t (&v)[PER], int32_t* s_red) {
     int32_t lo = INT32_MAX, hi = INT32_MIN;
 #pragma unroll
-    for (int k = 0; k < kWinPerLane; ++k)
+    for (int k = 0; k < PER; ++k)
         if (v[k] >= 0) { lo = min(lo, v[k]); hi = max(hi, v[k]); }
     for (int o = 32; o > 0; o >>= 1) {
         lo = min(lo, __shfl_xor(lo, o, 64));
@@ -97,32 +100,34 @@ __device__ __forceinline__ WinRange win_range(const int32_t (&v)[kWinPerLane], i
     return r;
 }
 // the block's corners, lane-strided (corner c0 + k 256 + lane); -1 past the end
-__device__ __forceinline__ void win_load(const int32_t* __restrict__ f, int64_t n3, int64_t c0, int32_t (&v)[kWinPerLane]) {
+template <int PER>
+__device__ __forceinline__ void win_load(const int32_t* __restrict__ f, int64_t n3, int64_t c0, int32_t (&v)[PER]) {
 #pragma unroll
-    for (int k = 0; k < kWinPerLane; ++k) {
+    for (int k = 0; k < PER; ++k) {
         const int64_t i = c0 + k * 256 + threadIdx.x;
         v[k] = i < n3 ? f[i] : -1;
     }
 }
+template <int PER>
 __global__ __launch_bounds__(256) void k_degree_win(const int32_t* __restrict__ f, int64_t n3, uint32_t* __restrict__ deg) {
     __shared__ uint32_t cnt[kWinSlots];
     __shared__ int32_t s_red[8];
-    const int64_t c0 = (int64_t)blockIdx.x * kWinCorners;
-    int32_t v[kWinPerLane];
+    const int64_t c0 = (int64_t)blockIdx.x * (256 * PER);
+    int32_t v[PER];
     win_load(f, n3, c0, v);
     const WinRange r = win_range(v, s_red);
     if (r.hi < r.lo) return;   // (no corner: never, the grid covers n3)
     const int span = r.hi - r.lo + 1;
     if (r.hi - r.lo >= kWinSlots) {
 #pragma unroll
-        for (int k = 0; k < kWinPerLane; ++k)
+        for (int k = 0; k < PER; ++k)
             if (v[k] >= 0) atomicAdd(&deg[v[k]], 1u);
         return;
     }
     for (int k = threadIdx.x; k < span; k += 256) cnt[k] = 0u;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kWinPerLane; ++k)
+    for (int k = 0; k < PER; ++k)
         if (v[k] >= 0) atomicAdd(&cnt[v[k] - r.lo], 1u);
     __syncthreads();
     for (int k = threadIdx.x; k < span; k += 256)
@@ -255,20 +260,21 @@ __global__ void k_ranges_set(int64_t* __restrict__ rng, int64_t v0, int64_t v1, 
 // The umbrellas' face lists, the block's slot claims in LDS (see k_degree_win): each corner's rank among
 // the block's corners of its vertex from an LDS atomic, one global atomic per vertex for the block's
 // base in that umbrella
+template <int PER>
 __global__ __launch_bounds__(256) void k_fill_umbrella_win(const int32_t* __restrict__ f, int64_t n3,
                                                            const uint32_t* __restrict__ off, uint32_t* __restrict__ fill,
                                                            int32_t* __restrict__ lst) {
     __shared__ uint32_t cnt[kWinSlots];
     __shared__ int32_t s_red[8];
-    const int64_t c0 = (int64_t)blockIdx.x * kWinCorners;
-    int32_t v[kWinPerLane];
+    const int64_t c0 = (int64_t)blockIdx.x * (256 * PER);
+    int32_t v[PER];
     win_load(f, n3, c0, v);
     const WinRange r = win_range(v, s_red);
     if (r.hi < r.lo) return;
     const int span = r.hi - r.lo + 1;
     if (r.hi - r.lo >= kWinSlots) {
 #pragma unroll
-        for (int k = 0; k < kWinPerLane; ++k)
+        for (int k = 0; k < PER; ++k)
             if (v[k] >= 0) {
                 const uint32_t p = atomicAdd(&fill[v[k]], 1u);
                 lst[off[v[k]] + p] = (int32_t)((c0 + k * 256 + threadIdx.x) / 3);
@@ -277,15 +283,15 @@ __global__ __launch_bounds__(256) void k_fill_umbrella_win(const int32_t* __rest
     }
     for (int k = threadIdx.x; k < span; k += 256) cnt[k] = 0u;
     __syncthreads();
-    uint32_t rank[kWinPerLane];
+    uint32_t rank[PER];
 #pragma unroll
-    for (int k = 0; k < kWinPerLane; ++k) rank[k] = v[k] >= 0 ? atomicAdd(&cnt[v[k] - r.lo], 1u) : 0u;
+    for (int k = 0; k < PER; ++k) rank[k] = v[k] >= 0 ? atomicAdd(&cnt[v[k] - r.lo], 1u) : 0u;
     __syncthreads();
     for (int k = threadIdx.x; k < span; k += 256)   // counts -> the block's base in each umbrella
         if (cnt[k]) cnt[k] = atomicAdd(&fill[r.lo + k], cnt[k]);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kWinPerLane; ++k)
+    for (int k = 0; k < PER; ++k)
         if (v[k] >= 0) lst[off[v[k]] + cnt[v[k] - r.lo] + rank[k]] = (int32_t)((c0 + k * 256 + threadIdx.x) / 3);
 }
 
@@ -402,6 +408,12 @@ __device__ __forceinline__ int32_t fof_at(const int32_t* __restrict__ f, const u
         }
     }
     return (int32_t)((first != (uint32_t)fi) ? first : (c >= 2 ? last : 0u));
+}
+__global__ __launch_bounds__(256) void k_fof_umbrella(const int32_t* __restrict__ f, int64_t nf,
+                                                      const uint32_t* __restrict__ off, const int32_t* __restrict__ lst,
+                                                      int32_t* __restrict__ fof) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < 3 * nf) fof[i] = fof_at(f, off, lst, i);
 }
 // fof_at per vertex: vertex a's lane loads its umbrella's faces once (up to kFofRegs, in
 // registers; the loads issue together) and answers fof_at for every half-edge leaving a, where the
@@ -2240,16 +2252,27 @@ void Ob02::build_topology(bool deg_zeroed) {
     // umbrellas
     reserve_topology();
     if (!deg_zeroed) IMPLI_HIP(hipMemsetAsync(deg_.p, 0, (size_t)(nv + 1) * 4, s));
-    const unsigned wblocks = (unsigned)((3 * nf + kWinCorners - 1) / kWinCorners);
-    if (nf) k_degree_win<<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
+    // 16 corners per lane from 1.5 M corners (512^3: 2.2 M), else 4 (at 128^3, 340 k corners, the
+    // 16-corner blocks were 83: slower than the per-corner atomics of round 5)
+    const bool big = 3 * nf >= 1500000;
+    const int64_t per_block = big ? 256 * 16 : 256 * 4;
+    const unsigned wblocks = (unsigned)((3 * nf + per_block - 1) / per_block);
+    if (nf && big) k_degree_win<16><<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
+    else if (nf) k_degree_win<4><<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, deg_.as<uint32_t>());
     scan(deg_.as<uint32_t>(), uoff_.as<uint32_t>(), nv, true);   // deg_ left zeroed: the fill counters
-    if (nf) k_fill_umbrella_win<<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, uoff_.as<uint32_t>(),
+    if (nf && big) k_fill_umbrella_win<16><<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, uoff_.as<uint32_t>(),
+                                                        deg_.as<uint32_t>(), ulst_.as<int32_t>());
+    else if (nf) k_fill_umbrella_win<4><<<wblocks, 256, 0, s>>>(faces_.as<int32_t>(), 3 * nf, uoff_.as<uint32_t>(),
                                                         deg_.as<uint32_t>(), ulst_.as<int32_t>());
     if (nv) k_sort_umbrella<<<blocks_for(nv), 256, 0, s>>>(uoff_.as<uint32_t>(), ulst_.as<int32_t>(), nv);
     // faces of faces, from the umbrellas (the edge table is built only for subdivision)
-    if (nf && nv)
+    // per vertex on large meshes; per half-edge on small ones (more lanes in flight)
+    if (nf && nv && big)
         k_fof_vertex<<<blocks_for(nv), 256, 0, s>>>(faces_.as<int32_t>(), nv, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
                                                     fof_.as<int32_t>());
+    else if (nf)
+        k_fof_umbrella<<<blocks_for(3 * nf), 256, 0, s>>>(faces_.as<int32_t>(), nf, uoff_.as<uint32_t>(), ulst_.as<int32_t>(),
+                                                          fof_.as<int32_t>());
     etab_valid_ = false;
     IMPLI_HIP(hipGetLastError());
     topo_valid_ = true;
