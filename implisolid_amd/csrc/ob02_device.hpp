@@ -310,12 +310,12 @@ __device__ __forceinline__ void project_prep_body(const Ev& ev, const ProjArgs& 
 // meshes: see project_early_body)
 template <int W, class Ev>
 __device__ __forceinline__ void project_early_face(const Ev& ev, const ProjArgs& a, const GrpW<W>& g, int64_t j) {
-    // bisection levels per evaluation round and the nodes evaluated: every lane a node, the heap's
-    // first W (8 lanes: 3 levels and the first node of the 4th; 4 lanes: 2 levels and the first of
-    // the 3rd; 2 lanes: the mid and its child after f < -tol), so a round walks one level more when
-    // the serial walk goes down the evaluated side
-    constexpr int kLevels = W >= 8 ? 4 : W >= 4 ? 3 : 2;
-    constexpr int kNodes = W;
+    // bisection levels per evaluation round and the nodes evaluated: the whole tree of 3 / 2 levels
+    // for 8 / 4 lanes; 2 lanes evaluate the mid and its child after f < -tol (2 levels when the walk
+    // goes that way, 1 otherwise).  (Every lane a node for 4 lanes too, 3 levels with the first node
+    // of the third, measured 1-2 % slower at 256^3 and even at 512^3: profiles/r06v_*.)
+    constexpr int kLevels = W >= 8 ? 3 : 2;
+    constexpr int kNodes = W >= 8 ? 7 : W >= 4 ? 3 : 2;
     const V3 x{a.cen[3 * j], a.cen[3 * j + 1], a.cen[3 * j + 2]};
     const V3 fnv{a.fn[3 * j], a.fn[3 * j + 1], a.fn[3 * j + 2]};
     const V3 d0{a.dir[3 * j], a.dir[3 * j + 1], a.dir[3 * j + 2]};
@@ -555,7 +555,7 @@ __device__ __forceinline__ void project_late_face(const Ev& ev, const ProjArgs& 
             break;
         }
     }
-    finalize_g(g, 32 - __clz(g.w), ev, x, fcv, found, best, bf, a.out + 3 * j, a, evals, g.w);   // every lane a node
+    finalize_g(g, 31 - __clz(g.w), ev, x, fcv, found, best, bf, a.out + 3 * j, a, evals);
     if (a.evals && g.sub == 0) a.evals[j] += evals;
 }
 
